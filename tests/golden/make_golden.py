@@ -1,0 +1,290 @@
+"""Generates the committed golden fixtures by running the REFERENCE itself on CPU.
+
+Container-only (needs ``/root/reference``): ``python tests/golden/make_golden.py``.
+The outputs (``tests/golden/*.npz``) are data — seeded inputs and the reference's
+outputs on them — and are what pins ``oracle/``.  Nothing from the
+reference is copied; it is imported and executed via ``_refload.py``.
+
+Fixtures:
+  gpis_<state>.npz    GPIS.pred mean/std, compute_normal, and d(cm·mean + cs·std)/dX at
+                      seeded queries (gpis.py:43-87), for the 7 stored states and the
+                      N = 2000 synthetic banana state (SURVEY §8d recipe; its X1/y/noise
+                      are saved so the state can be refit without the reference).
+  fk_<robot>_<mode>.npz  compute_forward_kinematics pos/quat and d(cot·pos)/dq
+                      (robot_model.py:224-264) for Allegro, Leap, iiwa7_allegro; recursive=False
+                      only (the prob path, optimize_pregrasp.py:665).  recursive=True composes
+                      with each body's stale ``self.pose`` from the previous call
+                      (rigid_body.py:111-118) and is used only by out-of-scope optimizers.
+  closure_<case>.npz  ProbabilisticGraspOptimizer.closure (optimize_pregrasp.py:741-769):
+                      inputs, the captured Kabsch noise (``rand_like`` at :61), total_loss,
+                      total_margin, pregrasp tips and the 5 parameter gradients.
+  optimize_<case>.npz ProbabilisticGraspOptimizer.optimize (:771-839) for 30 iterations
+                      with a replayed noise sequence.
+"""
+from __future__ import annotations
+
+import contextlib
+import io
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import _refload  # noqa: E402
+
+OUT = HERE
+STATES = ["banana", "coffeebottle", "hammer", "lego", "mug", "mug2", "dummy"]
+
+
+def obj_vertices(path):
+    vs = []
+    with open(path) as f:
+        for line in f:
+            if line.startswith("v "):
+                vs.append([float(x) for x in line.split()[1:4]])
+    return np.asarray(vs)
+
+
+class NoiseTape:
+    """Replaces torch.rand_like on the Kabsch path with a recorded / replayed stream."""
+
+    def __init__(self, torch, seed=0, replay=None):
+        self.torch = torch
+        self.gen = torch.Generator().manual_seed(seed)
+        self.replay = list(replay) if replay is not None else None
+        self.record = []
+        self._orig = torch.rand_like
+
+    def __enter__(self):
+        torch = self.torch
+
+        def rand_like(t, *a, **k):
+            if self.replay is not None:
+                out = self.replay.pop(0).to(t.dtype)
+            else:
+                out = torch.rand(t.shape, dtype=t.dtype, generator=self.gen)
+            self.record.append(out.clone())
+            return out
+
+        torch.rand_like = rand_like
+        return self
+
+    def __exit__(self, *exc):
+        self.torch.rand_like = self._orig
+
+
+def load_state(ns, name):
+    g = ns.gpis.GPIS(0.08, 1.0)
+    cwd = os.getcwd()
+    os.chdir(ns.ref)
+    try:
+        g.load_state_data(f"{name}_state")
+    finally:
+        os.chdir(cwd)
+    return g
+
+
+def synthetic_banana(ns, n_total=2000):
+    """SURVEY §8d recipe, following optimize_pregrasp.py:904-922."""
+    torch = ns.torch
+    pcd = np.load(os.path.join(ns.ref, "partial_pcd/banana.npy"))
+    center = 0.5 * (pcd.min(0) + pcd.max(0))
+    n_ext, n_int = 14, 50
+    n_surf = n_total - n_ext - n_int
+    rng = np.random.default_rng(0)
+    surf = pcd[rng.permutation(len(pcd))[:n_surf]]
+    bound = 0.15
+    ext = np.array([[-1, -1, -1], [1, -1, -1], [-1, 1, -1], [1, 1, -1],
+                    [-1, -1, 1], [1, -1, 1], [-1, 1, 1], [1, 1, 1],
+                    [-1, 0, 0], [0, -1, 0], [1, 0, 0], [0, 1, 0],
+                    [0, 0, 1], [0, 0, -1]], dtype=np.float64) * bound + center
+    gen = torch.Generator().manual_seed(0)
+    w = torch.rand(n_int, n_surf, generator=gen).double()
+    internal = (torch.softmax(w * 30, dim=1) @ torch.from_numpy(surf)).numpy()
+    X1 = np.vstack([ext, surf, internal])
+    y = np.concatenate([np.full(n_ext, bound), np.zeros(n_surf), np.full(n_int, -bound)])[:, None]
+    noise = np.concatenate([np.full(n_ext, 0.2), np.full(n_surf, 0.005), np.full(n_int, 0.1)])
+    g = ns.gpis.GPIS(0.08, 1.0)
+    g.fit(torch.from_numpy(X1), torch.from_numpy(y), noise=torch.from_numpy(noise))
+    g.bias = torch.tensor(1.0, dtype=torch.float64)
+    return g, dict(syn_X1=X1, syn_y=y, syn_noise=noise)
+
+
+def gen_gpis(ns):
+    torch = ns.torch
+    rng = np.random.default_rng(1)
+    cases = [(s, load_state(ns, s), {}) for s in STATES]
+    g, extra = synthetic_banana(ns)
+    cases.append(("synthetic2000", g, extra))
+    for name, g, extra in cases:
+        X1 = g.X1.numpy()
+        lo, hi = X1.min(0) - 0.03, X1.max(0) + 0.03
+        M = 96
+        Xq = lo + (hi - lo) * rng.random((M, 3))
+        # include a few points ON training points (exact-surface case) and near them
+        Xq[:4] = X1[rng.integers(0, len(X1), 4)] + 1e-4 * rng.standard_normal((4, 3))
+        X = torch.from_numpy(Xq).requires_grad_(True)
+        mean, std = g.pred(X)
+        cm = rng.standard_normal(M)
+        cs = rng.standard_normal(M)
+        (mean * torch.from_numpy(cm)).sum().add((std * torch.from_numpy(cs)).sum()).backward()
+        normal = g.compute_normal(torch.from_numpy(Xq))
+        # batched 3-D input path (gpis.py:48-50): [M/4, 4, 3] -> [M/4, 4]
+        mean3, std3 = g.pred(torch.from_numpy(Xq).view(-1, 4, 3))
+        np.savez_compressed(
+            os.path.join(OUT, f"gpis_{name}.npz"),
+            X=Xq, mean=mean.detach().numpy(), std=std.detach().numpy(), cm=cm, cs=cs,
+            grad_X=X.grad.numpy(), normal=normal.numpy(),
+            mean3=mean3.detach().numpy(), std3=std3.detach().numpy(),
+            R=float(g.R), bias=float(g.bias), **extra)
+        print("gpis", name, len(X1))
+
+
+def gen_fk(ns):
+    torch = ns.torch
+    rng = np.random.default_rng(2)
+    ee_offsets = ns.opt.EE_OFFSETS
+    specs = [
+        ("allegro", ns.robot_configs["allegro"]["ee_link_name"], ns.robot_configs["allegro"]["ee_link_offset"].tolist(),
+         ns.robot_configs["allegro"]["ref_q"], "cfg"),
+        ("allegro", ns.robot_configs["allegro"]["ee_link_name"], ee_offsets, ns.robot_configs["allegro"]["ref_q"], "eeoff"),
+        ("leap", ns.robot_configs["leap"]["ee_link_name"], ns.robot_configs["leap"]["ee_link_offset"].tolist(),
+         ns.robot_configs["leap"]["ref_q"], "cfg"),
+        ("iiwa7_allegro", ["link_3.0_tip", "link_7.0_tip", "link_11.0_tip", "link_15.0_tip"], ee_offsets, None, "eeoff"),
+    ]
+    for robot, links, offsets, ref_q, tag in specs:
+        model = ns.rm.DifferentiableRobotModel(os.path.join(ns.ref, _refload.URDFS[robot]))
+        B = 32
+        dof = model._n_dofs
+        base = np.zeros(dof) if ref_q is None else np.asarray(ref_q)
+        scale = 0.3 if ref_q is None else 0.1
+        q = (base + scale * rng.standard_normal((B, dof))).astype(np.float32)
+        for recursive in (False,):
+            qt = torch.from_numpy(q).requires_grad_(True)
+            with contextlib.redirect_stdout(io.StringIO()):
+                pos, quat = model.compute_forward_kinematics(qt, links, recursive=recursive, offsets=offsets)
+            cot = rng.standard_normal(pos.shape).astype(np.float32)
+            (pos * torch.from_numpy(cot)).sum().backward()
+            mode = "rec" if recursive else "nonrec"
+            np.savez_compressed(
+                os.path.join(OUT, f"fk_{robot}_{tag}_{mode}.npz"),
+                q=q, pos=pos.detach().numpy(), quat=quat.detach().numpy(), cot=cot,
+                grad_q=qt.grad.numpy(), links=np.array(links), offsets=np.asarray(offsets, dtype=np.float64))
+            print("fk", robot, tag, mode)
+
+
+def problem_inputs(ns, hand, E, seed, perturb_target):
+    """Mirrors optimize_pregrasp.py __main__ (:872-999) with --use_config, headless.
+
+    The object centre is the banana mesh's vertex AABB centre (the reference uses the
+    AABB of a random Poisson sample of the same mesh, :885-888)."""
+    torch = ns.torch
+    cfg = {"wrist_x": 0.0, "wrist_y": 0.015, "wrist_z": 0.11, "floor_offset": 0.02}
+    verts = obj_vertices(os.path.join(ns.ref, "assets/banana/banana.obj"))
+    center = 0.5 * (verts.min(0) + verts.max(0))
+    W = np.array(ns.opt.WRIST_OFFSET, dtype=np.float64).copy()
+    W[:, 0] += center[0]
+    W[:, 1] += center[1]
+    W[:, 2] += 2 * center[2]
+    W[:, 0] += cfg["wrist_x"]
+    W[:, 1] += cfg["wrist_y"]
+    W[:, 2] += cfg["wrist_z"] - cfg["floor_offset"]
+    rng = np.random.default_rng(seed)
+    idx = np.arange(E) % len(W)
+    palm = W[idx]
+    ref_q = np.asarray(ns.robot_configs[hand]["ref_q"], dtype=np.float64)
+    q = np.tile(ref_q, (E, 1))
+    target = np.tile(center, (E, 4, 1)).astype(np.float64)
+    if E > len(W):
+        q = q + 0.1 * rng.standard_normal(q.shape)
+        palm = palm + np.concatenate([0.005 * rng.standard_normal((E, 3)), 0.05 * rng.standard_normal((E, 3))], 1)
+    if perturb_target:
+        target = target + 0.01 * rng.standard_normal(target.shape)
+    comp = np.tile(np.array([10.0, 10.0, 10.0, 20.0]), (E, 1))
+    return dict(q=q, comp=comp, target=target, palm=palm, center=center, W=W)
+
+
+def make_optimizer(ns, hand, palm, num_iters):
+    rc = ns.robot_configs[hand]
+    with contextlib.redirect_stdout(io.StringIO()):
+        o = ns.opt.ProbabilisticGraspOptimizer(
+            os.path.join(ns.ref, _refload.URDFS[hand]),
+            ee_link_names=rc["ee_link_name"], ee_link_offsets=rc["ee_link_offset"].tolist(),
+            anchor_link_names=rc["collision_links"], anchor_link_offsets=rc["collision_offsets"].tolist(),
+            collision_pairs=rc["collision_pairs"],
+            tip_bounding_box=[ns.opt.FINGERTIP_LB, ns.opt.FINGERTIP_UB],
+            ref_q=rc["ref_q"].tolist(), optimize_target=True, optimize_palm=True,
+            num_iters=num_iters, palm_offset=palm, mass=0.1, com=[0.0, 0.0, 0.0],
+            gravity=True, uncertainty=20.0)
+    return o
+
+
+def gen_closure(ns, name, hand, state, E, seed, perturb_target, gpis_obj=None):
+    torch = ns.torch
+    inp = problem_inputs(ns, hand, E, seed, perturb_target)
+    g = gpis_obj if gpis_obj is not None else load_state(ns, state)
+    o = make_optimizer(ns, hand, inp["palm"], 1)
+    q = torch.from_numpy(inp["q"]).clone().requires_grad_(True)
+    comp = torch.from_numpy(inp["comp"]).clone().requires_grad_(True)
+    target = torch.from_numpy(inp["target"]).clone().requires_grad_(True)
+    palm_pos = torch.from_numpy(inp["palm"][:, :3]).clone().requires_grad_(True)
+    palm_ori = torch.from_numpy(inp["palm"][:, 3:]).clone().requires_grad_(True)
+    o.optim = torch.optim.Adam([q, comp, target, palm_pos, palm_ori])
+    with NoiseTape(torch, seed=seed) as tape, contextlib.redirect_stdout(io.StringIO()):
+        loss = o.closure(q, comp, target, palm_pos, palm_ori, 1, g, E)
+    noise = torch.stack(tape.record).numpy()
+    np.savez_compressed(
+        os.path.join(OUT, f"closure_{name}.npz"),
+        hand=hand, state=state, q=inp["q"], comp=inp["comp"], target=inp["target"], palm=inp["palm"],
+        center=inp["center"], noise=noise, loss=float(loss), total_loss=o.total_loss.detach().numpy(),
+        total_margin=o.total_margin.detach().numpy(), pregrasp_tip=o.pregrasp_tip_pose.detach().numpy(),
+        grad_q=q.grad.numpy(), grad_comp=comp.grad.numpy(), grad_target=target.grad.numpy(),
+        grad_palm_pos=palm_pos.grad.numpy(), grad_palm_ori=palm_ori.grad.numpy())
+    print("closure", name, float(loss))
+
+
+def gen_optimize(ns, name, hand, state, E, seed, iters):
+    torch = ns.torch
+    inp = problem_inputs(ns, hand, E, seed, False)
+    g = load_state(ns, state)
+    o = make_optimizer(ns, hand, inp["palm"], iters)
+    gen = torch.Generator().manual_seed(seed)
+    tape = [torch.rand((3 * E, 3, 3), dtype=torch.float64, generator=gen) for _ in range(iters)]
+    with NoiseTape(torch, replay=tape), contextlib.redirect_stdout(io.StringIO()):
+        out = o.optimize(torch.from_numpy(inp["q"]), torch.from_numpy(inp["target"]),
+                         torch.from_numpy(inp["comp"]), 1, g)
+    opt_q, opt_comp, opt_target, opt_palm, opt_margin = [t.detach().numpy() for t in out]
+    np.savez_compressed(
+        os.path.join(OUT, f"optimize_{name}.npz"),
+        hand=hand, state=state, iters=iters, q=inp["q"], comp=inp["comp"], target=inp["target"],
+        palm=inp["palm"], noise=torch.stack(tape).numpy(), opt_q=opt_q, opt_comp=opt_comp,
+        opt_target=opt_target, opt_palm=opt_palm, opt_margin=opt_margin)
+    print("optimize", name)
+
+
+def main():
+    ns = _refload.load()
+    torch = ns.torch
+    torch.set_num_threads(8)
+    what = sys.argv[1:] or ["gpis", "fk", "closure", "optimize"]
+    if "gpis" in what:
+        gen_gpis(ns)
+    if "fk" in what:
+        gen_fk(ns)
+    if "closure" in what:
+        gen_closure(ns, "allegro_banana_e6", "allegro", "banana", 6, 10, False)
+        gen_closure(ns, "allegro_banana_e64", "allegro", "banana", 64, 11, False)
+        gen_closure(ns, "allegro_banana_e64_spread", "allegro", "banana", 64, 12, True)
+        gen_closure(ns, "leap_banana_e64", "leap", "banana", 64, 13, False)
+        gen_closure(ns, "leap_banana_e64_spread", "leap", "banana", 64, 14, True)
+        gen_closure(ns, "allegro_mug_e16_spread", "allegro", "mug", 16, 15, True)
+        g, _ = synthetic_banana(ns)
+        gen_closure(ns, "allegro_syn2000_e16_spread", "allegro", "synthetic2000", 16, 16, True, gpis_obj=g)
+    if "optimize" in what:
+        gen_optimize(ns, "allegro_banana_e6", "allegro", "banana", 6, 20, 30)
+
+
+if __name__ == "__main__":
+    main()
