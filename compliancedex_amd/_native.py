@@ -1,0 +1,113 @@
+"""ctypes binding of the C ABI in ``include/cdx.h`` (libcdx.so, gfx950).
+
+There is no CPU fallback: if the library is missing or fails to load, every operator
+raises.  Struct layouts are checked against the library's own ``sizeof`` at load time.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+
+MAX_BODIES, MAX_TIPS, MAX_DOFS, MAX_LEVELS = 32, 8, 32, 4
+KERNELS = {"tps": 0, "rbf": 1, "joint": 2}
+ERRORS = {-1: "invalid argument", -2: "unsupported GPIS kernel", -3: "chain exceeds descriptor capacity",
+          -10: "HIP launch failed"}
+
+
+class CdxGpis(C.Structure):
+    _fields_ = [("X1", C.c_void_p), ("alpha", C.c_void_p), ("Ainv", C.c_void_p), ("N", C.c_int32),
+                ("N_pad", C.c_int32), ("kernel", C.c_int32), ("_pad", C.c_int32), ("R", C.c_double),
+                ("sigma", C.c_double), ("bias", C.c_double)]
+
+
+class CdxBody(C.Structure):
+    _fields_ = [("F", C.c_float * 9), ("t", C.c_float * 3), ("sign", C.c_float), ("axis", C.c_int8),
+                ("parent", C.c_int8), ("dof", C.c_int8), ("_pad", C.c_int8)]
+
+
+class CdxChain(C.Structure):
+    _fields_ = [("n_bodies", C.c_int32), ("n_dofs", C.c_int32), ("n_tips", C.c_int32), ("has_offsets", C.c_int32),
+                ("tip_body", C.c_int32 * MAX_TIPS), ("tip_offset", (C.c_float * 3) * MAX_TIPS),
+                ("bodies", CdxBody * MAX_BODIES)]
+
+
+class CdxProblem(C.Structure):
+    _fields_ = [("chain", CdxChain), ("gpis", CdxGpis), ("n_levels", C.c_int32), ("n_query_levels", C.c_int32),
+                ("level_query", C.c_int32 * MAX_LEVELS), ("coeff", (C.c_float * MAX_TIPS) * MAX_LEVELS),
+                ("weight", C.c_double * MAX_LEVELS), ("ref_q", C.c_float * MAX_DOFS), ("cos_mu", C.c_float),
+                ("gravity", C.c_int32), ("optimize_palm", C.c_int32), ("_pad", C.c_int32), ("com", C.c_float * 3),
+                ("dummy_target_z", C.c_float), ("dummy_comp", C.c_float), ("_pad2", C.c_float),
+                ("uncertainty", C.c_double)]
+
+
+_P = C.c_void_p
+_I64 = C.c_int64
+_SIGS = {
+    "cdx_gpis_mean": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P, _P]),
+    "cdx_gpis_std_workspace": (C.c_size_t, [C.POINTER(CdxGpis), _I64]),
+    "cdx_gpis_std": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P, _P]),
+    "cdx_fk_forward": (C.c_int, [C.POINTER(CdxChain), _P, _I64, _P, _P, _P]),
+    "cdx_fk_backward": (C.c_int, [C.POINTER(CdxChain), _P, _I64, _P, _P, _P]),
+    "cdx_closure_workspace": (C.c_size_t, [C.POINTER(CdxProblem), _I64]),
+    "cdx_closure": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, _P, _P, _P, _P, _P, C.c_uint64, _P,
+                              _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cdx_sdf_forward": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
+    "cdx_sdf_backward": (C.c_int, [_P, _P, _P, _I64, _P, _P]),
+    "cdx_version": (C.c_char_p, []),
+    "cdx_abi_sizes": (None, [C.POINTER(C.c_size_t)]),
+    "cdx_selftest_mfma_f64": (C.c_int, [_P, _P, _P, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib_path():
+    return os.environ.get("CDX_LIB", os.path.join(LIB_DIR, "libcdx.so"))
+
+
+def load():
+    """Loads libcdx.so (raises ImportError if it is missing — there is no fallback)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = lib_path()
+        if not os.path.exists(path):
+            raise ImportError(f"compliancedex_amd native library not built: {path} "
+                              "(run `python -m compliancedex_amd.build`)")
+        lib = C.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        sizes = (C.c_size_t * 4)()
+        lib.cdx_abi_sizes(sizes)
+        mine = [C.sizeof(CdxGpis), C.sizeof(CdxBody), C.sizeof(CdxChain), C.sizeof(CdxProblem)]
+        if list(sizes) != mine:
+            raise ImportError(f"ABI struct size mismatch: library {list(sizes)} vs binding {mine}")
+        _lib = lib
+        return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {ERRORS.get(rc, rc)} (code {rc})")
+
+
+def ptr(t):
+    """Device pointer of a (contiguous) tensor, or None."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("tensor must be contiguous")
+    return t.data_ptr()
+
+
+def stream_ptr(device=None):
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,87 @@
+"""In-tree build of the native libraries (no cmake/ninja; plain hipcc / g++ / gcc).
+
+  compliancedex_amd/lib/libcdx.so        gfx950 kernels + C ABI (include/cdx.h) — the product
+  compliancedex_amd/lib/libcdx_host.so   host build of the per-candidate code — CPU tests only
+  oracle/build/libsdf_oracle.so          C oracle of the TorchSDF kernel — CPU tests only
+
+``python -m compliancedex_amd.build`` or ``__graft_entry__.build()``.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "lib")
+ARCH = os.environ.get("CDX_OFFLOAD_ARCH", "gfx950")
+
+HIP_SOURCES = ["cdx_gpis.hip", "cdx_closure.hip", "cdx_sdf.hip"]
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _deps():
+    return [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(REPO, "include", "cdx.h")]
+
+
+def build_device(force=False):
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, "libcdx.so")
+    if not force and not _stale(out, _deps()):
+        return out
+    objs = []
+    for src in HIP_SOURCES:
+        obj = os.path.join(LIB, src.replace(".hip", ".o"))
+        flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(REPO, "include")]
+        if src == "cdx_sdf.hip":
+            flags.append("-ffp-contract=off")
+        _run([HIPCC, *flags, "-c", os.path.join(CSRC, src), "-o", obj])
+        objs.append(obj)
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out])
+    for o in objs:
+        os.remove(o)
+    return out
+
+
+def build_host(force=False):
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, "libcdx_host.so")
+    if not force and not _stale(out, _deps()):
+        return out
+    _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wno-unknown-pragmas",
+          "-I", os.path.join(REPO, "include"), os.path.join(CSRC, "host_ref.cpp"), "-o", out])
+    return out
+
+
+def build_oracle(force=False):
+    bdir = os.path.join(REPO, "oracle", "build")
+    os.makedirs(bdir, exist_ok=True)
+    src = os.path.join(REPO, "oracle", "sdf_oracle.c")
+    out = os.path.join(bdir, "libsdf_oracle.so")
+    if not force and not _stale(out, [src]):
+        return out
+    _run(["gcc", "-O2", "-fPIC", "-shared", "-ffp-contract=off", src, "-o", out, "-lm"])
+    return out
+
+
+def build_all(force=False):
+    return build_device(force), build_host(force), build_oracle(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

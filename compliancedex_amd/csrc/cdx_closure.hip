@@ -1,0 +1,269 @@
+// Prob-mode closure on gfx950: FK + query generation, GPIS queries, fused cost+backward.
+//
+// Launch sequence of cdx_closure (all on the caller's stream, no host sync):
+//   1. closure_queries_kernel   one thread per candidate: f32 FK of the pregrasp tips,
+//                               palm transform, writes every GPIS query point
+//                               (all-tip rows deduplicated over identical coefficient rows,
+//                               targets once, pregrasp tips, palm)      — :657-669, :743-750
+//   2. gpis_mean (cdx_gpis.hip) mean/∇mean/normal at all queries      — gpis.py:43-87
+//   3. gpis_std  (cdx_gpis.hip) std/∇std at the all-tip queries (fp64 MFMA)
+//   4. closure_cost_kernel      one thread per candidate: seven cost terms per level,
+//                               Kabsch + SVD backward, FK backward; writes loss, margin
+//                               and the five parameter gradients        — :713-769, :49-118
+#include <hip/hip_runtime.h>
+
+#include "cdx_cost.h"
+
+namespace {
+
+// --------------------------------------------------------------- standalone FK
+__global__ __launch_bounds__(64) void fk_forward_kernel(cdx_chain c, const float* __restrict__ q, int64_t B,
+                                                        float* __restrict__ pos, float* __restrict__ quat) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float qb[CDX_MAX_DOFS];
+  for (int i = 0; i < c.n_dofs; ++i) qb[i] = q[b * c.n_dofs + i];
+  for (int k = 0; k < c.n_tips; ++k) {
+    float p[3], qt[4];
+    cdx::fk_tip(c, k, qb, p, qt);
+    for (int i = 0; i < 3; ++i) pos[(b * c.n_tips + k) * 3 + i] = p[i];
+    if (quat)
+      for (int i = 0; i < 4; ++i) quat[(b * c.n_tips + k) * 4 + i] = qt[i];
+  }
+}
+
+__global__ __launch_bounds__(64) void fk_backward_kernel(cdx_chain c, const float* __restrict__ q, int64_t B,
+                                                         const float* __restrict__ gpos, float* __restrict__ gq) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float qb[CDX_MAX_DOFS], g[CDX_MAX_DOFS];
+  for (int i = 0; i < c.n_dofs; ++i) { qb[i] = q[b * c.n_dofs + i]; g[i] = 0.f; }
+  for (int k = 0; k < c.n_tips; ++k) cdx::fk_tip_bwd(c, k, qb, gpos + (b * c.n_tips + k) * 3, g);
+  for (int i = 0; i < c.n_dofs; ++i) gq[b * c.n_dofs + i] = g[i];
+}
+
+// --------------------------------------------------------------- closure stages
+__global__ __launch_bounds__(64) void closure_queries_kernel(cdx_problem P, int64_t E, const double* __restrict__ q,
+                                                             const double* __restrict__ target,
+                                                             const double* __restrict__ palm_pos,
+                                                             const double* __restrict__ palm_ori,
+                                                             double* __restrict__ X, double* __restrict__ pre_out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int T = P.chain.n_tips, D = P.chain.n_dofs, Lq = P.n_query_levels;
+  double tip[CDX_MAX_TIPS][3], Rp[9];
+  float tl[CDX_MAX_TIPS][3];
+  cdx::pregrasp_tips(P, q + e * D, palm_pos + 3 * e, palm_ori + 3 * e, tip, tl, Rp);
+  const double* tg = target + e * T * 3;
+  for (int u = 0; u < Lq; ++u) {
+    int k = 0;
+    while (k < P.n_levels - 1 && P.level_query[k] != u) ++k;
+    for (int f = 0; f < T; ++f) {
+      const double c = (double)P.coeff[k][f];
+      const int64_t qi = cdx::q_alltip(u, e, f, E, T);
+      for (int i = 0; i < 3; ++i) X[3 * qi + i] = tg[3 * f + i] + c * (tip[f][i] - tg[3 * f + i]);
+    }
+  }
+  for (int f = 0; f < T; ++f) {
+    const int64_t qt = cdx::q_target(Lq, e, f, E, T), qp = cdx::q_pre(Lq, e, f, E, T);
+    for (int i = 0; i < 3; ++i) {
+      X[3 * qt + i] = tg[3 * f + i];
+      X[3 * qp + i] = tip[f][i];
+      if (pre_out) pre_out[(e * T + f) * 3 + i] = tip[f][i];
+    }
+  }
+  if (P.optimize_palm) {
+    const int64_t qm = cdx::q_palm(Lq, e, E, T);
+    for (int i = 0; i < 3; ++i) X[3 * qm + i] = palm_pos[3 * e + i];
+  }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+struct GpisView {
+  const double *mean, *gmean, *normal, *std_, *gstd;
+  int64_t E;
+  int T, Lq;
+  __device__ cdx::GpisPoint operator()(int kind, int u, int f) const;
+  int64_t e;
+};
+
+__device__ cdx::GpisPoint GpisView::operator()(int kind, int u, int f) const {
+  cdx::GpisPoint p;
+  int64_t qi;
+  if (kind == 0) qi = cdx::q_alltip(u, e, f, E, T);
+  else if (kind == 1) qi = cdx::q_target(Lq, e, f, E, T);
+  else if (kind == 2) qi = cdx::q_pre(Lq, e, f, E, T);
+  else qi = cdx::q_palm(Lq, e, E, T);
+  p.mean = mean[qi];
+  for (int i = 0; i < 3; ++i) p.gmean[i] = gmean[3 * qi + i];
+  if (kind == 0) {
+    p.std = std_[qi];
+    for (int i = 0; i < 3; ++i) { p.gstd[i] = gstd[3 * qi + i]; p.normal[i] = normal[3 * qi + i]; }
+  } else {
+    p.std = 0;
+    for (int i = 0; i < 3; ++i) { p.gstd[i] = 0; p.normal[i] = 0; }
+  }
+  return p;
+}
+
+__global__ __launch_bounds__(64) void closure_cost_kernel(
+    cdx_problem P, int64_t E, const double* __restrict__ q, const double* __restrict__ comp,
+    const double* __restrict__ target, const double* __restrict__ palm_pos, const double* __restrict__ palm_ori,
+    const double* __restrict__ noise, uint64_t seed, GpisView gv, double* __restrict__ total_loss,
+    double* __restrict__ total_margin, double* __restrict__ g_q, double* __restrict__ g_comp,
+    double* __restrict__ g_target, double* __restrict__ g_palm_pos, double* __restrict__ g_palm_ori,
+    int32_t* __restrict__ flip) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int T = P.chain.n_tips, D = P.chain.n_dofs, K = P.n_levels;
+  double nz[CDX_MAX_LEVELS * 9];
+  cdx::CandidateIn in;
+  in.q = q + e * D;
+  in.comp = comp + e * T;
+  in.target = target + e * T * 3;
+  in.palm_pos = palm_pos + 3 * e;
+  in.palm_ori = palm_ori + 3 * e;
+  if (noise) {
+    in.noise = noise + e * 9;
+    in.noise_stride = E * 9;
+  } else {
+    for (int k = 0; k < K; ++k)
+      for (int i = 0; i < 9; ++i) {
+        const uint64_t r = splitmix64(seed ^ splitmix64((uint64_t)((k * E + e) * 9 + i)));
+        nz[9 * k + i] = (double)(r >> 11) * 0x1.0p-53;
+      }
+    in.noise = nz;
+    in.noise_stride = 9;
+  }
+  GpisView g = gv;
+  g.e = e;
+  cdx::CandidateOut out;
+  cdx::closure_candidate(P, in, g, out);
+  total_loss[e] = out.loss;
+  for (int f = 0; f < T; ++f) {
+    total_margin[e * T + f] = out.margin[f];
+    g_comp[e * T + f] = out.g_comp[f];
+    for (int i = 0; i < 3; ++i) g_target[(e * T + f) * 3 + i] = out.g_target[f][i];
+  }
+  for (int i = 0; i < D; ++i) g_q[e * D + i] = out.g_q[i];
+  for (int i = 0; i < 3; ++i) { g_palm_pos[3 * e + i] = out.g_palm_pos[i]; g_palm_ori[3 * e + i] = out.g_palm_ori[i]; }
+  if (flip)
+    for (int k = 0; k < K; ++k) flip[k * E + e] = out.flip[k];
+}
+
+bool chain_ok(const cdx_chain* c) {
+  return c && c->n_bodies > 0 && c->n_bodies <= CDX_MAX_BODIES && c->n_dofs >= 0 && c->n_dofs <= CDX_MAX_DOFS &&
+         c->n_tips > 0 && c->n_tips <= CDX_MAX_TIPS;
+}
+
+size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+
+struct ClosureWs {
+  double *X, *mean, *gmean, *normal, *std_, *gstd;
+  void* std_ws;
+  size_t bytes;
+};
+
+ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
+  ClosureWs w;
+  const int64_t Mq = cdx::n_queries(*p, E);
+  const int64_t Ms = (int64_t)p->n_query_levels * E * p->chain.n_tips;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char* r = base ? base + off : nullptr; off += align256(bytes); return r; };
+  w.X = (double*)take(Mq * 3 * sizeof(double));
+  w.mean = (double*)take(Mq * sizeof(double));
+  w.gmean = (double*)take(Mq * 3 * sizeof(double));
+  w.normal = (double*)take(Mq * 3 * sizeof(double));
+  w.std_ = (double*)take(Ms * sizeof(double));
+  w.gstd = (double*)take(Ms * 3 * sizeof(double));
+  w.std_ws = take(cdx_gpis_std_workspace(&p->gpis, Ms));
+  w.bytes = off;
+  return w;
+}
+
+bool problem_ok(const cdx_problem* p) {
+  if (!p || !chain_ok(&p->chain)) return false;
+  if (p->n_levels < 1 || p->n_levels > CDX_MAX_LEVELS) return false;
+  if (p->n_query_levels < 1 || p->n_query_levels > p->n_levels) return false;
+  for (int k = 0; k < p->n_levels; ++k)
+    if (p->level_query[k] < 0 || p->level_query[k] >= p->n_query_levels) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cdx_fk_forward(const cdx_chain* chain, const float* q, int64_t B, float* pos, float* quat, cdx_stream_t stream) {
+  if (!chain_ok(chain)) return CDX_ECHAIN;
+  if (B < 0 || (B > 0 && (!q || !pos))) return CDX_EINVAL;
+  if (B == 0) return CDX_OK;
+  hipLaunchKernelGGL(fk_forward_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0,
+                     reinterpret_cast<hipStream_t>(stream), *chain, q, B, pos, quat);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+int cdx_fk_backward(const cdx_chain* chain, const float* q, int64_t B, const float* grad_pos, float* grad_q,
+                    cdx_stream_t stream) {
+  if (!chain_ok(chain)) return CDX_ECHAIN;
+  if (B < 0 || (B > 0 && (!q || !grad_pos || !grad_q))) return CDX_EINVAL;
+  if (B == 0) return CDX_OK;
+  hipLaunchKernelGGL(fk_backward_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0,
+                     reinterpret_cast<hipStream_t>(stream), *chain, q, B, grad_pos, grad_q);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+size_t cdx_closure_workspace(const cdx_problem* p, int64_t E) {
+  if (!problem_ok(p) || E <= 0) return 0;
+  return closure_ws_layout(p, E, nullptr).bytes;
+}
+
+int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* comp, const double* target,
+                const double* palm_pos, const double* palm_ori, const double* kabsch_noise, uint64_t seed,
+                void* workspace, double* total_loss, double* total_margin, double* pregrasp_tip, double* g_q,
+                double* g_comp, double* g_target, double* g_palm_pos, double* g_palm_ori, int32_t* flip,
+                cdx_stream_t stream) {
+  if (!problem_ok(p)) return CDX_EINVAL;
+  if (E < 0) return CDX_EINVAL;
+  if (E == 0) return CDX_OK;
+  if (!q || !comp || !target || !palm_pos || !palm_ori || !workspace || !total_loss || !total_margin || !g_q ||
+      !g_comp || !g_target || !g_palm_pos || !g_palm_ori)
+    return CDX_EINVAL;
+  if (!p->gpis.Ainv || !p->gpis.X1 || !p->gpis.alpha) return CDX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  ClosureWs w = closure_ws_layout(p, E, static_cast<char*>(workspace));
+  const int64_t Mq = cdx::n_queries(*p, E);
+  const int64_t Ms = (int64_t)p->n_query_levels * E * p->chain.n_tips;
+  const dim3 grid((unsigned)((E + 63) / 64));
+  hipLaunchKernelGGL(closure_queries_kernel, grid, dim3(64), 0, s, *p, E, q, target, palm_pos, palm_ori, w.X,
+                     pregrasp_tip);
+  if (hipGetLastError() != hipSuccess) return CDX_ELAUNCH;
+  int rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
+  if (rc) return rc;
+  rc = cdx_gpis_std(&p->gpis, w.X, Ms, w.std_, w.gstd, w.std_ws, stream);
+  if (rc) return rc;
+  GpisView gv;
+  gv.mean = w.mean; gv.gmean = w.gmean; gv.normal = w.normal; gv.std_ = w.std_; gv.gstd = w.gstd;
+  gv.E = E; gv.T = p->chain.n_tips; gv.Lq = p->n_query_levels; gv.e = 0;
+  hipLaunchKernelGGL(closure_cost_kernel, grid, dim3(64), 0, s, *p, E, q, comp, target, palm_pos, palm_ori,
+                     kabsch_noise, seed, gv, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori,
+                     flip);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+const char* cdx_version(void) { return "compliancedex_amd 0.1 gfx950"; }
+
+}  // extern "C"
+
+extern "C" void cdx_abi_sizes(size_t* out) {
+  out[0] = sizeof(cdx_gpis);
+  out[1] = sizeof(cdx_body);
+  out[2] = sizeof(cdx_chain);
+  out[3] = sizeof(cdx_problem);
+}

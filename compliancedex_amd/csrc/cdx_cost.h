@@ -1,0 +1,507 @@
+// Per-candidate prob-mode closure: cost terms, their reverse-mode gradient and the FK
+// backward, in float64 (FK in float32) — one candidate per call.
+//
+// Reference: optimize_pregrasp.py
+//   closure               :741-769    (pregrasp levels, weights, pre/palm GPIS terms)
+//   compute_loss          :713-739    (seven cost terms)
+//   force_eq_reward       :73-118     (dummy gravity spring, equilibrium, friction margin)
+//   optimal_transformation_batch :49-69 (weighted Kabsch, SVD of H + 1e-6·noise)
+//   compute_contact_margin :703-710
+//   forward_kinematics    :657-669    (+ math_utils.py:68-123 euler XYZ)
+// The SVD backward is torch's formula for U,V cotangents (gS = 0):
+//   gH = U·[(skew(UᵀgU)∘S_k + S_j∘skew(VᵀgV)) / (S_k² − S_j²)]·Vᵀ
+// evaluated on our own one-sided-Jacobi SVD (R and its gradient are invariant to the
+// singular vectors' sign gauge).
+#pragma once
+#include "cdx_fk.h"
+
+namespace cdx {
+
+// ---------------------------------------------------------------- 3×3 SVD (f64)
+// One-sided Jacobi on the columns of A: A·V = U·diag(S), S descending.  Backward-stable
+// with high relative accuracy for the small singular values the rank-1-plus-noise
+// Kabsch matrices of the reference's initial configuration have.
+CDX_HD void svd3(const double* H, double* U, double* S, double* V) {
+  double A[9];
+  for (int i = 0; i < 9; ++i) { A[i] = H[i]; V[i] = (i % 4 == 0) ? 1.0 : 0.0; }
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    double off = 0.0;
+    for (int pr = 0; pr < 3; ++pr) {
+      const int p = pr == 2 ? 1 : 0, qq = pr == 0 ? 1 : 2;
+      double a = 0, b = 0, g = 0;
+      for (int i = 0; i < 3; ++i) {
+        a += A[3 * i + p] * A[3 * i + p];
+        b += A[3 * i + qq] * A[3 * i + qq];
+        g += A[3 * i + p] * A[3 * i + qq];
+      }
+      if (g == 0.0) continue;
+      const double rel = fabs(g) / sqrt(a * b);
+      off = rel > off ? rel : off;
+      if (rel < 1e-17) continue;
+      const double zeta = (b - a) / (2.0 * g);
+      const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+      const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+      for (int i = 0; i < 3; ++i) {
+        const double ap = A[3 * i + p], aq = A[3 * i + qq];
+        A[3 * i + p] = c * ap - s * aq;
+        A[3 * i + qq] = s * ap + c * aq;
+        const double vp = V[3 * i + p], vq = V[3 * i + qq];
+        V[3 * i + p] = c * vp - s * vq;
+        V[3 * i + qq] = s * vp + c * vq;
+      }
+    }
+    if (off < 1e-16) break;
+  }
+  double s[3];
+  for (int j = 0; j < 3; ++j) s[j] = sqrt(A[j] * A[j] + A[3 + j] * A[3 + j] + A[6 + j] * A[6 + j]);
+  int o[3] = {0, 1, 2};
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2 - i; ++j)
+      if (s[o[j]] < s[o[j + 1]]) { const int t = o[j]; o[j] = o[j + 1]; o[j + 1] = t; }
+  double Vs[9];
+  for (int j = 0; j < 3; ++j) {
+    const int c = o[j];
+    S[j] = s[c];
+    for (int i = 0; i < 3; ++i) {
+      U[3 * i + j] = s[c] > 0 ? A[3 * i + c] / s[c] : 0.0;
+      Vs[3 * i + j] = V[3 * i + c];
+    }
+  }
+  for (int i = 0; i < 9; ++i) V[i] = Vs[i];
+  if (!(S[2] > 0)) {  // exactly singular: complete U with the cross product
+    U[2] = U[3] * U[7] - U[6] * U[4];
+    U[5] = U[6] * U[1] - U[0] * U[7];
+    U[8] = U[0] * U[4] - U[3] * U[1];
+  }
+}
+
+CDX_HD double det3(const double* m) {
+  return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) + m[2] * (m[3] * m[7] - m[4] * m[6]);
+}
+
+// Kabsch state kept for the backward pass.
+struct KabschTape {
+  double U[9], S[3], V[9];
+  double d;  // +1, or -1 when det(V·Uᵀ) < 0 (the reference's `mask`, :64-66)
+};
+
+// R = V·diag(1,1,d)·Uᵀ of H' = H + 1e-6·noise.
+CDX_HD void kabsch_rotation(const double* H, const double* noise, KabschTape& tp, double* R) {
+  double Hn[9];
+  for (int i = 0; i < 9; ++i) Hn[i] = H[i] + 1e-6 * noise[i];
+  svd3(Hn, tp.U, tp.S, tp.V);
+  double R0[9];
+  mat3_mul_nt(tp.V, tp.U, R0);
+  tp.d = det3(R0) < 0.0 ? -1.0 : 1.0;
+  double Vd[9];
+  for (int i = 0; i < 3; ++i) { Vd[3 * i] = tp.V[3 * i]; Vd[3 * i + 1] = tp.V[3 * i + 1]; Vd[3 * i + 2] = tp.V[3 * i + 2] * tp.d; }
+  mat3_mul_nt(Vd, tp.U, R);
+}
+
+// gH from gR through R = V·D·Uᵀ and the SVD.
+CDX_HD void kabsch_rotation_bwd(const KabschTape& tp, const double* gR, double* gH) {
+  const double* U = tp.U;
+  const double* V = tp.V;
+  const double* S = tp.S;
+  // gU = gRᵀ·V·D ; gV = gR·U·D
+  double gU[9], gV[9], t[9];
+  mat3_mul_tn(gR, V, t);
+  for (int i = 0; i < 3; ++i) { gU[3 * i] = t[3 * i]; gU[3 * i + 1] = t[3 * i + 1]; gU[3 * i + 2] = t[3 * i + 2] * tp.d; }
+  mat3_mul(gR, U, t);
+  for (int i = 0; i < 3; ++i) { gV[3 * i] = t[3 * i]; gV[3 * i + 1] = t[3 * i + 1]; gV[3 * i + 2] = t[3 * i + 2] * tp.d; }
+  double UgU[9], VgV[9];
+  mat3_mul_tn(U, gU, UgU);
+  mat3_mul_tn(V, gV, VgV);
+  double X[9];
+  for (int j = 0; j < 3; ++j)
+    for (int k = 0; k < 3; ++k) {
+      if (j == k) { X[3 * j + k] = 0.0; continue; }
+      const double sku = UgU[3 * j + k] - UgU[3 * k + j];
+      const double skv = VgV[3 * j + k] - VgV[3 * k + j];
+      X[3 * j + k] = (sku * S[k] + S[j] * skv) / (S[k] * S[k] - S[j] * S[j]);
+    }
+  double UX[9];
+  mat3_mul(U, X, UX);
+  mat3_mul_nt(UX, V, gH);
+}
+
+// ------------------------------------------------------------- euler XYZ (f64)
+CDX_HD void rot_axis_d(int axis, double a, double* R, double* dR) {
+  const double c = cos(a), s = sin(a);
+  for (int i = 0; i < 9; ++i) { R[i] = 0.0; dR[i] = 0.0; }
+  if (axis == 0) {
+    R[0] = 1; R[4] = c; R[5] = -s; R[7] = s; R[8] = c;
+    dR[4] = -s; dR[5] = -c; dR[7] = c; dR[8] = -s;
+  } else if (axis == 1) {
+    R[0] = c; R[2] = s; R[4] = 1; R[6] = -s; R[8] = c;
+    dR[0] = -s; dR[2] = c; dR[6] = -c; dR[8] = -s;
+  } else {
+    R[0] = c; R[1] = -s; R[3] = s; R[4] = c; R[8] = 1;
+    dR[0] = -s; dR[1] = -c; dR[3] = c; dR[4] = -s;
+  }
+}
+
+// R = (Rx(a)·Ry(b))·Rz(c)  (math_utils.py:97-123); optionally the three partials.
+CDX_HD void euler_xyz(const double* ang, double* R, double* dRa, double* dRb, double* dRc) {
+  double X[9], dX[9], Y[9], dY[9], Z[9], dZ[9], XY[9];
+  rot_axis_d(0, ang[0], X, dX);
+  rot_axis_d(1, ang[1], Y, dY);
+  rot_axis_d(2, ang[2], Z, dZ);
+  mat3_mul(X, Y, XY);
+  mat3_mul(XY, Z, R);
+  if (dRa) {
+    double t[9];
+    mat3_mul(dX, Y, t); mat3_mul(t, Z, dRa);
+    mat3_mul(X, dY, t); mat3_mul(t, Z, dRb);
+    mat3_mul(XY, dZ, dRc);
+  }
+}
+
+// --------------------------------------------------------------- GPIS at a point
+struct GpisPoint {
+  double mean, gmean[3];
+  double std, gstd[3];   // only for all-tip queries
+  double normal[3];
+};
+
+// ------------------------------------------------------------ closure per candidate
+// Query-array layout (T tips, Lq distinct coefficient rows, E candidates):
+//   all-tip row u : u·E·T + e·T + f        target : Lq·E·T + e·T + f
+//   pregrasp      : (Lq+1)·E·T + e·T + f    palm   : (Lq+2)·E·T + e
+CDX_HD int64_t q_alltip(int u, int64_t e, int f, int64_t E, int T) { return (int64_t)u * E * T + e * T + f; }
+CDX_HD int64_t q_target(int Lq, int64_t e, int f, int64_t E, int T) { return (int64_t)Lq * E * T + e * T + f; }
+CDX_HD int64_t q_pre(int Lq, int64_t e, int f, int64_t E, int T) { return (int64_t)(Lq + 1) * E * T + e * T + f; }
+CDX_HD int64_t q_palm(int Lq, int64_t e, int64_t E, int T) { return (int64_t)(Lq + 2) * E * T + e; }
+CDX_HD int64_t n_queries(const cdx_problem& P, int64_t E) {
+  const int T = P.chain.n_tips;
+  return (int64_t)(P.n_query_levels + 2) * E * T + (P.optimize_palm ? E : 0);
+}
+
+// Pregrasp fingertips in world frame for candidate e: f32 FK, cast to f64, palm transform.
+CDX_HD void pregrasp_tips(const cdx_problem& P, const double* q, const double* palm_pos, const double* palm_ori,
+                          double (*tip)[3], float (*tl)[3], double* Rp) {
+  const int T = P.chain.n_tips;
+  float qf[CDX_MAX_DOFS];
+  for (int i = 0; i < P.chain.n_dofs; ++i) qf[i] = (float)q[i];
+  euler_xyz(palm_ori, Rp, nullptr, nullptr, nullptr);
+  for (int f = 0; f < T; ++f) {
+    fk_tip(P.chain, f, qf, tl[f], nullptr);
+    const double v[3] = {(double)tl[f][0], (double)tl[f][1], (double)tl[f][2]};
+    double w[3];
+    mat3_vec(Rp, v, w);
+    for (int i = 0; i < 3; ++i) tip[f][i] = w[i] + palm_pos[i];
+  }
+}
+
+struct CandidateIn {
+  const double *q, *comp, *target, *palm_pos, *palm_ori;  // this candidate's rows
+  const double* noise;                                     // [K][9] for this candidate (stride via noise_stride)
+  int64_t noise_stride;                                    // doubles between levels
+};
+
+struct CandidateOut {
+  double loss;
+  double margin[CDX_MAX_TIPS];
+  double g_q[CDX_MAX_DOFS];
+  double g_comp[CDX_MAX_TIPS];
+  double g_target[CDX_MAX_TIPS][3];
+  double g_palm_pos[3];
+  double g_palm_ori[3];
+  int flip[CDX_MAX_LEVELS];
+};
+
+// Forward + backward of Σ_levels w_k·l_k − 5·Σ pre_dist + 1/palm_dist for one candidate.
+// gp(kind, level_or_0, finger) returns the GPIS results at the corresponding query.
+template <typename GpisAt>
+CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisAt gp, CandidateOut& out) {
+  const int T = P.chain.n_tips;
+  const int K = P.n_levels;
+  const double cos_mu = (double)P.cos_mu;
+  double tip[CDX_MAX_TIPS][3];
+  float tl[CDX_MAX_TIPS][3];
+  double Rp[9];
+  pregrasp_tips(P, in.q, in.palm_pos, in.palm_ori, tip, tl, Rp);
+
+  double g_tip[CDX_MAX_TIPS][3];
+  for (int f = 0; f < T; ++f) {
+    g_tip[f][0] = g_tip[f][1] = g_tip[f][2] = 0.0;
+    out.g_target[f][0] = out.g_target[f][1] = out.g_target[f][2] = 0.0;
+    out.g_comp[f] = 0.0;
+    out.margin[f] = 0.0;
+  }
+  for (int i = 0; i < P.chain.n_dofs; ++i) out.g_q[i] = 0.0;
+
+  // ref_cost is identical on every level: ‖q − ref_q‖ with ref_q float32 (:732)
+  double dq[CDX_MAX_DOFS], qn2 = 0.0;
+  for (int i = 0; i < P.chain.n_dofs; ++i) {
+    dq[i] = in.q[i] - (double)P.ref_q[i];
+    qn2 += dq[i] * dq[i];
+  }
+  const double qnorm = sqrt(qn2);
+
+  double total = 0.0;
+  for (int k = 0; k < K; ++k) {
+    const int u = P.level_query[k];
+    const double wk = P.weight[k];
+    // ---- forward of compute_loss for this level
+    double a[CDX_MAX_TIPS][3], d[CDX_MAX_TIPS], s[CDX_MAX_TIPS], n[CDX_MAX_TIPS][3], td[CDX_MAX_TIPS];
+    for (int f = 0; f < T; ++f) {
+      const double c = (double)P.coeff[k][f];
+      for (int i = 0; i < 3; ++i) a[f][i] = in.target[3 * f + i] + c * (tip[f][i] - in.target[3 * f + i]);
+      const GpisPoint& ga = gp(0, u, f);
+      d[f] = ga.mean;
+      s[f] = ga.std;
+      for (int i = 0; i < 3; ++i) n[f][i] = ga.normal[i];
+      td[f] = gp(1, 0, f).mean;
+    }
+    // Kabsch on [tips, dummy] / [targets, dummy] with weights [comp, dummy_comp]
+    const int NP = P.gravity ? T + 1 : T;
+    double S1[CDX_MAX_TIPS + 1][3], S2[CDX_MAX_TIPS + 1][3], w[CDX_MAX_TIPS + 1];
+    for (int f = 0; f < T; ++f) {
+      for (int i = 0; i < 3; ++i) { S1[f][i] = a[f][i]; S2[f][i] = in.target[3 * f + i]; }
+      w[f] = in.comp[f];
+    }
+    if (P.gravity) {
+      for (int i = 0; i < 3; ++i) S1[T][i] = (double)P.com[i];
+      S2[T][0] = 0.0; S2[T][1] = 0.0; S2[T][2] = (double)P.dummy_target_z;
+      w[T] = (double)P.dummy_comp;
+    }
+    double c1[3] = {0, 0, 0}, c2[3] = {0, 0, 0};
+    for (int i = 0; i < NP; ++i)
+      for (int j = 0; j < 3; ++j) { c1[j] += S1[i][j]; c2[j] += S2[i][j]; }
+    for (int j = 0; j < 3; ++j) { c1[j] /= NP; c2[j] /= NP; }
+    double Pm[CDX_MAX_TIPS + 1][3], Qm[CDX_MAX_TIPS + 1][3];
+    for (int i = 0; i < NP; ++i)
+      for (int j = 0; j < 3; ++j) { Pm[i][j] = w[i] * (S1[i][j] - c1[j]); Qm[i][j] = w[i] * (S2[i][j] - c2[j]); }
+    double H[9];
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        double acc = 0.0;
+        for (int i = 0; i < NP; ++i) acc += Pm[i][r] * Qm[i][c];
+        H[3 * r + c] = acc;
+      }
+    KabschTape tp;
+    double R[9];
+    kabsch_rotation(H, in.noise + k * in.noise_stride, tp, R);
+    out.flip[k] = tp.d < 0 ? 1 : 0;
+    double W = 0.0, num[3] = {0, 0, 0}, RS1[CDX_MAX_TIPS + 1][3];
+    for (int i = 0; i < NP; ++i) {
+      W += w[i];
+      mat3_vec(R, S1[i], RS1[i]);
+      for (int j = 0; j < 3; ++j) num[j] += w[i] * (S2[i][j] - RS1[i][j]);
+    }
+    double t[3] = {num[0] / W, num[1] / W, num[2] / W};
+    double diff[CDX_MAX_TIPS][3], dn[CDX_MAX_TIPS], dir[CDX_MAX_TIPS][3], ne[CDX_MAX_TIPS][3];
+    double ang[CDX_MAX_TIPS], mpre[CDX_MAX_TIPS], margin[CDX_MAX_TIPS], fn[CDX_MAX_TIPS], force[CDX_MAX_TIPS][3];
+    double reward = 0.0;
+    for (int f = 0; f < T; ++f) {
+      for (int i = 0; i < 3; ++i) diff[f][i] = RS1[f][i] + t[i] - in.target[3 * f + i];
+      dn[f] = sqrt(dot3(diff[f], diff[f]));
+      for (int i = 0; i < 3; ++i) { dir[f][i] = diff[f][i] / dn[f]; force[f][i] = in.comp[f] * (-diff[f][i]); }
+      mat3_vec(R, n[f], ne[f]);
+      ang[f] = dot3(dir[f], ne[f]);
+      mpre[f] = ang[f] - cos_mu;
+      margin[f] = mpre[f] < -0.9999 ? -0.9999 : mpre[f];
+      fn[f] = sqrt(dot3(force[f], force[f]));
+      reward += 0.2 * log(ang[f] + 1) + 0.8 * log(margin[f] + 1);
+    }
+    // contact margin (unclamped)
+    double cd[CDX_MAX_TIPS][3], cdn[CDX_MAX_TIPS], cdir[CDX_MAX_TIPS][3], cang[CDX_MAX_TIPS];
+    double creward = 0.0;
+    for (int f = 0; f < T; ++f) {
+      for (int i = 0; i < 3; ++i) cd[f][i] = a[f][i] - in.target[3 * f + i];
+      cdn[f] = sqrt(dot3(cd[f], cd[f]));
+      for (int i = 0; i < 3; ++i) cdir[f][i] = cd[f][i] / cdn[f];
+      cang[f] = dot3(cdir[f], n[f]);
+      creward += 0.1 * log(cang[f] + 1) + 0.9 * log(cang[f] - cos_mu + 1);
+    }
+    // force cost: −Σ clamp(fn·softmin(fn), max=10)
+    double zmax = -fn[0];
+    for (int f = 1; f < T; ++f) zmax = -fn[f] > zmax ? -fn[f] : zmax;
+    double ez[CDX_MAX_TIPS], esum = 0.0;
+    for (int f = 0; f < T; ++f) { ez[f] = exp(-fn[f] - zmax); esum += ez[f]; }
+    double sm[CDX_MAX_TIPS], v[CDX_MAX_TIPS], fcost = 0.0;
+    for (int f = 0; f < T; ++f) {
+      sm[f] = ez[f] / esum;
+      v[f] = fn[f] * sm[f];
+      fcost += v[f] > 10.0 ? 10.0 : v[f];
+    }
+    fcost = -fcost;
+    // variance cost: uncertainty · max_f log(100 std)
+    int fmax = 0;
+    double lmax = log(100 * s[0]);
+    for (int f = 1; f < T; ++f) {
+      const double lv = log(100 * s[f]);
+      if (lv > lmax) { lmax = lv; fmax = f; }
+    }
+    double dcost = 0.0, tcost = 0.0;
+    for (int f = 0; f < T; ++f) { dcost += fabs(d[f]); tcost += td[f]; }
+    const double l = -reward * 200.0 + 1000 * dcost + 20 * tcost + (-creward * 200.0) + fcost + qnorm * 10.0 +
+                     P.uncertainty * lmax;
+    total += wk * l;
+    for (int f = 0; f < T; ++f) out.margin[f] += wk * margin[f];
+
+    // ---- backward of this level with dL/dl = wk
+    double g_a[CDX_MAX_TIPS][3];
+    for (int f = 0; f < T; ++f) g_a[f][0] = g_a[f][1] = g_a[f][2] = 0.0;
+    // dist / tar_dist / variance (GPIS gradients at the query points)
+    for (int f = 0; f < T; ++f) {
+      const GpisPoint& ga = gp(0, u, f);
+      const double sg = d[f] > 0 ? 1.0 : (d[f] < 0 ? -1.0 : 0.0);
+      const double gd = wk * 1000.0 * sg;
+      for (int i = 0; i < 3; ++i) g_a[f][i] += gd * ga.gmean[i];
+      const GpisPoint& gt = gp(1, 0, f);
+      for (int i = 0; i < 3; ++i) out.g_target[f][i] += wk * 20.0 * gt.gmean[i];
+    }
+    {
+      const GpisPoint& ga = gp(0, u, fmax);
+      const double gs = wk * P.uncertainty / s[fmax];
+      for (int i = 0; i < 3; ++i) g_a[fmax][i] += gs * ga.gstd[i];
+    }
+    // ref cost
+    if (qnorm > 0)
+      for (int i = 0; i < P.chain.n_dofs; ++i) out.g_q[i] += wk * 10.0 * dq[i] / qnorm;
+    // force cost
+    double g_fn[CDX_MAX_TIPS], g_sm[CDX_MAX_TIPS];
+    double gsm_dot = 0.0;
+    for (int f = 0; f < T; ++f) {
+      const double gv = v[f] <= 10.0 ? -wk : 0.0;
+      g_fn[f] = gv * sm[f];
+      g_sm[f] = gv * fn[f];
+      gsm_dot += g_sm[f] * sm[f];
+    }
+    for (int f = 0; f < T; ++f) g_fn[f] += -(sm[f] * (g_sm[f] - gsm_dot));
+    // contact margin reward (gain −200·wk)
+    const double g_cr = -200.0 * wk;
+    for (int f = 0; f < T; ++f) {
+      const double gcang = g_cr * (0.1 / (cang[f] + 1) + 0.9 / (cang[f] - cos_mu + 1));
+      double gdir[3] = {gcang * n[f][0], gcang * n[f][1], gcang * n[f][2]};
+      const double pd = dot3(cdir[f], gdir);
+      for (int i = 0; i < 3; ++i) {
+        const double gcd = (gdir[i] - cdir[f][i] * pd) / cdn[f];
+        g_a[f][i] += gcd;
+        out.g_target[f][i] -= gcd;
+      }
+    }
+    // force_eq reward (gain −200·wk) + force norms
+    const double g_rw = -200.0 * wk;
+    double gR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g_t[3] = {0, 0, 0};
+    double g_S1[CDX_MAX_TIPS + 1][3], g_S2[CDX_MAX_TIPS + 1][3], g_w[CDX_MAX_TIPS + 1];
+    for (int i = 0; i < NP; ++i) { g_S1[i][0] = g_S1[i][1] = g_S1[i][2] = 0; g_S2[i][0] = g_S2[i][1] = g_S2[i][2] = 0; g_w[i] = 0; }
+    for (int f = 0; f < T; ++f) {
+      double gang = g_rw * 0.2 / (ang[f] + 1);
+      if (mpre[f] >= -0.9999) gang += g_rw * 0.8 / (margin[f] + 1);
+      double gdiff[3] = {0, 0, 0};
+      // force norm → force = −comp·diff
+      if (fn[f] > 0) {
+        double gforce[3];
+        for (int i = 0; i < 3; ++i) gforce[i] = g_fn[f] * force[f][i] / fn[f];
+        g_w[f] += -dot3(gforce, diff[f]);
+        for (int i = 0; i < 3; ++i) gdiff[i] += -in.comp[f] * gforce[i];
+      }
+      // ang = dir·ne ; ne = R·n (n detached)
+      double gdir[3], gne[3];
+      for (int i = 0; i < 3; ++i) { gdir[i] = gang * ne[f][i]; gne[i] = gang * dir[f][i]; }
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) gR[3 * r + c] += gne[r] * n[f][c];
+      const double pd = dot3(dir[f], gdir);
+      for (int i = 0; i < 3; ++i) gdiff[i] += (gdir[i] - dir[f][i] * pd) / dn[f];
+      // diff = R·S1_f + t − target_f
+      for (int i = 0; i < 3; ++i) { g_t[i] += gdiff[i]; out.g_target[f][i] -= gdiff[i]; }
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) gR[3 * r + c] += gdiff[r] * S1[f][c];
+      double rt[3];
+      mat3t_vec(R, gdiff, rt);
+      for (int i = 0; i < 3; ++i) g_S1[f][i] += rt[i];
+    }
+    // t = Σ w_i (S2_i − R·S1_i) / W
+    {
+      double gnum[3] = {g_t[0] / W, g_t[1] / W, g_t[2] / W};
+      const double gW = -dot3(g_t, t) / W;
+      for (int i = 0; i < NP; ++i) {
+        double r_i[3] = {S2[i][0] - RS1[i][0], S2[i][1] - RS1[i][1], S2[i][2] - RS1[i][2]};
+        g_w[i] += gW + dot3(gnum, r_i);
+        for (int j = 0; j < 3; ++j) g_S2[i][j] += w[i] * gnum[j];
+        for (int r = 0; r < 3; ++r)
+          for (int c = 0; c < 3; ++c) gR[3 * r + c] -= w[i] * gnum[r] * S1[i][c];
+        double rt[3], wg[3] = {w[i] * gnum[0], w[i] * gnum[1], w[i] * gnum[2]};
+        mat3t_vec(R, wg, rt);
+        for (int j = 0; j < 3; ++j) g_S1[i][j] -= rt[j];
+      }
+    }
+    // R ← SVD(H') ← H = Σ P_i Q_iᵀ
+    double gH[9];
+    kabsch_rotation_bwd(tp, gR, gH);
+    double g_c1[3] = {0, 0, 0}, g_c2[3] = {0, 0, 0};
+    for (int i = 0; i < NP; ++i) {
+      double gP[3], gQ[3];
+      mat3_vec(gH, Qm[i], gP);
+      mat3t_vec(gH, Pm[i], gQ);
+      double d1[3] = {S1[i][0] - c1[0], S1[i][1] - c1[1], S1[i][2] - c1[2]};
+      double d2[3] = {S2[i][0] - c2[0], S2[i][1] - c2[1], S2[i][2] - c2[2]};
+      g_w[i] += dot3(gP, d1) + dot3(gQ, d2);
+      for (int j = 0; j < 3; ++j) {
+        g_S1[i][j] += w[i] * gP[j];
+        g_c1[j] -= w[i] * gP[j];
+        g_S2[i][j] += w[i] * gQ[j];
+        g_c2[j] -= w[i] * gQ[j];
+      }
+    }
+    for (int i = 0; i < NP; ++i)
+      for (int j = 0; j < 3; ++j) { g_S1[i][j] += g_c1[j] / NP; g_S2[i][j] += g_c2[j] / NP; }
+    for (int f = 0; f < T; ++f) {
+      for (int i = 0; i < 3; ++i) { g_a[f][i] += g_S1[f][i]; out.g_target[f][i] += g_S2[f][i]; }
+      out.g_comp[f] += g_w[f];
+    }
+    // all-tip interpolation a = target + c·(tip − target)
+    for (int f = 0; f < T; ++f) {
+      const double c = (double)P.coeff[k][f];
+      for (int i = 0; i < 3; ++i) {
+        g_tip[f][i] += c * g_a[f][i];
+        out.g_target[f][i] += g_a[f][i] - c * g_a[f][i];
+      }
+    }
+  }
+  // pregrasp-distance and palm-distance terms
+  for (int f = 0; f < T; ++f) {
+    const GpisPoint& gpp = gp(2, 0, f);
+    for (int i = 0; i < 3; ++i) g_tip[f][i] += -5.0 * gpp.gmean[i];
+  }
+  double pre_sum = 0.0;
+  for (int f = 0; f < T; ++f) pre_sum += gp(2, 0, f).mean;
+  total = total - pre_sum * 5.0;
+  for (int i = 0; i < 3; ++i) out.g_palm_pos[i] = 0.0;
+  if (P.optimize_palm) {
+    const GpisPoint& gpm = gp(3, 0, 0);
+    total = total + 1.0 / gpm.mean;
+    const double g = -1.0 / (gpm.mean * gpm.mean);
+    for (int i = 0; i < 3; ++i) out.g_palm_pos[i] += g * gpm.gmean[i];
+  }
+  out.loss = total;
+  // tip = Rp·tl + palm_pos
+  double gRp[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  float gtl[CDX_MAX_TIPS * 3];
+  for (int f = 0; f < T; ++f) {
+    for (int i = 0; i < 3; ++i) out.g_palm_pos[i] += g_tip[f][i];
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) gRp[3 * r + c] += g_tip[f][r] * (double)tl[f][c];
+    double gl[3];
+    mat3t_vec(Rp, g_tip[f], gl);
+    for (int i = 0; i < 3; ++i) gtl[3 * f + i] = (float)gl[i];
+  }
+  double R_[9], dRa[9], dRb[9], dRc[9];
+  euler_xyz(in.palm_ori, R_, dRa, dRb, dRc);
+  out.g_palm_ori[0] = out.g_palm_ori[1] = out.g_palm_ori[2] = 0.0;
+  for (int i = 0; i < 9; ++i) {
+    out.g_palm_ori[0] += gRp[i] * dRa[i];
+    out.g_palm_ori[1] += gRp[i] * dRb[i];
+    out.g_palm_ori[2] += gRp[i] * dRc[i];
+  }
+  // FK backward in float32, then cast (q.float() backward)
+  float qf[CDX_MAX_DOFS], gqf[CDX_MAX_DOFS];
+  for (int i = 0; i < P.chain.n_dofs; ++i) { qf[i] = (float)in.q[i]; gqf[i] = 0.f; }
+  for (int f = 0; f < T; ++f) fk_tip_bwd(P.chain, f, qf, &gtl[3 * f], gqf);
+  for (int i = 0; i < P.chain.n_dofs; ++i) out.g_q[i] += (double)gqf[i];
+}
+
+}  // namespace cdx

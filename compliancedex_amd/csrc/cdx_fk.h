@@ -1,0 +1,210 @@
+// Fingertip forward kinematics (float32) and its vector-Jacobian product.
+//
+// Forward follows the non-recursive path of the reference:
+//   joint pose  Rj = F·A(sign·q), F = (Rz(yaw)·Ry(pitch))·Rx(roll)   rigid_body.py:130-157
+//   world pose  R_i = R_p·Rj_i,  t_i = R_p·t_i + t_p                 robot_model.py:174-194,
+//                                                                    spatial_vector_algebra.py:98-103
+//   quaternion  xyzw from the 4×4 M = [R t; 0 1] with the trace branch
+//               and scale 0.5/sqrt(tn·M33)                           spatial_vector_algebra.py:108-136
+//   tip         t_L + quat_rotate(quat, offset)                       robot_model.py:256-262,
+//                                                                    se3_so3_util.py:240-250
+// Backward reproduces the reference autograd graph, including its one artifact: the
+// quaternion scale goes through math.sqrt on a tensor and is therefore a CONSTANT for
+// autograd, so d tip/dR only sees the un-normalised quaternion times that constant.
+#pragma once
+#include "cdx_hd.h"
+
+namespace cdx {
+
+// Rotation about a principal axis by th and its derivative (spatial_vector_algebra.py:14-53).
+CDX_HD void axis_rot(int axis, float th, float* A, float* dA) {
+  const float c = cdx_cosf(th), s = cdx_sinf(th);
+  for (int i = 0; i < 9; ++i) { A[i] = 0.f; dA[i] = 0.f; }
+  if (axis == 0) {
+    A[0] = 1.f; A[4] = c; A[5] = -s; A[7] = s; A[8] = c;
+    dA[4] = -s; dA[5] = -c; dA[7] = c; dA[8] = -s;
+  } else if (axis == 1) {
+    A[0] = c; A[2] = s; A[4] = 1.f; A[6] = -s; A[8] = c;
+    dA[0] = -s; dA[2] = c; dA[6] = -c; dA[8] = -s;
+  } else {
+    A[0] = c; A[1] = -s; A[3] = s; A[4] = c; A[8] = 1.f;
+    dA[0] = -s; dA[1] = -c; dA[3] = c; dA[4] = -s;
+  }
+}
+
+// Longest root→tip path a chain may have (iiwa7_allegro: 13).
+#define CDX_MAX_DEPTH 16
+
+// Path from the root's child down to `body` (root = body 0 is the identity pose).
+CDX_HD int chain_path(const cdx_chain& c, int body, int* path) {
+  int rev[CDX_MAX_DEPTH];
+  int n = 0;
+  while (body > 0 && n < CDX_MAX_DEPTH) { rev[n++] = body; body = c.bodies[body].parent; }
+  for (int i = 0; i < n; ++i) path[i] = rev[n - 1 - i];
+  return n;
+}
+
+CDX_HD void joint_rot(const cdx_body& b, const float* q, float* Rj) {
+  if (b.dof < 0) {
+    for (int i = 0; i < 9; ++i) Rj[i] = b.F[i];
+    return;
+  }
+  float A[9], dA[9];
+  axis_rot(b.axis, b.sign * q[b.dof], A, dA);
+  mat3_mul(b.F, A, Rj);
+}
+
+// Quaternion (xyzw) of a rotation with the reference branch; returns the un-scaled
+// components in raw[4], the detached scale, and the branch id (-1 = trace branch,
+// else the pivot index i of the other branch).
+CDX_HD int quat_raw(const float* R, float* raw, float* scale) {
+  const float M33 = 1.f;
+  const float t = ((R[0] + R[4]) + R[8]) + M33;
+  float tn;
+  int br;
+  if (t > M33) {
+    tn = t;
+    raw[3] = tn;
+    raw[2] = R[3] - R[1];
+    raw[1] = R[2] - R[6];
+    raw[0] = R[7] - R[5];
+    br = -1;
+  } else {
+    int i = 0, j = 1, k = 2;
+    if (R[4] > R[0]) { i = 1; j = 2; k = 0; }
+    if (R[8] > R[4 * i]) { i = 2; j = 0; k = 1; }
+    tn = R[4 * i] - (R[4 * j] + R[4 * k]) + M33;
+    raw[i] = tn;
+    raw[j] = R[3 * i + j] + R[3 * j + i];
+    raw[k] = R[3 * k + i] + R[3 * i + k];
+    raw[3] = R[3 * k + j] - R[3 * j + k];
+    br = i;
+  }
+  *scale = (float)(0.5 / sqrt((double)(tn * M33)));
+  return br;
+}
+
+// d raw / dR accumulated into gR given g_raw.
+CDX_HD void quat_raw_bwd(int br, const float* g, float* gR) {
+  if (br < 0) {
+    gR[0] += g[3]; gR[4] += g[3]; gR[8] += g[3];
+    gR[3] += g[2]; gR[1] -= g[2];
+    gR[2] += g[1]; gR[6] -= g[1];
+    gR[7] += g[0]; gR[5] -= g[0];
+  } else {
+    const int i = br, j = (br + 1) % 3, k = (br + 2) % 3;
+    gR[4 * i] += g[i]; gR[4 * j] -= g[i]; gR[4 * k] -= g[i];
+    gR[3 * i + j] += g[j]; gR[3 * j + i] += g[j];
+    gR[3 * k + i] += g[k]; gR[3 * i + k] += g[k];
+    gR[3 * k + j] += g[3]; gR[3 * j + k] -= g[3];
+  }
+}
+
+// v(2w²−1) + 2w(q×v) + 2q(q·v)  (se3_so3_util.py:240-250)
+CDX_HD void quat_rotate(const float* q, const float* v, float* out) {
+  const float w = q[3];
+  const float a = 2.0f * (w * w) - 1.0f;
+  const float cx = q[1] * v[2] - q[2] * v[1];
+  const float cy = q[2] * v[0] - q[0] * v[2];
+  const float cz = q[0] * v[1] - q[1] * v[0];
+  const float d = q[0] * v[0] + q[1] * v[1] + q[2] * v[2];
+  out[0] = v[0] * a + cx * w * 2.0f + q[0] * d * 2.0f;
+  out[1] = v[1] * a + cy * w * 2.0f + q[1] * d * 2.0f;
+  out[2] = v[2] * a + cz * w * 2.0f + q[2] * d * 2.0f;
+}
+
+// gq += ∂(G·quat_rotate(q,v))/∂q
+CDX_HD void quat_rotate_bwd(const float* q, const float* v, const float* G, float* gq) {
+  const float w = q[3];
+  const float d = q[0] * v[0] + q[1] * v[1] + q[2] * v[2];
+  const float Gv = G[0] * v[0] + G[1] * v[1] + G[2] * v[2];
+  const float Gq = G[0] * q[0] + G[1] * q[1] + G[2] * q[2];
+  // G·(q×v) = q·(v×G)
+  const float vxG0 = v[1] * G[2] - v[2] * G[1];
+  const float vxG1 = v[2] * G[0] - v[0] * G[2];
+  const float vxG2 = v[0] * G[1] - v[1] * G[0];
+  const float Gqv = q[0] * vxG0 + q[1] * vxG1 + q[2] * vxG2;
+  gq[3] += 4.0f * w * Gv + 2.0f * Gqv;
+  gq[0] += 2.0f * w * vxG0 + 2.0f * (d * G[0] + Gq * v[0]);
+  gq[1] += 2.0f * w * vxG1 + 2.0f * (d * G[1] + Gq * v[1]);
+  gq[2] += 2.0f * w * vxG2 + 2.0f * (d * G[2] + Gq * v[2]);
+}
+
+// World pose of every body on `path` (root→tip).  Rs/ts hold n+1 entries, entry 0 = root.
+CDX_HD void chain_forward(const cdx_chain& c, const int* path, int n, const float* q, float (*Rs)[9],
+                          float (*ts)[3]) {
+  for (int i = 0; i < 9; ++i) Rs[0][i] = (i % 4 == 0) ? 1.f : 0.f;
+  ts[0][0] = ts[0][1] = ts[0][2] = 0.f;
+  for (int l = 0; l < n; ++l) {
+    const cdx_body& b = c.bodies[path[l]];
+    float Rj[9], tt[3];
+    joint_rot(b, q, Rj);
+    mat3_vec(Rs[l], b.t, tt);
+    ts[l + 1][0] = tt[0] + ts[l][0];
+    ts[l + 1][1] = tt[1] + ts[l][1];
+    ts[l + 1][2] = tt[2] + ts[l][2];
+    mat3_mul(Rs[l], Rj, Rs[l + 1]);
+  }
+}
+
+// Tip position (and quaternion) of tip `k`.
+CDX_HD void fk_tip(const cdx_chain& c, int k, const float* q, float* pos, float* quat) {
+  int path[CDX_MAX_DEPTH];
+  float Rs[CDX_MAX_DEPTH + 1][9], ts[CDX_MAX_DEPTH + 1][3];
+  const int n = chain_path(c, c.tip_body[k], path);
+  chain_forward(c, path, n, q, Rs, ts);
+  float raw[4], sc;
+  quat_raw(Rs[n], raw, &sc);
+  float qt[4] = {raw[0] * sc, raw[1] * sc, raw[2] * sc, raw[3] * sc};
+  pos[0] = ts[n][0]; pos[1] = ts[n][1]; pos[2] = ts[n][2];
+  if (c.has_offsets) {
+    float o[3];
+    quat_rotate(qt, c.tip_offset[k], o);
+    pos[0] = pos[0] + o[0]; pos[1] = pos[1] + o[1]; pos[2] = pos[2] + o[2];
+  }
+  if (quat) for (int i = 0; i < 4; ++i) quat[i] = qt[i];
+}
+
+// g_q += (∂pos_k/∂q)ᵀ·gpos with the reference's gradient semantics.
+CDX_HD void fk_tip_bwd(const cdx_chain& c, int k, const float* q, const float* gpos, float* g_q) {
+  int path[CDX_MAX_DEPTH];
+  float Rs[CDX_MAX_DEPTH + 1][9], ts[CDX_MAX_DEPTH + 1][3];
+  const int n = chain_path(c, c.tip_body[k], path);
+  chain_forward(c, path, n, q, Rs, ts);
+  float GR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  float Gt[3] = {gpos[0], gpos[1], gpos[2]};
+  if (c.has_offsets) {
+    float raw[4], sc;
+    const int br = quat_raw(Rs[n], raw, &sc);
+    float qt[4] = {raw[0] * sc, raw[1] * sc, raw[2] * sc, raw[3] * sc};
+    float gq[4] = {0, 0, 0, 0};
+    quat_rotate_bwd(qt, c.tip_offset[k], gpos, gq);
+    for (int i = 0; i < 4; ++i) gq[i] *= sc;  // scale is detached: only d raw flows
+    quat_raw_bwd(br, gq, GR);
+  }
+  for (int l = n - 1; l >= 0; --l) {
+    const cdx_body& b = c.bodies[path[l]];
+    float Rj[9], A[9], dA[9];
+    if (b.dof >= 0) {
+      axis_rot(b.axis, b.sign * q[b.dof], A, dA);
+      mat3_mul(b.F, A, Rj);
+      // G_Rj = R_pᵀ·G_R ;  G_A = Fᵀ·G_Rj ; dθ = <G_A, dA>
+      float GRj[9], GA[9];
+      mat3_mul_tn(Rs[l], GR, GRj);
+      mat3_mul_tn(b.F, GRj, GA);
+      float dth = 0.f;
+      for (int i = 0; i < 9; ++i) dth += GA[i] * dA[i];
+      g_q[b.dof] += b.sign * dth;
+    } else {
+      for (int i = 0; i < 9; ++i) Rj[i] = b.F[i];
+    }
+    // G_R_p = G_R·Rjᵀ + G_t ⊗ t_b ;  G_t_p = G_t
+    float GRp[9];
+    mat3_mul_nt(GR, Rj, GRp);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) GRp[3 * i + j] += Gt[i] * b.t[j];
+    for (int i = 0; i < 9; ++i) GR[i] = GRp[i];
+  }
+}
+
+}  // namespace cdx

@@ -1,0 +1,67 @@
+// Point → triangle closest point (float32), shared by the gfx950 kernel and the host
+// build.  Follows the Voronoi-region test order of the reference TorchSDF kernel
+// (thirdparty/TorchSDF/torchsdf/csrc/unbatched_triangle_distance_cuda.cu:132-174 helpers,
+// :201-237 per-face body).  Compiled with FP contraction OFF and 1/sqrt correctly rounded so
+// the device result is bit-identical to the CPU oracle (the reference's CUDA rsqrt is a
+// ≤2-ulp approximation and not reproducible on other hardware).
+#pragma once
+#include "cdx_hd.h"
+
+#pragma clang fp contract(off)
+
+namespace cdx {
+
+struct F3 { float x, y, z; };
+CDX_HD F3 f3(float x, float y, float z) { F3 r; r.x = x; r.y = y; r.z = z; return r; }
+CDX_HD F3 sub(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+CDX_HD F3 add(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+CDX_HD F3 scl(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }
+CDX_HD float dotf(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+CDX_HD F3 crossf(F3 a, F3 b) { return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+CDX_HD float rsqrt_cr(float x) { return 1.0f / sqrtf(x); }
+
+// Distance of p to one face; returns squared distance, writes closest point, unit
+// (p − c) direction and the ±1 side of the (v1−v2)×(v1−v3) face normal.
+CDX_HD float point_face(F3 p, F3 v1, F3 v2, F3 v3, F3& clst, F3& nrm, int& sgn) {
+  const F3 e12 = sub(v2, v1), e23 = sub(v3, v2), e31 = sub(v1, v3);
+  const F3 normal = crossf(sub(v1, v2), e31);
+  const float uab = dotf(sub(p, v1), e12) / dotf(e12, e12);
+  const float uca = dotf(sub(p, v3), e31) / dotf(e31, e31);
+  F3 c;
+  if (uca > 1 && uab < 0) {
+    c = v1;
+  } else {
+    const float ubc = dotf(sub(p, v2), e23) / dotf(e23, e23);
+    if (uab > 1 && ubc < 0) {
+      c = v2;
+    } else if (ubc > 1 && uca < 0) {
+      c = v3;
+    } else if (uab <= 1 && uab >= 0 && dotf(crossf(normal, e12), sub(p, v1)) <= 0) {
+      c = add(v1, scl(e12, uab));
+    } else if (ubc <= 1 && ubc >= 0 && dotf(crossf(normal, e23), sub(p, v2)) <= 0) {
+      c = add(v2, scl(e23, ubc));
+    } else if (uca <= 1 && uca >= 0 && dotf(crossf(normal, e31), sub(p, v3)) <= 0) {
+      c = add(v3, scl(e31, uca));
+    } else {
+      const float inv_len = rsqrt_cr(dotf(normal, normal));
+      const F3 un = scl(normal, inv_len);
+      const float d = (p.x - v1.x) * un.x + (p.y - v1.y) * un.y + (p.z - v1.z) * un.z;
+      c = sub(p, scl(un, d));
+    }
+  }
+  const F3 dv = sub(p, c);
+  const float dd = dotf(dv, dv);
+  nrm = scl(dv, rsqrt_cr(1e-16f + dd));
+  sgn = dotf(dv, normal) >= 0 ? 1 : -1;
+  clst = c;
+  return dd;
+}
+
+// The reference scans faces in 512-face tiles (.cu:186-246): inside a tile the first
+// face is always taken and later faces replace it only when strictly closer (:238);
+// a tile's winner replaces the running result only when strictly closer (:245), except
+// that tile 0's winner is always taken.  With NaN distances (degenerate faces) this is
+// not a plain argmin, so every implementation keeps this exact rule.
+#define CDX_SDF_REF_TILE 512
+
+}  // namespace cdx

@@ -1,0 +1,183 @@
+/* compliancedex_amd — C ABI of the MI355X (gfx950) probabilistic-pregrasp hot path.
+ *
+ * Conventions:
+ *   - every array argument is a DEVICE pointer owned by the caller, row-major, dense;
+ *   - work is stream-ordered on the given hipStream_t (0 = null stream); nothing is
+ *     allocated and nothing synchronises inside these calls;
+ *   - return 0 on success, a negative CDX_E* code on a bad argument (checked before any
+ *     launch), or CDX_ELAUNCH if the HIP launch itself failed.
+ *
+ * The reference has no FFI on this path except TorchSDF's pybind module; the entry
+ * points below replace the Python/torch operators the reference calls, as cited on
+ * each declaration.  Descriptor structs are plain data passed by host pointer; they
+ * hold device pointers and scalars only.
+ */
+#ifndef CDX_H
+#define CDX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* cdx_stream_t; /* == hipStream_t */
+
+enum {
+  CDX_OK = 0,
+  CDX_EINVAL = -1,     /* null pointer / bad size */
+  CDX_EKERNEL = -2,    /* unsupported GPIS kernel id */
+  CDX_ECHAIN = -3,     /* chain too large for the fixed-capacity descriptor */
+  CDX_ELAUNCH = -10    /* hipLaunch / hipGetLastError failure */
+};
+
+/* ------------------------------------------------------------------ GPIS --------
+ * Replaces the GPIS object of gpis.py:4-168 (pred :43-59, compute_normal :63-87).
+ * State precomputed once per object (gpis.py:33-40 fit / :162-168 load):
+ *   X1     [N_pad*3]  inducing points, AoS xyz, rows >= N padded with any finite point
+ *   alpha  [N_pad]    E11^{-1} y1 (zero-padded); mean = Σ alpha_j k(x, x_j) + bias
+ *   Ainv   [N_pad*N_pad] E11^{-1}, symmetric, zero-padded; only used by the std path
+ * kernel: 0 = thin-plate spline 2r³-3Rr²+R³ (gpis.py:21-26, the default),
+ *         1 = RBF exp(-r²/2σ²) (:16-19), 2 = 0.3·RBF + 0.7·TPS (:28-29). */
+enum { CDX_KERNEL_TPS = 0, CDX_KERNEL_RBF = 1, CDX_KERNEL_JOINT = 2 };
+
+typedef struct {
+  const double* X1;
+  const double* alpha;
+  const double* Ainv;
+  int32_t N;
+  int32_t N_pad;      /* multiple of 64, >= N */
+  int32_t kernel;
+  int32_t _pad;
+  double R;           /* TPS radius = max pairwise training distance */
+  double sigma;       /* RBF length scale */
+  double bias;
+} cdx_gpis;
+
+/* Posterior mean and its spatial gradient at M query points (gpis.py:43-55 mean part,
+ * and the autograd gradient the reference takes through it).  normal (optional) is
+ * ∇mean / (‖∇mean‖ + 1e-8) — compute_normal (gpis.py:63-87), detached.
+ * X [M*3]; mean [M]; grad_mean [M*3] (nullable); normal [M*3] (nullable). */
+int cdx_gpis_mean(const cdx_gpis* g, const double* X, int64_t M, double* mean,
+                  double* grad_mean, double* normal, cdx_stream_t stream);
+
+/* Workspace bytes cdx_gpis_std needs for M queries. */
+size_t cdx_gpis_std_workspace(const cdx_gpis* g, int64_t M);
+
+/* Posterior standard deviation sqrt|k(0) - kᵀ E11^{-1} k| (gpis.py:56-59, the value the
+ * reference returns as "var") and its gradient -sign·(E11^{-1}k)ᵀ(∂k/∂x)/std.
+ * One fp64 MFMA GEMM with K* generated on chip.  std [M]; grad_std [M*3] (nullable). */
+int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std, double* grad_std,
+                 void* workspace, cdx_stream_t stream);
+
+/* ------------------------------------------------------------------ FK ----------
+ * Replaces DifferentiableRobotModel.compute_forward_kinematics(q, link_names,
+ * recursive=False, offsets) (robot_model.py:224-264 with update_kinematic_state
+ * :140-196, rigid_body.py:130-157, spatial_vector_algebra.py:14-136,
+ * se3_so3_util.py:240-250).  Computes in float32 like the reference. */
+#define CDX_MAX_BODIES 32
+#define CDX_MAX_TIPS 8
+#define CDX_MAX_DOFS 32
+
+typedef struct {
+  float F[9];        /* fixed rotation (Rz(yaw)·Ry(pitch))·Rx(roll), row-major */
+  float t[3];        /* joint origin translation */
+  float sign;        /* sign of the recognised joint axis component (0 ⇒ identity) */
+  int8_t axis;       /* 0 = x, 1 = y, 2 = z */
+  int8_t parent;     /* parent body index, -1 for the root */
+  int8_t dof;        /* DOF index, -1 for fixed joints */
+  int8_t _pad;
+} cdx_body;
+
+typedef struct {
+  int32_t n_bodies;
+  int32_t n_dofs;
+  int32_t n_tips;
+  int32_t has_offsets;
+  int32_t tip_body[CDX_MAX_TIPS];
+  float tip_offset[CDX_MAX_TIPS][3];
+  cdx_body bodies[CDX_MAX_BODIES];
+} cdx_chain;
+
+/* q [B*n_dofs] f32 → pos [B*3*n_tips] f32, quat [B*4*n_tips] f32 (xyzw, nullable). */
+int cdx_fk_forward(const cdx_chain* chain, const float* q, int64_t B, float* pos, float* quat,
+                   cdx_stream_t stream);
+/* Vector-Jacobian product of pos with the reference's gradient semantics (detached
+ * quaternion scale, spatial_vector_algebra.py:135).  grad_pos [B*3*n_tips] → grad_q [B*n_dofs]. */
+int cdx_fk_backward(const cdx_chain* chain, const float* q, int64_t B, const float* grad_pos,
+                    float* grad_q, cdx_stream_t stream);
+
+/* ------------------------------------------------------ prob-mode closure -------
+ * Replaces ProbabilisticGraspOptimizer.closure (optimize_pregrasp.py:741-769) —
+ * forward AND backward for E candidates — plus its callees compute_loss (:713-739),
+ * force_eq_reward (:73-118), optimal_transformation_batch (:49-69),
+ * compute_contact_margin (:703-710), forward_kinematics (:657-669). */
+#define CDX_MAX_LEVELS 4
+
+typedef struct {
+  cdx_chain chain;
+  cdx_gpis gpis;
+  int32_t n_levels;                     /* pregrasp levels K (3 in the reference) */
+  int32_t n_query_levels;               /* distinct coefficient rows (1 if all equal) */
+  int32_t level_query[CDX_MAX_LEVELS];  /* level → distinct row */
+  float coeff[CDX_MAX_LEVELS][CDX_MAX_TIPS]; /* pregrasp coefficients, f32 (:644) */
+  double weight[CDX_MAX_LEVELS];        /* pregrasp weights, f64 (:645) */
+  float ref_q[CDX_MAX_DOFS];            /* f32 (:634) */
+  float cos_mu;                         /* sqrt(1/(1+mu²)) in f32 (:111, :707) */
+  int32_t gravity;                      /* dummy gravity spring on (:87-97) */
+  int32_t optimize_palm;                /* palm-distance term (:760-763) */
+  int32_t _pad;
+  float com[3];                         /* dummy tip = COM (f32 tensor, :90-91) */
+  float dummy_target_z;                 /* -M (:93) */
+  float dummy_comp;                     /* gravity·mass/M (f32, :94) */
+  float _pad2;
+  double uncertainty;                   /* variance-cost weight (:733) */
+} cdx_problem;
+
+/* Workspace bytes for E candidates. */
+size_t cdx_closure_workspace(const cdx_problem* p, int64_t E);
+
+/* One cost+grad eval for E candidates.
+ * q [E*n_dofs] f64, comp [E*n_tips], target [E*n_tips*3], palm_pos [E*3], palm_ori [E*3];
+ * kabsch_noise [n_levels*E*9] f64, the reference's rand_like(H) draw (:61); when NULL the
+ *   noise is drawn on device from a counter-based generator keyed by (seed, row, entry).
+ * Outputs: total_loss [E], total_margin [E*n_tips], pregrasp_tip [E*n_tips*3] (nullable),
+ *   gradients of Σ total_loss: g_q [E*n_dofs], g_comp [E*n_tips], g_target [E*n_tips*3],
+ *   g_palm_pos [E*3], g_palm_ori [E*3]; flip [n_levels*E] int32 Kabsch det<0 mask (nullable). */
+int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* comp,
+                const double* target, const double* palm_pos, const double* palm_ori,
+                const double* kabsch_noise, uint64_t seed, void* workspace,
+                double* total_loss, double* total_margin, double* pregrasp_tip,
+                double* g_q, double* g_comp, double* g_target, double* g_palm_pos,
+                double* g_palm_ori, int32_t* flip, cdx_stream_t stream);
+
+/* --------------------------------------------------------------- TorchSDF -------
+ * Replaces torchsdf._C.unbatched_triangle_distance_forward_cuda / _backward_cuda
+ * (thirdparty/TorchSDF/torchsdf/csrc/bindings.cpp:22-27, kernels
+ * unbatched_triangle_distance_cuda.cu:176-270).  float32 only (the dtype the reference
+ * path uses, optimize_pregrasp.py:165-168).  Outputs are caller-allocated.
+ * points [P*3], faces [F*9] → sqdist [P], sign [P] (±1), normals [P*3], clst [P*3],
+ * face_idx [P] (argmin face, first minimum; nullable). */
+int cdx_sdf_forward(const float* points, int64_t P, const float* faces, int64_t F,
+                    float* sqdist, int32_t* sign, float* normals, float* clst,
+                    int32_t* face_idx, cdx_stream_t stream);
+/* grad_points = 2·grad_dist·(p − clst) (unbatched_triangle_distance_cuda.cu:256-270). */
+int cdx_sdf_backward(const float* grad_dist, const float* points, const float* clst, int64_t P,
+                     float* grad_points, cdx_stream_t stream);
+
+/* Library identification (gfx arch string compiled in). */
+const char* cdx_version(void);
+
+/* sizeof(cdx_gpis), sizeof(cdx_body), sizeof(cdx_chain), sizeof(cdx_problem) — lets a
+ * binding verify its struct layout before the first call. */
+void cdx_abi_sizes(size_t* out4);
+
+/* Test hook: D[16×16] = A[16×4]·B[4×16] through one v_mfma_f64_16x16x4_f64 (checks the
+ * fragment layout the GPIS std kernel relies on). */
+int cdx_selftest_mfma_f64(const double* A, const double* B, double* D, cdx_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CDX_H */

@@ -1,0 +1,106 @@
+/* ORACLE — test infrastructure only.  Plain-C restatement of the TorchSDF forward and
+ * backward kernels (thirdparty/TorchSDF/torchsdf/csrc/unbatched_triangle_distance_cuda.cu),
+ * used to check the gfx950 kernel bit-for-bit on integer outputs (sign, argmin face) and
+ * floats.  Build: see oracle/build_oracle.py (gcc -O2 -ffp-contract=off).
+ *
+ * Parity pinning: the reference kernel cannot run here (its _C.so is a missing blob and it
+ * is CUDA-only, unbatched_triangle_distance.cpp:48-53) and its own tests compare against
+ * Kaolin, which is absent, so value/sign parity vs the reference is UNPINNED; the one
+ * self-contained reference invariant, tests/normal.py:36-39 (normals·2·sqrt(d) equals the
+ * autograd gradient, atol 5e-7), is checked in tests/test_sdf.py.
+ *
+ * Deliberate restatement choices:
+ *   - rsqrt(x) is computed as 1.0f/sqrtf(x) (correctly rounded).  CUDA's rsqrtf is a
+ *     ≤2-ulp approximation, not reproducible on any other device.
+ *   - float accumulation of the squared distance (.cu:237) and float t in point_at (.cu:172)
+ *     are kept (only float32 is supported, as on the reference's live path).
+ */
+#include <math.h>
+#include <stdint.h>
+
+typedef struct { float x, y, z; } v3;
+
+static v3 mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static v3 vsub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static v3 vadd(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static v3 vmul(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+static float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static v3 vcross(v3 a, v3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+
+/* project_edge (.cu:132-139) */
+static float edge_param(v3 vertex, v3 edge, v3 p) { return vdot(vsub(p, vertex), edge) / vdot(edge, edge); }
+/* is_not_above (.cu:163-168) */
+static int not_above(v3 vertex, v3 edge, v3 normal, v3 p) { return vdot(vcross(normal, edge), vsub(p, vertex)) <= 0; }
+static int unit_range(float a) { return a <= 1 && a >= 0; }
+
+/* per-face body of the forward kernel (.cu:201-237) */
+static float face_dist(v3 p, v3 v1, v3 v2, v3 v3_, v3* clst, v3* nrm, int* sgn) {
+  v3 e12 = vsub(v2, v1), e23 = vsub(v3_, v2), e31 = vsub(v1, v3_);
+  v3 n = vcross(vsub(v1, v2), e31);
+  float uab = edge_param(v1, e12, p);
+  float uca = edge_param(v3_, e31, p);
+  v3 c;
+  if (uca > 1 && uab < 0) {
+    c = v1;
+  } else {
+    float ubc = edge_param(v2, e23, p);
+    if (uab > 1 && ubc < 0) c = v2;
+    else if (ubc > 1 && uca < 0) c = v3_;
+    else if (unit_range(uab) && not_above(v1, e12, n, p)) c = vadd(v1, vmul(e12, uab));
+    else if (unit_range(ubc) && not_above(v2, e23, n, p)) c = vadd(v2, vmul(e23, ubc));
+    else if (unit_range(uca) && not_above(v3_, e31, n, p)) c = vadd(v3_, vmul(e31, uca));
+    else { /* project_plane (.cu:141-150) */
+      float il = 1.0f / sqrtf(vdot(n, n));
+      v3 un = vmul(n, il);
+      float d = (p.x - v1.x) * un.x + (p.y - v1.y) * un.y + (p.z - v1.z) * un.z;
+      c = vsub(p, vmul(un, d));
+    }
+  }
+  v3 dv = vsub(p, c);
+  float dd = vdot(dv, dv);
+  *nrm = vmul(dv, 1.0f / sqrtf(1e-16f + dd));
+  *sgn = vdot(dv, n) >= 0 ? 1 : -1;
+  *clst = c;
+  return dd;
+}
+
+/* Forward: the reference's 512-face tile rule (.cu:186-246). */
+void sdf_oracle_forward(const float* points, int64_t P, const float* faces, int64_t F, float* dist, int32_t* sign,
+                        float* normals, float* clst, int32_t* face_idx) {
+  const int64_t TILE = 512;
+  for (int64_t i = 0; i < P; ++i) {
+    v3 p = mk(points[3 * i], points[3 * i + 1], points[3 * i + 2]);
+    float best = 0;
+    int bs = 0;
+    int64_t bf = -1;
+    v3 bn = mk(0, 0, 0), bc = bn;
+    for (int64_t f0 = 0; f0 < F; f0 += TILE) {
+      int64_t nt = F - f0 < TILE ? F - f0 : TILE;
+      float tb = 0;
+      int ts = 0;
+      int64_t tf = -1;
+      v3 tn = mk(0, 0, 0), tc = tn;
+      for (int64_t s = 0; s < nt; ++s) {
+        const float* v = faces + 9 * (f0 + s);
+        v3 c, n;
+        int sg;
+        float d = face_dist(p, mk(v[0], v[1], v[2]), mk(v[3], v[4], v[5]), mk(v[6], v[7], v[8]), &c, &n, &sg);
+        if (s == 0 || tb > d) { tb = d; ts = sg; tn = n; tc = c; tf = f0 + s; }
+      }
+      if (f0 == 0 || best > tb) { best = tb; bs = ts; bn = tn; bc = tc; bf = tf; }
+    }
+    dist[i] = best;
+    sign[i] = bs;
+    normals[3 * i] = bn.x; normals[3 * i + 1] = bn.y; normals[3 * i + 2] = bn.z;
+    clst[3 * i] = bc.x; clst[3 * i + 1] = bc.y; clst[3 * i + 2] = bc.z;
+    if (face_idx) face_idx[i] = (int32_t)bf;
+  }
+}
+
+/* Backward (.cu:256-270): grad_points = 2·grad·(p − clst). */
+void sdf_oracle_backward(const float* grad, const float* points, const float* clst, int64_t P, float* gp) {
+  for (int64_t i = 0; i < P; ++i) {
+    float g = 2.0f * grad[i];
+    for (int c = 0; c < 3; ++c) gp[3 * i + c] = (points[3 * i + c] - clst[3 * i + c]) * g;
+  }
+}

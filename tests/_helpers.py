@@ -42,3 +42,30 @@ def oracle_problem(hand, state):
 def rel_err(a, b):
     a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def product_chain(robot):
+    from compliancedex_amd.chain import Chain
+    from compliancedex_amd.urdf import load_robot
+    return Chain(load_robot(robot))
+
+
+def host_problem(hand):
+    from compliancedex_amd.problem import build_problem
+    ch = product_chain(hand)
+    cfg = ch.config
+    return build_problem(ch.descriptor(cfg["ee_link_name"], cfg["ee_link_offset"]), None, ref_q=cfg["ref_q"])
+
+
+def oracle_gpis_at(g, X, with_std):
+    """mean/∇mean/normal (and std/∇std) at each row of X via the oracle's autograd."""
+    import torch
+    Xt = torch.from_numpy(np.ascontiguousarray(X)).requires_grad_(True)
+    mean, std = g.pred(Xt)
+    gmean, = torch.autograd.grad(mean.sum(), Xt, retain_graph=True)
+    out = dict(mean=mean.detach().numpy(), gmean=gmean.numpy(),
+               normal=g.compute_normal(torch.from_numpy(np.ascontiguousarray(X))).numpy())
+    if with_std:
+        gstd, = torch.autograd.grad(std.sum(), Xt)
+        out.update(std=std.detach().numpy(), gstd=gstd.numpy())
+    return out

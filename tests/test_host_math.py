@@ -1,0 +1,61 @@
+"""The per-candidate device code (FK, Kabsch/SVD, cost, backward), compiled for the host,
+checked against the reference's golden vectors and the oracle.  CPU only."""
+import numpy as np
+import pytest
+
+from tests import _host
+from tests._helpers import (golden, golden_names, host_problem, oracle_gpis, oracle_gpis_at, product_chain,
+                            rel_err)
+
+FK_CASES = golden_names("fk_")
+CLOSURE_CASES = golden_names("closure_")
+
+
+@pytest.mark.parametrize("name", FK_CASES)
+def test_fk_host_vs_reference(name):
+    d = golden(name)
+    robot = "iiwa7_allegro" if name.startswith("fk_iiwa7") else name.split("_")[1]
+    ch = product_chain(robot)
+    desc = ch.descriptor([str(s) for s in d["links"]], d["offsets"].tolist())
+    pos, quat = _host.fk_forward(desc, d["q"])
+    assert rel_err(pos, d["pos"]) < 2e-6
+    assert rel_err(quat, d["quat"]) < 2e-6
+    gq = _host.fk_backward(desc, d["q"], d["cot"])
+    assert rel_err(gq, d["grad_q"]) < 2e-5
+
+
+def test_svd3_accuracy():
+    rng = np.random.default_rng(0)
+    for trial in range(200):
+        if trial % 2:
+            a, b = rng.standard_normal(3), rng.standard_normal(3)
+            H = np.outer(a, b) * 10 + 1e-6 * rng.random((3, 3))  # rank-1 + noise, as at init
+        else:
+            H = rng.standard_normal((3, 3))
+        U, S, V = _host.svd3(H)
+        assert np.all(np.diff(S) <= 0)
+        assert np.abs(U @ np.diag(S) @ V.T - H).max() < 1e-14 * np.abs(H).max() * 10
+        assert np.abs(U.T @ U - np.eye(3)).max() < 1e-12
+        assert np.abs(V.T @ V - np.eye(3)).max() < 1e-12
+        S_ref = np.linalg.svd(H, compute_uv=False)
+        assert np.abs(S - S_ref).max() < 1e-14 * S_ref[0] * 10
+
+
+@pytest.mark.parametrize("name", CLOSURE_CASES)
+def test_closure_host_vs_reference(name):
+    d = golden(name)
+    prob = host_problem(str(d["hand"]))
+    X = _host.closure_queries(prob, d["q"], d["target"], d["palm"])
+    E, T = d["q"].shape[0], prob.chain.n_tips
+    pre = X[(prob.n_query_levels + 1) * E * T:(prob.n_query_levels + 2) * E * T].reshape(E, T, 3)
+    assert rel_err(pre, d["pregrasp_tip"]) < 1e-6  # float32 FK, op order differs from torch
+    g = oracle_gpis(str(d["state"]))
+    Ms = prob.n_query_levels * E * T
+    gp = oracle_gpis_at(g, X, with_std=False)
+    gs = oracle_gpis_at(g, X[:Ms], with_std=True)
+    gp["std"], gp["gstd"] = gs["std"], gs["gstd"]
+    out = _host.closure_cost(prob, d["q"], d["comp"], d["target"], d["palm"], d["noise"][0], gp)
+    errs = {k: rel_err(out[k], d[k]) for k in ("total_loss", "total_margin", "grad_q", "grad_comp", "grad_target",
+                                               "grad_palm_pos", "grad_palm_ori")}
+    print(name, errs)
+    assert all(v < 1e-4 for v in errs.values()), errs
