@@ -1,0 +1,182 @@
+"""Benchmark: candidate-grasp cost+grad evals/sec (BASELINE.json metric), config 2.
+
+One step = one prob-mode closure (forward + backward, optimize_pregrasp.py:741-769) over
+E candidates per GPU on the N = 2000 synthetic banana GPIS with the Allegro hand — the
+whole hot path (FK → GPIS mean/normal/std → cost + analytic backward) through the C ABI.
+
+  python bench.py [--gpus N --steps K --warmup W --E 4096 --n-inducing 2000]
+  N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+Each rank evaluates its own E candidates (weak scaling, no data-path collective;
+SURVEY §8e).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6  # gfx950 vendor spec; MI355X_MICROARCH.md has no f64 row
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--E", type=int, default=4096, help="candidates per GPU")
+    ap.add_argument("--n-inducing", type=int, default=2000)
+    ap.add_argument("--hand", default="allegro")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-E", type=int, default=256)
+    return ap.parse_args()
+
+
+def cpu_baseline(args, ref_q, cfg):
+    """Oracle (CPU restatement of the reference path) on a bounded sample of the same workload."""
+    import numpy as np
+    import torch
+
+    from compliancedex_amd.urdf import load_robot
+    from compliancedex_amd.workloads import prob_inputs, synthetic_banana_arrays
+    from oracle.cdx_oracle import OracleChain, OracleGPIS, OracleProblem, closure_with_grads
+
+    X1, y, noise = synthetic_banana_arrays(args.n_inducing)
+    prob = OracleProblem(OracleChain(load_robot(args.hand)["bodies"]), cfg["ee_link_name"], cfg["ee_link_offset"],
+                         ref_q, OracleGPIS.fit(X1, y, noise, bias=1.0))
+    E = args.cpu_E
+    q, comp, target, palm = prob_inputs(ref_q, E, seed=99, spread=True)
+    kn = np.random.default_rng(98).random((3 * E, 3, 3))
+    times = []
+    for i in range(4):
+        t0 = time.perf_counter()
+        closure_with_grads(prob, q, comp, target, palm, kn)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times[1:])
+    return {"value": E / med, "unit": "evals/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/cdx_oracle.py closure (reference algorithm incl. per-call LU solve and M×M "
+                      f"posterior), E={E} candidates, N={args.n_inducing} GPIS, {args.hand}; median of 3 after "
+                      f"1 warm-up; host os.cpu_count()={os.cpu_count()}"}
+
+
+def hbm_traffic(E, n):
+    """Per-launch HBM bytes of gpis_std_kernel from the committed rocprofv3 PMC summary
+    (profiles/*_pmc.json, written by tools/pmc_summary.py), when one matches this config."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("E") == E and d.get("n_inducing") == n and "gpis_std_bytes_per_launch" in d:
+            best = d["gpis_std_bytes_per_launch"]
+    return best
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from compliancedex_amd import ProbabilisticGraspOptimizer
+    from compliancedex_amd import _native as N
+    from compliancedex_amd.urdf import load_robot
+    from compliancedex_amd.workloads import prob_inputs, synthetic_banana_gpis
+
+    cfg = load_robot(args.hand)["config"]
+    ref_q = cfg["ref_q"]
+    E = args.E
+    gpis = synthetic_banana_gpis(args.n_inducing, dev)
+    q, comp, target, palm = prob_inputs(ref_q, E, seed=1000 + rank, spread=True)
+    opt = ProbabilisticGraspOptimizer(args.hand, cfg["ee_link_name"], cfg["ee_link_offset"], palm_offset=palm,
+                                      ref_q=ref_q, optimize_target=True, optimize_palm=True, device=dev, seed=rank << 32)
+    qt = torch.from_numpy(q).to(dev).requires_grad_(True)
+    ct = torch.from_numpy(comp).to(dev).requires_grad_(True)
+    tt = torch.from_numpy(target).to(dev).requires_grad_(True)
+    pp = torch.from_numpy(palm[:, :3]).to(dev).requires_grad_(True)
+    po = torch.from_numpy(palm[:, 3:]).to(dev).requires_grad_(True)
+
+    def step():
+        qt.grad = ct.grad = tt.grad = pp.grad = po.grad = None
+        opt.closure(qt, ct, tt, pp, po, 1, gpis, E)
+
+    for _ in range(args.warmup):
+        step()
+    lib = N.load()
+    lib.cdx_profile_enable(1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    import ctypes
+    ms = (ctypes.c_double * 4)()
+    cnt = (ctypes.c_int64 * 4)()
+    N.check(lib.cdx_profile_read(ms, cnt), "cdx_profile_read")
+    lib.cdx_profile_enable(0)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    finite = bool(torch.isfinite(opt.total_loss).all())
+
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = E * world / (elapsed / args.steps)
+    stage_names = ["queries", "gpis_mean", "gpis_std_gemm", "cost_bwd"]
+    stage_ms = {n: (ms[i] / cnt[i] if cnt[i] else None) for i, n in enumerate(stage_names)}
+    m_std = opt.problem(gpis, 1).n_query_levels * E * 4
+    n_ind = args.n_inducing
+    flops = m_std * 2.0 * n_ind * n_ind      # W = K*·E11⁻¹ per launch (algorithmic, unpadded N)
+    std_ms = stage_ms["gpis_std_gemm"]
+    achieved = flops / (std_ms * 1e-3) / 1e12 if std_ms else None
+
+    if rank == 0:
+        out = {
+            "metric": "candidate-grasp cost+grad evals/sec (GPIS+FK+SDF), 1/2/4/8 GPU",
+            "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"prob-mode closure fwd+bwd, banana GPIS N={n_ind} (in-repo fit recipe), "
+                                   f"{E} candidates/GPU, {args.hand} FK (f32), 3 pregrasp levels",
+                       "candidates_per_gpu": E, "n_inducing": n_ind, "hand": args.hand,
+                       "parallelism": f"candidates sharded over {world} GPU(s), GPIS replicated"},
+            "stage_ms": stage_ms,
+            "roofline": {"bound": "mfma", "kernel": "gpis_std_kernel (v_mfma_f64_16x16x4_f64)",
+                         "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
+                         "traffic": hbm_traffic(E, n_ind),
+                         "flops_per_launch": flops, "note": f"{m_std} std queries x 2·N² (dedup of 3 identical "
+                                                            f"pregrasp levels; reference does 3x)"},
+            "finite": finite,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, ref_q, cfg)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

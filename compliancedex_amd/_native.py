@@ -60,6 +60,8 @@ _SIGS = {
     "cdx_version": (C.c_char_p, []),
     "cdx_abi_sizes": (None, [C.POINTER(C.c_size_t)]),
     "cdx_selftest_mfma_f64": (C.c_int, [_P, _P, _P, _P]),
+    "cdx_profile_enable": (C.c_int, [C.c_int]),
+    "cdx_profile_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
 }
 
 _lib = None

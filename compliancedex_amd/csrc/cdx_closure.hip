@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "cdx_cost.h"
+#include "cdx_prof.h"
 
 namespace {
 
@@ -241,8 +242,10 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   const int64_t Mq = cdx::n_queries(*p, E);
   const int64_t Ms = (int64_t)p->n_query_levels * E * p->chain.n_tips;
   const dim3 grid((unsigned)((E + 63) / 64));
+  cdx::prof_mark(cdx::PROF_QUERIES, true, s);
   hipLaunchKernelGGL(closure_queries_kernel, grid, dim3(64), 0, s, *p, E, q, target, palm_pos, palm_ori, w.X,
                      pregrasp_tip);
+  cdx::prof_mark(cdx::PROF_QUERIES, false, s);
   if (hipGetLastError() != hipSuccess) return CDX_ELAUNCH;
   int rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
   if (rc) return rc;
@@ -251,15 +254,69 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   GpisView gv;
   gv.mean = w.mean; gv.gmean = w.gmean; gv.normal = w.normal; gv.std_ = w.std_; gv.gstd = w.gstd;
   gv.E = E; gv.T = p->chain.n_tips; gv.Lq = p->n_query_levels; gv.e = 0;
+  cdx::prof_mark(cdx::PROF_COST, true, s);
   hipLaunchKernelGGL(closure_cost_kernel, grid, dim3(64), 0, s, *p, E, q, comp, target, palm_pos, palm_ori,
                      kabsch_noise, seed, gv, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori,
                      flip);
+  cdx::prof_mark(cdx::PROF_COST, false, s);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
 const char* cdx_version(void) { return "compliancedex_amd 0.1 gfx950"; }
 
 }  // extern "C"
+
+namespace cdx {
+namespace {
+constexpr int PROF_POOL = 4096;
+struct Prof {
+  bool on = false;
+  hipEvent_t ev[PROF_STAGES][PROF_POOL][2];
+  int n[PROF_STAGES] = {0, 0, 0, 0};
+  bool created = false;
+} g_prof;
+}  // namespace
+
+void prof_mark(int stage, bool begin, hipStream_t s) {
+  if (!g_prof.on) return;
+  const int i = g_prof.n[stage];
+  if (i >= PROF_POOL) return;
+  (void)hipEventRecord(g_prof.ev[stage][i][begin ? 0 : 1], s);
+  if (!begin) g_prof.n[stage] = i + 1;
+}
+}  // namespace cdx
+
+extern "C" int cdx_profile_enable(int on) {
+  using cdx::g_prof;
+  if (on && !g_prof.created) {
+    for (int st = 0; st < cdx::PROF_STAGES; ++st)
+      for (int i = 0; i < cdx::PROF_POOL; ++i)
+        for (int j = 0; j < 2; ++j)
+          if (hipEventCreate(&g_prof.ev[st][i][j]) != hipSuccess) return CDX_ELAUNCH;
+    g_prof.created = true;
+  }
+  g_prof.on = on != 0;
+  for (int st = 0; st < cdx::PROF_STAGES; ++st) g_prof.n[st] = 0;
+  return CDX_OK;
+}
+
+// Sums the recorded kernel times per stage (ms) and launch counts, then resets the pool.
+extern "C" int cdx_profile_read(double* ms, int64_t* count) {
+  using cdx::g_prof;
+  for (int st = 0; st < cdx::PROF_STAGES; ++st) {
+    double tot = 0;
+    for (int i = 0; i < g_prof.n[st]; ++i) {
+      if (hipEventSynchronize(g_prof.ev[st][i][1]) != hipSuccess) return CDX_ELAUNCH;
+      float t = 0;
+      if (hipEventElapsedTime(&t, g_prof.ev[st][i][0], g_prof.ev[st][i][1]) != hipSuccess) return CDX_ELAUNCH;
+      tot += t;
+    }
+    ms[st] = tot;
+    count[st] = g_prof.n[st];
+    g_prof.n[st] = 0;
+  }
+  return CDX_OK;
+}
 
 extern "C" void cdx_abi_sizes(size_t* out) {
   out[0] = sizeof(cdx_gpis);

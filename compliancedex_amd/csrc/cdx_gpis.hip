@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include "cdx_gpis.h"
+#include "cdx_prof.h"
 
 using cdx::gpis_k;
 using cdx::gpis_k0;
@@ -232,11 +233,13 @@ int cdx_gpis_mean(const cdx_gpis* g, const double* X, int64_t M, double* mean, d
   if (M == 0) return CDX_OK;
   const dim3 grid((unsigned)((M + MEAN_BLOCK - 1) / MEAN_BLOCK));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  cdx::prof_mark(cdx::PROF_GPIS_MEAN, true, s);
   switch (g->kernel) {
     case CDX_KERNEL_TPS: hipLaunchKernelGGL(gpis_mean_kernel<CDX_KERNEL_TPS>, grid, dim3(MEAN_BLOCK), 0, s, *g, X, M, mean, grad_mean, normal); break;
     case CDX_KERNEL_RBF: hipLaunchKernelGGL(gpis_mean_kernel<CDX_KERNEL_RBF>, grid, dim3(MEAN_BLOCK), 0, s, *g, X, M, mean, grad_mean, normal); break;
     default: hipLaunchKernelGGL(gpis_mean_kernel<CDX_KERNEL_JOINT>, grid, dim3(MEAN_BLOCK), 0, s, *g, X, M, mean, grad_mean, normal); break;
   }
+  cdx::prof_mark(cdx::PROF_GPIS_MEAN, false, s);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
@@ -259,15 +262,21 @@ int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std_out,
   const dim3 fgrid((unsigned)((M + 255) / 256));
   switch (g->kernel) {
     case CDX_KERNEL_TPS:
+      cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
       hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_TPS>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad);
+      cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_TPS>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;
     case CDX_KERNEL_RBF:
+      cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
       hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_RBF>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad);
+      cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_RBF>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;
     default:
+      cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
       hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_JOINT>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad);
+      cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_JOINT>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;
   }

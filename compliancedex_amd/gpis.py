@@ -1,0 +1,244 @@
+"""Drop-in for the reference GPIS class (gpis.py:4-168) on MI355X.
+
+Same constructor, attributes (``R, X1, y1, E11, bias, sigma, noise``), state files and
+methods (``fit``, ``pred``, ``compute_normal``, ``compute_multinormals``,
+``save_state_data``, ``load_state_data``, ``get_visualization_data``).  Queries run on the
+gfx950 kernels (cdx_gpis_mean / cdx_gpis_std); there is no CPU path.
+
+Differences in *how*, not *what*: E11⁻¹ and α = E11⁻ᵀ y1 are computed once per state
+(the reference re-solves E11 on every ``pred`` and inverts it on every
+``compute_normal``), and only the diagonal of the posterior covariance is formed (the
+reference builds the M×M matrix, gpis.py:57-58).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+_PKG_STATES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "gpis_states")
+
+
+def _require_cuda(t, what):
+    if not (torch.is_tensor(t) and t.is_cuda):
+        raise RuntimeError(f"{what} must be a CUDA (ROCm) tensor: compliancedex_amd has no CPU path")
+
+
+class _State:
+    """Device-resident padded state + the cdx_gpis descriptor pointing at it."""
+
+    def __init__(self, X1, y1, E11, R, bias, kernel, sigma):
+        dev = X1.device
+        N = X1.shape[0]
+        Np = (N + 63) // 64 * 64
+        E11 = E11.to(dev, torch.float64)
+        A = torch.linalg.inv(E11)
+        alpha = (A.T @ y1.to(dev, torch.float64).reshape(-1, 1)).reshape(-1)  # E11⁻ᵀ y1 (gpis.py:53-55)
+        A = 0.5 * (A + A.T)
+        self.X1 = X1[:1].to(torch.float64).repeat(Np, 1).contiguous()
+        self.X1[:N] = X1.to(torch.float64)
+        self.alpha = torch.zeros(Np, dtype=torch.float64, device=dev)
+        self.alpha[:N] = alpha
+        self.Ainv = torch.zeros(Np, Np, dtype=torch.float64, device=dev)
+        self.Ainv[:N, :N] = A
+        self.desc = N.CdxGpis(X1=self.X1.data_ptr(), alpha=self.alpha.data_ptr(), Ainv=self.Ainv.data_ptr(), N=N,
+                              N_pad=Np, kernel=N.KERNELS[kernel], R=float(R), sigma=float(sigma), bias=float(bias))
+        self.ws = None
+
+    def workspace(self, M):
+        need = N.load().cdx_gpis_std_workspace(self.desc, M)
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(max(need, 1), dtype=torch.uint8, device=self.X1.device)
+        return self.ws
+
+
+def gpis_mean(state, X, want_grad=True, want_normal=False):
+    lib = N.load()
+    X = X.contiguous()
+    M = X.shape[0]
+    mean = torch.empty(M, dtype=torch.float64, device=X.device)
+    gmean = torch.empty(M, 3, dtype=torch.float64, device=X.device) if want_grad else None
+    normal = torch.empty(M, 3, dtype=torch.float64, device=X.device) if want_normal else None
+    N.check(lib.cdx_gpis_mean(state.desc, N.ptr(X), M, N.ptr(mean), N.ptr(gmean), N.ptr(normal),
+                              N.stream_ptr(X.device)), "cdx_gpis_mean")
+    return mean, gmean, normal
+
+
+def gpis_std(state, X, want_grad=True):
+    lib = N.load()
+    X = X.contiguous()
+    M = X.shape[0]
+    std = torch.empty(M, dtype=torch.float64, device=X.device)
+    gstd = torch.empty(M, 3, dtype=torch.float64, device=X.device) if want_grad else None
+    if M:
+        ws = state.workspace(M)
+        N.check(lib.cdx_gpis_std(state.desc, N.ptr(X), M, N.ptr(std), N.ptr(gstd), N.ptr(ws),
+                                 N.stream_ptr(X.device)), "cdx_gpis_std")
+    return std, gstd
+
+
+class _Pred(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, state):
+        need = ctx.needs_input_grad[0]
+        mean, gmean, _ = gpis_mean(state, X, want_grad=need)
+        std, gstd = gpis_std(state, X, want_grad=need)
+        ctx.save_for_backward(gmean if need else None, gstd if need else None)
+        return mean, std
+
+    @staticmethod
+    def backward(ctx, g_mean, g_std):
+        gmean, gstd = ctx.saved_tensors
+        gX = None
+        if ctx.needs_input_grad[0]:
+            gX = torch.zeros_like(gmean)
+            if g_mean is not None:
+                gX = gX + g_mean.unsqueeze(1) * gmean
+            if g_std is not None:
+                gX = gX + g_std.unsqueeze(1) * gstd
+        return gX, None
+
+
+class GPIS:
+    """GP implicit surface (gpis.py:4-168)."""
+
+    def __init__(self, sigma=0.6, bias=2, kernel="tps"):
+        if kernel not in N.KERNELS:
+            raise ValueError(f"unknown kernel {kernel!r}")
+        self.sigma = sigma
+        self.bias = bias
+        self.fraction = None
+        self.kernel = kernel
+        self._state = None
+        self._state_key = None
+
+    # ---------------------------------------------------------------- kernel fns
+    def _k(self, xa, xb):
+        r = torch.cdist(xa, xb)
+        tps = lambda: 2 * r ** 3 - 3 * self.R * r ** 2 + self.R ** 3  # noqa: E731
+        rbf = lambda: torch.exp(-0.5 * r ** 2 / self.sigma ** 2)  # noqa: E731
+        if self.kernel == "tps":
+            return tps()
+        if self.kernel == "rbf":
+            return rbf()
+        return 0.3 * rbf() + 0.7 * tps()
+
+    # ----------------------------------------------------------------- fit / io
+    def fit(self, X1, y1, noise=0.0):
+        """E11 = K(X1, X1) + diag(noise²) (gpis.py:33-40)."""
+        if self.kernel in ("tps", "joint"):
+            self.R = torch.max(torch.cdist(X1, X1))
+        self.X1 = X1
+        self.y1 = y1 - self.bias
+        self.noise = noise
+        self.E11 = self._k(X1, X1) + (self.noise ** 2) * torch.eye(len(X1), device=X1.device)
+        self._state = None
+
+    def save_state_data(self, name="gpis_state"):
+        """npz {R, X1, y1, E11, bias} under gpis_states/ (gpis.py:155-160)."""
+        os.makedirs("gpis_states", exist_ok=True)
+        bias = self.bias.cpu().numpy() if torch.is_tensor(self.bias) else self.bias
+        np.savez(f"gpis_states/{name}.npz", R=self.R.cpu().numpy(), X1=self.X1.cpu().numpy(),
+                 y1=self.y1.cpu().numpy(), E11=self.E11.cpu().numpy(), bias=bias)
+
+    def load_state_data(self, name="gpis_state", device="cuda"):
+        """Reads gpis_states/{name}.npz (cwd first, then the packaged states) (gpis.py:162-168)."""
+        path = f"gpis_states/{name}.npz"
+        if not os.path.exists(path):
+            path = os.path.join(_PKG_STATES, f"{name}.npz")
+        data = np.load(path)
+        self.R = torch.from_numpy(data["R"]).to(device)
+        self.X1 = torch.from_numpy(data["X1"]).to(device)
+        self.y1 = torch.from_numpy(data["y1"]).to(device)
+        self.E11 = torch.from_numpy(data["E11"]).to(device)
+        self.bias = torch.from_numpy(data["bias"]).double().to(device)
+        self._state = None
+
+    # ------------------------------------------------------------ native state
+    def native_state(self):
+        # identity key: no device->host sync per query; fit/load reset the state
+        key = (id(self.X1), id(self.y1), id(self.E11), id(getattr(self, "R", None)), id(self.bias), self.kernel,
+               self.sigma)
+        if self._state is None or self._state_key != key:
+            _require_cuda(self.X1, "GPIS state")
+            R = float(self.R) if hasattr(self, "R") else 0.0
+            self._state = _State(self.X1, self.y1, self.E11, R, float(self.bias), self.kernel, self.sigma)
+            self._state_key = key
+        return self._state
+
+    # ---------------------------------------------------------------- queries
+    def pred(self, X2):
+        """(mean, sqrt|diag Σ|) with the reference's shape rule (gpis.py:43-59)."""
+        _require_cuda(X2, "GPIS query")
+        shape = list(X2.shape)
+        shape[-1] = 1
+        Xf = X2.reshape(-1, 3).to(torch.float64)
+        mean, std = _Pred.apply(Xf, self.native_state())
+        return mean.view(shape[:-1]), std.view(shape[:-1])
+
+    def pred_mean(self, X2):
+        """Mean only (no posterior-variance GEMM); same shape rule as ``pred``."""
+        _require_cuda(X2, "GPIS query")
+        shape = list(X2.shape[:-1])
+        mean, _, _ = gpis_mean(self.native_state(), X2.reshape(-1, 3).to(torch.float64).detach(), want_grad=False)
+        return mean.view(shape)
+
+    def compute_normal(self, X2, index=None):
+        """∇mean/(‖∇mean‖+1e-8), detached (gpis.py:63-87).  ``index`` restricts the
+        inducing points whose weights contribute, as the reference does."""
+        _require_cuda(X2, "GPIS query")
+        input_shape = X2.shape
+        X = X2.detach().reshape(-1, 3).to(torch.float64).contiguous()
+        st = self.native_state()
+        if index is None:
+            _, _, normal = gpis_mean(st, X, want_grad=False, want_normal=True)
+            return normal.view(input_shape)
+        idx = torch.as_tensor(index, device=X.device, dtype=torch.long)
+        mask = torch.zeros_like(st.alpha)
+        mask[idx] = 1.0
+        sub = _State.__new__(_State)
+        sub.__dict__.update(st.__dict__)
+        sub.alpha = st.alpha * mask
+        sub.desc = N.CdxGpis(X1=st.desc.X1, alpha=sub.alpha.data_ptr(), Ainv=st.desc.Ainv, N=st.desc.N,
+                             N_pad=st.desc.N_pad, kernel=st.desc.kernel, R=st.desc.R, sigma=st.desc.sigma,
+                             bias=st.desc.bias)
+        _, _, normal = gpis_mean(sub, X, want_grad=False, want_normal=True)
+        return normal.view(input_shape), st.alpha[idx].sum()
+
+    def compute_multinormals(self, X2, num_normal_samples):
+        """Normals from nested subsets of the inducing points (gpis.py:89-111)."""
+        if self.fraction is None:
+            self.fraction = torch.linspace(0.8, 1, num_normal_samples // 2)
+            self.indices = []
+            n = len(self.X1)
+            for i in range(num_normal_samples // 2):
+                self.indices.append(list(range(int(self.fraction[i] * n))))
+            self.indices.append(list(range(n)))
+            for i in range(num_normal_samples // 2):
+                self.indices.append(list(range(int(1 - self.fraction[-i - 1]), n)))
+        normals, weights = [], []
+        for i in range(num_normal_samples):
+            nrm, w = self.compute_normal(X2, self.indices[i])
+            normals.append(nrm)
+            weights.append(w.reshape(1))
+        weights = torch.hstack(weights)
+        return torch.stack(normals, dim=1), weights / weights.sum()
+
+    def get_visualization_data(self, lb, ub, steps=100):
+        """Mean / std / normal on a steps³ grid (gpis.py:113-125)."""
+        dev = self.X1.device
+        grid = torch.stack(torch.meshgrid(torch.linspace(lb[0], ub[0], steps), torch.linspace(lb[1], ub[1], steps),
+                                          torch.linspace(lb[2], ub[2], steps), indexing="xy"), dim=3).double().to(dev)
+        m = torch.zeros(steps, steps, steps)
+        v = torch.zeros(steps, steps, steps)
+        nrm = torch.zeros(steps, steps, steps, 3)
+        with torch.no_grad():
+            for i in range(steps):
+                mean, var = self.pred(grid[i].reshape(-1, 3))
+                nrm[i] = self.compute_normal(grid[i].reshape(-1, 3)).view(steps, steps, 3).cpu()
+                m[i] = mean.view(steps, steps).cpu()
+                v[i] = var.view(steps, steps).cpu()
+        return m.numpy(), v.numpy(), nrm.numpy(), np.asarray(lb), np.asarray(ub)

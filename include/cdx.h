@@ -169,6 +169,13 @@ int cdx_sdf_backward(const float* grad_dist, const float* points, const float* c
 /* Library identification (gfx arch string compiled in). */
 const char* cdx_version(void);
 
+/* Per-stage kernel timing with HIP events recorded on the launch stream (off by default).
+ * Stages: 0 closure query generation, 1 GPIS mean, 2 GPIS std GEMM (gpis_std_kernel only),
+ * 3 closure cost+backward.  cdx_profile_read syncs on the recorded events, returns the summed
+ * milliseconds and launch counts per stage, and clears the pool (4096 launches per stage). */
+int cdx_profile_enable(int on);
+int cdx_profile_read(double* ms4, int64_t* count4);
+
 /* sizeof(cdx_gpis), sizeof(cdx_body), sizeof(cdx_chain), sizeof(cdx_problem) — lets a
  * binding verify its struct layout before the first call. */
 void cdx_abi_sizes(size_t* out4);

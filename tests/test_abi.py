@@ -1,0 +1,55 @@
+"""The C-ABI library loads (no GPU needed) and exports every symbol include/cdx.h declares;
+binding struct layouts match the library's sizeof.  CPU only."""
+import os
+import re
+
+from tests.conftest import REPO
+
+
+def declared_functions():
+    src = open(os.path.join(REPO, "include", "cdx.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(cdx_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_path():
+    names = declared_functions()
+    for n in ("cdx_gpis_mean", "cdx_gpis_std", "cdx_fk_forward", "cdx_fk_backward", "cdx_closure",
+              "cdx_sdf_forward", "cdx_sdf_backward"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    from compliancedex_amd import _native
+    lib = _native.load()  # also checks struct sizes against the library
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.cdx_version().startswith(b"compliancedex_amd")
+
+
+def test_bad_arguments_are_rejected_without_launch():
+    import ctypes
+    from compliancedex_amd import _native as N
+    lib = N.load()
+    g = N.CdxGpis()
+    assert lib.cdx_gpis_mean(g, None, 10, None, None, None, None) == -1
+    g.kernel = 7
+    g.X1 = g.alpha = 1
+    g.N, g.N_pad = 1, 64
+    assert lib.cdx_gpis_mean(g, None, 10, None, None, None, None) == -2
+    c = N.CdxChain()
+    assert lib.cdx_fk_forward(c, None, 1, None, None, None) == -3
+    assert lib.cdx_sdf_forward(None, 5, None, 0, None, None, None, None, None, None) == -1
+    p = N.CdxProblem()
+    assert lib.cdx_closure_workspace(p, 10) == 0
+    assert lib.cdx_closure(p, 10, *([None] * 6), ctypes.c_uint64(0), *([None] * 11)) == -1
+
+
+def test_product_refuses_cpu_tensors():
+    import pytest
+    import torch
+    from compliancedex_amd import GPIS
+    g = GPIS(0.08, 1.0)
+    g.load_state_data("banana_state", device="cpu")
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        g.pred(torch.zeros(4, 3, dtype=torch.float64))

@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU call: parity tests → smoke → bench → rocprofv3 kernel-trace summary.
+# Each GPU step has its own time limit; a crash/timeout (rc not 0/1) ends the call.
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$ROOT"
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+TAG=${1:-r01}
+STEPS=${STEPS:-20}
+
+stop_if_fault() { if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "GPU step failed hard (rc=$1): stopping"; exit "$1"; fi; }
+
+echo "== pytest -m gpu"; date
+timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=240 -rf > "$OUT/pytest_gpu_$TAG.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu_$TAG.log"; stop_if_fault $rc
+
+echo "== smoke"; date
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 "$OUT/smoke_$TAG.log"; stop_if_fault $rc
+
+echo "== bench"; date
+timeout -k 10 300 python bench.py --steps "$STEPS" --warmup 3 > "$OUT/bench_$TAG.log" 2>&1
+rc=$?; echo "bench rc=$rc"; tail -1 "$OUT/bench_$TAG.log"; stop_if_fault $rc
+
+echo "== rocprofv3 kernel trace"; date
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/rocprof_$TAG.log" 2>&1
+rc=$?; echo "rocprof rc=$rc"; tail -2 "$OUT/rocprof_$TAG.log"
+find "$OUT/prof_$TAG" -name "*stats*" | head
+date
