@@ -32,19 +32,19 @@ class _State:
 
     def __init__(self, X1, y1, E11, R, bias, kernel, sigma):
         dev = X1.device
-        N = X1.shape[0]
-        Np = (N + 63) // 64 * 64
+        n = X1.shape[0]
+        Np = (n + 63) // 64 * 64
         E11 = E11.to(dev, torch.float64)
         A = torch.linalg.inv(E11)
         alpha = (A.T @ y1.to(dev, torch.float64).reshape(-1, 1)).reshape(-1)  # E11⁻ᵀ y1 (gpis.py:53-55)
         A = 0.5 * (A + A.T)
         self.X1 = X1[:1].to(torch.float64).repeat(Np, 1).contiguous()
-        self.X1[:N] = X1.to(torch.float64)
+        self.X1[:n] = X1.to(torch.float64)
         self.alpha = torch.zeros(Np, dtype=torch.float64, device=dev)
-        self.alpha[:N] = alpha
+        self.alpha[:n] = alpha
         self.Ainv = torch.zeros(Np, Np, dtype=torch.float64, device=dev)
-        self.Ainv[:N, :N] = A
-        self.desc = N.CdxGpis(X1=self.X1.data_ptr(), alpha=self.alpha.data_ptr(), Ainv=self.Ainv.data_ptr(), N=N,
+        self.Ainv[:n, :n] = A
+        self.desc = N.CdxGpis(X1=self.X1.data_ptr(), alpha=self.alpha.data_ptr(), Ainv=self.Ainv.data_ptr(), N=n,
                               N_pad=Np, kernel=N.KERNELS[kernel], R=float(R), sigma=float(sigma), bias=float(bias))
         self.ws = None
 

@@ -25,7 +25,14 @@ rc=$?; echo "bench rc=$rc"; tail -1 "$OUT/bench_$TAG.log"; stop_if_fault $rc
 
 echo "== rocprofv3 kernel trace"; date
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/rocprof_$TAG.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/rocprof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -2 "$OUT/rocprof_$TAG.log"
 find "$OUT/prof_$TAG" -name "*stats*" | head
+date
+
+echo "== rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs)"; date
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${C}_$TAG" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_${C}_$TAG.log" 2>&1
+  rc=$?; echo "pmc $C rc=$rc"; stop_if_fault $rc
+done
 date

@@ -1,0 +1,61 @@
+"""Summarises rocprofv3 outputs of tools/gpu_round.sh into profiles/.
+
+  python tools/pmc_summary.py TAG [E N]
+Reads gpurun_out/prof_TAG (kernel-trace stats), gpurun_out/pmc_FETCH_SIZE_TAG and
+gpurun_out/pmc_WRITE_SIZE_TAG (counter CSVs) and writes
+  profiles/TAG_kernel_stats.csv   the rocprofv3 --stats summary (copied)
+  profiles/TAG_pmc.json           per-dispatch HBM bytes per kernel, gfx950-corrected:
+                                  bytes = (2·FETCH_SIZE + WRITE_SIZE)·1024 (FETCH_SIZE reads ½ of a
+                                  16-B/lane coalesced stream on gfx950: MI355X_MICROARCH.md §HBM)
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(dirpath, name):
+    files = glob.glob(os.path.join(dirpath, "**", "*counter_collection*.csv"), recursive=True)
+    per = defaultdict(list)
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name") != name:
+                continue
+            per[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    return per
+
+
+def short(k):
+    return k.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+
+
+def main():
+    tag = sys.argv[1]
+    E = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    N = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
+    out = os.path.join(REPO, "gpurun_out")
+    os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
+    for f in glob.glob(os.path.join(out, f"prof_{tag}", "**", "*kernel_stats.csv"), recursive=True):
+        shutil.copyfile(f, os.path.join(REPO, "profiles", f"{tag}_kernel_stats.csv"))
+    fetch = counters(os.path.join(out, f"pmc_FETCH_SIZE_{tag}"), "FETCH_SIZE")
+    write = counters(os.path.join(out, f"pmc_WRITE_SIZE_{tag}"), "WRITE_SIZE")
+    summary = {"tag": tag, "E": E, "n_inducing": N, "unit": "bytes per dispatch",
+               "correction": "(2*FETCH_SIZE + WRITE_SIZE) * 1024", "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f = sum(fetch.get(k, [0])) / max(len(fetch.get(k, [])), 1)
+        w = sum(write.get(k, [0])) / max(len(write.get(k, [])), 1)
+        summary["kernels"][short(k)] = {"FETCH_SIZE_kB": f, "WRITE_SIZE_kB": w, "hbm_bytes": (2 * f + w) * 1024,
+                                        "dispatches": len(fetch.get(k, []))}
+        if "gpis_std_kernel" in k:
+            summary["gpis_std_bytes_per_launch"] = (2 * f + w) * 1024
+    json.dump(summary, open(os.path.join(REPO, "profiles", f"{tag}_pmc.json"), "w"), indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
