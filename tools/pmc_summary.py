@@ -31,7 +31,8 @@ def counters(dirpath, name):
 
 
 def short(k):
-    return k.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+    k = k.replace("void ", "").replace("(anonymous namespace)::", "")
+    return k.split("(")[0]
 
 
 def main():
@@ -47,6 +48,8 @@ def main():
     summary = {"tag": tag, "E": E, "n_inducing": N, "unit": "bytes per dispatch",
                "correction": "(2*FETCH_SIZE + WRITE_SIZE) * 1024", "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
+        if k.startswith("Cijk_") or "rocsolver" in k:
+            continue  # setup-time library kernels (E11 inverse), not the hot path
         f = sum(fetch.get(k, [0])) / max(len(fetch.get(k, [])), 1)
         w = sum(write.get(k, [0])) / max(len(write.get(k, [])), 1)
         summary["kernels"][short(k)] = {"FETCH_SIZE_kB": f, "WRITE_SIZE_kB": w, "hbm_bytes": (2 * f + w) * 1024,
