@@ -211,6 +211,7 @@ class ProbabilisticGraspOptimizer:
             with torch.no_grad():
                 compliance.clamp_(min=80.0)
                 target_pose.clamp_(min=self.tip_bounding_box[0], max=self.tip_bounding_box[1])
+        self.best_loss = opt_value
         if verbose:
             print("Margin:", opt_margin)
         return opt_joint_angle, opt_compliance, opt_target_pose, opt_palm_poses, opt_margin
