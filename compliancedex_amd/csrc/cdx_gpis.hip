@@ -68,120 +68,160 @@ __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const
 }
 
 // ------------------------------------------------------------------ std (MFMA)
-// Tile: 64 queries × 64 output columns per 256-thread workgroup, K-step 16.
-// Wave w owns rows 32·(w>>1)…+32 and columns 32·(w&1)…+32 as 2×2 MFMA 16×16 tiles.
-// v_mfma_f64_16x16x4_f64 operand maps (cdna_hip_programming.md §3):
+// W = K*·E11⁻¹ tile of 128 queries × 128 output columns per 256-thread workgroup, K-step 16,
+// two LDS buffers (register-staged: the K* tile is computed, not loaded), one barrier per
+// K-step.  Waves form a 2×2 grid; each owns 64×64 = 4×4 v_mfma_f64_16x16x4_f64 tiles.
+// Fragment maps (cdna_hip_programming.md §3, f64 form):
 //   A: lane l holds A[row l&15][k l>>4];  B: B[k l>>4][col l&15]
 //   C/D: reg r of lane l is D[row (l>>4) + 4r][col l&15]
-constexpr int ST_BM = 64, ST_BN = 64, ST_BK = 16, ST_LD = 80;  // LD padded: conflict-free b64 reads
+// LDS rows are padded to 144 doubles (row stride ≡ 32 dwords mod 64): the two half-waves of a
+// ds_read_b64 (rows k, k+1) land on disjoint banks.
+constexpr int ST_BM = 128, ST_BN = 128, ST_BK = 16, ST_LD = 144;
+constexpr int ST_TILE = ST_BK * ST_LD;                          // doubles per staged matrix
+constexpr int ST_SMEM = 4 * ST_TILE + ST_BM * 3;                // 2 buffers × (K*, E11⁻¹) + query tile
+
+typedef double dbl2v __attribute__((ext_vector_type(2)));
 
 template <int KT>
-__global__ __launch_bounds__(256) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
-                                                       double* __restrict__ partial, int64_t M_pad) {
-  __shared__ double Kt[ST_BK][ST_LD];  // K* tile, [k][m]
-  __shared__ double As[ST_BK][ST_LD];  // E11⁻¹ tile, [k][n]
-  __shared__ double xq[ST_BM][3];
-  __shared__ double red[2][ST_BM][4];
+__global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
+                                                          double* __restrict__ partial, int64_t M_pad, int Mt,
+                                                          int Nt) {
+  __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
+  double* xq = smem + 4 * ST_TILE;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * ST_BM;
-  const int n0 = blockIdx.y * ST_BN;
+  // XCD-aware order: blocks b and b+8 share an XCD (round-robin dispatch); give each XCD a
+  // contiguous run of n-major tiles so its L2 serves the same E11⁻¹ column stripes.
+  const int T = Mt * Nt;
+  const int b = blockIdx.x;
+  const int t = (T & 7) == 0 ? (b & 7) * (T >> 3) + (b >> 3) : b;
+  const int nt = t / Mt, mt = t - nt * Mt;
+  const int64_t m0 = (int64_t)mt * ST_BM;
+  const int n0 = nt * ST_BN;
   const int Np = g.N_pad;
   const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
-  if (tid < ST_BM) {
-    const int64_t m = min(m0 + tid, M - 1);  // pad rows replicate a valid query
-    xq[tid][0] = X[3 * m]; xq[tid][1] = X[3 * m + 1]; xq[tid][2] = X[3 * m + 2];
-  }
-  __syncthreads();
-  const int gm = tid & 63, gk = (tid >> 6) * 4;  // generation: this thread's query row and k sub-block
-  const double qx = xq[gm][0], qy = xq[gm][1], qz = xq[gm][2];
-  const int ar = tid >> 4, ac = (tid & 15) * 4;  // A-tile load: row, 4 columns
-  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
-  dbl4 acc00 = {0, 0, 0, 0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
 
-  for (int kb = 0; kb < Np; kb += ST_BK) {
-    const double2* src = reinterpret_cast<const double2*>(g.Ainv + (int64_t)(kb + ar) * Np + n0 + ac);
-    const double2 v0 = src[0], v1 = src[1];
-    double kv[4];
+  const int gm = tid & (ST_BM - 1);
+  const int gk = __builtin_amdgcn_readfirstlane((tid >> 7) * 8);  // wave-uniform k sub-block
+  double qx, qy, qz;
+  {
+    const int64_t m = min(m0 + gm, M - 1);  // pad rows replicate a valid query
+    qx = X[3 * m]; qy = X[3 * m + 1]; qz = X[3 * m + 2];
+    if (tid < ST_BM) { xq[3 * tid] = qx; xq[3 * tid + 1] = qy; xq[3 * tid + 2] = qz; }
+  }
+  const int ar = tid >> 4, ac = (tid & 15) * 8;      // E11⁻¹ tile: row, 8 columns
+  const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
+
+  dbl2v av[4];
+  double kv[8];
+  auto stage_load = [&](int kb) {
+    const dbl2v* src = reinterpret_cast<const dbl2v*>(g.Ainv + (int64_t)(kb + ar) * Np + n0 + ac);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = kb + gk + i;
-      const double dx = qx - g.X1[3 * j], dy = qy - g.X1[3 * j + 1], dz = qz - g.X1[3 * j + 2];
+    for (int i = 0; i < 4; ++i) av[i] = src[i];
+    const double* x1 = g.X1 + 3 * (kb + gk);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
       double kd;
       gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
     }
-    __syncthreads();
-    As[ar][ac] = v0.x; As[ar][ac + 1] = v0.y; As[ar][ac + 2] = v1.x; As[ar][ac + 3] = v1.y;
+  };
+  auto stage_write = [&](int buf) {
+    double* Kt = smem + buf * 2 * ST_TILE;
+    double* As = Kt + ST_TILE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) Kt[gk + i][gm] = kv[i];
-    __syncthreads();
+    for (int i = 0; i < 8; ++i) Kt[(gk + i) * ST_LD + gm] = kv[i];
+    dbl2v* dst = reinterpret_cast<dbl2v*>(As + ar * ST_LD + ac);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dst[i] = av[i];
+  };
+
+  dbl4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0, 0, 0, 0};
+
+  const int nK = Np / ST_BK;
+  stage_load(0);
+  stage_write(0);
+  __syncthreads();
+  for (int s = 0; s < nK; ++s) {
+    const bool more = s + 1 < nK;
+    if (more) stage_load((s + 1) * ST_BK);
+    const double* Kt = smem + (s & 1) * 2 * ST_TILE;
+    const double* As = Kt + ST_TILE;
 #pragma unroll
     for (int kk = 0; kk < ST_BK; kk += 4) {
-      const int kr = kk + (lane >> 4);
-      const double a0 = Kt[kr][wr + (lane & 15)], a1 = Kt[kr][wr + 16 + (lane & 15)];
-      const double b0 = As[kr][wc + (lane & 15)], b1 = As[kr][wc + 16 + (lane & 15)];
-      acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc00, 0, 0, 0);
-      acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc01, 0, 0, 0);
-      acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc10, 0, 0, 0);
-      acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc11, 0, 0, 0);
+      const int kr = (kk + (lane >> 4)) * ST_LD + (lane & 15);
+      double a[4], bb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { a[i] = Kt[kr + wr + 16 * i]; bb[i] = As[kr + wc + 16 * i]; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], bb[j], acc[i][j], 0, 0, 0);
     }
+    if (more) stage_write((s + 1) & 1);
+    __syncthreads();
   }
 
-  // Epilogue: per owned row, s = Σ W k and g = Σ W kd (x_m − x_n) over this wave's 32 columns.
-  double ps[2][4][4];
+  // Epilogue: per owned row, s = Σ_n W k and g = Σ_n W kd (x_m − x_n) over this wave's 64 columns,
+  // reduced over the 16 lanes of a row (xor-shuffles), then over the two column waves in LDS.
+  double* red = smem;  // [2][ST_BM][4], reuses the staging buffers (loop ended on a barrier)
+  double nxs[4][3];
 #pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc + 16 * j + (lane & 15);
+    nxs[j][0] = g.X1[3 * n]; nxs[j][1] = g.X1[3 * n + 1]; nxs[j][2] = g.X1[3 * n + 2];
+  }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ps[ti][r][0] = ps[ti][r][1] = ps[ti][r][2] = ps[ti][r][3] = 0.0;
+  for (int i = 0; i < 4; ++i) {
+    double ps[4][4];
 #pragma unroll
-  for (int tj = 0; tj < 2; ++tj) {
-    const int n = n0 + wc + tj * 16 + (lane & 15);
-    const double nx = g.X1[3 * n], ny = g.X1[3 * n + 1], nz = g.X1[3 * n + 2];
+    for (int r = 0; r < 4; ++r) ps[r][0] = ps[r][1] = ps[r][2] = ps[r][3] = 0.0;
 #pragma unroll
-    for (int ti = 0; ti < 2; ++ti) {
-      const dbl4 a = ti == 0 ? (tj == 0 ? acc00 : acc01) : (tj == 0 ? acc10 : acc11);
+    for (int r = 0; r < 4; ++r) {
+      const int row = wr + 16 * i + (lane >> 4) + 4 * r;
+      const double mx = xq[3 * row], my = xq[3 * row + 1], mz = xq[3 * row + 2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr + ti * 16 + (lane >> 4) + 4 * r;
-        const double dx = xq[row][0] - nx, dy = xq[row][1] - ny, dz = xq[row][2] - nz;
+      for (int j = 0; j < 4; ++j) {
+        const double dx = mx - nxs[j][0], dy = my - nxs[j][1], dz = mz - nxs[j][2];
         double k, kd;
         gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, k, kd);
-        const double w = a[r];
+        const double w = acc[i][j][r];
         const double wkd = w * kd;
-        ps[ti][r][0] += w * k;
-        ps[ti][r][1] += wkd * dx;
-        ps[ti][r][2] += wkd * dy;
-        ps[ti][r][3] += wkd * dz;
+        ps[r][0] += w * k;
+        ps[r][1] += wkd * dx;
+        ps[r][2] += wkd * dy;
+        ps[r][3] += wkd * dz;
       }
     }
-  }
-  // reduce over the 16 lanes sharing (lane>>4)
-#pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        double v = ps[ti][r][c];
+        double v = ps[r][c];
         v += __shfl_xor(v, 1);
         v += __shfl_xor(v, 2);
         v += __shfl_xor(v, 4);
         v += __shfl_xor(v, 8);
-        ps[ti][r][c] = v;
+        ps[r][c] = v;
       }
-  if ((lane & 15) == 0) {
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
+    if ((lane & 15) == 0) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wr + ti * 16 + (lane >> 4) + 4 * r;
+        const int row = wr + 16 * i + (lane >> 4) + 4 * r;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) red[wave & 1][row][c] = ps[ti][r][c];
+        for (int c = 0; c < 4; ++c) red[((wave & 1) * ST_BM + row) * 4 + c] = ps[r][c];
       }
+    }
   }
   __syncthreads();
-  {
-    const int row = tid >> 2, c = tid & 3;  // 64 rows × 4 values = 256 threads
-    partial[((int64_t)blockIdx.y * M_pad + m0 + row) * 4 + c] = red[0][row][c] + red[1][row][c];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = tid + 256 * h;  // 128 rows × 4 values
+    const int row = idx >> 2, c = idx & 3;
+    partial[((int64_t)nt * M_pad + m0 + row) * 4 + c] = red[row * 4 + c] + red[(ST_BM + row) * 4 + c];
   }
 }
 
@@ -216,7 +256,7 @@ __global__ void mfma_f64_selftest_kernel(const double* A, const double* B, doubl
 }
 
 bool gpis_ok(const cdx_gpis* g) {
-  return g && g->X1 && g->alpha && g->N > 0 && g->N_pad >= g->N && g->N_pad % 64 == 0 && g->kernel >= 0 &&
+  return g && g->X1 && g->alpha && g->N > 0 && g->N_pad >= g->N && g->N_pad % 128 == 0 && g->kernel >= 0 &&
          g->kernel <= 2;
 }
 
@@ -255,27 +295,28 @@ int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std_out,
   if (M == 0) return CDX_OK;
   const int64_t M_pad = round_up(M, ST_BM);
   const int n_tiles = g->N_pad / ST_BN;
-  if (M_pad / ST_BM > 0x7fffffff) return CDX_EINVAL;
+  if (M_pad / ST_BM * n_tiles > 0x7fffffff) return CDX_EINVAL;
+  const int Mt = (int)(M_pad / ST_BM);
   double* partial = static_cast<double*>(workspace);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid((unsigned)(M_pad / ST_BM), (unsigned)n_tiles);
+  const dim3 grid((unsigned)(Mt * n_tiles));
   const dim3 fgrid((unsigned)((M + 255) / 256));
   switch (g->kernel) {
     case CDX_KERNEL_TPS:
       cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_TPS>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad);
+      hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_TPS>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
       cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_TPS>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;
     case CDX_KERNEL_RBF:
       cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_RBF>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad);
+      hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_RBF>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
       cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_RBF>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;
     default:
       cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_JOINT>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad);
+      hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_JOINT>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
       cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_JOINT>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;
