@@ -39,15 +39,20 @@ def _deps():
     return [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(REPO, "include", "cdx.h")]
 
 
-def build_device(force=False):
+# Tuning switches compiled into the product library.
+DEFAULT_DEFINES = ("CDX_FAST_SQRT", "CDX_STD_SCHED")
+
+
+def build_device(force=False, defines=DEFAULT_DEFINES, out_name="libcdx.so"):
     os.makedirs(LIB, exist_ok=True)
-    out = os.path.join(LIB, "libcdx.so")
+    out = os.path.join(LIB, out_name)
     if not force and not _stale(out, _deps()):
         return out
     objs = []
     for src in HIP_SOURCES:
-        obj = os.path.join(LIB, src.replace(".hip", ".o"))
+        obj = os.path.join(LIB, out_name + "." + src.replace(".hip", ".o"))
         flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(REPO, "include")]
+        flags += [f"-D{d}" for d in defines]
         if src == "cdx_sdf.hip":
             flags.append("-ffp-contract=off")
         _run([HIPCC, *flags, "-c", os.path.join(CSRC, src), "-o", obj])

@@ -8,17 +8,38 @@
 
 namespace cdx {
 
+// sqrt of a non-negative squared distance.  Device: v_rsq_f64 + one Goldschmidt step + two
+// Newton corrections (the core of the compiler's sqrt without its denormal/inf scaling, which
+// a clamped r² ≥ 1e-200 never needs); r² = 0 returns 1e-100, harmless in every use here
+// (k(1e-100) = k(0) to 1e-200, and ∂k/∂x carries a factor (x − x_j) = 0).
+CDX_HD double sqrt_r2(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(CDX_FAST_SQRT)
+  x = fmax(x, 1e-200);
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double e = fma(-h, g, 0.5);
+  g = fma(g, e, g);
+  h = fma(h, e, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  return fma(d, h, g);
+#else
+  return sqrt(x);
+#endif
+}
+
 template <int KT>
 CDX_HD void gpis_k(double r2, double R, double inv_s2, double& k, double& kd) {
   if (KT == CDX_KERNEL_TPS) {
-    const double r = sqrt(r2);
+    const double r = sqrt_r2(r2);
     k = 2.0 * (r2 * r) - 3.0 * R * r2 + R * R * R;
     kd = 6.0 * r - 6.0 * R;
   } else if (KT == CDX_KERNEL_RBF) {
     k = exp(-0.5 * r2 * inv_s2);
     kd = -k * inv_s2;
   } else {
-    const double r = sqrt(r2);
+    const double r = sqrt_r2(r2);
     const double kr = exp(-0.5 * r2 * inv_s2);
     k = 0.3 * kr + 0.7 * (2.0 * (r2 * r) - 3.0 * R * r2 + R * R * R);
     kd = 0.3 * (-kr * inv_s2) + 0.7 * (6.0 * r - 6.0 * R);

@@ -146,8 +146,14 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const doub
   stage_write(0);
   __syncthreads();
   for (int s = 0; s < nK; ++s) {
-    const bool more = s + 1 < nK;
-    if (more) stage_load((s + 1) * ST_BK);
+    // Stage s+1 (clamped at the end: the extra stage lands in the buffer nobody reads again).
+    const int kn = (s + 1 < nK ? s + 1 : s) * ST_BK;
+    {
+      const dbl2v* src = reinterpret_cast<const dbl2v*>(g.Ainv + (int64_t)(kn + ar) * Np + n0 + ac);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = src[i];
+    }
+    const double* x1 = g.X1 + 3 * (kn + gk);
     const double* Kt = smem + (s & 1) * 2 * ST_TILE;
     const double* As = Kt + ST_TILE;
 #pragma unroll
@@ -159,9 +165,34 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const doub
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], bb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+#if defined(CDX_DIAG_NOMFMA)  // timing-only diagnostic build: outputs are wrong
+          acc[i][j][0] += a[i] * bb[j];
+#else
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], bb[j], acc[i][j], 0, 0, 0);
+#endif
+        }
+      // K* of the next stage, two elements per 16 MFMAs (overlaps the matrix pipe)
+#pragma unroll
+      for (int i = kk / 2; i < kk / 2 + 2; ++i) {
+#if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
+        kv[i] = qx - x1[3 * i];
+#else
+        const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
+        double kd;
+        gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
+#endif
+      }
+#if defined(CDX_STD_SCHED)
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // fragment reads first
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // then up to four VALU
+      }
+#endif
     }
-    if (more) stage_write((s + 1) & 1);
+    stage_write((s + 1) & 1);
     __syncthreads();
   }
 

@@ -1,0 +1,73 @@
+"""A/B timing of gpis_std_kernel build variants (one process per variant, same inputs).
+
+  python tools/std_variants.py build            # builds lib/libcdx_<name>.so for each variant (CPU)
+  python tools/std_variants.py run [M] [N]      # on the GPU: times cdx_gpis_std for each built variant
+"""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+VARIANTS = {"base": (), "fastsqrt": ("CDX_FAST_SQRT",), "fastsqrt_sched": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),
+            # timing-only diagnostics (wrong outputs): generation removed / MFMA removed
+            "diag_nogen": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOGEN"),
+            "diag_nomfma": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOMFMA")}
+
+
+def build():
+    from compliancedex_amd.build import build_device
+    for name, defs in VARIANTS.items():
+        build_device(force=True, defines=defs, out_name=f"libcdx_{name}.so")
+
+
+def child(lib, M, N, ref_path):
+    os.environ["CDX_LIB"] = lib
+    import numpy as np
+    import torch
+    from compliancedex_amd.gpis import gpis_std
+    from compliancedex_amd.workloads import synthetic_banana_gpis
+    g = synthetic_banana_gpis(N, "cuda")
+    st = g.native_state()
+    X1 = g.X1.cpu().numpy()
+    rng = np.random.default_rng(0)
+    lo, hi = X1.min(0) - 0.03, X1.max(0) + 0.03
+    X = torch.from_numpy(lo + (hi - lo) * rng.random((M, 3))).cuda()
+    for _ in range(3):
+        std, gstd = gpis_std(st, X)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    reps = 20
+    ev[0].record()
+    for _ in range(reps):
+        std, gstd = gpis_std(st, X)
+    ev[1].record()
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    out = torch.cat([std.unsqueeze(1), gstd], 1).cpu().numpy()
+    if not os.path.exists(ref_path):
+        np.save(ref_path, out)
+    ref = np.load(ref_path)
+    err = float(np.abs(out - ref).max() / np.abs(ref).max())
+    tf = M * 2.0 * N * N / (ms * 1e-3) / 1e12
+    print(json.dumps({"lib": os.path.basename(lib), "M": M, "N": N, "ms": ms, "TFLOPs": tf, "rel_diff_vs_first": err}))
+
+
+def run(M, N):
+    ref = os.path.join(REPO, "gpurun_out", f"std_ref_{M}_{N}.npy")
+    if os.path.exists(ref):
+        os.remove(ref)
+    for name in VARIANTS:
+        lib = os.path.join(REPO, "compliancedex_amd", "lib", f"libcdx_{name}.so")
+        if os.path.exists(lib):
+            subprocess.run([sys.executable, __file__, "child", lib, str(M), str(N), ref], check=True, timeout=300)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build()
+    elif sys.argv[1] == "run":
+        run(int(sys.argv[2]) if len(sys.argv) > 2 else 16384, int(sys.argv[3]) if len(sys.argv) > 3 else 2000)
+    else:
+        child(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
