@@ -113,49 +113,160 @@ __device__ cdx::GpisPoint GpisView::operator()(int kind, int u, int f) const {
   return p;
 }
 
-__global__ __launch_bounds__(64) void closure_cost_kernel(
-    cdx_problem P, int64_t E, const double* __restrict__ q, const double* __restrict__ comp,
-    const double* __restrict__ target, const double* __restrict__ palm_pos, const double* __restrict__ palm_ori,
-    const double* __restrict__ noise, uint64_t seed, GpisView gv, double* __restrict__ total_loss,
-    double* __restrict__ total_margin, double* __restrict__ g_q, double* __restrict__ g_comp,
-    double* __restrict__ g_target, double* __restrict__ g_palm_pos, double* __restrict__ g_palm_ori,
-    int32_t* __restrict__ flip) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  const int T = P.chain.n_tips, D = P.chain.n_dofs, K = P.n_levels;
-  double nz[CDX_MAX_LEVELS * 9];
+// Per-(level, candidate) thread: compute_loss of one pregrasp level, forward + backward.
+// Record per (k, e): [l, margin[T], g_tip[T][3], g_target[T][3], g_comp[T]]  (1 + 8T doubles).
+CDX_HD int level_record_width(int T) { return 1 + 8 * T; }
+
+__device__ __forceinline__ void device_noise(uint64_t seed, int64_t row, double* nz) {
+  for (int i = 0; i < 9; ++i) {
+    const uint64_t r = splitmix64(seed ^ splitmix64((uint64_t)(row * 9 + i)));
+    nz[i] = (double)(r >> 11) * 0x1.0p-53;
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_t E, const double* __restrict__ q,
+                                                           const double* __restrict__ comp,
+                                                           const double* __restrict__ target,
+                                                           const double* __restrict__ X,
+                                                           const double* __restrict__ noise, uint64_t seed,
+                                                           GpisView gv, double* __restrict__ lvl,
+                                                           int32_t* __restrict__ flip) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int K = P.n_levels;
+  if (t >= K * E) return;
+  const int k = (int)(t / E);
+  const int64_t e = t - (int64_t)k * E;
+  const int T = NT > 0 ? NT : P.chain.n_tips, D = P.chain.n_dofs, Lq = P.n_query_levels;
+  double tip[CDX_MAX_TIPS][3];
+  for (int f = 0; f < T; ++f)
+    for (int i = 0; i < 3; ++i) tip[f][i] = X[3 * cdx::q_pre(Lq, e, f, E, T) + i];
+  double nz[9];
   cdx::CandidateIn in;
   in.q = q + e * D;
   in.comp = comp + e * T;
   in.target = target + e * T * 3;
-  in.palm_pos = palm_pos + 3 * e;
-  in.palm_ori = palm_ori + 3 * e;
+  in.palm_pos = in.palm_ori = nullptr;
   if (noise) {
-    in.noise = noise + e * 9;
-    in.noise_stride = E * 9;
+    in.noise = noise + t * 9;
   } else {
-    for (int k = 0; k < K; ++k)
-      for (int i = 0; i < 9; ++i) {
-        const uint64_t r = splitmix64(seed ^ splitmix64((uint64_t)((k * E + e) * 9 + i)));
-        nz[9 * k + i] = (double)(r >> 11) * 0x1.0p-53;
-      }
+    device_noise(seed, t, nz);
     in.noise = nz;
-    in.noise_stride = 9;
   }
+  in.noise_stride = 0;
+  double dq[CDX_MAX_DOFS];
+  const double qnorm = cdx::ref_dist(P, in.q, dq);
   GpisView g = gv;
   g.e = e;
-  cdx::CandidateOut out;
-  cdx::closure_candidate(P, in, g, out);
-  total_loss[e] = out.loss;
+  cdx::LevelOut lo;
+  cdx::level_fwd_bwd<NT>(P, k, in, tip, qnorm, g, lo);
+  double* r = lvl + t * level_record_width(T);
+  r[0] = lo.l;
   for (int f = 0; f < T; ++f) {
-    total_margin[e * T + f] = out.margin[f];
-    g_comp[e * T + f] = out.g_comp[f];
-    for (int i = 0; i < 3; ++i) g_target[(e * T + f) * 3 + i] = out.g_target[f][i];
+    r[1 + f] = lo.margin[f];
+    r[1 + 7 * T + f] = lo.g_comp[f];
+    for (int i = 0; i < 3; ++i) {
+      r[1 + T + 3 * f + i] = lo.g_tip[f][i];
+      r[1 + 4 * T + 3 * f + i] = lo.g_target[f][i];
+    }
   }
-  for (int i = 0; i < D; ++i) g_q[e * D + i] = out.g_q[i];
-  for (int i = 0; i < 3; ++i) { g_palm_pos[3 * e + i] = out.g_palm_pos[i]; g_palm_ori[3 * e + i] = out.g_palm_ori[i]; }
-  if (flip)
-    for (int k = 0; k < K; ++k) flip[k * E + e] = out.flip[k];
+  if (flip) flip[t] = lo.flip;
+}
+
+// Per-candidate group of GS lanes, lane f = fingertip f: sums the levels, adds the pregrasp
+// and palm GPIS terms (:757-763), the palm/euler backward and the fingertip's FK VJP, then
+// reduces the shared gradients (palm, q) across the group with xor-shuffles.
+template <int GS>
+__global__ __launch_bounds__(256) void closure_combine_kernel(cdx_problem P, int64_t E, const double* __restrict__ q,
+                                                              const double* __restrict__ palm_pos,
+                                                              const double* __restrict__ palm_ori, GpisView gv,
+                                                              const double* __restrict__ lvl,
+                                                              double* __restrict__ total_loss,
+                                                              double* __restrict__ total_margin,
+                                                              double* __restrict__ g_q, double* __restrict__ g_comp,
+                                                              double* __restrict__ g_target,
+                                                              double* __restrict__ g_palm_pos,
+                                                              double* __restrict__ g_palm_ori) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e = gid / GS;
+  const int f = (int)(gid % GS);
+  const int T = P.chain.n_tips, D = P.chain.n_dofs, K = P.n_levels, Lq = P.n_query_levels;
+  const bool valid = e < E;
+  const bool live = valid && f < T;
+  const int LW = level_record_width(T);
+  const int64_t ec = valid ? e : 0;
+  GpisView g = gv;
+  g.e = ec;
+
+  double gt[3] = {0, 0, 0}, gtar[3] = {0, 0, 0}, gcomp = 0, marg = 0;
+  if (live) {
+    for (int k = 0; k < K; ++k) {
+      const double* r = lvl + ((int64_t)k * E + e) * LW;
+      marg += P.weight[k] * r[1 + f];
+      gcomp += r[1 + 7 * T + f];
+      for (int i = 0; i < 3; ++i) { gt[i] += r[1 + T + 3 * f + i]; gtar[i] += r[1 + 4 * T + 3 * f + i]; }
+    }
+    const cdx::GpisPoint gpp = g(2, 0, f);
+    for (int i = 0; i < 3; ++i) gt[i] += -5.0 * gpp.gmean[i];
+  }
+  // palm transform backward: tip = Rp·tl + palm_pos
+  float qf[CDX_MAX_DOFS];
+  for (int i = 0; i < D; ++i) qf[i] = (float)q[ec * D + i];
+  float tl[3] = {0.f, 0.f, 0.f};
+  if (live) cdx::fk_tip(P.chain, f, qf, tl, nullptr);
+  double Rp[9], dRa[9], dRb[9], dRc[9];
+  cdx::euler_xyz(palm_ori + 3 * ec, Rp, dRa, dRb, dRc);
+  double red[12];  // g_palm_pos (3) + g_Rp (9)
+  for (int i = 0; i < 3; ++i) red[i] = gt[i];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) red[3 + 3 * r + c] = gt[r] * (double)tl[c];
+  double gl[3];
+  cdx::mat3t_vec(Rp, gt, gl);
+  float gtl[3] = {(float)gl[0], (float)gl[1], (float)gl[2]};
+  float gqf[CDX_MAX_DOFS];
+  for (int i = 0; i < D; ++i) gqf[i] = 0.f;
+  if (live) cdx::fk_tip_bwd(P.chain, f, qf, gtl, gqf);
+  double gqd[CDX_MAX_DOFS];
+  for (int i = 0; i < D; ++i) gqd[i] = (double)gqf[i];
+#pragma unroll
+  for (int m = 1; m < GS; m <<= 1) {
+    for (int i = 0; i < 12; ++i) red[i] += __shfl_xor(red[i], m);
+    for (int i = 0; i < D; ++i) gqd[i] += __shfl_xor(gqd[i], m);
+  }
+  if (live) {
+    total_margin[e * T + f] = marg;
+    g_comp[e * T + f] = gcomp;
+    for (int i = 0; i < 3; ++i) g_target[(e * T + f) * 3 + i] = gtar[i];
+  }
+  if (!valid || f != 0) return;
+  double total = 0.0;
+  for (int k = 0; k < K; ++k) total += P.weight[k] * lvl[((int64_t)k * E + e) * LW];
+  double pre_sum = 0.0;
+  for (int ff = 0; ff < T; ++ff) pre_sum += g(2, 0, ff).mean;
+  total = total - pre_sum * 5.0;
+  double gpp[3] = {red[0], red[1], red[2]};
+  if (P.optimize_palm) {
+    const cdx::GpisPoint gpm = g(3, 0, 0);
+    total = total + 1.0 / gpm.mean;
+    const double gm = -1.0 / (gpm.mean * gpm.mean);
+    for (int i = 0; i < 3; ++i) gpp[i] = gm * gpm.gmean[i] + gpp[i];
+  }
+  total_loss[e] = total;
+  double go[3] = {0, 0, 0};
+  for (int i = 0; i < 9; ++i) {
+    go[0] += red[3 + i] * dRa[i];
+    go[1] += red[3 + i] * dRb[i];
+    go[2] += red[3 + i] * dRc[i];
+  }
+  for (int i = 0; i < 3; ++i) { g_palm_pos[3 * e + i] = gpp[i]; g_palm_ori[3 * e + i] = go[i]; }
+  double dq[CDX_MAX_DOFS];
+  const double qnorm = cdx::ref_dist(P, q + e * D, dq);
+  for (int i = 0; i < D; ++i) {
+    double v = 0.0;
+    if (qnorm > 0)
+      for (int k = 0; k < K; ++k) v += P.weight[k] * 10.0 * dq[i] / qnorm;
+    g_q[e * D + i] = v + gqd[i];
+  }
 }
 
 bool chain_ok(const cdx_chain* c) {
@@ -166,7 +277,7 @@ bool chain_ok(const cdx_chain* c) {
 size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 struct ClosureWs {
-  double *X, *mean, *gmean, *normal, *std_, *gstd;
+  double *X, *mean, *gmean, *normal, *std_, *gstd, *lvl;
   void* std_ws;
   size_t bytes;
 };
@@ -184,6 +295,7 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   w.std_ = (double*)take(Ms * sizeof(double));
   w.gstd = (double*)take(Ms * 3 * sizeof(double));
   w.std_ws = take(cdx_gpis_std_workspace(&p->gpis, Ms));
+  w.lvl = (double*)take((size_t)p->n_levels * E * level_record_width(p->chain.n_tips) * sizeof(double));
   w.bytes = off;
   return w;
 }
@@ -255,9 +367,25 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   gv.mean = w.mean; gv.gmean = w.gmean; gv.normal = w.normal; gv.std_ = w.std_; gv.gstd = w.gstd;
   gv.E = E; gv.T = p->chain.n_tips; gv.Lq = p->n_query_levels; gv.e = 0;
   cdx::prof_mark(cdx::PROF_COST, true, s);
-  hipLaunchKernelGGL(closure_cost_kernel, grid, dim3(64), 0, s, *p, E, q, comp, target, palm_pos, palm_ori,
-                     kabsch_noise, seed, gv, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori,
-                     flip);
+  {
+    const int64_t KE = (int64_t)p->n_levels * E;
+    const dim3 lgrid((unsigned)((KE + 63) / 64));
+    if (p->chain.n_tips == 4)
+      hipLaunchKernelGGL(closure_level_kernel<4>, lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X, kabsch_noise,
+                         seed, gv, w.lvl, flip);
+    else
+      hipLaunchKernelGGL(closure_level_kernel<0>, lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X, kabsch_noise,
+                         seed, gv, w.lvl, flip);
+    if (hipGetLastError() != hipSuccess) return CDX_ELAUNCH;
+    if (p->chain.n_tips <= 4)
+      hipLaunchKernelGGL(closure_combine_kernel<4>, dim3((unsigned)((E * 4 + 255) / 256)), dim3(256), 0, s, *p, E, q,
+                         palm_pos, palm_ori, gv, w.lvl, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos,
+                         g_palm_ori);
+    else
+      hipLaunchKernelGGL(closure_combine_kernel<8>, dim3((unsigned)((E * 8 + 255) / 256)), dim3(256), 0, s, *p, E, q,
+                         palm_pos, palm_ori, gv, w.lvl, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos,
+                         g_palm_ori);
+  }
   cdx::prof_mark(cdx::PROF_COST, false, s);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }

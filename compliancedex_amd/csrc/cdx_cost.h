@@ -193,6 +193,16 @@ CDX_HD void pregrasp_tips(const cdx_problem& P, const double* q, const double* p
   }
 }
 
+// ‖q − ref_q‖ with ref_q float32 (:732); dq receives q − ref_q.
+CDX_HD double ref_dist(const cdx_problem& P, const double* q, double* dq) {
+  double qn2 = 0.0;
+  for (int i = 0; i < P.chain.n_dofs; ++i) {
+    dq[i] = q[i] - (double)P.ref_q[i];
+    qn2 += dq[i] * dq[i];
+  }
+  return sqrt(qn2);
+}
+
 struct CandidateIn {
   const double *q, *comp, *target, *palm_pos, *palm_ori;  // this candidate's rows
   const double* noise;                                     // [K][9] for this candidate (stride via noise_stride)
@@ -210,41 +220,32 @@ struct CandidateOut {
   int flip[CDX_MAX_LEVELS];
 };
 
-// Forward + backward of Σ_levels w_k·l_k − 5·Σ pre_dist + 1/palm_dist for one candidate.
-// gp(kind, level_or_0, finger) returns the GPIS results at the corresponding query.
-template <typename GpisAt>
-CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisAt gp, CandidateOut& out) {
-  const int T = P.chain.n_tips;
-  const int K = P.n_levels;
-  const double cos_mu = (double)P.cos_mu;
-  double tip[CDX_MAX_TIPS][3];
-  float tl[CDX_MAX_TIPS][3];
-  double Rp[9];
-  pregrasp_tips(P, in.q, in.palm_pos, in.palm_ori, tip, tl, Rp);
-
+// One pregrasp level of compute_loss (:713-739) for one candidate, forward AND backward with
+// dL/dl_k = w_k: returns l_k, margin_k, the Kabsch mask and the level's gradient w.r.t. the
+// pregrasp tips, targets and compliances.  NT = fingertip count at compile time (0: runtime).
+struct LevelOut {
+  double l;
+  double margin[CDX_MAX_TIPS];
   double g_tip[CDX_MAX_TIPS][3];
+  double g_target[CDX_MAX_TIPS][3];
+  double g_comp[CDX_MAX_TIPS];
+  int flip;
+};
+
+template <int NT, typename GpisAt>
+CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, const double (*tip)[3], double qnorm,
+                          GpisAt gp, LevelOut& o) {
+  constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
+  const int T = NT > 0 ? NT : P.chain.n_tips;
+  const double cos_mu = (double)P.cos_mu;
   for (int f = 0; f < T; ++f) {
-    g_tip[f][0] = g_tip[f][1] = g_tip[f][2] = 0.0;
-    out.g_target[f][0] = out.g_target[f][1] = out.g_target[f][2] = 0.0;
-    out.g_comp[f] = 0.0;
-    out.margin[f] = 0.0;
+    for (int i = 0; i < 3; ++i) { o.g_target[f][i] = 0.0; o.g_tip[f][i] = 0.0; }
+    o.g_comp[f] = 0.0;
   }
-  for (int i = 0; i < P.chain.n_dofs; ++i) out.g_q[i] = 0.0;
-
-  // ref_cost is identical on every level: ‖q − ref_q‖ with ref_q float32 (:732)
-  double dq[CDX_MAX_DOFS], qn2 = 0.0;
-  for (int i = 0; i < P.chain.n_dofs; ++i) {
-    dq[i] = in.q[i] - (double)P.ref_q[i];
-    qn2 += dq[i] * dq[i];
-  }
-  const double qnorm = sqrt(qn2);
-
-  double total = 0.0;
-  for (int k = 0; k < K; ++k) {
     const int u = P.level_query[k];
     const double wk = P.weight[k];
     // ---- forward of compute_loss for this level
-    double a[CDX_MAX_TIPS][3], d[CDX_MAX_TIPS], s[CDX_MAX_TIPS], n[CDX_MAX_TIPS][3], td[CDX_MAX_TIPS];
+    double a[NTA][3], d[NTA], s[NTA], n[NTA][3], td[NTA];
     for (int f = 0; f < T; ++f) {
       const double c = (double)P.coeff[k][f];
       for (int i = 0; i < 3; ++i) a[f][i] = in.target[3 * f + i] + c * (tip[f][i] - in.target[3 * f + i]);
@@ -256,7 +257,7 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
     }
     // Kabsch on [tips, dummy] / [targets, dummy] with weights [comp, dummy_comp]
     const int NP = P.gravity ? T + 1 : T;
-    double S1[CDX_MAX_TIPS + 1][3], S2[CDX_MAX_TIPS + 1][3], w[CDX_MAX_TIPS + 1];
+    double S1[NTA + 1][3], S2[NTA + 1][3], w[NTA + 1];
     for (int f = 0; f < T; ++f) {
       for (int i = 0; i < 3; ++i) { S1[f][i] = a[f][i]; S2[f][i] = in.target[3 * f + i]; }
       w[f] = in.comp[f];
@@ -270,7 +271,7 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { c1[j] += S1[i][j]; c2[j] += S2[i][j]; }
     for (int j = 0; j < 3; ++j) { c1[j] /= NP; c2[j] /= NP; }
-    double Pm[CDX_MAX_TIPS + 1][3], Qm[CDX_MAX_TIPS + 1][3];
+    double Pm[NTA + 1][3], Qm[NTA + 1][3];
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { Pm[i][j] = w[i] * (S1[i][j] - c1[j]); Qm[i][j] = w[i] * (S2[i][j] - c2[j]); }
     double H[9];
@@ -283,16 +284,16 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
     KabschTape tp;
     double R[9];
     kabsch_rotation(H, in.noise + k * in.noise_stride, tp, R);
-    out.flip[k] = tp.d < 0 ? 1 : 0;
-    double W = 0.0, num[3] = {0, 0, 0}, RS1[CDX_MAX_TIPS + 1][3];
+    o.flip = tp.d < 0 ? 1 : 0;
+    double W = 0.0, num[3] = {0, 0, 0}, RS1[NTA + 1][3];
     for (int i = 0; i < NP; ++i) {
       W += w[i];
       mat3_vec(R, S1[i], RS1[i]);
       for (int j = 0; j < 3; ++j) num[j] += w[i] * (S2[i][j] - RS1[i][j]);
     }
     double t[3] = {num[0] / W, num[1] / W, num[2] / W};
-    double diff[CDX_MAX_TIPS][3], dn[CDX_MAX_TIPS], dir[CDX_MAX_TIPS][3], ne[CDX_MAX_TIPS][3];
-    double ang[CDX_MAX_TIPS], mpre[CDX_MAX_TIPS], margin[CDX_MAX_TIPS], fn[CDX_MAX_TIPS], force[CDX_MAX_TIPS][3];
+    double diff[NTA][3], dn[NTA], dir[NTA][3], ne[NTA][3];
+    double ang[NTA], mpre[NTA], margin[NTA], fn[NTA], force[NTA][3];
     double reward = 0.0;
     for (int f = 0; f < T; ++f) {
       for (int i = 0; i < 3; ++i) diff[f][i] = RS1[f][i] + t[i] - in.target[3 * f + i];
@@ -306,7 +307,7 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
       reward += 0.2 * log(ang[f] + 1) + 0.8 * log(margin[f] + 1);
     }
     // contact margin (unclamped)
-    double cd[CDX_MAX_TIPS][3], cdn[CDX_MAX_TIPS], cdir[CDX_MAX_TIPS][3], cang[CDX_MAX_TIPS];
+    double cd[NTA][3], cdn[NTA], cdir[NTA][3], cang[NTA];
     double creward = 0.0;
     for (int f = 0; f < T; ++f) {
       for (int i = 0; i < 3; ++i) cd[f][i] = a[f][i] - in.target[3 * f + i];
@@ -318,9 +319,9 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
     // force cost: −Σ clamp(fn·softmin(fn), max=10)
     double zmax = -fn[0];
     for (int f = 1; f < T; ++f) zmax = -fn[f] > zmax ? -fn[f] : zmax;
-    double ez[CDX_MAX_TIPS], esum = 0.0;
+    double ez[NTA], esum = 0.0;
     for (int f = 0; f < T; ++f) { ez[f] = exp(-fn[f] - zmax); esum += ez[f]; }
-    double sm[CDX_MAX_TIPS], v[CDX_MAX_TIPS], fcost = 0.0;
+    double sm[NTA], v[NTA], fcost = 0.0;
     for (int f = 0; f < T; ++f) {
       sm[f] = ez[f] / esum;
       v[f] = fn[f] * sm[f];
@@ -338,11 +339,11 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
     for (int f = 0; f < T; ++f) { dcost += fabs(d[f]); tcost += td[f]; }
     const double l = -reward * 200.0 + 1000 * dcost + 20 * tcost + (-creward * 200.0) + fcost + qnorm * 10.0 +
                      P.uncertainty * lmax;
-    total += wk * l;
-    for (int f = 0; f < T; ++f) out.margin[f] += wk * margin[f];
+    o.l = l;
+    for (int f = 0; f < T; ++f) o.margin[f] = margin[f];
 
     // ---- backward of this level with dL/dl = wk
-    double g_a[CDX_MAX_TIPS][3];
+    double g_a[NTA][3];
     for (int f = 0; f < T; ++f) g_a[f][0] = g_a[f][1] = g_a[f][2] = 0.0;
     // dist / tar_dist / variance (GPIS gradients at the query points)
     for (int f = 0; f < T; ++f) {
@@ -351,18 +352,15 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
       const double gd = wk * 1000.0 * sg;
       for (int i = 0; i < 3; ++i) g_a[f][i] += gd * ga.gmean[i];
       const GpisPoint& gt = gp(1, 0, f);
-      for (int i = 0; i < 3; ++i) out.g_target[f][i] += wk * 20.0 * gt.gmean[i];
+      for (int i = 0; i < 3; ++i) o.g_target[f][i] += wk * 20.0 * gt.gmean[i];
     }
     {
       const GpisPoint& ga = gp(0, u, fmax);
       const double gs = wk * P.uncertainty / s[fmax];
       for (int i = 0; i < 3; ++i) g_a[fmax][i] += gs * ga.gstd[i];
     }
-    // ref cost
-    if (qnorm > 0)
-      for (int i = 0; i < P.chain.n_dofs; ++i) out.g_q[i] += wk * 10.0 * dq[i] / qnorm;
     // force cost
-    double g_fn[CDX_MAX_TIPS], g_sm[CDX_MAX_TIPS];
+    double g_fn[NTA], g_sm[NTA];
     double gsm_dot = 0.0;
     for (int f = 0; f < T; ++f) {
       const double gv = v[f] <= 10.0 ? -wk : 0.0;
@@ -380,13 +378,13 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
       for (int i = 0; i < 3; ++i) {
         const double gcd = (gdir[i] - cdir[f][i] * pd) / cdn[f];
         g_a[f][i] += gcd;
-        out.g_target[f][i] -= gcd;
+        o.g_target[f][i] -= gcd;
       }
     }
     // force_eq reward (gain −200·wk) + force norms
     const double g_rw = -200.0 * wk;
     double gR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g_t[3] = {0, 0, 0};
-    double g_S1[CDX_MAX_TIPS + 1][3], g_S2[CDX_MAX_TIPS + 1][3], g_w[CDX_MAX_TIPS + 1];
+    double g_S1[NTA + 1][3], g_S2[NTA + 1][3], g_w[NTA + 1];
     for (int i = 0; i < NP; ++i) { g_S1[i][0] = g_S1[i][1] = g_S1[i][2] = 0; g_S2[i][0] = g_S2[i][1] = g_S2[i][2] = 0; g_w[i] = 0; }
     for (int f = 0; f < T; ++f) {
       double gang = g_rw * 0.2 / (ang[f] + 1);
@@ -407,7 +405,7 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
       const double pd = dot3(dir[f], gdir);
       for (int i = 0; i < 3; ++i) gdiff[i] += (gdir[i] - dir[f][i] * pd) / dn[f];
       // diff = R·S1_f + t − target_f
-      for (int i = 0; i < 3; ++i) { g_t[i] += gdiff[i]; out.g_target[f][i] -= gdiff[i]; }
+      for (int i = 0; i < 3; ++i) { g_t[i] += gdiff[i]; o.g_target[f][i] -= gdiff[i]; }
       for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) gR[3 * r + c] += gdiff[r] * S1[f][c];
       double rt[3];
@@ -450,17 +448,57 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { g_S1[i][j] += g_c1[j] / NP; g_S2[i][j] += g_c2[j] / NP; }
     for (int f = 0; f < T; ++f) {
-      for (int i = 0; i < 3; ++i) { g_a[f][i] += g_S1[f][i]; out.g_target[f][i] += g_S2[f][i]; }
-      out.g_comp[f] += g_w[f];
+      for (int i = 0; i < 3; ++i) { g_a[f][i] += g_S1[f][i]; o.g_target[f][i] += g_S2[f][i]; }
+      o.g_comp[f] += g_w[f];
     }
     // all-tip interpolation a = target + c·(tip − target)
     for (int f = 0; f < T; ++f) {
       const double c = (double)P.coeff[k][f];
       for (int i = 0; i < 3; ++i) {
-        g_tip[f][i] += c * g_a[f][i];
-        out.g_target[f][i] += g_a[f][i] - c * g_a[f][i];
+        o.g_tip[f][i] = c * g_a[f][i];
+        o.g_target[f][i] += g_a[f][i] - c * g_a[f][i];
       }
     }
+  }
+
+// Forward + backward of Σ_levels w_k·l_k − 5·Σ pre_dist + 1/palm_dist for one candidate.
+// gp(kind, level_or_0, finger) returns the GPIS results at the corresponding query.
+template <typename GpisAt>
+CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisAt gp, CandidateOut& out) {
+  const int T = P.chain.n_tips;
+  const int K = P.n_levels;
+  double tip[CDX_MAX_TIPS][3];
+  float tl[CDX_MAX_TIPS][3];
+  double Rp[9];
+  pregrasp_tips(P, in.q, in.palm_pos, in.palm_ori, tip, tl, Rp);
+
+  double g_tip[CDX_MAX_TIPS][3];
+  for (int f = 0; f < T; ++f) {
+    g_tip[f][0] = g_tip[f][1] = g_tip[f][2] = 0.0;
+    out.g_target[f][0] = out.g_target[f][1] = out.g_target[f][2] = 0.0;
+    out.g_comp[f] = 0.0;
+    out.margin[f] = 0.0;
+  }
+  for (int i = 0; i < P.chain.n_dofs; ++i) out.g_q[i] = 0.0;
+
+  // ref_cost is identical on every level: ‖q − ref_q‖ with ref_q float32 (:732)
+  double dq[CDX_MAX_DOFS];
+  const double qnorm = ref_dist(P, in.q, dq);
+
+  double total = 0.0;
+  for (int k = 0; k < K; ++k) {
+    const double wk = P.weight[k];
+    LevelOut lo;
+    level_fwd_bwd<0>(P, k, in, tip, qnorm, gp, lo);
+    total += wk * lo.l;
+    out.flip[k] = lo.flip;
+    for (int f = 0; f < T; ++f) {
+      out.margin[f] += wk * lo.margin[f];
+      out.g_comp[f] += lo.g_comp[f];
+      for (int i = 0; i < 3; ++i) { g_tip[f][i] += lo.g_tip[f][i]; out.g_target[f][i] += lo.g_target[f][i]; }
+    }
+    if (qnorm > 0)
+      for (int i = 0; i < P.chain.n_dofs; ++i) out.g_q[i] += wk * 10.0 * dq[i] / qnorm;
   }
   // pregrasp-distance and palm-distance terms
   for (int f = 0; f < T; ++f) {
