@@ -23,34 +23,44 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-constexpr int MEAN_BLOCK = 64;
+// Mean kernel: 256-thread workgroups = 64 queries × 4 lanes; each workgroup stages 256
+// inducing points (xyz, α) per step in LDS and every lane sums a quarter of them
+// (broadcast LDS reads: the 16 lanes of a split read one address), then the 4 lanes of a
+// query reduce with xor-shuffles.  4 waves per 64 queries keep ≈3 waves per SIMD resident.
+constexpr int MEAN_Q = 64, MEAN_SPLIT = 4, MEAN_BLOCK = MEAN_Q * MEAN_SPLIT;
 
 template <int KT>
 __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
                                                                double* __restrict__ mean, double* __restrict__ gmean,
                                                                double* __restrict__ normal) {
-  __shared__ double sx[MEAN_BLOCK], sy[MEAN_BLOCK], sz[MEAN_BLOCK], sa[MEAN_BLOCK];
-  const int64_t m = (int64_t)blockIdx.x * MEAN_BLOCK + threadIdx.x;
+  __shared__ double sp[4 * MEAN_BLOCK];  // [point][x, y, z, α]
+  const int tid = threadIdx.x;
+  const int split = tid & (MEAN_SPLIT - 1);
+  const int64_t m = (int64_t)blockIdx.x * MEAN_Q + (tid >> 2);
   double x0 = 0, x1 = 0, x2 = 0;
   if (m < M) { x0 = X[3 * m]; x1 = X[3 * m + 1]; x2 = X[3 * m + 2]; }
   const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
   double acc = 0, g0 = 0, g1 = 0, g2 = 0;
   for (int j0 = 0; j0 < g.N; j0 += MEAN_BLOCK) {
-    const int j = j0 + threadIdx.x;
+    const int j = j0 + tid;
     __syncthreads();
     if (j < g.N) {
-      sx[threadIdx.x] = g.X1[3 * j];
-      sy[threadIdx.x] = g.X1[3 * j + 1];
-      sz[threadIdx.x] = g.X1[3 * j + 2];
-      sa[threadIdx.x] = g.alpha[j];
+      sp[4 * tid] = g.X1[3 * j];
+      sp[4 * tid + 1] = g.X1[3 * j + 1];
+      sp[4 * tid + 2] = g.X1[3 * j + 2];
+      sp[4 * tid + 3] = g.alpha[j];
+    } else {
+      sp[4 * tid] = x0 + 1.0;  // any finite point; α = 0
+      sp[4 * tid + 1] = sp[4 * tid + 2] = 0.0;
+      sp[4 * tid + 3] = 0.0;
     }
     __syncthreads();
-    const int cnt = min(MEAN_BLOCK, g.N - j0);
-    for (int jj = 0; jj < cnt; ++jj) {
-      const double dx = x0 - sx[jj], dy = x1 - sy[jj], dz = x2 - sz[jj];
+#pragma unroll 4
+    for (int jj = split; jj < MEAN_BLOCK; jj += MEAN_SPLIT) {
+      const double dx = x0 - sp[4 * jj], dy = x1 - sp[4 * jj + 1], dz = x2 - sp[4 * jj + 2];
       double k, kd;
       gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, k, kd);
-      const double a = sa[jj];
+      const double a = sp[4 * jj + 3];
       acc += a * k;
       const double ak = a * kd;
       g0 += ak * dx;
@@ -58,7 +68,14 @@ __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const
       g2 += ak * dz;
     }
   }
-  if (m >= M) return;
+#pragma unroll
+  for (int w = 1; w < MEAN_SPLIT; w <<= 1) {
+    acc += __shfl_xor(acc, w);
+    g0 += __shfl_xor(g0, w);
+    g1 += __shfl_xor(g1, w);
+    g2 += __shfl_xor(g2, w);
+  }
+  if (m >= M || split != 0) return;
   mean[m] = acc + g.bias;
   if (gmean) { gmean[3 * m] = g0; gmean[3 * m + 1] = g1; gmean[3 * m + 2] = g2; }
   if (normal) {
@@ -256,6 +273,193 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const doub
   }
 }
 
+// v3: the same 128×128 tile, K-step 16, staging and epilogue contract as gpis_std_kernel, on
+// v_mfma_f64_4x4x4_4b_f64 (measured 72-75 TF/s sustained on MI355X vs 47-49 for 16x16x4;
+// tools/microbench/mfma_f64_peak.hip).  Lane layout (probed, tools/microbench/
+// mfma_f64_4x4_layout.hip): A lane 16k+4β+i = A_β[i][k], B lane 16k+4β+j = B_β[k][j],
+// D lane 16i+4β+j = D_β[i][j].  β is used as a 4-row sub-block with B broadcast over β, so one
+// instruction is a 16-row × 4-column × 4-deep product.  Each wave owns 64 rows × 64 columns:
+// 4 row groups rg × 16 column groups cg, one f64 accumulator each.  Row/column maps are chosen so
+// every lane's fragments are contiguous in LDS (2 + 8 ds_read_b128 per 4-deep step):
+//   A (K*):   lane l, group rg → row wr + 4·(l&15) + rg,            k = k0 + (l>>4)
+//   B (E11⁻¹): lane l, group cg → col wc + 16·(l&3) + cg,            k = k0 + (l>>4)
+//   D:        lane l, (rg, cg) → row wr + 4·(4·((l>>2)&3) + (l>>4)) + rg, col wc + 16·(l&3) + cg
+template <int KT>
+__global__ __launch_bounds__(256, 2) void gpis_std_kernel4(cdx_gpis g, const double* __restrict__ X, int64_t M,
+                                                           double* __restrict__ partial, int64_t M_pad, int Mt,
+                                                           int Nt) {
+  __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
+  double* xq = smem + 4 * ST_TILE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = Mt * Nt;
+  const int b = blockIdx.x;
+  const int t = (T & 7) == 0 ? (b & 7) * (T >> 3) + (b >> 3) : b;
+  const int nt = t / Mt, mt = t - nt * Mt;
+  const int64_t m0 = (int64_t)mt * ST_BM;
+  const int n0 = nt * ST_BN;
+  const int Np = g.N_pad;
+  const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
+
+  const int gm = tid & (ST_BM - 1);
+  const int gk = __builtin_amdgcn_readfirstlane((tid >> 7) * 8);
+  double qx, qy, qz;
+  {
+    const int64_t m = min(m0 + gm, M - 1);
+    qx = X[3 * m]; qy = X[3 * m + 1]; qz = X[3 * m + 2];
+    if (tid < ST_BM) { xq[3 * tid] = qx; xq[3 * tid + 1] = qy; xq[3 * tid + 2] = qz; }
+  }
+  const int ar = tid >> 4, ac = (tid & 15) * 8;
+  const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
+
+  dbl2v av[4];
+  double kv[8];
+  {
+    const dbl2v* src = reinterpret_cast<const dbl2v*>(g.Ainv + (int64_t)ar * Np + n0 + ac);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) av[i] = src[i];
+    const double* x1 = g.X1 + 3 * gk;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
+      double kd;
+      gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
+    }
+  }
+  auto stage_write = [&](int buf) {
+    double* Kt = smem + buf * 2 * ST_TILE;
+    double* As = Kt + ST_TILE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Kt[(gk + i) * ST_LD + gm] = kv[i];
+    dbl2v* dst = reinterpret_cast<dbl2v*>(As + ar * ST_LD + ac);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dst[i] = av[i];
+  };
+
+  double acc[4][16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.0;
+
+  const int nK = Np / ST_BK;
+  stage_write(0);
+  __syncthreads();
+  const int arow = wr + 4 * (lane & 15);         // + rg
+  const int bcol = wc + 16 * (lane & 3);         // + cg
+  for (int s = 0; s < nK; ++s) {
+    const int kn = (s + 1 < nK ? s + 1 : s) * ST_BK;
+    {
+      const dbl2v* src = reinterpret_cast<const dbl2v*>(g.Ainv + (int64_t)(kn + ar) * Np + n0 + ac);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = src[i];
+    }
+    const double* x1 = g.X1 + 3 * (kn + gk);
+    const double* Kt = smem + (s & 1) * 2 * ST_TILE;
+    const double* As = Kt + ST_TILE;
+#pragma unroll
+    for (int kk = 0; kk < ST_BK; kk += 4) {
+      const int kr = (kk + (lane >> 4)) * ST_LD;
+      const dbl2v* ap = reinterpret_cast<const dbl2v*>(Kt + kr + arow);
+      const dbl2v* bp = reinterpret_cast<const dbl2v*>(As + kr + bcol);
+      const dbl2v a01 = ap[0], a23 = ap[1];
+      const double a[4] = {a01.x, a01.y, a23.x, a23.y};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // B fragments in two halves of 8 columns (register budget)
+        double bb[8];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) { const dbl2v v = bp[4 * h + c]; bb[2 * c] = v.x; bb[2 * c + 1] = v.y; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+#if defined(CDX_DIAG_NOMFMA)  // timing-only diagnostic build: outputs are wrong
+            acc[i][8 * h + j] += a[i] * bb[j];
+#else
+            acc[i][8 * h + j] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[i], bb[j], acc[i][8 * h + j], 0, 0, 0);
+#endif
+          }
+      }
+#pragma unroll
+      for (int i = kk / 2; i < kk / 2 + 2; ++i) {
+#if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
+        kv[i] = qx - x1[3 * i];
+#else
+        const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
+        double kd;
+        gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
+#endif
+      }
+#if defined(CDX_STD_SCHED)
+      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+      for (int q = 0; q < 64; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      }
+#endif
+    }
+    stage_write((s + 1) & 1);
+    __syncthreads();
+  }
+
+  // Epilogue: lane's rows: wr + 4·r16 + rg with r16 = 4·((l>>2)&3) + (l>>4); columns
+  // wc + 16·(l&3) + cg.  Row sums over this lane's 16 columns, then over the 4 lanes of a row
+  // (xor 1, 2), then over the two column waves in LDS.
+  double* red = smem;
+  const int r16 = 4 * ((lane >> 2) & 3) + (lane >> 4);
+  double ps[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ps[i][0] = ps[i][1] = ps[i][2] = ps[i][3] = 0.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int n = n0 + bcol + j;
+    const double nx = g.X1[3 * n], ny = g.X1[3 * n + 1], nz = g.X1[3 * n + 2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr + 4 * r16 + i;
+      const double dx = xq[3 * row] - nx, dy = xq[3 * row + 1] - ny, dz = xq[3 * row + 2] - nz;
+      double k, kd;
+      gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, k, kd);
+      const double w = acc[i][j];
+      const double wkd = w * kd;
+      ps[i][0] += w * k;
+      ps[i][1] += wkd * dx;
+      ps[i][2] += wkd * dy;
+      ps[i][3] += wkd * dz;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double v = ps[i][c];
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      ps[i][c] = v;
+    }
+  if ((lane & 3) == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr + 4 * r16 + i;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) red[((wave & 1) * ST_BM + row) * 4 + c] = ps[i][c];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = tid + 256 * h;
+    const int row = idx >> 2, c = idx & 3;
+    partial[((int64_t)nt * M_pad + m0 + row) * 4 + c] = red[row * 4 + c] + red[(ST_BM + row) * 4 + c];
+  }
+}
+
+#if defined(CDX_STD_MFMA4)
+#define CDX_STD_KERNEL gpis_std_kernel4
+#else
+#define CDX_STD_KERNEL gpis_std_kernel
+#endif
+
 template <int KT>
 __global__ __launch_bounds__(256) void gpis_std_finalize(cdx_gpis g, const double* __restrict__ partial, int64_t M,
                                                          int64_t M_pad, int n_tiles, double* __restrict__ std_out,
@@ -302,7 +506,7 @@ int cdx_gpis_mean(const cdx_gpis* g, const double* X, int64_t M, double* mean, d
   if (!gpis_ok(g)) return g && (g->kernel < 0 || g->kernel > 2) ? CDX_EKERNEL : CDX_EINVAL;
   if (M < 0 || (M > 0 && (!X || !mean))) return CDX_EINVAL;
   if (M == 0) return CDX_OK;
-  const dim3 grid((unsigned)((M + MEAN_BLOCK - 1) / MEAN_BLOCK));
+  const dim3 grid((unsigned)((M + MEAN_Q - 1) / MEAN_Q));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   cdx::prof_mark(cdx::PROF_GPIS_MEAN, true, s);
   switch (g->kernel) {
@@ -335,19 +539,19 @@ int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std_out,
   switch (g->kernel) {
     case CDX_KERNEL_TPS:
       cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_TPS>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
+      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_TPS>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
       cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_TPS>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;
     case CDX_KERNEL_RBF:
       cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_RBF>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
+      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_RBF>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
       cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_RBF>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;
     default:
       cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(gpis_std_kernel<CDX_KERNEL_JOINT>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
+      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_JOINT>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
       cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_JOINT>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;

@@ -10,10 +10,13 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-VARIANTS = {"base": (), "fastsqrt": ("CDX_FAST_SQRT",), "fastsqrt_sched": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),
-            # timing-only diagnostics (wrong outputs): generation removed / MFMA removed
-            "diag_nogen": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOGEN"),
-            "diag_nomfma": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOMFMA")}
+VARIANTS = {"mfma16": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),
+            "mfma4": ("CDX_FAST_SQRT", "CDX_STD_MFMA4"),
+            "mfma4_sched": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_STD_MFMA4"),
+            # timing-only diagnostics (wrong outputs)
+            "mfma4_nogen": ("CDX_FAST_SQRT", "CDX_STD_MFMA4", "CDX_DIAG_NOGEN"),
+            "mfma4_nomfma": ("CDX_FAST_SQRT", "CDX_STD_MFMA4", "CDX_DIAG_NOMFMA"),
+            "mfma4_nogen_nomfma": ("CDX_FAST_SQRT", "CDX_STD_MFMA4", "CDX_DIAG_NOGEN", "CDX_DIAG_NOMFMA")}
 
 
 def build():
