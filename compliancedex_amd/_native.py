@@ -44,6 +44,22 @@ class CdxProblem(C.Structure):
                 ("uncertainty", C.c_double)]
 
 
+class CdxAdam(C.Structure):
+    _fields_ = [("lr", C.c_double * 5), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double),
+                ("comp_min", C.c_double), ("target_lb", C.c_double * (MAX_TIPS * 3)),
+                ("target_ub", C.c_double * (MAX_TIPS * 3)), ("clamp_target", C.c_int32), ("best_after", C.c_int32)]
+
+
+OPT_BUFFER_FIELDS = ["q", "comp", "target", "palm_pos", "palm_ori", "g_q", "g_comp", "g_target", "g_palm_pos",
+                     "g_palm_ori", "m_q", "v_q", "m_comp", "v_comp", "m_target", "v_target", "m_palm_pos",
+                     "v_palm_pos", "m_palm_ori", "v_palm_ori", "total_loss", "total_margin", "opt_value", "opt_margin",
+                     "opt_q", "opt_comp", "opt_target", "opt_palm"]
+
+
+class CdxOptBuffers(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in OPT_BUFFER_FIELDS]
+
+
 _P = C.c_void_p
 _I64 = C.c_int64
 _SIGS = {
@@ -61,6 +77,8 @@ _SIGS = {
     "cdx_abi_sizes": (None, [C.POINTER(C.c_size_t)]),
     "cdx_selftest_mfma_f64": (C.c_int, [_P, _P, _P, _P]),
     "cdx_profile_enable": (C.c_int, [C.c_int]),
+    "cdx_optimizer_step": (C.c_int, [C.POINTER(CdxAdam), C.POINTER(CdxOptBuffers), _I64, C.c_int32, C.c_int32,
+                                     C.c_int32, _P]),
     "cdx_profile_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
 }
 

@@ -122,17 +122,40 @@ class ProbabilisticGraspOptimizer:
             self._problem_key = key
         return self._problem
 
+    def _closure_into(self, p, q, comp, target, pp, po, noise, out):
+        """cdx_closure on contiguous f64 device tensors, writing into the preallocated ``out``."""
+        lib = N.load()
+        E = q.shape[0]
+        need = lib.cdx_closure_workspace(p, E)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=q.device)
+        self._seed += 1
+        N.check(lib.cdx_closure(p, E, N.ptr(q), N.ptr(comp), N.ptr(target), N.ptr(pp), N.ptr(po), N.ptr(noise),
+                                self._seed, N.ptr(self._ws), N.ptr(out["total_loss"]), N.ptr(out["total_margin"]),
+                                N.ptr(out.get("pregrasp_tip")), N.ptr(out["g_q"]), N.ptr(out["g_comp"]),
+                                N.ptr(out["g_target"]), N.ptr(out["g_palm_pos"]), N.ptr(out["g_palm_ori"]),
+                                N.ptr(out.get("flip")), N.stream_ptr(q.device)), "cdx_closure")
+
+    @staticmethod
+    def _outputs(E, T, D, K, dev, with_pre=True):
+        f64 = dict(dtype=torch.float64, device=dev)
+        out = dict(total_loss=torch.empty(E, **f64), total_margin=torch.empty(E, T, **f64),
+                   g_q=torch.empty(E, D, **f64), g_comp=torch.empty(E, T, **f64), g_target=torch.empty(E, T, 3, **f64),
+                   g_palm_pos=torch.empty(E, 3, **f64), g_palm_ori=torch.empty(E, 3, **f64),
+                   flip=torch.empty(K * E, dtype=torch.int32, device=dev))
+        if with_pre:
+            out["pregrasp_tip"] = torch.empty(E, T, 3, **f64)
+        return out
+
     def closure(self, joint_angles, compliance, target_pose, palm_poses, palm_oris, friction_mu, gpis, num_envs,
                 kabsch_noise=None):
         """One cost+grad eval for all candidates (:741-769).  ``kabsch_noise`` [K·E, 3, 3]
         replays the reference's ``rand_like(H)`` draw; by default it is drawn on device."""
         if self.optim is not None:
             self.optim.zero_grad()
-        lib = N.load()
         p = self.problem(gpis, friction_mu)
         E = int(num_envs)
         dev = joint_angles.device
-        f64 = dict(dtype=torch.float64, device=dev)
         q = joint_angles.detach().to(torch.float64).contiguous()
         comp = compliance.detach().to(torch.float64).contiguous()
         target = target_pose.detach().to(torch.float64).contiguous()
@@ -141,39 +164,34 @@ class ProbabilisticGraspOptimizer:
         T, D = p.chain.n_tips, p.chain.n_dofs
         if q.shape != (E, D) or comp.shape != (E, T) or target.shape != (E, T, 3) or pp.shape != (E, 3) or po.shape != (E, 3):
             raise ValueError("closure input shapes do not match num_envs / the hand")
-        need = lib.cdx_closure_workspace(p, E)
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
-        total_loss = torch.empty(E, **f64)
-        total_margin = torch.empty(E, T, **f64)
-        pre = torch.empty(E, T, 3, **f64)
-        g = [torch.empty(E, D, **f64), torch.empty(E, T, **f64), torch.empty(E, T, 3, **f64), torch.empty(E, 3, **f64),
-             torch.empty(E, 3, **f64)]
         noise = None
         if kabsch_noise is not None:
-            noise = kabsch_noise.to(**f64).contiguous()
+            noise = kabsch_noise.to(dtype=torch.float64, device=dev).contiguous()
             if noise.numel() != p.n_levels * E * 9:
                 raise ValueError("kabsch_noise must be [K*E, 3, 3]")
-        flip = torch.empty(p.n_levels * E, dtype=torch.int32, device=dev)
-        self._seed += 1
-        N.check(lib.cdx_closure(p, E, N.ptr(q), N.ptr(comp), N.ptr(target), N.ptr(pp), N.ptr(po), N.ptr(noise),
-                                self._seed, N.ptr(self._ws), N.ptr(total_loss), N.ptr(total_margin), N.ptr(pre),
-                                *[N.ptr(t) for t in g], N.ptr(flip), N.stream_ptr(dev)), "cdx_closure")
-        for param, grad in zip((joint_angles, compliance, target_pose, palm_poses, palm_oris), g):
+        out = self._outputs(E, T, D, p.n_levels, dev)
+        self._closure_into(p, q, comp, target, pp, po, noise, out)
+        grads = (out["g_q"], out["g_comp"], out["g_target"], out["g_palm_pos"], out["g_palm_ori"])
+        for param, grad in zip((joint_angles, compliance, target_pose, palm_poses, palm_oris), grads):
             if param.requires_grad and param.is_leaf:
                 grad = grad.to(param.dtype)
                 param.grad = grad if param.grad is None else param.grad + grad
-        self.pregrasp_tip_pose = pre
-        self.total_loss = total_loss
-        self.total_margin = total_margin
-        self.kabsch_flip = flip  # det(V·Uᵀ) < 0 mask per (level, candidate) (:64)
-        return total_loss.sum()
+        self.pregrasp_tip_pose = out["pregrasp_tip"]
+        self.total_loss = out["total_loss"]
+        self.total_margin = out["total_margin"]
+        self.kabsch_flip = out["flip"]  # det(V·Uᵀ) < 0 mask per (level, candidate) (:64)
+        return out["total_loss"].sum()
 
     # -------------------------------------------------------------- optimize
     def optimize(self, init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose=True,
-                 noise_tape=None):
-        """The reference's Adam loop (:771-839).  ``noise_tape``: optional per-iteration
-        Kabsch noise tensors (parity replay)."""
+                 noise_tape=None, fused=True):
+        """The reference's optimisation loop (:771-839).  ``fused=True`` (default): per iteration
+        one cdx_closure + one cdx_optimizer_step (Adam, best iterate, clamps on device, no host
+        sync); ``fused=False``: the same loop with torch.optim.Adam.  ``noise_tape``: optional
+        per-iteration Kabsch noise tensors (parity replay)."""
+        if fused:
+            return self._optimize_fused(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
+                                        noise_tape)
         joint_angles = init_joint_angles.clone().requires_grad_(True)
         compliance = compliance.clone().requires_grad_(True)
         params_list = [{"params": joint_angles, "lr": 1e-3}, {"params": compliance, "lr": 0.2}]
@@ -215,3 +233,61 @@ class ProbabilisticGraspOptimizer:
         if verbose:
             print("Margin:", opt_margin)
         return opt_joint_angle, opt_compliance, opt_target_pose, opt_palm_poses, opt_margin
+
+    def adam_config(self):
+        """Param groups of optimize (:782-792) with torch.optim.Adam defaults."""
+        cfg = N.CdxAdam()
+        lrs = [1e-3, 0.2, 2e-3 if self.optimize_target else 0.0, 1e-4 if self.optimize_palm else 0.0,
+               1e-4 if self.optimize_palm else 0.0]
+        for i, v in enumerate(lrs):
+            cfg.lr[i] = v
+        cfg.beta1, cfg.beta2, cfg.eps = 0.9, 0.999, 1e-8
+        cfg.comp_min = 80.0
+        lb = self.tip_bounding_box[0].reshape(-1).double().tolist()
+        ub = self.tip_bounding_box[1].reshape(-1).double().tolist()
+        for j in range(len(lb)):
+            cfg.target_lb[j], cfg.target_ub[j] = lb[j], ub[j]
+        cfg.clamp_target = 1
+        cfg.best_after = 20
+        return cfg
+
+    def _optimize_fused(self, init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose, noise_tape):
+        lib = N.load()
+        p = self.problem(gpis, friction_mu)
+        E = init_joint_angles.shape[0]
+        T, D, K = p.chain.n_tips, p.chain.n_dofs, p.n_levels
+        dev = init_joint_angles.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        q = init_joint_angles.detach().to(**f64).clone()
+        comp = compliance.detach().to(**f64).clone()
+        target = target_pose.detach().to(**f64).clone()
+        pp = self.palm_offset[:, :3].to(**f64).clone()
+        po = self.palm_offset[:, 3:].to(**f64).clone()
+        out = self._outputs(E, T, D, K, dev, with_pre=False)
+        z = torch.zeros_like
+        st = dict(m_q=z(q), v_q=z(q), m_comp=z(comp), v_comp=z(comp), m_target=z(target), v_target=z(target),
+                  m_palm_pos=z(pp), v_palm_pos=z(pp), m_palm_ori=z(po), v_palm_ori=z(po),
+                  opt_value=torch.full((E,), float("inf"), **f64), opt_margin=torch.zeros(E, T, **f64),
+                  opt_q=init_joint_angles.detach().to(**f64).clone(), opt_comp=comp.clone(), opt_target=target.clone(),
+                  opt_palm=self.palm_offset.to(**f64).clone())
+        bufs = N.CdxOptBuffers(q=q.data_ptr(), comp=comp.data_ptr(), target=target.data_ptr(), palm_pos=pp.data_ptr(),
+                               palm_ori=po.data_ptr(), g_q=out["g_q"].data_ptr(), g_comp=out["g_comp"].data_ptr(),
+                               g_target=out["g_target"].data_ptr(), g_palm_pos=out["g_palm_pos"].data_ptr(),
+                               g_palm_ori=out["g_palm_ori"].data_ptr(), total_loss=out["total_loss"].data_ptr(),
+                               total_margin=out["total_margin"].data_ptr(),
+                               **{k: v.data_ptr() for k, v in st.items()})
+        cfg = self.adam_config()
+        stream = N.stream_ptr(dev)
+        for s in range(self.num_iters):
+            noise = None
+            if noise_tape is not None:
+                noise = noise_tape[s].to(**f64).contiguous()
+            self._closure_into(p, q, comp, target, pp, po, noise, out)
+            N.check(lib.cdx_optimizer_step(cfg, bufs, E, D, T, s, stream), "cdx_optimizer_step")
+        if not self.optimize_target and torch.is_tensor(target_pose):
+            target_pose.copy_(target)  # the reference clamps the caller's target in place (:834)
+        self.total_loss, self.total_margin = out["total_loss"], out["total_margin"]
+        self.best_loss = st["opt_value"]
+        if verbose:
+            print("Margin:", st["opt_margin"])
+        return st["opt_q"], st["opt_comp"], st["opt_target"], st["opt_palm"], st["opt_margin"]

@@ -152,6 +152,35 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                 double* g_q, double* g_comp, double* g_target, double* g_palm_pos,
                 double* g_palm_ori, int32_t* flip, cdx_stream_t stream);
 
+/* ------------------------------------------------------- fused optimizer step ------
+ * One launch per iteration of ProbabilisticGraspOptimizer.optimize (optimize_pregrasp.py:805-836)
+ * after the closure: best-iterate update (:821-829, before the step, only when s > best_after),
+ * torch.optim.Adam for the five parameter groups (:782-796; the single-tensor / foreach update
+ * order: m.lerp_(g, 1-β1), v·β2 + (1-β2)·g·g, p += -lr/(1-β1^t) · m / (sqrt(v)/sqrt(1-β2^t) + eps)),
+ * then the clamps compliance ≥ comp_min and target ∈ [lb, ub] (:833-834).  No host sync. */
+typedef struct {
+  double lr[5];                        /* q, compliance, target, palm_pos, palm_ori; 0 = frozen */
+  double beta1, beta2, eps;
+  double comp_min;
+  double target_lb[CDX_MAX_TIPS * 3];
+  double target_ub[CDX_MAX_TIPS * 3];
+  int32_t clamp_target;
+  int32_t best_after;                  /* best-iterate tracking from iteration best_after+1 */
+} cdx_adam;
+
+typedef struct {                       /* all device pointers, candidate-major */
+  double *q, *comp, *target, *palm_pos, *palm_ori;                 /* parameters (in place) */
+  const double *g_q, *g_comp, *g_target, *g_palm_pos, *g_palm_ori; /* closure gradients */
+  double *m_q, *v_q, *m_comp, *v_comp, *m_target, *v_target;       /* Adam moments */
+  double *m_palm_pos, *v_palm_pos, *m_palm_ori, *v_palm_ori;
+  const double *total_loss, *total_margin;                         /* closure outputs */
+  double *opt_value, *opt_margin, *opt_q, *opt_comp, *opt_target, *opt_palm;  /* best iterate */
+} cdx_opt_buffers;
+
+/* iteration = 0-based loop index s; Adam's step count is s + 1. */
+int cdx_optimizer_step(const cdx_adam* cfg, const cdx_opt_buffers* buf, int64_t E, int32_t n_dofs,
+                       int32_t n_tips, int32_t iteration, cdx_stream_t stream);
+
 /* --------------------------------------------------------------- TorchSDF -------
  * Replaces torchsdf._C.unbatched_triangle_distance_forward_cuda / _backward_cuda
  * (thirdparty/TorchSDF/torchsdf/csrc/bindings.cpp:22-27, kernels

@@ -186,14 +186,15 @@ def test_closure_device_noise_is_deterministic_and_in_range():
     assert rel_err(outs[0], d["total_loss"]) < 1e-3  # different noise draw: only ~1e-5 effect
 
 
-def test_optimize_vs_reference():
+@pytest.mark.parametrize("fused", [True, False])
+def test_optimize_vs_reference(fused):
     d = golden("optimize_allegro_banana_e6.npz")
     iters = int(d["iters"])
     opt = _opt(str(d["hand"]), d["palm"], iters)
     g = _gpis(str(d["state"]))
     tape = [torch.from_numpy(n).to(DEV) for n in d["noise"]]
     out = opt.optimize(torch.from_numpy(d["q"]).to(DEV), torch.from_numpy(d["target"]).to(DEV),
-                       torch.from_numpy(d["comp"]).to(DEV), 1, g, verbose=False, noise_tape=tape)
+                       torch.from_numpy(d["comp"]).to(DEV), 1, g, verbose=False, noise_tape=tape, fused=fused)
     names = ["opt_q", "opt_comp", "opt_target", "opt_palm", "opt_margin"]
     for name, t in zip(names, out):
         assert rel_err(t.detach().cpu().numpy(), d[name]) < 1e-4, (name, rel_err(t.detach().cpu().numpy(), d[name]))
