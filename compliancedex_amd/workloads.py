@@ -82,3 +82,41 @@ def prob_inputs(ref_q, E, seed=0, spread=True, center=None):
         target = target + 0.01 * rng.standard_normal(target.shape)
     comp = np.tile(np.array([10.0, 10.0, 10.0, 20.0]), (E, 1))
     return q, comp, target, palm
+
+
+def box_gpis(side=0.065, n_surface=400, device="cuda", seed=0):
+    """Config 3's "box": the 0.065 m cube of assets/cube_visualization.urdf:7 (no stored state),
+    fitted with the same recipe as the synthetic banana: surface samples (y = 0, noise 0.005),
+    14 external points at ±0.15 (y = +0.15, noise 0.2), 50 internal points (y = −0.15, noise 0.1)."""
+    from .gpis import GPIS
+    rng = np.random.default_rng(seed)
+    h = side / 2
+    face = rng.integers(0, 6, n_surface)
+    uv = rng.uniform(-h, h, (n_surface, 2))
+    surf = np.zeros((n_surface, 3))
+    for i, (f, (u, v)) in enumerate(zip(face, uv)):
+        ax, sgn = f // 2, (1 if f % 2 else -1)
+        p = [u, v]
+        p.insert(ax, sgn * h)
+        surf[i] = p
+    bound = 0.15
+    ext = np.array([[-1, -1, -1], [1, -1, -1], [-1, 1, -1], [1, 1, -1], [-1, -1, 1], [1, -1, 1], [-1, 1, 1],
+                    [1, 1, 1], [-1, 0, 0], [0, -1, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1], [0, 0, -1]], float) * bound
+    internal = rng.uniform(-0.6 * h, 0.6 * h, (50, 3))
+    X1 = np.vstack([ext, surf, internal])
+    y = np.concatenate([np.full(14, bound), np.zeros(n_surface), np.full(50, -bound)])[:, None]
+    noise = np.concatenate([np.full(14, 0.2), np.full(n_surface, 0.005), np.full(50, 0.1)])
+    g = GPIS(0.08, 1.0)
+    g.fit(torch.from_numpy(X1).to(device), torch.from_numpy(y).to(device), noise=torch.from_numpy(noise).to(device))
+    g.bias = torch.tensor(1.0, dtype=torch.float64, device=device)
+    return g
+
+
+# config 3: one object per GPU; "realsense" (fit on the fly from an absent point cloud) is
+# stood in for by the stored dummy state, "box" by box_gpis (SURVEY §8d).
+CONFIG3_OBJECTS = ["banana", "mug", "mug2", "hammer", "lego", "coffeebottle", "box", "dummy"]
+
+
+def config3_gpis(rank, device="cuda"):
+    name = CONFIG3_OBJECTS[rank % len(CONFIG3_OBJECTS)]
+    return name, (box_gpis(device=device) if name == "box" else stored_gpis(name, device))

@@ -1,0 +1,155 @@
+"""Secondary measurements for BASELINE.json configs other than the headline (bench.py = config 2).
+
+  python tools/bench_configs.py [--only c1,c2opt,c3,c4]        (one GPU; prints one JSON line per case)
+
+c1     config 1: banana stored GPIS (N = 361), 64 candidates, Allegro and Leap — closure evals/s
+       (launch-bound at this size) next to the oracle on the host cores.
+c2opt  config 2 with the optimiser: closure + fused Adam/best-iterate/clamp step, iterations/s.
+c3     config 3 objects (stored states, box fit, dummy for realsense), 4096 candidates each — closure
+       evals/s per object on one GPU (one object per GPU on a node).
+c4     config 4 primitives: iiwa7_allegro FK (23 DOF, 4 tips) fwd+bwd for 16 384 candidates and the
+       TorchSDF kernel on the banana mesh (16 384 faces) for the 3 SDF calls of an SDF/Kin-mode iteration
+       (tips vs deflated mesh, tips vs mesh, targets vs mesh: 3 × 65 536 points) + SDF backward.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def timed(fn, reps, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps
+
+
+def make_opt(hand, palm, dev, iters=1):
+    from compliancedex_amd import ProbabilisticGraspOptimizer
+    from compliancedex_amd.urdf import load_robot
+    cfg = load_robot(hand)["config"]
+    return ProbabilisticGraspOptimizer(hand, cfg["ee_link_name"], cfg["ee_link_offset"], palm_offset=palm,
+                                       ref_q=cfg["ref_q"], optimize_target=True, optimize_palm=True, device=dev,
+                                       num_iters=iters), cfg
+
+
+def closure_case(hand, gpis, E, dev, center=None, reps=20):
+    from compliancedex_amd.workloads import prob_inputs
+    opt, cfg = make_opt(hand, np.zeros((E, 6)), dev)
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=5, spread=True, center=center)
+    opt.palm_offset = torch.from_numpy(palm).to(dev)
+    t = [torch.from_numpy(a).to(dev).requires_grad_(True) for a in (q, comp, target, palm[:, :3], palm[:, 3:])]
+
+    def step():
+        for x in t:
+            x.grad = None
+        opt.closure(*t, 1, gpis, E)
+    sec = timed(step, reps)
+    return sec, int((~torch.isfinite(opt.total_loss)).sum())
+
+
+def case_c1(dev):
+    from compliancedex_amd.urdf import load_robot
+    from compliancedex_amd.workloads import prob_inputs, stored_gpis
+    from oracle.cdx_oracle import OracleChain, OracleGPIS, OracleProblem, closure_with_grads
+    g = stored_gpis("banana", dev)
+    for hand in ("allegro", "leap"):
+        E = 64
+        sec, nan = closure_case(hand, g, E, dev, reps=50)
+        cfg = load_robot(hand)["config"]
+        prob = OracleProblem(OracleChain(load_robot(hand)["bodies"]), cfg["ee_link_name"], cfg["ee_link_offset"],
+                             cfg["ref_q"], OracleGPIS.from_npz(os.path.join(REPO, "compliancedex_amd", "data",
+                                                                           "gpis_states", "banana_state.npz")))
+        q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=5, spread=True)
+        kn = np.random.default_rng(1).random((3 * E, 3, 3))
+        ts = []
+        for _ in range(6):
+            t0 = time.perf_counter()
+            closure_with_grads(prob, q, comp, target, palm, kn)
+            ts.append(time.perf_counter() - t0)
+        cpu = float(np.median(ts[1:]))
+        print(json.dumps({"case": f"config1_{hand}", "E": E, "n_inducing": 361, "gpu_ms_per_closure": sec * 1e3,
+                          "gpu_evals_per_s": E / sec, "cpu_oracle_evals_per_s": E / cpu,
+                          "cpu_threads": torch.get_num_threads(), "nan_candidates": nan}), flush=True)
+
+
+def case_c2opt(dev):
+    from compliancedex_amd.workloads import prob_inputs, synthetic_banana_gpis
+    g = synthetic_banana_gpis(2000, dev)
+    E, iters = 4096, 30
+    opt, cfg = make_opt("allegro", np.zeros((E, 6)), dev, iters)
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=6, spread=True)
+    opt.palm_offset = torch.from_numpy(palm).to(dev)
+    args = [torch.from_numpy(a).to(dev) for a in (q, target, comp)]
+    for fused in (True, False):
+        sec = timed(lambda: opt.optimize(*args, 1, g, verbose=False, fused=fused), 2, warm=1)
+        print(json.dumps({"case": "config2_optimize", "fused_step": fused, "E": E, "iterations": iters,
+                          "ms_per_iteration": sec / iters * 1e3, "evals_per_s": E * iters / sec}), flush=True)
+
+
+def case_c3(dev):
+    from compliancedex_amd.workloads import CONFIG3_OBJECTS, config3_gpis
+    for r in range(len(CONFIG3_OBJECTS)):
+        name, g = config3_gpis(r, dev)
+        X1, y1 = g.X1.cpu().numpy(), g.y1.cpu().numpy().reshape(-1)
+        surf = X1[np.abs(y1 - y1.min() if name == "box" else y1 - np.median(y1)) < 1e-9]
+        surf = surf if len(surf) else X1
+        center = 0.5 * (surf.min(0) + surf.max(0))
+        sec, nan = closure_case("allegro", g, 4096, dev, center=center, reps=10)
+        print(json.dumps({"case": "config3_object", "object": name, "n_inducing": int(len(X1)), "E": 4096,
+                          "ms_per_closure": sec * 1e3, "evals_per_s": 4096 / sec, "nan_candidates": nan}), flush=True)
+
+
+def case_c4(dev):
+    from compliancedex_amd import DifferentiableRobotModel, compute_sdf
+    from compliancedex_amd.urdf import load_robot
+    E = 16384
+    m = DifferentiableRobotModel("iiwa7_allegro", device=dev)
+    links = load_robot("iiwa7_allegro")["config"]["ee_link_name"]
+    q = (0.3 * torch.randn(E, m._n_dofs, device=dev)).requires_grad_(True)
+    off = [[0.0, -0.04, 0.015]] * 4
+
+    def fk():
+        q.grad = None
+        pos, _ = m.compute_forward_kinematics(q, links, offsets=off)
+        pos.sum().backward()
+    fk_s = timed(fk, 20)
+    faces = torch.from_numpy(np.load(os.path.join(REPO, "compliancedex_amd", "data", "meshes",
+                                                  "banana_faces.npy"))).to(dev)
+    lo, hi = faces.reshape(-1, 3).min(0)[0], faces.reshape(-1, 3).max(0)[0]
+    pts = [(lo - 0.02 + (hi - lo + 0.04) * torch.rand(4 * E, 3, device=dev)).requires_grad_(True) for _ in range(3)]
+    deflated = faces * 0.9
+
+    def sdf():
+        outs = [compute_sdf(pts[0], deflated), compute_sdf(pts[1], faces), compute_sdf(pts[2], faces)]
+        sum(o[0].sum() for o in outs).backward()
+    sdf_s = timed(sdf, 5, warm=1)
+    pairs = 3 * 4 * E * faces.shape[0]
+    print(json.dumps({"case": "config4_primitives", "E": E, "fk_fwd_bwd_ms": fk_s * 1e3,
+                      "fk_evals_per_s": E / fk_s, "sdf_3calls_fwd_bwd_ms": sdf_s * 1e3,
+                      "sdf_point_face_pairs_per_s": pairs / sdf_s, "faces": int(faces.shape[0]),
+                      "sdf_evals_per_s": E / sdf_s}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="c1,c2opt,c3,c4")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    for c in args.only.split(","):
+        globals()[f"case_{c}"](dev)
+
+
+if __name__ == "__main__":
+    main()
