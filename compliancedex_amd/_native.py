@@ -14,6 +14,7 @@ LIB_DIR = os.path.join(_HERE, "lib")
 
 MAX_BODIES, MAX_TIPS, MAX_DOFS, MAX_LEVELS = 32, 8, 32, 4
 KERNELS = {"tps": 0, "rbf": 1, "joint": 2}
+NPAD_ALIGN = 256  # CDX_NPAD_ALIGN
 ERRORS = {-1: "invalid argument", -2: "unsupported GPIS kernel", -3: "chain exceeds descriptor capacity",
           -10: "HIP launch failed"}
 

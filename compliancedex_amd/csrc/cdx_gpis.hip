@@ -85,26 +85,40 @@ __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const
 }
 
 // ------------------------------------------------------------------ std (MFMA)
-// W = K*·E11⁻¹ tile of 128 queries × 128 output columns per 256-thread workgroup, K-step 16,
-// two LDS buffers (register-staged: the K* tile is computed, not loaded), one barrier per
-// K-step.  Waves form a 2×2 grid; each owns 64×64 = 4×4 v_mfma_f64_16x16x4_f64 tiles.
+// W = K*·E11⁻¹ tile of 128 queries × 256 output columns per 512-thread workgroup (one per CU),
+// K-step 16, two LDS buffers (register-staged: the K* tile is computed, not loaded), one barrier
+// per K-step.  Waves form a 2×4 grid; each owns 64×64 = 4×4 v_mfma_f64_16x16x4_f64 tiles.  The
+// 256-wide tile halves the per-output-column cost of generating K* on chip against the 128-wide
+// tile of 2×2 waves (-DCDX_STD_WN2): 2.41 vs 2.58 ms at M = 16 384, N = 2000.
 // Fragment maps (cdna_hip_programming.md §3, f64 form):
 //   A: lane l holds A[row l&15][k l>>4];  B: B[k l>>4][col l&15]
 //   C/D: reg r of lane l is D[row (l>>4) + 4r][col l&15]
 // LDS rows are padded to 144 doubles (row stride ≡ 32 dwords mod 64): the two half-waves of a
 // ds_read_b64 (rows k, k+1) land on disjoint banks.
-constexpr int ST_BM = 128, ST_BN = 128, ST_BK = 16, ST_LD = 144;
-constexpr int ST_TILE = ST_BK * ST_LD;                          // doubles per staged matrix
-constexpr int ST_SMEM = 4 * ST_TILE + ST_BM * 3;                // 2 buffers × (K*, E11⁻¹) + query tile
+constexpr int ST_BM = 128, ST_BK = 16, ST_LD = 144;
+constexpr int ST_TILE = ST_BK * ST_LD;                          // doubles per staged K* tile
+#if defined(CDX_STD_WN2) || defined(CDX_STD_MFMA4)
+constexpr int ST_WN = 2;                                        // waves along N (2 or 4)
+#else
+constexpr int ST_WN = 4;
+#endif
+static_assert(CDX_NPAD_ALIGN % (64 * ST_WN) == 0, "N_pad alignment must cover the tile width");
+constexpr int ST_BN = 64 * ST_WN;                               // output columns per workgroup
+constexpr int ST_THREADS = 128 * ST_WN;                         // 2 row-waves × ST_WN column-waves
+constexpr int ST_LDB = ST_BN + 16;                              // padded E11⁻¹ row (≡ 32 dwords mod 64)
+constexpr int ST_BTILE = ST_BK * ST_LDB;
+constexpr int ST_SMEM = 2 * (ST_TILE + ST_BTILE) + ST_BM * 3;   // 2 buffers × (K*, E11⁻¹) + query tile
 
 typedef double dbl2v __attribute__((ext_vector_type(2)));
 
+// v2: 128 queries × ST_BN output columns per workgroup of 2 × ST_WN waves, each wave owning
+// 64×64 = 4×4 v_mfma_f64_16x16x4_f64 tiles; K-step 16, two LDS buffers, one barrier per step.
 template <int KT>
-__global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
-                                                          double* __restrict__ partial, int64_t M_pad, int Mt,
-                                                          int Nt) {
+__global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X,
+                                                                        int64_t M, double* __restrict__ partial,
+                                                                        int64_t M_pad, int Mt, int Nt) {
   __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
-  double* xq = smem + 4 * ST_TILE;
+  double* xq = smem + 2 * (ST_TILE + ST_BTILE);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // XCD-aware order: blocks b and b+8 share an XCD (round-robin dispatch); give each XCD a
   // contiguous run of n-major tiles so its L2 serves the same E11⁻¹ column stripes.
@@ -117,37 +131,41 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const doub
   const int Np = g.N_pad;
   const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
 
+  // K* generation: thread → query row gm, GEN_PER k-columns starting at gk (wave-uniform)
+  constexpr int GEN_PER = ST_BM * ST_BK / ST_THREADS;  // 8 (2 col-waves) or 4 (4 col-waves)
   const int gm = tid & (ST_BM - 1);
-  const int gk = __builtin_amdgcn_readfirstlane((tid >> 7) * 8);  // wave-uniform k sub-block
+  const int gk = __builtin_amdgcn_readfirstlane((tid >> 7) * GEN_PER);
   double qx, qy, qz;
   {
     const int64_t m = min(m0 + gm, M - 1);  // pad rows replicate a valid query
     qx = X[3 * m]; qy = X[3 * m + 1]; qz = X[3 * m + 2];
     if (tid < ST_BM) { xq[3 * tid] = qx; xq[3 * tid + 1] = qy; xq[3 * tid + 2] = qz; }
   }
-  const int ar = tid >> 4, ac = (tid & 15) * 8;      // E11⁻¹ tile: row, 8 columns
-  const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
+  // E11⁻¹ tile: 16 rows × ST_BN columns, 8 consecutive doubles per thread
+  constexpr int A_TPR = ST_BN / 8;                      // threads per row
+  const int ar = tid / A_TPR, ac = (tid % A_TPR) * 8;
+  const int wr = (wave / ST_WN) * 64, wc = (wave % ST_WN) * 64;
 
   dbl2v av[4];
-  double kv[8];
+  double kv[GEN_PER];
   auto stage_load = [&](int kb) {
     const dbl2v* src = reinterpret_cast<const dbl2v*>(g.Ainv + (int64_t)(kb + ar) * Np + n0 + ac);
 #pragma unroll
     for (int i = 0; i < 4; ++i) av[i] = src[i];
     const double* x1 = g.X1 + 3 * (kb + gk);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < GEN_PER; ++i) {
       const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
       double kd;
       gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
     }
   };
   auto stage_write = [&](int buf) {
-    double* Kt = smem + buf * 2 * ST_TILE;
+    double* Kt = smem + buf * (ST_TILE + ST_BTILE);
     double* As = Kt + ST_TILE;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) Kt[(gk + i) * ST_LD + gm] = kv[i];
-    dbl2v* dst = reinterpret_cast<dbl2v*>(As + ar * ST_LD + ac);
+    for (int i = 0; i < GEN_PER; ++i) Kt[(gk + i) * ST_LD + gm] = kv[i];
+    dbl2v* dst = reinterpret_cast<dbl2v*>(As + ar * ST_LDB + ac);
 #pragma unroll
     for (int i = 0; i < 4; ++i) dst[i] = av[i];
   };
@@ -171,14 +189,15 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const doub
       for (int i = 0; i < 4; ++i) av[i] = src[i];
     }
     const double* x1 = g.X1 + 3 * (kn + gk);
-    const double* Kt = smem + (s & 1) * 2 * ST_TILE;
+    const double* Kt = smem + (s & 1) * (ST_TILE + ST_BTILE);
     const double* As = Kt + ST_TILE;
 #pragma unroll
     for (int kk = 0; kk < ST_BK; kk += 4) {
-      const int kr = (kk + (lane >> 4)) * ST_LD + (lane & 15);
+      const int kra = (kk + (lane >> 4)) * ST_LD + (lane & 15);
+      const int krb = (kk + (lane >> 4)) * ST_LDB + (lane & 15);
       double a[4], bb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { a[i] = Kt[kr + wr + 16 * i]; bb[i] = As[kr + wc + 16 * i]; }
+      for (int i = 0; i < 4; ++i) { a[i] = Kt[kra + wr + 16 * i]; bb[i] = As[krb + wc + 16 * i]; }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -189,9 +208,9 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const doub
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], bb[j], acc[i][j], 0, 0, 0);
 #endif
         }
-      // K* of the next stage, two elements per 16 MFMAs (overlaps the matrix pipe)
+      // K* of the next stage spread over the four 16-MFMA groups (overlaps the matrix pipe)
 #pragma unroll
-      for (int i = kk / 2; i < kk / 2 + 2; ++i) {
+      for (int i = kk * GEN_PER / ST_BK; i < (kk + 4) * GEN_PER / ST_BK; ++i) {
 #if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
         kv[i] = qx - x1[3 * i];
 #else
@@ -214,8 +233,8 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const doub
   }
 
   // Epilogue: per owned row, s = Σ_n W k and g = Σ_n W kd (x_m − x_n) over this wave's 64 columns,
-  // reduced over the 16 lanes of a row (xor-shuffles), then over the two column waves in LDS.
-  double* red = smem;  // [2][ST_BM][4], reuses the staging buffers (loop ended on a barrier)
+  // reduced over the 16 lanes of a row (xor-shuffles), then over the column waves in LDS.
+  double* red = smem;  // [ST_WN][ST_BM][4], reuses the staging buffers (loop ended on a barrier)
   double nxs[4][3];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -260,16 +279,17 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const doub
       for (int r = 0; r < 4; ++r) {
         const int row = wr + 16 * i + (lane >> 4) + 4 * r;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) red[((wave & 1) * ST_BM + row) * 4 + c] = ps[r][c];
+        for (int c = 0; c < 4; ++c) red[((wave % ST_WN) * ST_BM + row) * 4 + c] = ps[r][c];
       }
     }
   }
   __syncthreads();
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int idx = tid + 256 * h;  // 128 rows × 4 values
+  for (int idx = tid; idx < ST_BM * 4; idx += ST_THREADS) {
     const int row = idx >> 2, c = idx & 3;
-    partial[((int64_t)nt * M_pad + m0 + row) * 4 + c] = red[row * 4 + c] + red[(ST_BM + row) * 4 + c];
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < ST_WN; ++w) v += red[(w * ST_BM + row) * 4 + c];
+    partial[((int64_t)nt * M_pad + m0 + row) * 4 + c] = v;
   }
 }
 
@@ -284,11 +304,12 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel(cdx_gpis g, const doub
 //   A (K*):   lane l, group rg → row wr + 4·(l&15) + rg,            k = k0 + (l>>4)
 //   B (E11⁻¹): lane l, group cg → col wc + 16·(l&3) + cg,            k = k0 + (l>>4)
 //   D:        lane l, (rg, cg) → row wr + 4·(4·((l>>2)&3) + (l>>4)) + rg, col wc + 16·(l&3) + cg
+#if defined(CDX_STD_MFMA4)
 template <int KT>
 __global__ __launch_bounds__(256, 2) void gpis_std_kernel4(cdx_gpis g, const double* __restrict__ X, int64_t M,
                                                            double* __restrict__ partial, int64_t M_pad, int Mt,
                                                            int Nt) {
-  __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
+  __shared__ __attribute__((aligned(16))) double smem[4 * ST_TILE + ST_BM * 3];
   double* xq = smem + 4 * ST_TILE;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = Mt * Nt;
@@ -454,10 +475,14 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel4(cdx_gpis g, const dou
   }
 }
 
+#endif  // CDX_STD_MFMA4
+
 #if defined(CDX_STD_MFMA4)
 #define CDX_STD_KERNEL gpis_std_kernel4
+#define CDX_STD_THREADS 256
 #else
 #define CDX_STD_KERNEL gpis_std_kernel
+#define CDX_STD_THREADS ST_THREADS
 #endif
 
 template <int KT>
@@ -491,7 +516,7 @@ __global__ void mfma_f64_selftest_kernel(const double* A, const double* B, doubl
 }
 
 bool gpis_ok(const cdx_gpis* g) {
-  return g && g->X1 && g->alpha && g->N > 0 && g->N_pad >= g->N && g->N_pad % 128 == 0 && g->kernel >= 0 &&
+  return g && g->X1 && g->alpha && g->N > 0 && g->N_pad >= g->N && g->N_pad % CDX_NPAD_ALIGN == 0 && g->kernel >= 0 &&
          g->kernel <= 2;
 }
 
@@ -539,19 +564,19 @@ int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std_out,
   switch (g->kernel) {
     case CDX_KERNEL_TPS:
       cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_TPS>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
+      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_TPS>, grid, dim3(CDX_STD_THREADS), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
       cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_TPS>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;
     case CDX_KERNEL_RBF:
       cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_RBF>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
+      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_RBF>, grid, dim3(CDX_STD_THREADS), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
       cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_RBF>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;
     default:
       cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_JOINT>, grid, dim3(256), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
+      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_JOINT>, grid, dim3(CDX_STD_THREADS), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
       cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
       hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_JOINT>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
       break;

@@ -64,4 +64,69 @@ CDX_HD float point_face(F3 p, F3 v1, F3 v2, F3 v3, F3& clst, F3& nrm, int& sgn) 
 // not a plain argmin, so every implementation keeps this exact rule.
 #define CDX_SDF_REF_TILE 512
 
+// ---------------------------------------------------------------- culled path
+// Per-face quantities of point_face, computed once per face with the SAME IEEE operations
+// (FP contraction off), so face_dist2 below returns bit-for-bit the squared distance
+// point_face returns.  40 floats: one s_load_dwordx8 ×5 per face on the device.
+struct FaceRec {
+  F3 v1; int idx;  F3 v2; float den12;  F3 v3; float den23;  F3 e12; float den31;
+  F3 e23; float _p0;  F3 e31; float _p1;  F3 ne12; float _p2;  F3 ne23; float _p3;
+  F3 ne31; float _p4;  F3 un; float kappa;   // kappa = |e12||e31| / |n| (conditioning, 1/sinθ)
+};
+
+CDX_HD FaceRec face_rec(F3 v1, F3 v2, F3 v3, int idx) {
+  FaceRec r;
+  r.v1 = v1; r.v2 = v2; r.v3 = v3; r.idx = idx;
+  r.e12 = sub(v2, v1); r.e23 = sub(v3, v2); r.e31 = sub(v1, v3);
+  const F3 normal = crossf(sub(v1, v2), r.e31);
+  r.den12 = dotf(r.e12, r.e12); r.den23 = dotf(r.e23, r.e23); r.den31 = dotf(r.e31, r.e31);
+  r.ne12 = crossf(normal, r.e12); r.ne23 = crossf(normal, r.e23); r.ne31 = crossf(normal, r.e31);
+  const float nn = dotf(normal, normal);
+  r.un = scl(normal, rsqrt_cr(nn));
+  r.kappa = sqrtf(r.den12) * sqrtf(r.den31) / sqrtf(nn);
+  r._p0 = r._p1 = r._p2 = r._p3 = r._p4 = 0.f;
+  return r;
+}
+
+// A face whose point_face can produce NaN/inf for a finite point of magnitude ≤ 1e4
+// (zero-length edge, zero normal, non-finite or huge vertex).  Meshes holding one take
+// the exact tile-rule path, where NaN distances have the reference's semantics.
+CDX_HD bool face_may_nan(const FaceRec& r) {
+  const float lim = 1e4f;
+  const bool fin = fabsf(r.v1.x) <= lim && fabsf(r.v1.y) <= lim && fabsf(r.v1.z) <= lim &&
+                   fabsf(r.v2.x) <= lim && fabsf(r.v2.y) <= lim && fabsf(r.v2.z) <= lim &&
+                   fabsf(r.v3.x) <= lim && fabsf(r.v3.y) <= lim && fabsf(r.v3.z) <= lim;
+  const float nn = dotf(crossf(sub(r.v1, r.v2), r.e31), crossf(sub(r.v1, r.v2), r.e31));
+  return !(fin && r.den12 > 1e-20f && r.den23 > 1e-20f && r.den31 > 1e-20f && nn > 1e-30f);
+}
+
+// Squared distance of point_face from the precomputed record (same branch order).
+CDX_HD float face_dist2(F3 p, const FaceRec& r) {
+  const F3 w1 = sub(p, r.v1);
+  const float uab = dotf(w1, r.e12) / r.den12;
+  const F3 w3 = sub(p, r.v3);
+  const float uca = dotf(w3, r.e31) / r.den31;
+  const F3 w2 = sub(p, r.v2);
+  const float ubc = dotf(w2, r.e23) / r.den23;
+  F3 c;
+  if (uca > 1 && uab < 0) {
+    c = r.v1;
+  } else if (uab > 1 && ubc < 0) {
+    c = r.v2;
+  } else if (ubc > 1 && uca < 0) {
+    c = r.v3;
+  } else if (uab <= 1 && uab >= 0 && dotf(r.ne12, w1) <= 0) {
+    c = add(r.v1, scl(r.e12, uab));
+  } else if (ubc <= 1 && ubc >= 0 && dotf(r.ne23, w2) <= 0) {
+    c = add(r.v2, scl(r.e23, ubc));
+  } else if (uca <= 1 && uca >= 0 && dotf(r.ne31, w3) <= 0) {
+    c = add(r.v3, scl(r.e31, uca));
+  } else {
+    const float d = w1.x * r.un.x + w1.y * r.un.y + w1.z * r.un.z;
+    c = sub(p, scl(r.un, d));
+  }
+  const F3 dv = sub(p, c);
+  return dotf(dv, dv);
+}
+
 }  // namespace cdx

@@ -1,10 +1,28 @@
-// TorchSDF replacement for gfx950: brute-force point → triangle-mesh squared distance,
-// sign, unit (p − c) normal and closest point, plus the argmin face index.
+// TorchSDF replacement for gfx950: point → triangle-mesh squared distance, sign, unit (p − c)
+// normal and closest point, plus the argmin face index — bit-identical to the reference's
+// brute-force scan (unbatched_triangle_distance_cuda.cu:186-246) and to oracle/sdf_oracle.c.
 //
-// Mapping: one point per lane, 256-point workgroups; faces are streamed through LDS in
-// 512-face tiles (18 KiB) and every lane walks the tile with broadcast LDS reads.  The
-// 512-face tile is also the reference's tie/NaN semantics unit (cdx_sdf.h).
+// Culled path (meshes without NaN-capable faces, the normal case):
+//   1. bbox of points ∪ vertices; 30-bit Morton keys of face centroids and of points;
+//      hipCUB radix sort of both (faces once per call, points so a wave is spatially coherent).
+//   2. Face records (FaceRec: every per-face quantity of point_face, computed once) in Morton
+//      order, in 32-face chunks with a bounding sphere (centre, radius) and a conditioning
+//      margin alpha derived from the worst face's 1/sinθ.
+//   3. A workgroup = 64 sorted points × 4 waves; wave w owns chunks c ≡ w (mod 4).  Pass 1
+//      takes each lane's upper bound U over chunks (every face of a chunk is at most
+//      (|p−c|+r)(1+α)+β away, so the answer is ≤ U²); pass 2 evaluates a chunk only when some
+//      lane's lower bound L = |p−c|(1−α) − r(1+α) − β has L ≤ 0 or L² ≤ min(U², best).  β =
+//      1e-4·(|p|+|c|+r) and α ≥ 1e-4 exceed every rounding error of point_face by orders of
+//      magnitude, so a skipped face's computed distance is strictly greater
+//      than the winner's: it can neither win nor tie.  Faces are compared lexicographically on
+//      (distance, index), which, with no NaN distances, is exactly the reference's first-
+//      minimum tile rule.  The four waves' winners merge in LDS; the winner's closest point,
+//      normal and sign are recomputed with point_face (deterministic, so bit-identical).
+// Exact path: a mesh with a face that can produce NaN (face_may_nan) runs the brute-force
+// tile-rule kernel (512-face LDS tiles); a workgroup holding a non-finite or |p| > 1e4 point
+// runs the tile rule on its own wave.  The choice is made on the device (no host sync).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include "cdx_sdf.h"
 
@@ -14,12 +32,266 @@ namespace {
 
 constexpr int SDF_BLOCK = 256;
 constexpr int SDF_TILE = CDX_SDF_REF_TILE;
+constexpr int CHUNK = 32;           // faces per culling chunk
+constexpr float PT_LIM = 1e4f;      // |p| bound of the culled path (face_may_nan's premise)
 
-__global__ __launch_bounds__(SDF_BLOCK) void sdf_forward_kernel(const float* __restrict__ points, int64_t P,
-                                                                const float* __restrict__ faces, int64_t F,
-                                                                float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
-                                                                float* __restrict__ out_nrm, float* __restrict__ out_clst,
-                                                                int32_t* __restrict__ out_face) {
+struct Sphere { float cx, cy, cz, r, alpha, cnorm, _p0, _p1; };
+
+__device__ inline unsigned fkey(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float fkey_inv(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+__device__ inline unsigned spread10(unsigned v) {  // 10 bits → every third bit
+  v &= 1023u;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+// ws layout (unsigned words): [0..2] bbox min keys, [3..5] bbox max keys, [6] may-NaN flag
+__global__ void sdf_init_kernel(unsigned* ws) {
+  const int t = threadIdx.x;
+  if (t < 3) ws[t] = 0xFFFFFFFFu;
+  else if (t < 7) ws[t] = 0u;
+}
+
+__device__ inline void bb_acc(float x, float y, float z, unsigned (&lo)[3], unsigned (&hi)[3]) {
+  if (!(fabsf(x) <= PT_LIM && fabsf(y) <= PT_LIM && fabsf(z) <= PT_LIM)) return;
+  const unsigned k[3] = {fkey(x), fkey(y), fkey(z)};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) { lo[c] = min(lo[c], k[c]); hi[c] = max(hi[c], k[c]); }
+}
+
+__global__ __launch_bounds__(256) void sdf_bbox_kernel(const float* __restrict__ points, int64_t P,
+                                                       const float* __restrict__ faces, int64_t F, unsigned* ws) {
+  unsigned lo[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, hi[3] = {0u, 0u, 0u};
+  const int64_t n = P + 3 * F;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float* v = i < P ? points + 3 * i : faces + 3 * (i - P);
+    bb_acc(v[0], v[1], v[2], lo, hi);
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      lo[c] = min(lo[c], (unsigned)__shfl_xor((int)lo[c], o));
+      hi[c] = max(hi[c], (unsigned)__shfl_xor((int)hi[c], o));
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { atomicMin(ws + c, lo[c]); atomicMax(ws + 3 + c, hi[c]); }
+  }
+}
+
+__device__ inline unsigned morton(float x, float y, float z, const unsigned* ws) {
+  const float v[3] = {x, y, z};
+  unsigned m = 0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float lo = fkey_inv(ws[c]), hi = fkey_inv(ws[3 + c]);
+    const float ext = hi - lo;
+    float t = ext > 0.f ? (v[c] - lo) / ext : 0.f;
+    t = fminf(fmaxf(t, 0.f), 1.f);  // NaN → 0
+    m |= spread10((unsigned)(t * 1023.f)) << c;
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(256) void sdf_keys_kernel(const float* __restrict__ points, int64_t P,
+                                                       const float* __restrict__ faces, int64_t F,
+                                                       const unsigned* __restrict__ ws, unsigned* fkeys, int* fvals,
+                                                       unsigned* pkeys, int* pvals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < F) {
+    const float* v = faces + 9 * i;
+    const float third = 1.f / 3.f;
+    fkeys[i] = morton((v[0] + v[3] + v[6]) * third, (v[1] + v[4] + v[7]) * third, (v[2] + v[5] + v[8]) * third, ws);
+    fvals[i] = (int)i;
+  } else if (i < F + P) {
+    const int64_t j = i - F;
+    pkeys[j] = morton(points[3 * j], points[3 * j + 1], points[3 * j + 2], ws);
+    pvals[j] = (int)j;
+  }
+}
+
+// One thread per sorted face slot; a 32-lane half-wave builds one chunk's sphere.
+__global__ __launch_bounds__(256) void sdf_chunk_kernel(const float* __restrict__ faces, int64_t F,
+                                                        const int* __restrict__ order, cdx::FaceRec* __restrict__ rec,
+                                                        Sphere* __restrict__ sph, unsigned* ws) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = j < F;
+  cdx::FaceRec r;
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  float kappa = 0.f;
+  bool bad = false;
+  if (live) {
+    const int f = order[j];
+    const float* v = faces + 9 * (int64_t)f;
+    r = cdx::face_rec(cdx::f3(v[0], v[1], v[2]), cdx::f3(v[3], v[4], v[5]), cdx::f3(v[6], v[7], v[8]), f);
+    rec[j] = r;
+    bad = cdx::face_may_nan(r);
+    kappa = r.kappa;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      lo[c] = fminf(fminf(v[c], v[3 + c]), v[6 + c]);
+      hi[c] = fmaxf(fmaxf(v[c], v[3 + c]), v[6 + c]);
+    }
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(ws + 6, 1u);
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) {
+      lo[c] = fminf(lo[c], __shfl_xor(lo[c], o));
+      hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o));
+    }
+  const float cx = 0.5f * (lo[0] + hi[0]), cy = 0.5f * (lo[1] + hi[1]), cz = 0.5f * (lo[2] + hi[2]);
+  float rad = 0.f;
+  if (live) {
+    const cdx::F3 c = cdx::f3(cx, cy, cz);
+    rad = fmaxf(fmaxf(sqrtf(cdx::dotf(cdx::sub(r.v1, c), cdx::sub(r.v1, c))),
+                      sqrtf(cdx::dotf(cdx::sub(r.v2, c), cdx::sub(r.v2, c)))),
+                sqrtf(cdx::dotf(cdx::sub(r.v3, c), cdx::sub(r.v3, c))));
+  }
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) {
+    rad = fmaxf(rad, __shfl_xor(rad, o));
+    kappa = fmaxf(kappa, __shfl_xor(kappa, o));
+  }
+  if ((j & (CHUNK - 1)) == 0 && live) {
+    Sphere s;
+    s.cx = cx; s.cy = cy; s.cz = cz;
+    s.r = rad * (1.f + 1e-5f);
+    // normal-direction error of point_face's plane projection ≲ 10ε·κ; 1e-5·κ ≈ 170ε·κ.
+    // alpha ≥ 1 (or a NaN kappa) makes every lower bound ≤ 0: the chunk is always evaluated.
+    const float a = 1e-4f + 1e-5f * kappa;
+    s.alpha = a < 1.f ? a : 1.f;
+    s.cnorm = sqrtf(cx * cx + cy * cy + cz * cz);
+    s._p0 = s._p1 = 0.f;
+    sph[j / CHUNK] = s;
+  }
+}
+
+// Reference tile rule for one point over all faces (uniform face loads); writes outputs.
+__device__ void exact_point(cdx::F3 p, const float* __restrict__ faces, int64_t F, int64_t pi, float* out_dist,
+                            int32_t* out_sign, float* out_nrm, float* out_clst, int32_t* out_face, bool write) {
+  float best = 0.f;
+  int bsign = 0, bface = -1;
+  cdx::F3 bn = cdx::f3(0.f, 0.f, 0.f), bc = bn;
+  for (int64_t f0 = 0; f0 < F; f0 += SDF_TILE) {
+    const int nt = (int)min((int64_t)SDF_TILE, F - f0);
+    float tbest = 0.f;
+    int tsign = 0, tface = -1;
+    cdx::F3 tn = cdx::f3(0.f, 0.f, 0.f), tc = tn;
+    for (int s = 0; s < nt; ++s) {
+      const float* v = faces + 9 * (f0 + s);
+      cdx::F3 c, n;
+      int sg;
+      const float d = cdx::point_face(p, cdx::f3(v[0], v[1], v[2]), cdx::f3(v[3], v[4], v[5]),
+                                      cdx::f3(v[6], v[7], v[8]), c, n, sg);
+      if (s == 0 || tbest > d) { tbest = d; tsign = sg; tn = n; tc = c; tface = (int)(f0 + s); }
+    }
+    if (f0 == 0 || best > tbest) { best = tbest; bsign = tsign; bn = tn; bc = tc; bface = tface; }
+  }
+  if (!write) return;
+  out_dist[pi] = best;
+  out_sign[pi] = bsign;
+  out_nrm[3 * pi] = bn.x; out_nrm[3 * pi + 1] = bn.y; out_nrm[3 * pi + 2] = bn.z;
+  out_clst[3 * pi] = bc.x; out_clst[3 * pi + 1] = bc.y; out_clst[3 * pi + 2] = bc.z;
+  if (out_face) out_face[pi] = bface;
+}
+
+__global__ __launch_bounds__(SDF_BLOCK) void sdf_culled_kernel(
+    const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
+    int64_t F, const cdx::FaceRec* __restrict__ rec, const Sphere* __restrict__ sph, int C,
+    const unsigned* __restrict__ ws, float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
+    float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face) {
+  if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
+  __shared__ float s_val[4][64];
+  __shared__ int s_idx[4][64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t j = (int64_t)blockIdx.x * 64 + lane;
+  const bool live = j < P;
+  const int64_t pi = porder[live ? j : P - 1];  // dead lanes shadow a live point
+  const cdx::F3 p = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
+  const bool ok = fabsf(p.x) <= PT_LIM && fabsf(p.y) <= PT_LIM && fabsf(p.z) <= PT_LIM;
+  if (!__all(ok)) {  // same points in every wave: uniform over the workgroup
+    if (w == 0) exact_point(p, faces, F, pi, out_dist, out_sign, out_nrm, out_clst, out_face, live);
+    return;
+  }
+  const float pnorm = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+
+  // pass 1: upper bound on the answer
+  float ub = INFINITY;
+  for (int c = w; c < C; c += 4) {
+    const Sphere s = sph[c];
+    const float dx = p.x - s.cx, dy = p.y - s.cy, dz = p.z - s.cz;
+    const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
+    const float u = (dist + s.r) * (1.f + s.alpha) + 1e-4f * (pnorm + s.cnorm + s.r);
+    ub = fminf(ub, u);
+  }
+  s_val[w][lane] = ub;
+  __syncthreads();
+  ub = fminf(fminf(s_val[0][lane], s_val[1][lane]), fminf(s_val[2][lane], s_val[3][lane]));
+  const float T = ub * ub;
+  __syncthreads();
+
+  // pass 2: exact distances over the chunks some lane cannot rule out
+  float best = INFINITY;
+  int bidx = 0x7fffffff;
+  for (int c = w; c < C; c += 4) {
+    const Sphere s = sph[c];
+    const float dx = p.x - s.cx, dy = p.y - s.cy, dz = p.z - s.cz;
+    const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
+    const float L = dist * (1.f - s.alpha) - s.r * (1.f + s.alpha) - 1e-4f * (pnorm + s.cnorm + s.r);
+    const bool need = !(L > 0.f && L * L > fminf(T, best));
+    if (!__any(need)) continue;
+    const int f0 = c * CHUNK;
+    const int nf = (int)min((int64_t)CHUNK, F - f0);
+    for (int k = 0; k < nf; ++k) {
+      const cdx::FaceRec& r = rec[f0 + k];
+      const float d = cdx::face_dist2(p, r);
+      if (d < best || (d == best && r.idx < bidx)) { best = d; bidx = r.idx; }
+    }
+  }
+  s_val[w][lane] = best;
+  s_idx[w][lane] = bidx;
+  __syncthreads();
+  if (w != 0 || !live) return;
+#pragma unroll
+  for (int v = 1; v < 4; ++v) {
+    const float d = s_val[v][lane];
+    const int i = s_idx[v][lane];
+    if (d < best || (d == best && i < bidx)) { best = d; bidx = i; }
+  }
+  const float* v = faces + 9 * (int64_t)bidx;
+  cdx::F3 c, n;
+  int sg;
+  const float d = cdx::point_face(p, cdx::f3(v[0], v[1], v[2]), cdx::f3(v[3], v[4], v[5]),
+                                  cdx::f3(v[6], v[7], v[8]), c, n, sg);
+  out_dist[pi] = d;
+  out_sign[pi] = sg;
+  out_nrm[3 * pi] = n.x; out_nrm[3 * pi + 1] = n.y; out_nrm[3 * pi + 2] = n.z;
+  out_clst[3 * pi] = c.x; out_clst[3 * pi + 1] = c.y; out_clst[3 * pi + 2] = c.z;
+  if (out_face) out_face[pi] = bidx;
+}
+
+// Brute force with the reference's tile rule: one point per lane, faces streamed through LDS
+// in 512-face tiles.  Runs when ws (if given) flags a NaN-capable face.
+__global__ __launch_bounds__(SDF_BLOCK) void sdf_exact_kernel(const float* __restrict__ points, int64_t P,
+                                                              const float* __restrict__ faces, int64_t F,
+                                                              const unsigned* __restrict__ ws,
+                                                              float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
+                                                              float* __restrict__ out_nrm, float* __restrict__ out_clst,
+                                                              int32_t* __restrict__ out_face) {
+  if (ws && !ws[6]) return;
   __shared__ float sf[SDF_TILE * 9];
   const int64_t pi = (int64_t)blockIdx.x * SDF_BLOCK + threadIdx.x;
   const bool live = pi < P;
@@ -63,6 +335,16 @@ __global__ __launch_bounds__(256) void sdf_backward_kernel(const float* __restri
   for (int c = 0; c < 3; ++c) gp[3 * i + c] = (points[3 * i + c] - clst[3 * i + c]) * g;
 }
 
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int sdf_mode() {  // CDX_SDF_MODE=exact forces the brute-force kernel (benchmarks, A/B tests)
+  static const int m = [] {
+    const char* e = getenv("CDX_SDF_MODE");
+    return (e && e[0] == 'e') ? 1 : 0;
+  }();
+  return m;
+}
+
 }  // namespace
 
 extern "C" {
@@ -72,9 +354,62 @@ int cdx_sdf_forward(const float* points, int64_t P, const float* faces, int64_t 
   if (P < 0 || F < 0) return CDX_EINVAL;
   if (P == 0) return CDX_OK;
   if (F == 0 || !points || !faces || !sqdist || !sign || !normals || !clst) return CDX_EINVAL;
-  hipLaunchKernelGGL(sdf_forward_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0,
-                     reinterpret_cast<hipStream_t>(stream), points, P, faces, F, sqdist, sign, normals, clst, face_idx);
-  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+  if (P > INT32_MAX || F > INT32_MAX / 9) return CDX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const unsigned pblocks = (unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK);
+  if (sdf_mode() == 1) {
+    hipLaunchKernelGGL(sdf_exact_kernel, dim3(pblocks), dim3(SDF_BLOCK), 0, s, points, P, faces, F,
+                       (const unsigned*)nullptr, sqdist, sign, normals, clst, face_idx);
+    return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+  }
+  const int n = (int)F, m = (int)P;
+  const int C = (n + CHUNK - 1) / CHUNK;
+  size_t tf = 0, tp = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tf, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
+                                         (int*)nullptr, n, 0, 30, s) != hipSuccess ||
+      hipcub::DeviceRadixSort::SortPairs(nullptr, tp, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
+                                         (int*)nullptr, m, 0, 30, s) != hipSuccess)
+    return CDX_ELAUNCH;
+  // workspace: ws words | face keys/vals ×2 | point keys/vals ×2 | records | spheres | cub temp
+  size_t off = 0;
+  const size_t o_ws = off; off = align256(off + 8 * sizeof(unsigned));
+  const size_t o_fk = off; off = align256(off + 2 * (size_t)n * sizeof(unsigned));
+  const size_t o_fv = off; off = align256(off + 2 * (size_t)n * sizeof(int));
+  const size_t o_pk = off; off = align256(off + 2 * (size_t)m * sizeof(unsigned));
+  const size_t o_pv = off; off = align256(off + 2 * (size_t)m * sizeof(int));
+  const size_t o_rec = off; off = align256(off + (size_t)C * CHUNK * sizeof(cdx::FaceRec));
+  const size_t o_sph = off; off = align256(off + (size_t)C * sizeof(Sphere));
+  const size_t o_tmp = off; off = align256(off + (tf > tp ? tf : tp));
+  char* base = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&base), off, s) != hipSuccess) return CDX_ELAUNCH;
+  unsigned* ws = reinterpret_cast<unsigned*>(base + o_ws);
+  unsigned* fk = reinterpret_cast<unsigned*>(base + o_fk);
+  int* fv = reinterpret_cast<int*>(base + o_fv);
+  unsigned* pk = reinterpret_cast<unsigned*>(base + o_pk);
+  int* pv = reinterpret_cast<int*>(base + o_pv);
+  cdx::FaceRec* rec = reinterpret_cast<cdx::FaceRec*>(base + o_rec);
+  Sphere* sph = reinterpret_cast<Sphere*>(base + o_sph);
+  void* tmp = base + o_tmp;
+
+  hipLaunchKernelGGL(sdf_init_kernel, dim3(1), dim3(64), 0, s, ws);
+  const int64_t nbb = P + 3 * F;
+  const unsigned bbb = (unsigned)std::min<int64_t>((nbb + 255) / 256, 1024);
+  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(bbb), dim3(256), 0, s, points, P, faces, F, ws);
+  hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((F + P + 255) / 256)), dim3(256), 0, s, points, P, faces, F,
+                     (const unsigned*)ws, fk, fv, pk, pv);
+  size_t t1 = tf, t2 = tp;
+  bool ok = hipcub::DeviceRadixSort::SortPairs(tmp, t1, fk, fk + n, fv, fv + n, n, 0, 30, s) == hipSuccess;
+  ok = ok && hipcub::DeviceRadixSort::SortPairs(tmp, t2, pk, pk + m, pv, pv + m, m, 0, 30, s) == hipSuccess;
+  hipLaunchKernelGGL(sdf_chunk_kernel, dim3((unsigned)((C * CHUNK + 255) / 256)), dim3(256), 0, s, faces, F,
+                     (const int*)(fv + n), rec, sph, ws);
+  hipLaunchKernelGGL(sdf_culled_kernel, dim3((unsigned)((P + 63) / 64)), dim3(SDF_BLOCK), 0, s, points, P,
+                     (const int*)(pv + m), faces, F, (const cdx::FaceRec*)rec, (const Sphere*)sph, C,
+                     (const unsigned*)ws, sqdist, sign, normals, clst, face_idx);
+  hipLaunchKernelGGL(sdf_exact_kernel, dim3(pblocks), dim3(SDF_BLOCK), 0, s, points, P, faces, F,
+                     (const unsigned*)ws, sqdist, sign, normals, clst, face_idx);
+  ok = ok && hipGetLastError() == hipSuccess;
+  ok = (hipFreeAsync(base, s) == hipSuccess) && ok;
+  return ok ? CDX_OK : CDX_ELAUNCH;
 }
 
 int cdx_sdf_backward(const float* grad_dist, const float* points, const float* clst, int64_t P, float* grad_points,

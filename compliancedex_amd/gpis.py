@@ -33,7 +33,7 @@ class _State:
     def __init__(self, X1, y1, E11, R, bias, kernel, sigma):
         dev = X1.device
         n = X1.shape[0]
-        Np = (n + 127) // 128 * 128
+        Np = (n + N.NPAD_ALIGN - 1) // N.NPAD_ALIGN * N.NPAD_ALIGN
         E11 = E11.to(dev, torch.float64)
         A = torch.linalg.inv(E11)
         alpha = (A.T @ y1.to(dev, torch.float64).reshape(-1, 1)).reshape(-1)  # E11⁻ᵀ y1 (gpis.py:53-55)

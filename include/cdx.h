@@ -35,19 +35,20 @@ enum {
 /* ------------------------------------------------------------------ GPIS --------
  * Replaces the GPIS object of gpis.py:4-168 (pred :43-59, compute_normal :63-87).
  * State precomputed once per object (gpis.py:33-40 fit / :162-168 load):
- *   X1     [N_pad*3]  inducing points (N_pad: multiple of 128), AoS xyz, rows >= N padded with any finite point
+ *   X1     [N_pad*3]  inducing points (N_pad: multiple of CDX_NPAD_ALIGN), AoS xyz, rows >= N padded with any finite point
  *   alpha  [N_pad]    E11^{-1} y1 (zero-padded); mean = Σ alpha_j k(x, x_j) + bias
  *   Ainv   [N_pad*N_pad] E11^{-1}, symmetric, zero-padded; only used by the std path
  * kernel: 0 = thin-plate spline 2r³-3Rr²+R³ (gpis.py:21-26, the default),
  *         1 = RBF exp(-r²/2σ²) (:16-19), 2 = 0.3·RBF + 0.7·TPS (:28-29). */
 enum { CDX_KERNEL_TPS = 0, CDX_KERNEL_RBF = 1, CDX_KERNEL_JOINT = 2 };
+#define CDX_NPAD_ALIGN 256   /* column width of one std-GEMM workgroup tile */
 
 typedef struct {
   const double* X1;
   const double* alpha;
   const double* Ainv;
   int32_t N;
-  int32_t N_pad;      /* multiple of 128, >= N */
+  int32_t N_pad;      /* multiple of CDX_NPAD_ALIGN (256), >= N */
   int32_t kernel;
   int32_t _pad;
   double R;           /* TPS radius = max pairwise training distance */

@@ -227,6 +227,49 @@ def test_sdf_vs_oracle_bitwise(mesh):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+def test_sdf_culled_near_surface_bitwise():
+    """The culled path (Morton-sorted chunks with sphere bounds) against the brute-force C
+    oracle where culling margins matter most: points within 1e-6..1e-3 of the surface, on
+    vertices and on edges, where many faces tie or nearly tie."""
+    from compliancedex_amd import compute_sdf_with_faces
+    from tests import _sdf_oracle
+    faces = np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))
+    rng = np.random.default_rng(11)
+    n = 4000
+    f = rng.integers(0, len(faces), n)
+    bary = rng.dirichlet([1, 1, 1], n)
+    on = np.einsum("nk,nkc->nc", bary, faces[f].astype(np.float64))
+    nrm = np.cross(faces[f, 1] - faces[f, 0], faces[f, 2] - faces[f, 0]).astype(np.float64)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    off = 10.0 ** rng.uniform(-6, -3, n) * rng.choice([-1, 1], n)
+    pts = (on + off[:, None] * nrm).astype(np.float32)
+    pts[:500] = faces[f[:500], rng.integers(0, 3, 500)]                        # on vertices
+    pts[500:1000] = 0.5 * (faces[f[500:1000], 0] + faces[f[500:1000], 1])     # on edges
+    dist, sign, nrmo, clst, face = [t.cpu().numpy() for t in compute_sdf_with_faces(
+        torch.from_numpy(pts).to(DEV), torch.from_numpy(faces).to(DEV))]
+    o = _sdf_oracle.forward(pts, faces)
+    assert np.array_equal(face, o[4]) and np.array_equal(sign, o[1])
+    for a, b in zip((dist, nrmo, clst), (o[0], o[2], o[3])):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_sdf_nonfinite_points_take_exact_path():
+    """A workgroup holding a NaN / inf / |p| > 1e4 point runs the reference tile rule."""
+    from compliancedex_amd import compute_sdf_with_faces
+    from tests import _sdf_oracle
+    faces = np.load(os.path.join(DATA, "meshes", "sphere42_faces.npy"))
+    rng = np.random.default_rng(3)
+    pts = (rng.random((1000, 3)) * 3 - 1.5).astype(np.float32)
+    pts[5] = np.nan
+    pts[300] = [np.inf, 0, 0]
+    pts[700] = [2e4, 1, 1]
+    got = [t.cpu().numpy() for t in compute_sdf_with_faces(torch.from_numpy(pts).to(DEV),
+                                                           torch.from_numpy(faces).to(DEV))]
+    o = _sdf_oracle.forward(pts, faces)
+    for a, b in zip(got, o):
+        assert _bitwise_equal_nan_aware(a, b)
+
+
 def test_sdf_degenerate_and_autograd():
     from compliancedex_amd import compute_sdf, compute_sdf_with_faces
     from tests import _sdf_oracle

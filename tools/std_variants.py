@@ -10,13 +10,10 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-VARIANTS = {"mfma16": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),
-            "mfma4": ("CDX_FAST_SQRT", "CDX_STD_MFMA4"),
-            "mfma4_sched": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_STD_MFMA4"),
-            # timing-only diagnostics (wrong outputs)
-            "mfma4_nogen": ("CDX_FAST_SQRT", "CDX_STD_MFMA4", "CDX_DIAG_NOGEN"),
-            "mfma4_nomfma": ("CDX_FAST_SQRT", "CDX_STD_MFMA4", "CDX_DIAG_NOMFMA"),
-            "mfma4_nogen_nomfma": ("CDX_FAST_SQRT", "CDX_STD_MFMA4", "CDX_DIAG_NOGEN", "CDX_DIAG_NOMFMA")}
+VARIANTS = {"wn4": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),
+            "wn2": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_STD_WN2"),
+            "wn4_nosched": ("CDX_FAST_SQRT",),
+            "mfma4": ("CDX_FAST_SQRT", "CDX_STD_MFMA4")}
 
 
 def build():
