@@ -67,6 +67,9 @@ _SIGS = {
     "cdx_gpis_mean": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P, _P]),
     "cdx_gpis_std_workspace": (C.c_size_t, [C.POINTER(CdxGpis), _I64]),
     "cdx_gpis_std": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P, _P]),
+    "cdx_gpis_fit": (C.c_int, [_P, C.c_int32, _P, C.c_int32, C.c_double, _P, _P, _P]),
+    "cdx_gpis_factor_workspace": (C.c_size_t, [C.c_int32]),
+    "cdx_gpis_factor": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P]),
     "cdx_fk_forward": (C.c_int, [C.POINTER(CdxChain), _P, _I64, _P, _P, _P]),
     "cdx_fk_backward": (C.c_int, [C.POINTER(CdxChain), _P, _I64, _P, _P, _P]),
     "cdx_closure_workspace": (C.c_size_t, [C.POINTER(CdxProblem), _I64]),

@@ -1,0 +1,311 @@
+// On-device GPIS fit and state factorisation, f64 throughout.
+//
+//   cdx_gpis_fit     GPIS.fit (gpis.py:33-40): R = max pairwise distance of X1 (TPS / joint
+//                    kernels), E11 = K(X1, X1) + diag(noise²).
+//   cdx_gpis_factor  the query state: E11⁻¹ (zero-padded to N_pad) and α = E11⁻¹ y1, which
+//                    the reference re-derives per query with torch.linalg.solve (gpis.py:53-55).
+//
+// Factorisation on the N_pad × N_pad matrix M = [E11 0; 0 I] in 64 × 64 blocks (nb = N_pad/64):
+//   1. blocked right-looking Cholesky M = L Lᵀ — per block column k: diag (one workgroup:
+//      unblocked Cholesky of M_kk in LDS + its triangular inverse X_kk = L_kk⁻¹), trsm
+//      (L_ik = M_ik X_kkᵀ), update (M_ij −= L_ik L_jkᵀ for k < j ≤ i);
+//   2. X = L⁻¹ by block rows: X_ik = −X_ii Σ_{j=k}^{i−1} L_ij X_jk (block row i depends on rows < i);
+//   3. E11⁻¹ = Xᵀ X (lower block pairs, mirrored, padding zeroed), α = E11⁻¹ y1.
+// ≈ N³ flops (N = 2000: 8 GFLOP) in ≈ 4·nb launches; a fit happens once per object.  A non-
+// positive pivot stores its 1-based row in *info (LAPACK potrf convention) and the result is
+// garbage; the host checks info once.
+#include <hip/hip_runtime.h>
+
+#include "cdx.h"
+#include "cdx_gpis.h"
+
+namespace {
+
+constexpr int NB = 64;        // block size
+constexpr int LDT = NB + 1;   // LDS row pitch (odd: column walks hit distinct banks)
+
+// ------------------------------------------------------------------ fit
+__global__ __launch_bounds__(256) void fit_R_kernel(const double* __restrict__ X1, int N,
+                                                    unsigned long long* __restrict__ Rbits) {
+  const int i = blockIdx.y;
+  double m = 0.0;
+  const double xi = X1[3 * i], yi = X1[3 * i + 1], zi = X1[3 * i + 2];
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x) {
+    const double dx = xi - X1[3 * j], dy = yi - X1[3 * j + 1], dz = zi - X1[3 * j + 2];
+    m = fmax(m, sqrt(dx * dx + dy * dy + dz * dz));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+  // non-negative doubles order like their bit patterns
+  if ((threadIdx.x & 63) == 0) atomicMax(Rbits, (unsigned long long)__double_as_longlong(m));
+}
+
+template <int KT>
+__global__ __launch_bounds__(256) void fit_E11_kernel(const double* __restrict__ X1, int N,
+                                                      const double* __restrict__ noise, double sigma,
+                                                      const double* __restrict__ Rp, double* __restrict__ E11) {
+  const int i = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= N) return;
+  const double R = KT == CDX_KERNEL_RBF ? 0.0 : *Rp;
+  const double dx = X1[3 * i] - X1[3 * j], dy = X1[3 * i + 1] - X1[3 * j + 1], dz = X1[3 * i + 2] - X1[3 * j + 2];
+  double k, kd;
+  cdx::gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, 1.0 / (sigma * sigma), k, kd);
+  if (i == j && noise) k += noise[i] * noise[i];
+  E11[(int64_t)i * N + j] = k;
+}
+
+// ------------------------------------------------------------------ block helpers
+// 64×64 tile of a row-major matrix into LDS, optionally transposed.
+__device__ inline void load_tile(double* __restrict__ T, const double* __restrict__ A, int64_t ld, bool trans) {
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+    const int r = e / NB, c = e % NB;
+    const double v = A[r * ld + c];
+    if (trans) T[c * LDT + r] = v; else T[r * LDT + c] = v;
+  }
+}
+
+// acc[a][b] += Σ_t P[r0+a][t] · Q[t][c0+b], thread owns rows r0..r0+3, cols c0..c0+3.
+__device__ inline void tile_mac(double (&acc)[4][4], const double* P, const double* Q, int r0, int c0) {
+  for (int t = 0; t < NB; ++t) {
+    double p[4], q[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) p[a] = P[(r0 + a) * LDT + t];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) q[b] = Q[t * LDT + c0 + b];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = fma(p[a], q[b], acc[a][b]);
+  }
+}
+
+__device__ inline void owned(int& r0, int& c0) {
+  r0 = (threadIdx.x >> 4) * 4;
+  c0 = (threadIdx.x & 15) * 4;
+}
+
+// ------------------------------------------------------------------ factorisation
+__global__ __launch_bounds__(256) void pad_kernel(const double* __restrict__ E11, int N, int Np,
+                                                  double* __restrict__ M, double* __restrict__ X) {
+  const int i = blockIdx.y;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Np; j += gridDim.x * blockDim.x) {
+    double v = (i < N && j < N) ? E11[(int64_t)i * N + j] : (i == j ? 1.0 : 0.0);
+    M[(int64_t)i * Np + j] = v;
+    X[(int64_t)i * Np + j] = 0.0;
+  }
+}
+
+// Cholesky of the diagonal block k in LDS; writes L_kk (lower, upper zeroed) and X_kk = L_kk⁻¹.
+__global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ M, double* __restrict__ X, int Np, int k,
+                                                        int* __restrict__ info) {
+  __shared__ double T[NB * LDT];
+  __shared__ double V[NB * LDT];
+  double* Mk = M + (int64_t)k * NB * Np + k * NB;
+  load_tile(T, Mk, Np, false);
+  __syncthreads();
+  for (int j = 0; j < NB; ++j) {
+    const double d = T[j * LDT + j];
+    if (threadIdx.x == 0 && !(d > 0.0)) atomicCAS(info, 0, k * NB + j + 1);
+    const double s = sqrt(d);
+    __syncthreads();
+    for (int r = j + 1 + threadIdx.x; r < NB; r += blockDim.x) T[r * LDT + j] /= s;
+    __syncthreads();
+    if (threadIdx.x == 0) T[j * LDT + j] = s;
+    // trailing update of the lower triangle: T[r][c] −= T[r][j]·T[c][j], j < c ≤ r
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+      const int r = e / NB, c = e % NB;
+      if (c > j && c <= r) T[r * LDT + c] -= T[r * LDT + j] * T[c * LDT + j];
+    }
+    __syncthreads();
+  }
+  // triangular inverse: column c of V solves L v = e_c (forward substitution)
+  if (threadIdx.x < NB) {
+    const int c = threadIdx.x;
+    for (int r = 0; r < NB; ++r) {
+      if (r < c) { V[r * LDT + c] = 0.0; continue; }
+      double acc = r == c ? 1.0 : 0.0;
+      for (int t = c; t < r; ++t) acc -= T[r * LDT + t] * V[t * LDT + c];
+      V[r * LDT + c] = acc / T[r * LDT + r];
+    }
+  }
+  __syncthreads();
+  double* Xk = X + (int64_t)k * NB * Np + k * NB;
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+    const int r = e / NB, c = e % NB;
+    Mk[(int64_t)r * Np + c] = c <= r ? T[r * LDT + c] : 0.0;
+    Xk[(int64_t)r * Np + c] = V[r * LDT + c];
+  }
+}
+
+// L_ik = M_ik · X_kkᵀ for block rows i > k (one workgroup each).
+__global__ __launch_bounds__(256) void chol_trsm_kernel(double* __restrict__ M, const double* __restrict__ X, int Np,
+                                                        int k) {
+  __shared__ double P[NB * LDT];
+  __shared__ double Q[NB * LDT];
+  const int i = k + 1 + blockIdx.x;
+  double* Mik = M + (int64_t)i * NB * Np + k * NB;
+  load_tile(P, Mik, Np, false);
+  load_tile(Q, X + (int64_t)k * NB * Np + k * NB, Np, true);  // Q[t][c] = X_kk[c][t]
+  __syncthreads();
+  double acc[4][4] = {};
+  int r0, c0;
+  owned(r0, c0);
+  tile_mac(acc, P, Q, r0, c0);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) Mik[(int64_t)(r0 + a) * Np + c0 + b] = acc[a][b];
+}
+
+// M_ij −= L_ik · L_jkᵀ for k < j ≤ i; blockIdx.x enumerates the lower-triangular pairs.
+__global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ M, int Np, int k) {
+  __shared__ double P[NB * LDT];
+  __shared__ double Q[NB * LDT];
+  int t = blockIdx.x, i = 0;
+  while (t > i) { t -= i + 1; ++i; }  // (i, t) with t ≤ i, pairs ordered row by row
+  const int bi = k + 1 + i, bj = k + 1 + t;
+  load_tile(P, M + (int64_t)bi * NB * Np + k * NB, Np, false);
+  load_tile(Q, M + (int64_t)bj * NB * Np + k * NB, Np, true);  // Q[t][c] = L_jk[c][t]
+  __syncthreads();
+  double acc[4][4] = {};
+  int r0, c0;
+  owned(r0, c0);
+  tile_mac(acc, P, Q, r0, c0);
+  double* Mij = M + (int64_t)bi * NB * Np + bj * NB;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) Mij[(int64_t)(r0 + a) * Np + c0 + b] -= acc[a][b];
+}
+
+// Block row i of X = L⁻¹: X_ik = −X_ii Σ_{j=k}^{i−1} L_ij X_jk, one workgroup per k < i.
+__global__ __launch_bounds__(256) void tri_inv_row_kernel(const double* __restrict__ M, double* __restrict__ X, int Np,
+                                                          int i) {
+  __shared__ double P[NB * LDT];
+  __shared__ double Q[NB * LDT];
+  const int k = blockIdx.x;
+  double acc[4][4] = {};
+  int r0, c0;
+  owned(r0, c0);
+  for (int j = k; j < i; ++j) {
+    __syncthreads();
+    load_tile(P, M + (int64_t)i * NB * Np + j * NB, Np, false);
+    load_tile(Q, X + (int64_t)j * NB * Np + k * NB, Np, false);
+    __syncthreads();
+    tile_mac(acc, P, Q, r0, c0);
+  }
+  __syncthreads();
+  // P ← X_ii, Q ← the sum S; X_ik = −X_ii S
+  load_tile(P, X + (int64_t)i * NB * Np + i * NB, Np, false);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) Q[(r0 + a) * LDT + c0 + b] = acc[a][b];
+  __syncthreads();
+  double out[4][4] = {};
+  tile_mac(out, P, Q, r0, c0);
+  double* Xik = X + (int64_t)i * NB * Np + k * NB;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) Xik[(int64_t)(r0 + a) * Np + c0 + b] = -out[a][b];
+}
+
+// A = Xᵀ X: A_ij = Σ_{k ≥ i} X_kiᵀ X_kj for j ≤ i (X lower block-triangular), mirrored to A_ji;
+// rows/columns ≥ N zeroed.
+__global__ __launch_bounds__(256) void xtx_kernel(const double* __restrict__ X, int Np, int N, double* __restrict__ A) {
+  __shared__ double P[NB * LDT];
+  __shared__ double Q[NB * LDT];
+  int t = blockIdx.x, bi = 0;
+  while (t > bi) { t -= bi + 1; ++bi; }
+  const int bj = t;
+  const int nb = Np / NB;
+  double acc[4][4] = {};
+  int r0, c0;
+  owned(r0, c0);
+  for (int k = bi; k < nb; ++k) {
+    __syncthreads();
+    load_tile(P, X + (int64_t)k * NB * Np + bi * NB, Np, true);  // P[r][t] = X_ki[t][r]
+    load_tile(Q, X + (int64_t)k * NB * Np + bj * NB, Np, false);
+    __syncthreads();
+    tile_mac(acc, P, Q, r0, c0);
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int gr = bi * NB + r0 + a, gc = bj * NB + c0 + b;
+      const double v = (gr < N && gc < N) ? acc[a][b] : 0.0;
+      A[(int64_t)gr * Np + gc] = v;
+      A[(int64_t)gc * Np + gr] = v;
+    }
+}
+
+// alpha = A y1 (rows ≥ N zero): one wave per row.
+__global__ __launch_bounds__(256) void alpha_kernel(const double* __restrict__ A, const double* __restrict__ y1, int N,
+                                                    int Np, double* __restrict__ alpha) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= Np) return;
+  double s = 0.0;
+  if (row < N)
+    for (int j = lane; j < N; j += 64) s += A[(int64_t)row * Np + j] * y1[j];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) alpha[row] = s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cdx_gpis_fit(const double* X1, int32_t N, const double* noise, int32_t kernel, double sigma, double* E11,
+                 double* R, cdx_stream_t stream) {
+  if (!X1 || !E11 || !R || N <= 0 || N > 65535) return CDX_EINVAL;
+  if (kernel < 0 || kernel > 2) return CDX_EKERNEL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(R, 0, sizeof(double), s) != hipSuccess) return CDX_ELAUNCH;
+  if (kernel != CDX_KERNEL_RBF)
+    hipLaunchKernelGGL(fit_R_kernel, dim3((N + 255) / 256, N), dim3(256), 0, s, X1, N,
+                       reinterpret_cast<unsigned long long*>(R));
+  const dim3 grid((N + 255) / 256, N);
+  if (kernel == CDX_KERNEL_TPS)
+    hipLaunchKernelGGL(fit_E11_kernel<CDX_KERNEL_TPS>, grid, dim3(256), 0, s, X1, N, noise, sigma, R, E11);
+  else if (kernel == CDX_KERNEL_RBF)
+    hipLaunchKernelGGL(fit_E11_kernel<CDX_KERNEL_RBF>, grid, dim3(256), 0, s, X1, N, noise, sigma, R, E11);
+  else
+    hipLaunchKernelGGL(fit_E11_kernel<CDX_KERNEL_JOINT>, grid, dim3(256), 0, s, X1, N, noise, sigma, R, E11);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+size_t cdx_gpis_factor_workspace(int32_t N_pad) {
+  if (N_pad <= 0 || N_pad % CDX_NPAD_ALIGN) return 0;
+  return 2 * (size_t)N_pad * N_pad * sizeof(double);  // M (→ L) and X = L⁻¹
+}
+
+int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pad, void* ws, double* Ainv,
+                    double* alpha, int32_t* info, cdx_stream_t stream) {
+  if (!E11 || !y1 || !ws || !Ainv || !alpha || !info || N <= 0 || N_pad < N || N_pad % CDX_NPAD_ALIGN ||
+      N_pad > 65535)
+    return CDX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  double* M = static_cast<double*>(ws);
+  double* X = M + (size_t)N_pad * N_pad;
+  const int nb = N_pad / NB;
+  if (hipMemsetAsync(info, 0, sizeof(int32_t), s) != hipSuccess) return CDX_ELAUNCH;
+  hipLaunchKernelGGL(pad_kernel, dim3((N_pad + 255) / 256, N_pad), dim3(256), 0, s, E11, N, N_pad, M, X);
+  for (int k = 0; k < nb; ++k) {
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, s, M, X, N_pad, k, info);
+    const int m = nb - k - 1;
+    if (m == 0) break;
+    hipLaunchKernelGGL(chol_trsm_kernel, dim3(m), dim3(256), 0, s, M, (const double*)X, N_pad, k);
+    hipLaunchKernelGGL(chol_update_kernel, dim3(m * (m + 1) / 2), dim3(256), 0, s, M, N_pad, k);
+  }
+  for (int i = 1; i < nb; ++i)
+    hipLaunchKernelGGL(tri_inv_row_kernel, dim3(i), dim3(256), 0, s, (const double*)M, X, N_pad, i);
+  hipLaunchKernelGGL(xtx_kernel, dim3(nb * (nb + 1) / 2), dim3(256), 0, s, (const double*)X, N_pad, N, Ainv);
+  hipLaunchKernelGGL(alpha_kernel, dim3((N_pad + 3) / 4), dim3(256), 0, s, (const double*)Ainv, y1, N, N_pad, alpha);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+}  // extern "C"

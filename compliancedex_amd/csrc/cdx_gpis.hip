@@ -176,7 +176,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0, 0, 0, 0};
 
-  const int nK = Np / ST_BK;
+  const int nK = (g.N + ST_BK - 1) / ST_BK;  // E11⁻¹ rows ≥ N are zero: stop at the last live K-step
   stage_load(0);
   stage_write(0);
   __syncthreads();
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel4(cdx_gpis g, const dou
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.0;
 
-  const int nK = Np / ST_BK;
+  const int nK = (g.N + ST_BK - 1) / ST_BK;  // E11⁻¹ rows ≥ N are zero: stop at the last live K-step
   stage_write(0);
   __syncthreads();
   const int arow = wr + 4 * (lane & 15);         // + rg

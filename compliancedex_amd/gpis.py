@@ -5,10 +5,11 @@ methods (``fit``, ``pred``, ``compute_normal``, ``compute_multinormals``,
 ``save_state_data``, ``load_state_data``, ``get_visualization_data``).  Queries run on the
 gfx950 kernels (cdx_gpis_mean / cdx_gpis_std); there is no CPU path.
 
-Differences in *how*, not *what*: E11⁻¹ and α = E11⁻ᵀ y1 are computed once per state
-(the reference re-solves E11 on every ``pred`` and inverts it on every
-``compute_normal``), and only the diagonal of the posterior covariance is formed (the
-reference builds the M×M matrix, gpis.py:57-58).
+Differences in *how*, not *what*: ``fit`` builds R and E11 with cdx_gpis_fit, and E11⁻¹ and
+α = E11⁻¹ y1 are factored once per state on the device by cdx_gpis_factor (blocked Cholesky;
+the reference re-solves E11 on every ``pred`` and inverts it on every ``compute_normal``);
+only the diagonal of the posterior covariance is formed (the reference builds the M×M matrix,
+gpis.py:57-58).
 """
 from __future__ import annotations
 
@@ -34,16 +35,21 @@ class _State:
         dev = X1.device
         n = X1.shape[0]
         Np = (n + N.NPAD_ALIGN - 1) // N.NPAD_ALIGN * N.NPAD_ALIGN
-        E11 = E11.to(dev, torch.float64)
-        A = torch.linalg.inv(E11)
-        alpha = (A.T @ y1.to(dev, torch.float64).reshape(-1, 1)).reshape(-1)  # E11⁻ᵀ y1 (gpis.py:53-55)
-        A = 0.5 * (A + A.T)
+        lib = N.load()
+        E11 = E11.to(dev, torch.float64).contiguous()
+        y1 = y1.to(dev, torch.float64).reshape(-1).contiguous()
+        self.Ainv = torch.empty(Np, Np, dtype=torch.float64, device=dev)
+        self.alpha = torch.empty(Np, dtype=torch.float64, device=dev)
+        info = torch.zeros(1, dtype=torch.int32, device=dev)
+        ws = torch.empty(lib.cdx_gpis_factor_workspace(Np), dtype=torch.uint8, device=dev)
+        N.check(lib.cdx_gpis_factor(N.ptr(E11), N.ptr(y1), n, Np, N.ptr(ws), N.ptr(self.Ainv), N.ptr(self.alpha),
+                                    N.ptr(info), N.stream_ptr(dev)), "cdx_gpis_factor")
+        bad = int(info.item())  # one host sync per state build
+        del ws
+        if bad:
+            raise RuntimeError(f"GPIS E11 is not positive definite (pivot {bad} of {n})")
         self.X1 = X1[:1].to(torch.float64).repeat(Np, 1).contiguous()
         self.X1[:n] = X1.to(torch.float64)
-        self.alpha = torch.zeros(Np, dtype=torch.float64, device=dev)
-        self.alpha[:n] = alpha
-        self.Ainv = torch.zeros(Np, Np, dtype=torch.float64, device=dev)
-        self.Ainv[:n, :n] = A
         self.desc = N.CdxGpis(X1=self.X1.data_ptr(), alpha=self.alpha.data_ptr(), Ainv=self.Ainv.data_ptr(), N=n,
                               N_pad=Np, kernel=N.KERNELS[kernel], R=float(R), sigma=float(sigma), bias=float(bias))
         self.ws = None
@@ -115,26 +121,30 @@ class GPIS:
         self._state = None
         self._state_key = None
 
-    # ---------------------------------------------------------------- kernel fns
-    def _k(self, xa, xb):
-        r = torch.cdist(xa, xb)
-        tps = lambda: 2 * r ** 3 - 3 * self.R * r ** 2 + self.R ** 3  # noqa: E731
-        rbf = lambda: torch.exp(-0.5 * r ** 2 / self.sigma ** 2)  # noqa: E731
-        if self.kernel == "tps":
-            return tps()
-        if self.kernel == "rbf":
-            return rbf()
-        return 0.3 * rbf() + 0.7 * tps()
-
     # ----------------------------------------------------------------- fit / io
     def fit(self, X1, y1, noise=0.0):
-        """E11 = K(X1, X1) + diag(noise²) (gpis.py:33-40)."""
+        """R = max cdist, E11 = K(X1, X1) + diag(noise²) (gpis.py:33-40), built on the device
+        by cdx_gpis_fit; ``noise`` is a scalar or a per-point vector, as in the reference."""
+        _require_cuda(X1, "GPIS fit points")
+        dev = X1.device
+        X1d = X1.to(torch.float64).contiguous()
+        n = X1d.shape[0]
+        if torch.is_tensor(noise):
+            nz = noise.to(dev, torch.float64).reshape(-1)
+            nz = (nz.expand(n) if nz.numel() == 1 else nz).contiguous()
+        else:
+            nz = torch.full((n,), float(noise), dtype=torch.float64, device=dev)
+        E11 = torch.empty(n, n, dtype=torch.float64, device=dev)
+        R = torch.zeros((), dtype=torch.float64, device=dev)
+        lib = N.load()
+        N.check(lib.cdx_gpis_fit(N.ptr(X1d), n, N.ptr(nz), N.KERNELS[self.kernel], float(self.sigma), N.ptr(E11),
+                                 N.ptr(R), N.stream_ptr(dev)), "cdx_gpis_fit")
         if self.kernel in ("tps", "joint"):
-            self.R = torch.max(torch.cdist(X1, X1))
+            self.R = R
         self.X1 = X1
         self.y1 = y1 - self.bias
         self.noise = noise
-        self.E11 = self._k(X1, X1) + (self.noise ** 2) * torch.eye(len(X1), device=X1.device)
+        self.E11 = E11
         self._state = None
 
     def save_state_data(self, name="gpis_state"):

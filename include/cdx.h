@@ -72,6 +72,23 @@ size_t cdx_gpis_std_workspace(const cdx_gpis* g, int64_t M);
 int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std, double* grad_std,
                  void* workspace, cdx_stream_t stream);
 
+/* On-device fit.  Replaces GPIS.fit (gpis.py:33-40):
+ *   R   = max_ij ‖X1_i − X1_j‖ for the TPS / joint kernels (device scalar; 0 for RBF),
+ *   E11 = K(X1, X1) + diag(noise²)   [N*N] row-major; noise [N] per point (nullable = 0).
+ * N ≤ 65535. */
+int cdx_gpis_fit(const double* X1, int32_t N, const double* noise, int32_t kernel, double sigma,
+                 double* E11, double* R, cdx_stream_t stream);
+
+/* Workspace bytes of cdx_gpis_factor (2·N_pad²·8). */
+size_t cdx_gpis_factor_workspace(int32_t N_pad);
+
+/* Query state from a fitted E11 (the solve gpis.py:53 repeats on every pred, done once):
+ * Ainv = E11⁻¹ [N_pad*N_pad] zero-padded, alpha = E11⁻¹ y1 [N_pad] zero-padded, by blocked
+ * Cholesky + triangular inverse in f64.  *info (device int32) = 0, or the 1-based row of the
+ * first non-positive pivot (E11 not positive definite; outputs are then undefined). */
+int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pad, void* workspace,
+                    double* Ainv, double* alpha, int32_t* info, cdx_stream_t stream);
+
 /* ------------------------------------------------------------------ FK ----------
  * Replaces DifferentiableRobotModel.compute_forward_kinematics(q, link_names,
  * recursive=False, offsets) (robot_model.py:224-264 with update_kinematic_state

@@ -10,6 +10,8 @@ c3     config 3 objects (stored states, box fit, dummy for realsense), 4096 cand
 c4     config 4 primitives: iiwa7_allegro FK (23 DOF, 4 tips) fwd+bwd for 16 384 candidates and the
        TorchSDF kernel on the banana mesh (16 384 faces) for the 3 SDF calls of an SDF/Kin-mode iteration
        (tips vs deflated mesh, tips vs mesh, targets vs mesh: 3 × 65 536 points) + SDF backward.
+fit    §8f row 2: on-device GPIS fit (R, E11) + factor (Cholesky, E11⁻¹, α) for N = 361 / 1000 / 2000,
+       next to torch-CPU fit + inverse (the work the reference does per object) on the host cores.
 """
 import argparse
 import json
@@ -140,6 +142,30 @@ def case_c4(dev):
                       "fk_evals_per_s": E / fk_s, "sdf_3calls_fwd_bwd_ms": sdf_s * 1e3,
                       "sdf_point_face_pairs_per_s": pairs / sdf_s, "faces": int(faces.shape[0]),
                       "sdf_evals_per_s": E / sdf_s}), flush=True)
+
+
+def case_fit(dev):
+    from compliancedex_amd import GPIS
+    from compliancedex_amd.workloads import synthetic_banana_arrays
+    from oracle.cdx_oracle import OracleGPIS
+    for n in (361, 1000, 2000):
+        X1, y, noise = synthetic_banana_arrays(n)
+        Xd, yd, nd = (torch.from_numpy(a).to(dev) for a in (X1, y, noise))
+        g = GPIS(0.08, 1.0)
+
+        def fit():
+            g.fit(Xd, yd, noise=nd)
+            g.native_state()
+        sec = timed(fit, 5)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            o = OracleGPIS.fit(X1, y, noise, bias=1.0)
+            torch.linalg.inv(o.E11)
+            ts.append(time.perf_counter() - t0)
+        print(json.dumps({"case": "fit_factor", "n_inducing": n, "gpu_ms": sec * 1e3,
+                          "cpu_torch_fit_inverse_ms": float(np.median(ts)) * 1e3,
+                          "cpu_threads": torch.get_num_threads()}), flush=True)
 
 
 def main():
