@@ -64,8 +64,8 @@ def cpu_baseline(args, ref_q, cfg):
                       f"1 warm-up; host os.cpu_count()={os.cpu_count()}"}
 
 
-def hbm_traffic(E, n):
-    """Per-launch HBM bytes of gpis_std_kernel from the committed rocprofv3 PMC summary
+def hbm_traffic(E, n, key="gpis_var_bytes_per_launch"):
+    """Per-launch HBM bytes of a std kernel from the committed rocprofv3 PMC summary
     (profiles/*_pmc.json, written by tools/pmc_summary.py), when one matches this config."""
     import glob
     best = None
@@ -74,8 +74,8 @@ def hbm_traffic(E, n):
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("E") == E and d.get("n_inducing") == n and "gpis_std_bytes_per_launch" in d:
-            best = d["gpis_std_bytes_per_launch"]
+        if d.get("E") == E and d.get("n_inducing") == n and key in d:
+            best = d[key]
     return best
 
 
@@ -131,8 +131,8 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     import ctypes
-    ms = (ctypes.c_double * 4)()
-    cnt = (ctypes.c_int64 * 4)()
+    ms = (ctypes.c_double * 5)()
+    cnt = (ctypes.c_int64 * 5)()
     N.check(lib.cdx_profile_read(ms, cnt), "cdx_profile_read")
     lib.cdx_profile_enable(0)
     elapsed = t1 - t0
@@ -144,13 +144,18 @@ def main():
 
     ms_per_step = 1e3 * elapsed / args.steps
     value = E * world / (elapsed / args.steps)
-    stage_names = ["queries", "gpis_mean", "gpis_std_gemm", "cost_bwd"]
+    stage_names = ["queries", "gpis_mean", "gpis_std_var", "cost_bwd", "gpis_std_grad"]
     stage_ms = {n: (ms[i] / cnt[i] if cnt[i] else None) for i, n in enumerate(stage_names)}
-    m_std = opt.problem(gpis, 1).n_query_levels * E * 4
+    lq = opt.problem(gpis, 1).n_query_levels
+    m_std, m_grad = lq * E * 4, lq * E
     n_ind = args.n_inducing
-    flops = m_std * 2.0 * n_ind * n_ind      # W = K*·E11⁻¹ per launch (algorithmic, unpadded N)
-    std_ms = stage_ms["gpis_std_gemm"]
+    # algorithmic flops per launch (unpadded N): V = K*·L⁻ᵀ is triangular, N(N+1)/2 MACs per
+    # query; W = K*·E11⁻¹ at the variance cost's argmax fingertip only, N² MACs per query
+    flops = m_std * float(n_ind) * (n_ind + 1)
+    flops_g = m_grad * 2.0 * n_ind * n_ind
+    std_ms, grad_ms = stage_ms["gpis_std_var"], stage_ms["gpis_std_grad"]
     achieved = flops / (std_ms * 1e-3) / 1e12 if std_ms else None
+    achieved_g = flops_g / (grad_ms * 1e-3) / 1e12 if grad_ms else None
 
     if rank == 0:
         out = {
@@ -163,12 +168,19 @@ def main():
                        "candidates_per_gpu": E, "n_inducing": n_ind, "hand": args.hand,
                        "parallelism": f"candidates sharded over {world} GPU(s), GPIS replicated"},
             "stage_ms": stage_ms,
-            "roofline": {"bound": "mfma", "kernel": "gpis_std_kernel (v_mfma_f64_16x16x4_f64)",
+            "roofline": {"bound": "mfma", "kernel": "gpis_std_kernel<VAR> (v_mfma_f64_16x16x4_f64, K*·L⁻ᵀ)",
                          "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
                          "traffic": hbm_traffic(E, n_ind),
-                         "flops_per_launch": flops, "note": f"{m_std} std queries x 2·N² (dedup of 3 identical "
-                                                            f"pregrasp levels; reference does 3x)"},
+                         "flops_per_launch": flops,
+                         "note": f"{m_std} std queries x N(N+1) (triangular whitened form; all-tip queries "
+                                 f"deduplicated over the 3 identical pregrasp levels, the reference does 3x)"},
+            "roofline_grad": {"bound": "mfma", "kernel": "gpis_std_kernel<!VAR> (K*·E11⁻¹, ∇std)",
+                              "achieved": achieved_g, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": (achieved_g / FP64_MFMA_PEAK_TFLOPS) if achieved_g else None,
+                              "traffic": hbm_traffic(E, n_ind, "gpis_grad_bytes_per_launch"),
+                              "flops_per_launch": flops_g,
+                              "note": f"{m_grad} queries (the variance cost's argmax fingertip) x 2·N²"},
             "nan_candidates": nan_candidates,  # reference semantics: unclamped log in :708-709
         }
         if world == 1 and not args.no_cpu_baseline:

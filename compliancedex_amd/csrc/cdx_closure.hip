@@ -6,13 +6,16 @@
 //                               (all-tip rows deduplicated over identical coefficient rows,
 //                               targets once, pregrasp tips, palm)      — :657-669, :743-750
 //   2. gpis_mean (cdx_gpis.hip) mean/∇mean/normal at all queries      — gpis.py:43-87
-//   3. gpis_std  (cdx_gpis.hip) std/∇std at the all-tip queries (fp64 MFMA)
+//   3. gpis std  (cdx_gpis.hip) std at the all-tip queries (whitened, triangular fp64 MFMA),
+//      closure_std_select_kernel (the variance cost's argmax fingertip), ∇std at those
+//      queries only (fp64 MFMA)
 //   4. closure_cost_kernel      one thread per candidate: seven cost terms per level,
 //                               Kabsch + SVD backward, FK backward; writes loss, margin
 //                               and the five parameter gradients        — :713-769, :49-118
 #include <hip/hip_runtime.h>
 
 #include "cdx_cost.h"
+#include "cdx_gpis_launch.h"
 #include "cdx_prof.h"
 
 namespace {
@@ -277,10 +280,33 @@ bool chain_ok(const cdx_chain* c) {
 size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 struct ClosureWs {
-  double *X, *mean, *gmean, *normal, *std_, *gstd, *lvl;
-  void* std_ws;
+  double *X, *mean, *gmean, *normal, *std_, *var, *gstd, *Xg, *lvl;
+  int64_t* sel;
+  void *var_ws, *grad_ws;
   size_t bytes;
 };
+
+// The variance cost takes max_f log(100·std_f) (:730), so ∇std is only ever needed at one
+// fingertip per (distinct level, candidate): pick it exactly as level_fwd_bwd does (first
+// maximum of log(100·s)) and gather its query for the ∇std GEMM.
+__global__ __launch_bounds__(256) void closure_std_select_kernel(int64_t E, int T, int Lq,
+                                                                 const double* __restrict__ std_,
+                                                                 const double* __restrict__ X,
+                                                                 int64_t* __restrict__ sel, double* __restrict__ Xg) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)Lq * E) return;
+  const int u = (int)(t / E);
+  const int64_t e = t - (int64_t)u * E;
+  int fmax = 0;
+  double lmax = log(100 * std_[cdx::q_alltip(u, e, 0, E, T)]);
+  for (int f = 1; f < T; ++f) {
+    const double lv = log(100 * std_[cdx::q_alltip(u, e, f, E, T)]);
+    if (lv > lmax) { lmax = lv; fmax = f; }
+  }
+  const int64_t qi = cdx::q_alltip(u, e, fmax, E, T);
+  sel[t] = qi;
+  for (int i = 0; i < 3; ++i) Xg[3 * t + i] = X[3 * qi + i];
+}
 
 ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   ClosureWs w;
@@ -292,9 +318,14 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   w.mean = (double*)take(Mq * sizeof(double));
   w.gmean = (double*)take(Mq * 3 * sizeof(double));
   w.normal = (double*)take(Mq * 3 * sizeof(double));
+  const int64_t Mg = (int64_t)p->n_query_levels * E;
   w.std_ = (double*)take(Ms * sizeof(double));
+  w.var = (double*)take(Ms * sizeof(double));
   w.gstd = (double*)take(Ms * 3 * sizeof(double));
-  w.std_ws = take(cdx_gpis_std_workspace(&p->gpis, Ms));
+  w.sel = (int64_t*)take(Mg * sizeof(int64_t));
+  w.Xg = (double*)take(Mg * 3 * sizeof(double));
+  w.var_ws = take(cdx::gpis_var_ws_bytes(p->gpis, Ms));
+  w.grad_ws = take(cdx::gpis_grad_ws_bytes(p->gpis, Mg));
   w.lvl = (double*)take((size_t)p->n_levels * E * level_record_width(p->chain.n_tips) * sizeof(double));
   w.bytes = off;
   return w;
@@ -348,7 +379,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   if (!q || !comp || !target || !palm_pos || !palm_ori || !workspace || !total_loss || !total_margin || !g_q ||
       !g_comp || !g_target || !g_palm_pos || !g_palm_ori)
     return CDX_EINVAL;
-  if (!p->gpis.Ainv || !p->gpis.X1 || !p->gpis.alpha) return CDX_EINVAL;
+  if (!p->gpis.Ainv || !p->gpis.Linv_t || !p->gpis.X1 || !p->gpis.alpha) return CDX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   ClosureWs w = closure_ws_layout(p, E, static_cast<char*>(workspace));
   const int64_t Mq = cdx::n_queries(*p, E);
@@ -361,7 +392,12 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   if (hipGetLastError() != hipSuccess) return CDX_ELAUNCH;
   int rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
   if (rc) return rc;
-  rc = cdx_gpis_std(&p->gpis, w.X, Ms, w.std_, w.gstd, w.std_ws, stream);
+  rc = cdx::gpis_var_launch(p->gpis, w.X, Ms, w.std_, w.var, w.var_ws, s);
+  if (rc) return rc;
+  const int64_t Mg = (int64_t)p->n_query_levels * E;
+  hipLaunchKernelGGL(closure_std_select_kernel, dim3((unsigned)((Mg + 255) / 256)), dim3(256), 0, s, E,
+                     p->chain.n_tips, p->n_query_levels, (const double*)w.std_, (const double*)w.X, w.sel, w.Xg);
+  rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s);
   if (rc) return rc;
   GpisView gv;
   gv.mean = w.mean; gv.gmean = w.gmean; gv.normal = w.normal; gv.std_ = w.std_; gv.gstd = w.gstd;
@@ -400,7 +436,7 @@ constexpr int PROF_POOL = 4096;
 struct Prof {
   bool on = false;
   hipEvent_t ev[PROF_STAGES][PROF_POOL][2];
-  int n[PROF_STAGES] = {0, 0, 0, 0};
+  int n[PROF_STAGES] = {};
   bool created = false;
 } g_prof;
 }  // namespace

@@ -10,7 +10,8 @@
 //      unblocked Cholesky of M_kk in LDS + its triangular inverse X_kk = L_kk⁻¹), trsm
 //      (L_ik = M_ik X_kkᵀ), update (M_ij −= L_ik L_jkᵀ for k < j ≤ i);
 //   2. X = L⁻¹ by block rows: X_ik = −X_ii Σ_{j=k}^{i−1} L_ij X_jk (block row i depends on rows < i);
-//   3. E11⁻¹ = Xᵀ X (lower block pairs, mirrored, padding zeroed), α = E11⁻¹ y1.
+//   3. E11⁻¹ = Xᵀ X (lower block pairs, mirrored, padding zeroed), Linv_t = Xᵀ (padding
+//      zeroed) and α = Xᵀ (X y1).
 // ≈ N³ flops (N = 2000: 8 GFLOP) in ≈ 4·nb launches; a fit happens once per object.  A non-
 // positive pivot stores its 1-based row in *info (LAPACK potrf convention) and the result is
 // garbage; the host checks info once.
@@ -242,9 +243,24 @@ __global__ __launch_bounds__(256) void xtx_kernel(const double* __restrict__ X, 
     }
 }
 
-// alpha = A y1 (rows ≥ N zero): one wave per row.
-__global__ __launch_bounds__(256) void alpha_kernel(const double* __restrict__ A, const double* __restrict__ y1, int N,
-                                                    int Np, double* __restrict__ alpha) {
+// Linv_t = Xᵀ with rows/columns ≥ N zeroed (the pad block of X is the identity), through a
+// 64×64 LDS tile so both the read and the write are row-contiguous.
+__global__ __launch_bounds__(256) void transpose_kernel(const double* __restrict__ X, int Np, int N,
+                                                        double* __restrict__ Lt) {
+  __shared__ double T[NB * LDT];
+  const int bi = blockIdx.y, bj = blockIdx.x;  // output block (bi, bj) = X block (bj, bi)ᵀ
+  load_tile(T, X + (int64_t)bj * NB * Np + bi * NB, Np, true);
+  __syncthreads();
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+    const int r = e / NB, c = e % NB;
+    const int gr = bi * NB + r, gc = bj * NB + c;
+    Lt[(int64_t)gr * Np + gc] = (gr < N && gc < N) ? T[r * LDT + c] : 0.0;
+  }
+}
+
+// out = A y (rows ≥ N zero, columns ≥ N ignored): one wave per row.
+__global__ __launch_bounds__(256) void matvec_kernel(const double* __restrict__ A, const double* __restrict__ y1, int N,
+                                                     int Np, double* __restrict__ alpha) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= Np) return;
   double s = 0.0;
@@ -284,8 +300,8 @@ size_t cdx_gpis_factor_workspace(int32_t N_pad) {
 }
 
 int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pad, void* ws, double* Ainv,
-                    double* alpha, int32_t* info, cdx_stream_t stream) {
-  if (!E11 || !y1 || !ws || !Ainv || !alpha || !info || N <= 0 || N_pad < N || N_pad % CDX_NPAD_ALIGN ||
+                    double* Linv_t, double* alpha, int32_t* info, cdx_stream_t stream) {
+  if (!E11 || !y1 || !ws || !Ainv || !Linv_t || !alpha || !info || N <= 0 || N_pad < N || N_pad % CDX_NPAD_ALIGN ||
       N_pad > 65535)
     return CDX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -304,7 +320,12 @@ int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pa
   for (int i = 1; i < nb; ++i)
     hipLaunchKernelGGL(tri_inv_row_kernel, dim3(i), dim3(256), 0, s, (const double*)M, X, N_pad, i);
   hipLaunchKernelGGL(xtx_kernel, dim3(nb * (nb + 1) / 2), dim3(256), 0, s, (const double*)X, N_pad, N, Ainv);
-  hipLaunchKernelGGL(alpha_kernel, dim3((N_pad + 3) / 4), dim3(256), 0, s, (const double*)Ainv, y1, N, N_pad, alpha);
+  hipLaunchKernelGGL(transpose_kernel, dim3(nb, nb), dim3(256), 0, s, (const double*)X, N_pad, N, Linv_t);
+  // α = L⁻ᵀ (L⁻¹ y1): two triangular matvecs (6e-13 from the reference's solve where E11⁻¹·y1
+  // with the explicit inverse is 7e-10); M's storage is free again and holds L⁻¹ y1
+  hipLaunchKernelGGL(matvec_kernel, dim3((N_pad + 3) / 4), dim3(256), 0, s, (const double*)X, y1, N, N_pad, M);
+  hipLaunchKernelGGL(matvec_kernel, dim3((N_pad + 3) / 4), dim3(256), 0, s, (const double*)Linv_t, (const double*)M, N,
+                     N_pad, alpha);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 

@@ -2,11 +2,13 @@
 //
 //   gpis_mean_kernel   mean = Σ α_j k(x, x_j) + bias and ∇mean (VALU, fp64); optional
 //                      normal = ∇mean/(‖∇mean‖+1e-8)   — gpis.py:43-55 (mean), :63-87 (normal)
-//   gpis_std_kernel    W = K*·E11⁻¹ on fp64 MFMA (v_mfma_f64_16x16x4_f64) with the K* tile
-//                      generated on chip, fused epilogue reducing s = Σ_n W_mn k_mn and
-//                      g = Σ_n W_mn kd_mn (x_m − x_n) per query → partial sums per
-//                      column tile                                   — gpis.py:56-59
-//   gpis_std_finalize  std = sqrt|k0 − s|, ∇std = −sign·g/std
+//   gpis_std_kernel    fp64 MFMA (v_mfma_f64_16x16x4_f64) products with the K* tile generated
+//                      on chip, two modes                            — gpis.py:56-59
+//                      <VAR>  V = K*·L⁻ᵀ (triangular: N² flops/query), epilogue Σ V²
+//                      <!VAR> W = K*·E11⁻¹ (2N² flops/query), epilogue g = Σ_n W kd (x − x_n)
+//   gpis_var_finalize  std = sqrt|k0 − ‖L⁻¹k‖²|   (the whitened form: 1e-12 from the reference's
+//                      solve, where k·E11⁻¹k with an explicit inverse is 1e-7 on cond 1e7)
+//   gpis_grad_finalize ∇std = −sign(v)·g/std, optionally scattered to selected rows
 //
 // The reference builds the full M×M posterior covariance to read its diagonal and
 // re-solves E11 on every call; here E11⁻¹ and α are precomputed once per object and
@@ -14,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include "cdx_gpis.h"
+#include "cdx_gpis_launch.h"
 #include "cdx_prof.h"
 
 using cdx::gpis_k;
@@ -113,22 +116,44 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 
 // v2: 128 queries × ST_BN output columns per workgroup of 2 × ST_WN waves, each wave owning
 // 64×64 = 4×4 v_mfma_f64_16x16x4_f64 tiles; K-step 16, two LDS buffers, one barrier per step.
-template <int KT>
+//
+// VAR = false (∇std path): B = E11⁻¹, W = K*·E11⁻¹, epilogue Σ W·k and Σ W·kd·(x − x_n) → 4
+//   partials per (column tile, query).
+// VAR = true (std path, whitened): B = L⁻ᵀ (upper triangular), V = K*·L⁻ᵀ = (L⁻¹K*ᵀ)ᵀ, epilogue
+//   Σ V² → 1 partial per (column tile, query).  Column tile nt only needs K-rows j < n0 + ST_BN
+//   (and < N), so tile costs run 1..Nt K-sweeps: tiles are issued heaviest stripe first, and each
+//   XCD takes every eighth query tile of a stripe so all XCDs see the same cost mix while the 32
+//   CUs of one XCD still share the stripe's L⁻ᵀ rows in their L2.
+template <int KT, bool VAR>
 __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X,
                                                                         int64_t M, double* __restrict__ partial,
                                                                         int64_t M_pad, int Mt, int Nt) {
   __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
   double* xq = smem + 2 * (ST_TILE + ST_BTILE);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // XCD-aware order: blocks b and b+8 share an XCD (round-robin dispatch); give each XCD a
-  // contiguous run of n-major tiles so its L2 serves the same E11⁻¹ column stripes.
   const int T = Mt * Nt;
   const int b = blockIdx.x;
-  const int t = (T & 7) == 0 ? (b & 7) * (T >> 3) + (b >> 3) : b;
-  const int nt = t / Mt, mt = t - nt * Mt;
+  int nt, mt;
+  if (VAR) {
+    if ((Mt & 7) == 0) {
+      const int per = Mt >> 3, r = b >> 3;
+      nt = Nt - 1 - r / per;
+      mt = (r % per) * 8 + (b & 7);
+    } else {
+      nt = Nt - 1 - b / Mt;
+      mt = b % Mt;
+    }
+  } else {
+    // XCD-aware order: blocks b and b+8 share an XCD (round-robin dispatch); give each XCD a
+    // contiguous run of n-major tiles so its L2 serves the same E11⁻¹ column stripes.
+    const int t = (T & 7) == 0 ? (b & 7) * (T >> 3) + (b >> 3) : b;
+    nt = t / Mt;
+    mt = t - nt * Mt;
+  }
   const int64_t m0 = (int64_t)mt * ST_BM;
   const int n0 = nt * ST_BN;
   const int Np = g.N_pad;
+  const double* __restrict__ Bop = VAR ? g.Linv_t : g.Ainv;
   const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
 
   // K* generation: thread → query row gm, GEN_PER k-columns starting at gk (wave-uniform)
@@ -149,7 +174,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
   dbl2v av[4];
   double kv[GEN_PER];
   auto stage_load = [&](int kb) {
-    const dbl2v* src = reinterpret_cast<const dbl2v*>(g.Ainv + (int64_t)(kb + ar) * Np + n0 + ac);
+    const dbl2v* src = reinterpret_cast<const dbl2v*>(Bop + (int64_t)(kb + ar) * Np + n0 + ac);
 #pragma unroll
     for (int i = 0; i < 4; ++i) av[i] = src[i];
     const double* x1 = g.X1 + 3 * (kb + gk);
@@ -176,7 +201,9 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0, 0, 0, 0};
 
-  const int nK = (g.N + ST_BK - 1) / ST_BK;  // E11⁻¹ rows ≥ N are zero: stop at the last live K-step
+  // B rows ≥ N are zero: stop at the last live K-step (and, for L⁻ᵀ, at the tile's diagonal)
+  const int kend = VAR ? min(g.N, n0 + ST_BN) : g.N;
+  const int nK = (kend + ST_BK - 1) / ST_BK;
   stage_load(0);
   stage_write(0);
   __syncthreads();
@@ -184,7 +211,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     // Stage s+1 (clamped at the end: the extra stage lands in the buffer nobody reads again).
     const int kn = (s + 1 < nK ? s + 1 : s) * ST_BK;
     {
-      const dbl2v* src = reinterpret_cast<const dbl2v*>(g.Ainv + (int64_t)(kn + ar) * Np + n0 + ac);
+      const dbl2v* src = reinterpret_cast<const dbl2v*>(Bop + (int64_t)(kn + ar) * Np + n0 + ac);
 #pragma unroll
       for (int i = 0; i < 4; ++i) av[i] = src[i];
     }
@@ -230,6 +257,34 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     }
     stage_write((s + 1) & 1);
     __syncthreads();
+  }
+
+  if constexpr (VAR) {
+    // Epilogue: per owned row Σ V² over this wave's 64 columns, reduced over the 16 lanes of a
+    // row, then over the column waves in LDS.
+    double* red = smem;  // [ST_WN][ST_BM]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double v = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v = fma(acc[i][j][r], acc[i][j][r], v);
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if ((lane & 15) == 0) red[(wave % ST_WN) * ST_BM + wr + 16 * i + (lane >> 4) + 4 * r] = v;
+      }
+    }
+    __syncthreads();
+    if (tid < ST_BM) {
+      double v = 0.0;
+#pragma unroll
+      for (int w = 0; w < ST_WN; ++w) v += red[w * ST_BM + tid];
+      partial[(int64_t)nt * M_pad + m0 + tid] = v;
+    }
+    return;
   }
 
   // Epilogue: per owned row, s = Σ_n W k and g = Σ_n W kd (x_m − x_n) over this wave's 64 columns,
@@ -477,33 +532,38 @@ __global__ __launch_bounds__(256, 2) void gpis_std_kernel4(cdx_gpis g, const dou
 
 #endif  // CDX_STD_MFMA4
 
-#if defined(CDX_STD_MFMA4)
-#define CDX_STD_KERNEL gpis_std_kernel4
-#define CDX_STD_THREADS 256
-#else
-#define CDX_STD_KERNEL gpis_std_kernel
-#define CDX_STD_THREADS ST_THREADS
-#endif
 
+// std = sqrt|k0 − Σ_t V²-partials|; var_out keeps the signed k0 − ‖L⁻¹k‖² for the ∇std scale.
 template <int KT>
-__global__ __launch_bounds__(256) void gpis_std_finalize(cdx_gpis g, const double* __restrict__ partial, int64_t M,
+__global__ __launch_bounds__(256) void gpis_var_finalize(cdx_gpis g, const double* __restrict__ partial, int64_t M,
                                                          int64_t M_pad, int n_tiles, double* __restrict__ std_out,
-                                                         double* __restrict__ gstd) {
+                                                         double* __restrict__ var_out) {
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
-  double s = 0, g0 = 0, g1 = 0, g2 = 0;
+  double s = 0;
+  for (int t = 0; t < n_tiles; ++t) s += partial[(int64_t)t * M_pad + m];
+  const double v = gpis_k0<KT>(g.R) - s;
+  std_out[m] = sqrt(fabs(v));
+  if (var_out) var_out[m] = v;
+}
+
+// ∇std = −sign(v)·(Σ_n W kd (x − x_n))/sqrt|v| at query m, written to row sel[m] (identity when
+// sel is null) with v = var[sel[m]] from the whitened pass.
+__global__ __launch_bounds__(256) void gpis_grad_finalize(const double* __restrict__ partial, int64_t M,
+                                                          int64_t M_pad, int n_tiles, const int64_t* __restrict__ sel,
+                                                          const double* __restrict__ var, double* __restrict__ gstd) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  double g0 = 0, g1 = 0, g2 = 0;
   for (int t = 0; t < n_tiles; ++t) {
     const double* p = partial + ((int64_t)t * M_pad + m) * 4;
-    s += p[0]; g0 += p[1]; g1 += p[2]; g2 += p[3];
+    g0 += p[1]; g1 += p[2]; g2 += p[3];
   }
-  const double v = gpis_k0<KT>(g.R) - s;
-  const double sd = sqrt(fabs(v));
-  std_out[m] = sd;
-  if (gstd) {
-    const double sg = v > 0 ? 1.0 : (v < 0 ? -1.0 : 0.0);
-    const double f = -sg / sd;
-    gstd[3 * m] = f * g0; gstd[3 * m + 1] = f * g1; gstd[3 * m + 2] = f * g2;
-  }
+  const int64_t o = sel ? sel[m] : m;
+  const double v = var[o];
+  const double sg = v > 0 ? 1.0 : (v < 0 ? -1.0 : 0.0);
+  const double f = -sg / sqrt(fabs(v));
+  gstd[3 * o] = f * g0; gstd[3 * o + 1] = f * g1; gstd[3 * o + 2] = f * g2;
 }
 
 __global__ void mfma_f64_selftest_kernel(const double* A, const double* B, double* D) {
@@ -523,6 +583,77 @@ bool gpis_ok(const cdx_gpis* g) {
 int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
 }  // namespace
+
+namespace cdx {
+
+size_t gpis_var_ws_bytes(const cdx_gpis& g, int64_t M) {
+  return (size_t)(g.N_pad / ST_BN) * (size_t)round_up(M, ST_BM) * sizeof(double);
+}
+
+size_t gpis_grad_ws_bytes(const cdx_gpis& g, int64_t M) {
+  return (size_t)(g.N_pad / ST_BN) * (size_t)round_up(M, ST_BM) * 4 * sizeof(double);
+}
+
+template <int KT>
+static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double* std_out, double* var_out,
+                          double* partial, int64_t M_pad, int Mt, int n_tiles, hipStream_t s) {
+  prof_mark(PROF_GPIS_STD, true, s);
+  hipLaunchKernelGGL((gpis_std_kernel<KT, true>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g, X, M,
+                     partial, M_pad, Mt, n_tiles);
+  prof_mark(PROF_GPIS_STD, false, s);
+  hipLaunchKernelGGL(gpis_var_finalize<KT>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, g, partial, M, M_pad,
+                     n_tiles, std_out, var_out);
+}
+
+template <int KT>
+static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const int64_t* sel, const double* var,
+                           double* gstd, double* partial, int64_t M_pad, int Mt, int n_tiles, hipStream_t s) {
+  prof_mark(PROF_GPIS_GRAD, true, s);
+#if defined(CDX_STD_MFMA4)
+  hipLaunchKernelGGL(gpis_std_kernel4<KT>, dim3((unsigned)(Mt * n_tiles)), dim3(256), 0, s, g, X, M, partial, M_pad,
+                     Mt, n_tiles);
+#else
+  hipLaunchKernelGGL((gpis_std_kernel<KT, false>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g, X, M,
+                     partial, M_pad, Mt, n_tiles);
+#endif
+  prof_mark(PROF_GPIS_GRAD, false, s);
+  hipLaunchKernelGGL(gpis_grad_finalize, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, partial, M, M_pad,
+                     n_tiles, sel, var, gstd);
+}
+
+int gpis_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* std_out, double* var_out, void* ws,
+                    hipStream_t s) {
+  if (M <= 0) return CDX_OK;
+  const int64_t M_pad = round_up(M, ST_BM);
+  const int n_tiles = g.N_pad / ST_BN;
+  if (M_pad / ST_BM * n_tiles > 0x7fffffff) return CDX_EINVAL;
+  const int Mt = (int)(M_pad / ST_BM);
+  double* partial = static_cast<double*>(ws);
+  switch (g.kernel) {
+    case CDX_KERNEL_TPS: var_launch_kt<CDX_KERNEL_TPS>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, s); break;
+    case CDX_KERNEL_RBF: var_launch_kt<CDX_KERNEL_RBF>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, s); break;
+    default: var_launch_kt<CDX_KERNEL_JOINT>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, s); break;
+  }
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_t* sel, const double* var,
+                     double* gstd, void* ws, hipStream_t s) {
+  if (M <= 0) return CDX_OK;
+  const int64_t M_pad = round_up(M, ST_BM);
+  const int n_tiles = g.N_pad / ST_BN;
+  if (M_pad / ST_BM * n_tiles > 0x7fffffff) return CDX_EINVAL;
+  const int Mt = (int)(M_pad / ST_BM);
+  double* partial = static_cast<double*>(ws);
+  switch (g.kernel) {
+    case CDX_KERNEL_TPS: grad_launch_kt<CDX_KERNEL_TPS>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, s); break;
+    case CDX_KERNEL_RBF: grad_launch_kt<CDX_KERNEL_RBF>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, s); break;
+    default: grad_launch_kt<CDX_KERNEL_JOINT>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, s); break;
+  }
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+}  // namespace cdx
 
 extern "C" {
 
@@ -545,43 +676,22 @@ int cdx_gpis_mean(const cdx_gpis* g, const double* X, int64_t M, double* mean, d
 
 size_t cdx_gpis_std_workspace(const cdx_gpis* g, int64_t M) {
   if (!g || M <= 0 || g->N_pad <= 0) return 0;
-  return (size_t)(g->N_pad / ST_BN) * (size_t)round_up(M, ST_BM) * 4 * sizeof(double);
+  return cdx::gpis_var_ws_bytes(*g, M) + cdx::gpis_grad_ws_bytes(*g, M) + (size_t)round_up(M, 32) * sizeof(double);
 }
 
 int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std_out, double* grad_std, void* workspace,
                  cdx_stream_t stream) {
-  if (!gpis_ok(g) || !g->Ainv) return g && (g->kernel < 0 || g->kernel > 2) ? CDX_EKERNEL : CDX_EINVAL;
+  if (!gpis_ok(g) || !g->Ainv || !g->Linv_t) return g && (g->kernel < 0 || g->kernel > 2) ? CDX_EKERNEL : CDX_EINVAL;
   if (M < 0 || (M > 0 && (!X || !std_out || !workspace))) return CDX_EINVAL;
   if (M == 0) return CDX_OK;
-  const int64_t M_pad = round_up(M, ST_BM);
-  const int n_tiles = g->N_pad / ST_BN;
-  if (M_pad / ST_BM * n_tiles > 0x7fffffff) return CDX_EINVAL;
-  const int Mt = (int)(M_pad / ST_BM);
-  double* partial = static_cast<double*>(workspace);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid((unsigned)(Mt * n_tiles));
-  const dim3 fgrid((unsigned)((M + 255) / 256));
-  switch (g->kernel) {
-    case CDX_KERNEL_TPS:
-      cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_TPS>, grid, dim3(CDX_STD_THREADS), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
-      cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
-      hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_TPS>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
-      break;
-    case CDX_KERNEL_RBF:
-      cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_RBF>, grid, dim3(CDX_STD_THREADS), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
-      cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
-      hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_RBF>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
-      break;
-    default:
-      cdx::prof_mark(cdx::PROF_GPIS_STD, true, s);
-      hipLaunchKernelGGL(CDX_STD_KERNEL<CDX_KERNEL_JOINT>, grid, dim3(CDX_STD_THREADS), 0, s, *g, X, M, partial, M_pad, Mt, n_tiles);
-      cdx::prof_mark(cdx::PROF_GPIS_STD, false, s);
-      hipLaunchKernelGGL(gpis_std_finalize<CDX_KERNEL_JOINT>, fgrid, dim3(256), 0, s, *g, partial, M, M_pad, n_tiles, std_out, grad_std);
-      break;
-  }
-  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+  char* ws = static_cast<char*>(workspace);
+  double* var = reinterpret_cast<double*>(ws);
+  void* pv = ws + (size_t)round_up(M, 32) * sizeof(double);
+  void* pg = static_cast<char*>(pv) + cdx::gpis_var_ws_bytes(*g, M);
+  int rc = cdx::gpis_var_launch(*g, X, M, std_out, var, pv, s);
+  if (rc || !grad_std) return rc;
+  return cdx::gpis_grad_launch(*g, X, M, nullptr, var, grad_std, pg, s);
 }
 
 // Test hook: D[16×16] = A[16×4]·B[4×16] through one v_mfma_f64_16x16x4_f64 (layout check).

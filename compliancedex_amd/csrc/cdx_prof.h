@@ -5,6 +5,6 @@
 #include <hip/hip_runtime.h>
 
 namespace cdx {
-enum ProfStage { PROF_QUERIES = 0, PROF_GPIS_MEAN = 1, PROF_GPIS_STD = 2, PROF_COST = 3, PROF_STAGES = 4 };
+enum ProfStage { PROF_QUERIES = 0, PROF_GPIS_MEAN = 1, PROF_GPIS_STD = 2, PROF_COST = 3, PROF_GPIS_GRAD = 4, PROF_STAGES = 5 };
 void prof_mark(int stage, bool begin, hipStream_t s);  // defined in cdx_closure.hip
 }  // namespace cdx

@@ -5,11 +5,11 @@ methods (``fit``, ``pred``, ``compute_normal``, ``compute_multinormals``,
 ``save_state_data``, ``load_state_data``, ``get_visualization_data``).  Queries run on the
 gfx950 kernels (cdx_gpis_mean / cdx_gpis_std); there is no CPU path.
 
-Differences in *how*, not *what*: ``fit`` builds R and E11 with cdx_gpis_fit, and E11⁻¹ and
-α = E11⁻¹ y1 are factored once per state on the device by cdx_gpis_factor (blocked Cholesky;
-the reference re-solves E11 on every ``pred`` and inverts it on every ``compute_normal``);
-only the diagonal of the posterior covariance is formed (the reference builds the M×M matrix,
-gpis.py:57-58).
+Differences in *how*, not *what*: ``fit`` builds R and E11 with cdx_gpis_fit, and L⁻¹ (E11 = LLᵀ),
+E11⁻¹ and α = L⁻ᵀL⁻¹y1 are factored once per state on the device by cdx_gpis_factor (blocked
+Cholesky; the reference re-solves E11 on every ``pred`` and inverts it on every
+``compute_normal``); only the diagonal of the posterior covariance is formed, in the whitened
+form k0 − ‖L⁻¹k‖² (the reference builds the M×M matrix, gpis.py:57-58).
 """
 from __future__ import annotations
 
@@ -39,10 +39,11 @@ class _State:
         E11 = E11.to(dev, torch.float64).contiguous()
         y1 = y1.to(dev, torch.float64).reshape(-1).contiguous()
         self.Ainv = torch.empty(Np, Np, dtype=torch.float64, device=dev)
+        self.Linv_t = torch.empty(Np, Np, dtype=torch.float64, device=dev)
         self.alpha = torch.empty(Np, dtype=torch.float64, device=dev)
         info = torch.zeros(1, dtype=torch.int32, device=dev)
         ws = torch.empty(lib.cdx_gpis_factor_workspace(Np), dtype=torch.uint8, device=dev)
-        N.check(lib.cdx_gpis_factor(N.ptr(E11), N.ptr(y1), n, Np, N.ptr(ws), N.ptr(self.Ainv), N.ptr(self.alpha),
+        N.check(lib.cdx_gpis_factor(N.ptr(E11), N.ptr(y1), n, Np, N.ptr(ws), N.ptr(self.Ainv), N.ptr(self.Linv_t), N.ptr(self.alpha),
                                     N.ptr(info), N.stream_ptr(dev)), "cdx_gpis_factor")
         bad = int(info.item())  # one host sync per state build
         del ws
@@ -50,7 +51,8 @@ class _State:
             raise RuntimeError(f"GPIS E11 is not positive definite (pivot {bad} of {n})")
         self.X1 = X1[:1].to(torch.float64).repeat(Np, 1).contiguous()
         self.X1[:n] = X1.to(torch.float64)
-        self.desc = N.CdxGpis(X1=self.X1.data_ptr(), alpha=self.alpha.data_ptr(), Ainv=self.Ainv.data_ptr(), N=n,
+        self.desc = N.CdxGpis(X1=self.X1.data_ptr(), alpha=self.alpha.data_ptr(), Ainv=self.Ainv.data_ptr(),
+                              Linv_t=self.Linv_t.data_ptr(), N=n,
                               N_pad=Np, kernel=N.KERNELS[kernel], R=float(R), sigma=float(sigma), bias=float(bias))
         self.ws = None
 
@@ -212,7 +214,7 @@ class GPIS:
         sub = _State.__new__(_State)
         sub.__dict__.update(st.__dict__)
         sub.alpha = st.alpha * mask
-        sub.desc = N.CdxGpis(X1=st.desc.X1, alpha=sub.alpha.data_ptr(), Ainv=st.desc.Ainv, N=st.desc.N,
+        sub.desc = N.CdxGpis(X1=st.desc.X1, alpha=sub.alpha.data_ptr(), Ainv=st.desc.Ainv, Linv_t=st.desc.Linv_t, N=st.desc.N,
                              N_pad=st.desc.N_pad, kernel=st.desc.kernel, R=st.desc.R, sigma=st.desc.sigma,
                              bias=st.desc.bias)
         _, _, normal = gpis_mean(sub, X, want_grad=False, want_normal=True)

@@ -37,7 +37,10 @@ enum {
  * State precomputed once per object (gpis.py:33-40 fit / :162-168 load):
  *   X1     [N_pad*3]  inducing points (N_pad: multiple of CDX_NPAD_ALIGN), AoS xyz, rows >= N padded with any finite point
  *   alpha  [N_pad]    E11^{-1} y1 (zero-padded); mean = Σ alpha_j k(x, x_j) + bias
- *   Ainv   [N_pad*N_pad] E11^{-1}, symmetric, zero-padded; only used by the std path
+ *   Ainv   [N_pad*N_pad] E11^{-1}, symmetric, zero-padded; ∇std path
+ *   Linv_t [N_pad*N_pad] (L^{-1})^T for E11 = L L^T (upper triangular), zero-padded; std path:
+ *          std² = |k0 - ‖L^{-1} k‖²| (the whitened form: N² flops per query, and 1e-12 from the
+ *          reference's per-call solve where k^T E11^{-1} k with an explicit inverse is 1e-7)
  * kernel: 0 = thin-plate spline 2r³-3Rr²+R³ (gpis.py:21-26, the default),
  *         1 = RBF exp(-r²/2σ²) (:16-19), 2 = 0.3·RBF + 0.7·TPS (:28-29). */
 enum { CDX_KERNEL_TPS = 0, CDX_KERNEL_RBF = 1, CDX_KERNEL_JOINT = 2 };
@@ -47,6 +50,7 @@ typedef struct {
   const double* X1;
   const double* alpha;
   const double* Ainv;
+  const double* Linv_t;
   int32_t N;
   int32_t N_pad;      /* multiple of CDX_NPAD_ALIGN (256), >= N */
   int32_t kernel;
@@ -83,11 +87,12 @@ int cdx_gpis_fit(const double* X1, int32_t N, const double* noise, int32_t kerne
 size_t cdx_gpis_factor_workspace(int32_t N_pad);
 
 /* Query state from a fitted E11 (the solve gpis.py:53 repeats on every pred, done once):
- * Ainv = E11⁻¹ [N_pad*N_pad] zero-padded, alpha = E11⁻¹ y1 [N_pad] zero-padded, by blocked
- * Cholesky + triangular inverse in f64.  *info (device int32) = 0, or the 1-based row of the
- * first non-positive pivot (E11 not positive definite; outputs are then undefined). */
+ * E11 = L Lᵀ by blocked Cholesky + triangular inverse in f64, then Ainv = E11⁻¹ = L⁻ᵀL⁻¹ and
+ * Linv_t = L⁻ᵀ [N_pad*N_pad] zero-padded, alpha = L⁻ᵀ(L⁻¹ y1) [N_pad] zero-padded.
+ * *info (device int32) = 0, or the 1-based row of the first non-positive pivot (E11 not
+ * positive definite; outputs are then undefined). */
 int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pad, void* workspace,
-                    double* Ainv, double* alpha, int32_t* info, cdx_stream_t stream);
+                    double* Ainv, double* Linv_t, double* alpha, int32_t* info, cdx_stream_t stream);
 
 /* ------------------------------------------------------------------ FK ----------
  * Replaces DifferentiableRobotModel.compute_forward_kinematics(q, link_names,
@@ -217,11 +222,12 @@ int cdx_sdf_backward(const float* grad_dist, const float* points, const float* c
 const char* cdx_version(void);
 
 /* Per-stage kernel timing with HIP events recorded on the launch stream (off by default).
- * Stages: 0 closure query generation, 1 GPIS mean, 2 GPIS std GEMM (gpis_std_kernel only),
- * 3 closure cost+backward.  cdx_profile_read syncs on the recorded events, returns the summed
- * milliseconds and launch counts per stage, and clears the pool (4096 launches per stage). */
+ * Stages: 0 closure query generation, 1 GPIS mean, 2 GPIS std (whitened K*·L⁻ᵀ GEMM only),
+ * 3 closure cost+backward, 4 GPIS ∇std (K*·E11⁻¹ GEMM only).  cdx_profile_read syncs on the
+ * recorded events, returns the summed milliseconds and launch counts per stage (arrays of 5),
+ * and clears the pool (4096 launches per stage). */
 int cdx_profile_enable(int on);
-int cdx_profile_read(double* ms4, int64_t* count4);
+int cdx_profile_read(double* ms5, int64_t* count5);
 
 /* sizeof(cdx_gpis), sizeof(cdx_body), sizeof(cdx_chain), sizeof(cdx_problem) — lets a
  * binding verify its struct layout before the first call. */

@@ -55,7 +55,8 @@ def main():
         summary["kernels"][short(k)] = {"FETCH_SIZE_kB": f, "WRITE_SIZE_kB": w, "hbm_bytes": (2 * f + w) * 1024,
                                         "dispatches": len(fetch.get(k, []))}
         if "gpis_std_kernel" in k:
-            summary["gpis_std_bytes_per_launch"] = (2 * f + w) * 1024
+            key = "gpis_var_bytes_per_launch" if "true>" in k else "gpis_grad_bytes_per_launch"
+            summary[key] = (2 * f + w) * 1024
     json.dump(summary, open(os.path.join(REPO, "profiles", f"{tag}_pmc.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
 
