@@ -46,6 +46,14 @@ class CdxProblem(C.Structure):
                 ("uncertainty", C.c_double)]
 
 
+MAX_PAIRS = 28
+
+
+class CdxCollision(C.Structure):
+    _fields_ = [("chain", CdxChain), ("n_pairs", C.c_int32), ("palm_term", C.c_int32),
+                ("pairs", (C.c_int8 * 2) * MAX_PAIRS), ("pair_threshold", C.c_double), ("floor_z", C.c_double)]
+
+
 class CdxAdam(C.Structure):
     _fields_ = [("lr", C.c_double * 5), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double),
                 ("comp_min", C.c_double), ("target_lb", C.c_double * (MAX_TIPS * 3)),
@@ -73,6 +81,7 @@ _SIGS = {
     "cdx_gpis_factor": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P]),
     "cdx_fk_forward": (C.c_int, [C.POINTER(CdxChain), _P, _I64, _P, _P, _P]),
     "cdx_fk_backward": (C.c_int, [C.POINTER(CdxChain), _P, _I64, _P, _P, _P]),
+    "cdx_collision_loss": (C.c_int, [C.POINTER(CdxCollision), _I64, _P, _P, _P, _P, _P, _P, _P, C.c_int32, _P]),
     "cdx_closure_workspace": (C.c_size_t, [C.POINTER(CdxProblem), _I64]),
     "cdx_closure": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, _P, _P, _P, _P, _P, C.c_uint64, _P,
                               _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -110,9 +119,10 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        sizes = (C.c_size_t * 4)()
+        sizes = (C.c_size_t * 7)()
         lib.cdx_abi_sizes(sizes)
-        mine = [C.sizeof(CdxGpis), C.sizeof(CdxBody), C.sizeof(CdxChain), C.sizeof(CdxProblem)]
+        mine = [C.sizeof(CdxGpis), C.sizeof(CdxBody), C.sizeof(CdxChain), C.sizeof(CdxProblem),
+                C.sizeof(CdxCollision), C.sizeof(CdxAdam), C.sizeof(CdxOptBuffers)]
         if list(sizes) != mine:
             raise ImportError(f"ABI struct size mismatch: library {list(sizes)} vs binding {mine}")
         _lib = lib

@@ -14,6 +14,7 @@
 //                               and the five parameter gradients        — :713-769, :49-118
 #include <hip/hip_runtime.h>
 
+#include "cdx_collision.h"
 #include "cdx_cost.h"
 #include "cdx_gpis_launch.h"
 #include "cdx_prof.h"
@@ -44,6 +45,28 @@ __global__ __launch_bounds__(64) void fk_backward_kernel(cdx_chain c, const floa
   for (int i = 0; i < c.n_dofs; ++i) { qb[i] = q[b * c.n_dofs + i]; g[i] = 0.f; }
   for (int k = 0; k < c.n_tips; ++k) cdx::fk_tip_bwd(c, k, qb, gpos + (b * c.n_tips + k) * 3, g);
   for (int i = 0; i < c.n_dofs; ++i) gq[b * c.n_dofs + i] = g[i];
+}
+
+// --------------------------------------------------------------- collision loss
+__global__ __launch_bounds__(64) void collision_kernel(cdx_collision C, int64_t E, const double* __restrict__ q,
+                                                       const double* __restrict__ palm_pos,
+                                                       const double* __restrict__ palm_ori, double* __restrict__ cost,
+                                                       double* __restrict__ g_q, double* __restrict__ g_pp,
+                                                       double* __restrict__ g_po, int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int D = C.chain.n_dofs;
+  double c, gq[CDX_MAX_DOFS], gpp[3], gpo[3];
+  cdx::collision_candidate(C, q + e * D, palm_pos + 3 * e, palm_ori + 3 * e, c, gq, gpp, gpo);
+  if (accumulate) {
+    cost[e] += c;
+    for (int i = 0; i < D; ++i) g_q[e * D + i] += gq[i];
+    for (int i = 0; i < 3; ++i) { g_pp[3 * e + i] += gpp[i]; g_po[3 * e + i] += gpo[i]; }
+  } else {
+    cost[e] = c;
+    for (int i = 0; i < D; ++i) g_q[e * D + i] = gq[i];
+    for (int i = 0; i < 3; ++i) { g_pp[3 * e + i] = gpp[i]; g_po[3 * e + i] = gpo[i]; }
+  }
 }
 
 // --------------------------------------------------------------- closure stages
@@ -363,6 +386,23 @@ int cdx_fk_backward(const cdx_chain* chain, const float* q, int64_t B, const flo
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
+int cdx_collision_loss(const cdx_collision* c, int64_t E, const double* q, const double* palm_pos,
+                       const double* palm_ori, double* cost, double* g_q, double* g_palm_pos, double* g_palm_ori,
+                       int32_t accumulate, cdx_stream_t stream) {
+  if (!c || !chain_ok(&c->chain)) return CDX_ECHAIN;
+  if (c->n_pairs < 0 || c->n_pairs > CDX_MAX_PAIRS) return CDX_EINVAL;
+  for (int p = 0; p < c->n_pairs; ++p)
+    for (int j = 0; j < 2; ++j)
+      if (c->pairs[p][j] < 0 || c->pairs[p][j] >= c->chain.n_tips) return CDX_EINVAL;
+  if (E < 0 || (E > 0 && (!q || !palm_pos || !palm_ori || !cost || !g_q || !g_palm_pos || !g_palm_ori)))
+    return CDX_EINVAL;
+  if (E == 0) return CDX_OK;
+  hipLaunchKernelGGL(collision_kernel, dim3((unsigned)((E + 63) / 64)), dim3(64), 0,
+                     reinterpret_cast<hipStream_t>(stream), *c, E, q, palm_pos, palm_ori, cost, g_q, g_palm_pos,
+                     g_palm_ori, accumulate);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
 size_t cdx_closure_workspace(const cdx_problem* p, int64_t E) {
   if (!problem_ok(p) || E <= 0) return 0;
   return closure_ws_layout(p, E, nullptr).bytes;
@@ -487,4 +527,7 @@ extern "C" void cdx_abi_sizes(size_t* out) {
   out[1] = sizeof(cdx_body);
   out[2] = sizeof(cdx_chain);
   out[3] = sizeof(cdx_problem);
+  out[4] = sizeof(cdx_collision);
+  out[5] = sizeof(cdx_adam);
+  out[6] = sizeof(cdx_opt_buffers);
 }

@@ -1,10 +1,12 @@
-// Host (x86) build of the per-candidate device code in cdx_fk.h / cdx_cost.h / cdx_sdf.h.
+// Host (x86) build of the per-candidate device code in cdx_fk.h / cdx_cost.h / cdx_collision.h /
+// cdx_sdf.h.
 //
 // TEST-ONLY: libcdx_host.so lets the CPU test suite check the hand-derived backward
 // (Kabsch/SVD, cost terms, FK) against the oracle's autograd without a GPU.  The
 // product path never loads it; the Python package loads only the gfx950 libcdx.so.
 #include <string.h>
 
+#include "cdx_collision.h"
 #include "cdx_cost.h"
 #include "cdx_sdf.h"
 
@@ -108,6 +110,13 @@ void cdxh_closure_cost(const cdx_problem* P, int64_t E, const double* q, const d
     for (int i = 0; i < 3; ++i) { g_palm_pos[3 * e + i] = out.g_palm_pos[i]; g_palm_ori[3 * e + i] = out.g_palm_ori[i]; }
     for (int k = 0; k < P->n_levels; ++k) flip[k * E + e] = out.flip[k];
   }
+}
+
+void cdxh_collision(const cdx_collision* C, int64_t E, const double* q, const double* pp, const double* po,
+                    double* cost, double* g_q, double* g_pp, double* g_po) {
+  const int D = C->chain.n_dofs;
+  for (int64_t e = 0; e < E; ++e)
+    cdx::collision_candidate(*C, q + e * D, pp + 3 * e, po + 3 * e, cost[e], g_q + e * D, g_pp + 3 * e, g_po + 3 * e);
 }
 
 void cdxh_svd3(const double* H, double* U, double* S, double* V) { cdx::svd3(H, U, S, V); }

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .problem import build_problem
+from .problem import build_collision, build_problem
 from .robot_model import DifferentiableRobotModel
 
 EE_OFFSETS = [[0.0, -0.04, 0.015], [0.0, -0.04, 0.015], [0.0, -0.04, 0.015], [0.0, -0.05, -0.015]]
@@ -45,13 +45,39 @@ def euler_angles_to_matrix(euler_angles, convention="XYZ"):
     return torch.matmul(torch.matmul(mats[0], mats[1]), mats[2])
 
 
+class _Collision(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, palm, desc):
+        lib = N.load()
+        E = q.shape[0]
+        f64 = dict(dtype=torch.float64, device=q.device)
+        qd = q.detach().to(torch.float64).contiguous()
+        pd = palm.detach().to(torch.float64)
+        pp, po = pd[:, :3].contiguous(), pd[:, 3:].contiguous()
+        if qd.shape != (E, desc.chain.n_dofs) or pd.shape != (E, 6):
+            raise ValueError("compute_collision_loss: q must be [E, n_dofs] and palm poses [E, 6]")
+        cost = torch.empty(E, **f64)
+        g_q, g_pp, g_po = torch.empty(E, desc.chain.n_dofs, **f64), torch.empty(E, 3, **f64), torch.empty(E, 3, **f64)
+        N.check(lib.cdx_collision_loss(desc, E, N.ptr(qd), N.ptr(pp), N.ptr(po), N.ptr(cost), N.ptr(g_q), N.ptr(g_pp),
+                                       N.ptr(g_po), 0, N.stream_ptr(q.device)), "cdx_collision_loss")
+        ctx.save_for_backward(g_q, torch.cat([g_pp, g_po], 1))
+        ctx.dtypes = (q.dtype, palm.dtype)
+        return cost
+
+    @staticmethod
+    def backward(ctx, g):
+        g_q, g_palm = ctx.saved_tensors
+        g = g.to(torch.float64).unsqueeze(1)
+        return (g * g_q).to(ctx.dtypes[0]), (g * g_palm).to(ctx.dtypes[1]), None
+
+
 class ProbabilisticGraspOptimizer:
     def __init__(self, robot_urdf, ee_link_names, ee_link_offsets=EE_OFFSETS, palm_offset=WRIST_OFFSET,
                  num_iters=1000, optimize_target=False, ref_q=None, tip_bounding_box=(FINGERTIP_LB, FINGERTIP_UB),
                  pregrasp_coefficients=((0.8, 0.8, 0.8, 0.8),) * 3, pregrasp_weights=(0.1, 0.8, 0.1),
                  anchor_link_names=None, anchor_link_offsets=None, collision_pairs=None,
                  collision_pair_threshold=0.02, mass=0.1, com=(0.0, 0.0, 0.0), gravity=True, uncertainty=20.0,
-                 optimize_palm=False, device="cuda", seed=0):
+                 optimize_palm=False, device="cuda", seed=0, collision=False):
         self.device = torch.device(device)
         self.ref_q = torch.tensor(list(ref_q)).to(self.device)  # float32 (:634)
         self.robot_model = DifferentiableRobotModel(robot_urdf, device=device)
@@ -67,10 +93,13 @@ class ProbabilisticGraspOptimizer:
         self.pregrasp_weights = torch.tensor(list(pregrasp_weights)).double().to(self.device)
         self.anchor_link_names = anchor_link_names
         self.anchor_link_offsets = anchor_link_offsets
+        self.collision_pairs = [tuple(map(int, pr)) for pr in collision_pairs] if collision_pairs is not None else None
         if collision_pairs is not None:
             cp = torch.tensor(collision_pairs).long().to(self.device)
             self.collision_pair_left, self.collision_pair_right = cp[:, 0], cp[:, 1]
         self.collision_pair_threshold = collision_pair_threshold
+        self.collision = bool(collision)
+        self._collision = None
         self.mass, self.com, self.gravity, self.uncertainty = mass, list(com), gravity, uncertainty
         self._chain_desc = self.robot_model._descriptor(self.ee_link_names, self.ee_link_offsets)
         self._problem = self._problem_state = self._problem_key = None
@@ -88,24 +117,23 @@ class ProbabilisticGraspOptimizer:
         R = euler_angles_to_matrix(palm_poses[:, 3:], convention="XYZ")
         return torch.bmm(R, tips.transpose(1, 2)).transpose(1, 2) + palm_poses[:, :3].unsqueeze(1)
 
+    def collision_descriptor(self):
+        """cdx_collision for the anchor links / pairs given at construction (:626-632)."""
+        if self._collision is None:
+            if self.anchor_link_names is None or self.collision_pairs is None:
+                raise ValueError("compute_collision_loss needs anchor_link_names and collision_pairs")
+            self._collision = build_collision(self.robot_model._descriptor(self.anchor_link_names,
+                                                                           self.anchor_link_offsets),
+                                              self.collision_pairs, self.collision_pair_threshold, self.optimize_palm)
+        return self._collision
+
     def compute_collision_loss(self, joint_angles, palm_poses=None):
-        """Pairwise / floor / palm proximity penalty (:671-701; disabled in the reference closure, :765)."""
+        """Pairwise / floor / palm proximity penalty (:671-701; commented out of the reference
+        closure at :765, enabled here by ``collision=True``), differentiable w.r.t. the joint
+        angles and the palm pose through cdx_collision_loss."""
         if palm_poses is None:
             palm_poses = self.palm_offset
-        anchor = self.robot_model.compute_forward_kinematics(joint_angles.float(), self.anchor_link_names,
-                                                             offsets=self.anchor_link_offsets)[0].double()
-        anchor = anchor.view(-1, len(self.anchor_link_names), 3)
-        R = euler_angles_to_matrix(palm_poses[:, 3:], convention="XYZ")
-        anchor = torch.bmm(R, anchor.transpose(1, 2)).transpose(1, 2) + palm_poses[:, :3].unsqueeze(1)
-        dist = torch.norm(anchor[:, self.collision_pair_left] - anchor[:, self.collision_pair_right], dim=2)
-        inv = torch.where(dist < self.collision_pair_threshold, 1.0 / dist, torch.zeros_like(dist))
-        cost = inv.sum(dim=1)
-        z = anchor[:, :, 2]
-        cost = cost + torch.where(z < 0.02, 0.1 / z, torch.zeros_like(z)).sum(dim=1)
-        if self.optimize_palm:
-            pz = palm_poses[:, 2]
-            cost = cost + torch.where(pz < 0.02, 1 / pz, torch.zeros_like(pz))
-        return cost
+        return _Collision.apply(joint_angles, palm_poses, self.collision_descriptor())
 
     # --------------------------------------------------------------- closure
     def problem(self, gpis, friction_mu):
@@ -130,11 +158,16 @@ class ProbabilisticGraspOptimizer:
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=q.device)
         self._seed += 1
+        stream = N.stream_ptr(q.device)
         N.check(lib.cdx_closure(p, E, N.ptr(q), N.ptr(comp), N.ptr(target), N.ptr(pp), N.ptr(po), N.ptr(noise),
                                 self._seed, N.ptr(self._ws), N.ptr(out["total_loss"]), N.ptr(out["total_margin"]),
                                 N.ptr(out.get("pregrasp_tip")), N.ptr(out["g_q"]), N.ptr(out["g_comp"]),
                                 N.ptr(out["g_target"]), N.ptr(out["g_palm_pos"]), N.ptr(out["g_palm_ori"]),
-                                N.ptr(out.get("flip")), N.stream_ptr(q.device)), "cdx_closure")
+                                N.ptr(out.get("flip")), stream), "cdx_closure")
+        if self.collision:  # total_loss += compute_collision_loss(q, palm) (:765, enabled)
+            N.check(lib.cdx_collision_loss(self.collision_descriptor(), E, N.ptr(q), N.ptr(pp), N.ptr(po),
+                                           N.ptr(out["total_loss"]), N.ptr(out["g_q"]), N.ptr(out["g_palm_pos"]),
+                                           N.ptr(out["g_palm_ori"]), 1, stream), "cdx_collision_loss")
 
     @staticmethod
     def _outputs(E, T, D, K, dev, with_pre=True):

@@ -64,3 +64,20 @@ def build_problem(chain_desc, gpis_desc=None, ref_q=(), coeffs=DEFAULT_COEFFS, w
     p.dummy_comp = float((gravity_acc * mass / M * torch.ones(1))[0])
     p.uncertainty = float(uncertainty)
     return p
+
+
+def build_collision(anchor_chain_desc, pairs, threshold=0.02, palm_term=True, floor_z=0.02):
+    """``cdx_collision`` for compute_collision_loss (optimize_pregrasp.py:671-701): the anchor links
+    as the chain's tips, collision pairs as anchor indices, the 0.02 pair and floor thresholds."""
+    from ._native import MAX_PAIRS, CdxCollision
+    if len(pairs) > MAX_PAIRS:
+        raise ValueError(f"at most {MAX_PAIRS} collision pairs")
+    c = CdxCollision()
+    ctypes.memmove(ctypes.byref(c.chain), ctypes.byref(anchor_chain_desc), ctypes.sizeof(anchor_chain_desc))
+    c.n_pairs = len(pairs)
+    for i, (lft, rgt) in enumerate(pairs):
+        c.pairs[i][0], c.pairs[i][1] = int(lft), int(rgt)
+    c.pair_threshold = float(threshold)
+    c.floor_z = float(floor_z)
+    c.palm_term = int(bool(palm_term))
+    return c

@@ -175,6 +175,32 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                 double* g_q, double* g_comp, double* g_target, double* g_palm_pos,
                 double* g_palm_ori, int32_t* flip, cdx_stream_t stream);
 
+/* ------------------------------------------------------------ collision loss -------
+ * Replaces ProbabilisticGraspOptimizer.compute_collision_loss (optimize_pregrasp.py:671-701):
+ * anchor links by f32 FK (:674-676), palm transform R(euler XYZ)·a + palm_pos (:677-678), then
+ *   Σ_pairs 1/‖a_l − a_r‖ where < pair_threshold (:679-686)
+ * + Σ_anchors (1/z)·0.1 where z < floor_z (:688-691)
+ * + 1/palm_z where palm_z < floor_z, if palm_term (:693-698),
+ * and its gradient w.r.t. q and the palm pose.  The reference's closure leaves the call
+ * commented out (:765); config 4 ("self-collision enabled") turns it on. */
+#define CDX_MAX_PAIRS 28
+
+typedef struct {
+  cdx_chain chain;                      /* anchor links (collision_links + offsets) as tips */
+  int32_t n_pairs;
+  int32_t palm_term;                    /* optimize_palm */
+  int8_t pairs[CDX_MAX_PAIRS][2];       /* anchor indices (collision_pairs) */
+  double pair_threshold;                /* collision_pair_threshold (0.02) */
+  double floor_z;                       /* 0.02 (:688, :694) */
+} cdx_collision;
+
+/* q [E*n_dofs] f64, palm_pos [E*3], palm_ori [E*3] → cost [E], g_q [E*n_dofs], g_palm_pos [E*3],
+ * g_palm_ori [E*3] (gradients of Σ cost).  accumulate = 1 adds into the outputs (fusing the term
+ * into a closure's total_loss and gradients) instead of overwriting them. */
+int cdx_collision_loss(const cdx_collision* c, int64_t E, const double* q, const double* palm_pos,
+                       const double* palm_ori, double* cost, double* g_q, double* g_palm_pos,
+                       double* g_palm_ori, int32_t accumulate, cdx_stream_t stream);
+
 /* ------------------------------------------------------- fused optimizer step ------
  * One launch per iteration of ProbabilisticGraspOptimizer.optimize (optimize_pregrasp.py:805-836)
  * after the closure: best-iterate update (:821-829, before the step, only when s > best_after),
@@ -229,9 +255,10 @@ const char* cdx_version(void);
 int cdx_profile_enable(int on);
 int cdx_profile_read(double* ms5, int64_t* count5);
 
-/* sizeof(cdx_gpis), sizeof(cdx_body), sizeof(cdx_chain), sizeof(cdx_problem) — lets a
- * binding verify its struct layout before the first call. */
-void cdx_abi_sizes(size_t* out4);
+/* sizeof(cdx_gpis), sizeof(cdx_body), sizeof(cdx_chain), sizeof(cdx_problem),
+ * sizeof(cdx_collision), sizeof(cdx_adam), sizeof(cdx_opt_buffers) — lets a binding verify its
+ * struct layouts before the first call. */
+void cdx_abi_sizes(size_t* out7);
 
 /* Test hook: D[16×16] = A[16×4]·B[4×16] through one v_mfma_f64_16x16x4_f64 (checks the
  * fragment layout the GPIS std kernel relies on). */

@@ -69,3 +69,11 @@ def oracle_gpis_at(g, X, with_std):
         gstd, = torch.autograd.grad(std.sum(), Xt)
         out.update(std=std.detach().numpy(), gstd=gstd.numpy())
     return out
+
+
+def collision_desc(hand):
+    """cdx_collision for a packaged hand's collision links / pairs (robot config), palm term on."""
+    from compliancedex_amd.problem import build_collision
+    ch = product_chain(hand)
+    cfg = ch.config
+    return build_collision(ch.descriptor(cfg["collision_links"], cfg["collision_offsets"]), cfg["collision_pairs"])

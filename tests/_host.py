@@ -87,3 +87,13 @@ def sdf_forward(points, faces):
     c = np.zeros((P, 3), np.float32); f = np.zeros(P, np.int32)
     host().cdxh_sdf_forward(p(points), C.c_int64(P), p(faces), C.c_int64(F), p(d), p(s), p(n), p(c), p(f))
     return d, s, n, c, f
+
+
+def collision(desc, q, palm):
+    q = np.ascontiguousarray(q, np.float64)
+    pp, po = np.ascontiguousarray(palm[:, :3]), np.ascontiguousarray(palm[:, 3:])
+    E, D = q.shape
+    cost, g_q = np.zeros(E), np.zeros((E, D))
+    g_pp, g_po = np.zeros((E, 3)), np.zeros((E, 3))
+    host().cdxh_collision(C.byref(desc), C.c_int64(E), p(q), p(pp), p(po), p(cost), p(g_q), p(g_pp), p(g_po))
+    return cost, g_q, np.concatenate([g_pp, g_po], 1)

@@ -20,6 +20,7 @@ Fixtures:
                       total_margin, pregrasp tips and the 5 parameter gradients.
   optimize_<case>.npz ProbabilisticGraspOptimizer.optimize (:771-839) for 30 iterations
                       with a replayed noise sequence.
+  collision_<hand>.npz compute_collision_loss (:671-701) cost and d(Σ cost)/d(q, palm pose).
 """
 from __future__ import annotations
 
@@ -264,11 +265,32 @@ def gen_optimize(ns, name, hand, state, E, seed, iters):
     print("optimize", name)
 
 
+def gen_collision(ns, name, hand, E, seed):
+    """compute_collision_loss (:671-701) with its autograd gradient w.r.t. q and the palm pose.
+    Joint angles are perturbed hard and palm heights drawn low so the pairwise (< 0.02), anchor
+    floor (z < 0.02) and palm floor terms all fire on some candidates."""
+    torch = ns.torch
+    inp = problem_inputs(ns, hand, E, seed, True)
+    rng = np.random.default_rng(seed + 100)
+    q = inp["q"] + 0.6 * rng.standard_normal(inp["q"].shape)
+    palm = inp["palm"].copy()
+    palm[:, 2] = rng.uniform(0.004, 0.09, E)
+    o = make_optimizer(ns, hand, palm, 1)
+    qt = torch.from_numpy(q).clone().requires_grad_(True)
+    pt = torch.from_numpy(palm).clone().requires_grad_(True)
+    with contextlib.redirect_stdout(io.StringIO()):
+        cost = o.compute_collision_loss(qt, pt)
+    cost.sum().backward()
+    np.savez_compressed(os.path.join(OUT, f"collision_{name}.npz"), hand=hand, q=q, palm=palm,
+                        cost=cost.detach().numpy(), grad_q=qt.grad.numpy(), grad_palm=pt.grad.numpy())
+    print("collision", name, int((cost.detach() != 0).sum()), "of", E, "non-zero")
+
+
 def main():
     ns = _refload.load()
     torch = ns.torch
     torch.set_num_threads(8)
-    what = sys.argv[1:] or ["gpis", "fk", "closure", "optimize"]
+    what = sys.argv[1:] or ["gpis", "fk", "closure", "optimize", "collision"]
     if "gpis" in what:
         gen_gpis(ns)
     if "fk" in what:
@@ -282,6 +304,9 @@ def main():
         gen_closure(ns, "allegro_mug_e16_spread", "allegro", "mug", 16, 15, True)
         g, _ = synthetic_banana(ns)
         gen_closure(ns, "allegro_syn2000_e16_spread", "allegro", "synthetic2000", 16, 16, True, gpis_obj=g)
+    if "collision" in what:
+        gen_collision(ns, "allegro_e64", "allegro", 64, 30)
+        gen_collision(ns, "leap_e64", "leap", 64, 31)
     if "optimize" in what:
         gen_optimize(ns, "allegro_banana_e6", "allegro", "banana", 6, 20, 30)
 

@@ -374,3 +374,46 @@ def test_sdf_degenerate_and_autograd():
     d, s, n, c = compute_sdf(x, sph)
     gr, = torch.autograd.grad(d.sum(), x)
     assert torch.allclose(n * 2 * d.sqrt().unsqueeze(1), gr, atol=5e-7)
+
+
+@pytest.mark.parametrize("name", golden_names("collision_"))
+def test_collision_vs_reference(name):
+    """cdx_collision_loss through compute_collision_loss's autograd vs the reference (:671-701)."""
+    d = golden(name)
+    hand = str(d["hand"])
+    opt = _opt(hand, d["palm"])
+    q = torch.from_numpy(d["q"]).to(DEV).requires_grad_(True)
+    palm = torch.from_numpy(d["palm"]).to(DEV).requires_grad_(True)
+    cost = opt.compute_collision_loss(q, palm)
+    cost.sum().backward()
+    c = cost.detach().cpu().numpy()
+    assert np.array_equal(c != 0, d["cost"] != 0)
+    # f32 FK anchors, 1/z and 1/d amplify last-ulp differences near the floor: north-star 1e-4 bar
+    assert rel_err(c, d["cost"]) < 1e-4
+    assert rel_err(q.grad.cpu(), d["grad_q"]) < 1e-4
+    assert rel_err(palm.grad.cpu(), d["grad_palm"]) < 1e-4
+
+
+def test_closure_with_collision_adds_the_collision_term():
+    """collision=True fuses compute_collision_loss into the closure (the reference's commented-out
+    :765): total loss and gradients = closure + collision term, on the same inputs."""
+    c64 = golden("closure_allegro_banana_e64_spread.npz")
+    col = golden("collision_allegro_e64.npz")  # joint angles / palm poses that trigger every term
+    d = {k: c64[k] for k in c64.files}
+    d.update(q=col["q"], palm=col["palm"])
+    base = _closure_gpu(d)
+    opt = _opt("allegro", d["palm"])
+    opt.collision = True
+    fused = _closure_gpu(d, opt=opt)
+    q = torch.from_numpy(d["q"]).to(DEV).requires_grad_(True)
+    palm = torch.from_numpy(d["palm"]).to(DEV).requires_grad_(True)
+    cost = opt.compute_collision_loss(q, palm)
+    cost.sum().backward()
+    c = cost.detach().cpu().numpy()
+    assert (c != 0).sum() > 32
+    assert np.allclose(fused["total_loss"], base["total_loss"] + c, rtol=1e-12, atol=1e-9, equal_nan=True)
+    ok = np.isfinite(base["total_loss"])  # the closure's own NaN candidates stay NaN
+    assert np.allclose(fused["grad_q"][ok], (base["grad_q"] + q.grad.cpu().numpy())[ok], rtol=1e-12, atol=1e-9)
+    gp = palm.grad.cpu().numpy()
+    assert np.allclose(fused["grad_palm_pos"][ok], (base["grad_palm_pos"] + gp[:, :3])[ok], rtol=1e-12, atol=1e-9)
+    assert np.allclose(fused["grad_palm_ori"][ok], (base["grad_palm_ori"] + gp[:, 3:])[ok], rtol=1e-12, atol=1e-9)
