@@ -54,6 +54,11 @@ class CdxCollision(C.Structure):
                 ("pairs", (C.c_int8 * 2) * MAX_PAIRS), ("pair_threshold", C.c_double), ("floor_z", C.c_double)]
 
 
+class CdxForceEq(C.Structure):
+    _fields_ = [("cos_mu", C.c_float), ("gravity", C.c_int32), ("com", C.c_float * 3), ("dummy_target_z", C.c_float),
+                ("dummy_comp", C.c_float), ("n_tips", C.c_int32)]
+
+
 class CdxAdam(C.Structure):
     _fields_ = [("lr", C.c_double * 5), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double),
                 ("comp_min", C.c_double), ("target_lb", C.c_double * (MAX_TIPS * 3)),
@@ -81,6 +86,10 @@ _SIGS = {
     "cdx_gpis_factor": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P]),
     "cdx_fk_forward": (C.c_int, [C.POINTER(CdxChain), _P, _I64, _P, _P, _P]),
     "cdx_fk_backward": (C.c_int, [C.POINTER(CdxChain), _P, _I64, _P, _P, _P]),
+    "cdx_force_eq_forward": (C.c_int, [C.POINTER(CdxForceEq), _I64, _P, _P, _P, _P, _P, C.c_uint64, _P, _P, _P, _P,
+                                       _P]),
+    "cdx_force_eq_backward": (C.c_int, [C.POINTER(CdxForceEq), _I64, _P, _P, _P, _P, _P, C.c_uint64, _P, _P, _P, _P,
+                                        _P, _P]),
     "cdx_collision_loss": (C.c_int, [C.POINTER(CdxCollision), _I64, _P, _P, _P, _P, _P, _P, _P, C.c_int32, _P]),
     "cdx_closure_workspace": (C.c_size_t, [C.POINTER(CdxProblem), _I64]),
     "cdx_closure": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, _P, _P, _P, _P, _P, C.c_uint64, _P,
@@ -119,10 +128,10 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        sizes = (C.c_size_t * 7)()
+        sizes = (C.c_size_t * 8)()
         lib.cdx_abi_sizes(sizes)
         mine = [C.sizeof(CdxGpis), C.sizeof(CdxBody), C.sizeof(CdxChain), C.sizeof(CdxProblem),
-                C.sizeof(CdxCollision), C.sizeof(CdxAdam), C.sizeof(CdxOptBuffers)]
+                C.sizeof(CdxCollision), C.sizeof(CdxAdam), C.sizeof(CdxOptBuffers), C.sizeof(CdxForceEq)]
         if list(sizes) != mine:
             raise ImportError(f"ABI struct size mismatch: library {list(sizes)} vs binding {mine}")
         _lib = lib

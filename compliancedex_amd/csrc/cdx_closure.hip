@@ -150,6 +150,76 @@ __device__ __forceinline__ void device_noise(uint64_t seed, int64_t row, double*
   }
 }
 
+// --------------------------------------------------------------- force_eq_reward
+CDX_HD cdx::ForceEqParams force_eq_params(const cdx_force_eq& p) {
+  cdx::ForceEqParams fp;
+  fp.cos_mu = (double)p.cos_mu;
+  fp.gravity = p.gravity;
+  for (int i = 0; i < 3; ++i) fp.com[i] = (double)p.com[i];
+  fp.dummy_target_z = (double)p.dummy_target_z;
+  fp.dummy_comp = (double)p.dummy_comp;
+  return fp;
+}
+
+template <int NTA>
+__device__ __forceinline__ void force_eq_row(const cdx_force_eq& p, int64_t b, const double* tip,
+                                             const double* target, const double* comp, const double* normal,
+                                             const double* noise, uint64_t seed, cdx::ForceEq<NTA>& fe) {
+  const int T = p.n_tips;
+  double tp[NTA][3], nr[NTA][3], nz[9];
+  for (int f = 0; f < T; ++f)
+    for (int i = 0; i < 3; ++i) { tp[f][i] = tip[(b * T + f) * 3 + i]; nr[f][i] = normal[(b * T + f) * 3 + i]; }
+  if (noise) {
+    for (int i = 0; i < 9; ++i) nz[i] = noise[b * 9 + i];
+  } else {
+    device_noise(seed, b, nz);
+  }
+  fe.forward(force_eq_params(p), T, tp, target + b * T * 3, comp + b * T, nr, nz);
+}
+
+template <int NTA>
+__global__ __launch_bounds__(64) void force_eq_forward_kernel(cdx_force_eq p, int64_t B, const double* __restrict__ tip,
+                                                              const double* __restrict__ target,
+                                                              const double* __restrict__ comp,
+                                                              const double* __restrict__ normal,
+                                                              const double* __restrict__ noise, uint64_t seed,
+                                                              double* __restrict__ reward, double* __restrict__ margin,
+                                                              double* __restrict__ force_norm, int32_t* __restrict__ flip) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  cdx::ForceEq<NTA> fe;
+  force_eq_row<NTA>(p, b, tip, target, comp, normal, noise, seed, fe);
+  const int T = p.n_tips;
+  reward[b] = fe.reward;
+  for (int f = 0; f < T; ++f) { margin[b * T + f] = fe.margin[f]; force_norm[b * T + f] = fe.fn[f]; }
+  if (flip) flip[b] = fe.flip;
+}
+
+template <int NTA>
+__global__ __launch_bounds__(64) void force_eq_backward_kernel(
+    cdx_force_eq p, int64_t B, const double* __restrict__ tip, const double* __restrict__ target,
+    const double* __restrict__ comp, const double* __restrict__ normal, const double* __restrict__ noise, uint64_t seed,
+    const double* __restrict__ g_reward, const double* __restrict__ g_force_norm, double* __restrict__ g_tip,
+    double* __restrict__ g_target, double* __restrict__ g_comp) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  cdx::ForceEq<NTA> fe;
+  force_eq_row<NTA>(p, b, tip, target, comp, normal, noise, seed, fe);
+  const int T = p.n_tips;
+  double gfn[NTA], gt[NTA][3], gg[NTA][3], gc[NTA];
+  for (int f = 0; f < T; ++f) {
+    gfn[f] = g_force_norm ? g_force_norm[b * T + f] : 0.0;
+    gt[f][0] = gt[f][1] = gt[f][2] = 0.0;
+    gg[f][0] = gg[f][1] = gg[f][2] = 0.0;
+    gc[f] = 0.0;
+  }
+  fe.backward(g_reward ? g_reward[b] : 0.0, gfn, comp + b * T, gt, gg, gc);
+  for (int f = 0; f < T; ++f) {
+    for (int i = 0; i < 3; ++i) { g_tip[(b * T + f) * 3 + i] = gt[f][i]; g_target[(b * T + f) * 3 + i] = gg[f][i]; }
+    g_comp[b * T + f] = gc[f];
+  }
+}
+
 template <int NT>
 __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_t E, const double* __restrict__ q,
                                                            const double* __restrict__ comp,
@@ -386,6 +456,41 @@ int cdx_fk_backward(const cdx_chain* chain, const float* q, int64_t B, const flo
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
+int cdx_force_eq_forward(const cdx_force_eq* p, int64_t B, const double* tip, const double* target, const double* comp,
+                         const double* normal, const double* noise, uint64_t seed, double* reward, double* margin,
+                         double* force_norm, int32_t* flip, cdx_stream_t stream) {
+  if (!p || p->n_tips < 1 || p->n_tips > CDX_MAX_TIPS || B < 0) return CDX_EINVAL;
+  if (B == 0) return CDX_OK;
+  if (!tip || !target || !comp || !normal || !reward || !margin || !force_norm) return CDX_EINVAL;
+  const dim3 grid((unsigned)((B + 63) / 64));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (p->n_tips <= 4)
+    hipLaunchKernelGGL(force_eq_forward_kernel<4>, grid, dim3(64), 0, s, *p, B, tip, target, comp, normal, noise, seed,
+                       reward, margin, force_norm, flip);
+  else
+    hipLaunchKernelGGL(force_eq_forward_kernel<CDX_MAX_TIPS>, grid, dim3(64), 0, s, *p, B, tip, target, comp, normal,
+                       noise, seed, reward, margin, force_norm, flip);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+int cdx_force_eq_backward(const cdx_force_eq* p, int64_t B, const double* tip, const double* target, const double* comp,
+                          const double* normal, const double* noise, uint64_t seed, const double* g_reward,
+                          const double* g_force_norm, double* g_tip, double* g_target, double* g_comp,
+                          cdx_stream_t stream) {
+  if (!p || p->n_tips < 1 || p->n_tips > CDX_MAX_TIPS || B < 0) return CDX_EINVAL;
+  if (B == 0) return CDX_OK;
+  if (!tip || !target || !comp || !normal || !g_tip || !g_target || !g_comp) return CDX_EINVAL;
+  const dim3 grid((unsigned)((B + 63) / 64));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (p->n_tips <= 4)
+    hipLaunchKernelGGL(force_eq_backward_kernel<4>, grid, dim3(64), 0, s, *p, B, tip, target, comp, normal, noise, seed,
+                       g_reward, g_force_norm, g_tip, g_target, g_comp);
+  else
+    hipLaunchKernelGGL(force_eq_backward_kernel<CDX_MAX_TIPS>, grid, dim3(64), 0, s, *p, B, tip, target, comp, normal,
+                       noise, seed, g_reward, g_force_norm, g_tip, g_target, g_comp);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
 int cdx_collision_loss(const cdx_collision* c, int64_t E, const double* q, const double* palm_pos,
                        const double* palm_ori, double* cost, double* g_q, double* g_palm_pos, double* g_palm_ori,
                        int32_t accumulate, cdx_stream_t stream) {
@@ -530,4 +635,5 @@ extern "C" void cdx_abi_sizes(size_t* out) {
   out[4] = sizeof(cdx_collision);
   out[5] = sizeof(cdx_adam);
   out[6] = sizeof(cdx_opt_buffers);
+  out[7] = sizeof(cdx_force_eq);
 }

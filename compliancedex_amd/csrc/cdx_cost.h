@@ -220,58 +220,61 @@ struct CandidateOut {
   int flip[CDX_MAX_LEVELS];
 };
 
-// One pregrasp level of compute_loss (:713-739) for one candidate, forward AND backward with
-// dL/dl_k = w_k: returns l_k, margin_k, the Kabsch mask and the level's gradient w.r.t. the
-// pregrasp tips, targets and compliances.  NT = fingertip count at compile time (0: runtime).
-struct LevelOut {
-  double l;
-  double margin[CDX_MAX_TIPS];
-  double g_tip[CDX_MAX_TIPS][3];
-  double g_target[CDX_MAX_TIPS][3];
-  double g_comp[CDX_MAX_TIPS];
-  int flip;
+// ------------------------------------------------------------ force_eq_reward
+// force_eq_reward (:73-118) with optimal_transformation_batch (:49-69) for one row: the weighted
+// Kabsch fit of [tips, dummy] onto [targets, dummy] (dummy gravity spring: tip = COM, target z = −M,
+// weight gravity·mass/M, all float32 tensors in the reference), equilibrium tips, friction-cone
+// margin clamp(ang − cos_mu, −0.9999) and reward Σ 0.2·log(ang+1) + 0.8·log(margin+1).  forward()
+// keeps the tape; backward() takes dL/dreward and dL/dforce_norm and ACCUMULATES into the tip,
+// target and compliance gradients (normals are detached, as every caller passes them).
+struct ForceEqParams {
+  double cos_mu;
+  int gravity;
+  double com[3];
+  double dummy_target_z;
+  double dummy_comp;
 };
 
-template <int NT, typename GpisAt>
-CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, const double (*tip)[3], double qnorm,
-                          GpisAt gp, LevelOut& o) {
-  constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
-  const int T = NT > 0 ? NT : P.chain.n_tips;
-  const double cos_mu = (double)P.cos_mu;
-  for (int f = 0; f < T; ++f) {
-    for (int i = 0; i < 3; ++i) { o.g_target[f][i] = 0.0; o.g_tip[f][i] = 0.0; }
-    o.g_comp[f] = 0.0;
-  }
-    const int u = P.level_query[k];
-    const double wk = P.weight[k];
-    // ---- forward of compute_loss for this level
-    double a[NTA][3], d[NTA], s[NTA], n[NTA][3], td[NTA];
+CDX_HD ForceEqParams force_eq_params(const cdx_problem& P) {
+  ForceEqParams fp;
+  fp.cos_mu = (double)P.cos_mu;
+  fp.gravity = P.gravity;
+  for (int i = 0; i < 3; ++i) fp.com[i] = (double)P.com[i];
+  fp.dummy_target_z = (double)P.dummy_target_z;
+  fp.dummy_comp = (double)P.dummy_comp;
+  return fp;
+}
+
+template <int NTA>
+struct ForceEq {
+  int T, NP;
+  double S1[NTA + 1][3], S2[NTA + 1][3], w[NTA + 1], n[NTA][3];
+  double c1[3], c2[3], Pm[NTA + 1][3], Qm[NTA + 1][3];
+  KabschTape tp;
+  double R[9], W, t[3], RS1[NTA + 1][3];
+  double diff[NTA][3], dn[NTA], dir[NTA][3], ne[NTA][3], ang[NTA], mpre[NTA], margin[NTA], fn[NTA];
+  double force[NTA][3];
+  double reward;
+  int flip;
+
+  CDX_HDM void forward(const ForceEqParams& fp, int T_, const double (*tip)[3], const double* target,
+                      const double* comp, const double (*nrm)[3], const double* noise) {
+    T = T_;
+    NP = fp.gravity ? T + 1 : T;
     for (int f = 0; f < T; ++f) {
-      const double c = (double)P.coeff[k][f];
-      for (int i = 0; i < 3; ++i) a[f][i] = in.target[3 * f + i] + c * (tip[f][i] - in.target[3 * f + i]);
-      const GpisPoint& ga = gp(0, u, f);
-      d[f] = ga.mean;
-      s[f] = ga.std;
-      for (int i = 0; i < 3; ++i) n[f][i] = ga.normal[i];
-      td[f] = gp(1, 0, f).mean;
+      for (int i = 0; i < 3; ++i) { S1[f][i] = tip[f][i]; S2[f][i] = target[3 * f + i]; n[f][i] = nrm[f][i]; }
+      w[f] = comp[f];
     }
-    // Kabsch on [tips, dummy] / [targets, dummy] with weights [comp, dummy_comp]
-    const int NP = P.gravity ? T + 1 : T;
-    double S1[NTA + 1][3], S2[NTA + 1][3], w[NTA + 1];
-    for (int f = 0; f < T; ++f) {
-      for (int i = 0; i < 3; ++i) { S1[f][i] = a[f][i]; S2[f][i] = in.target[3 * f + i]; }
-      w[f] = in.comp[f];
+    if (fp.gravity) {
+      for (int i = 0; i < 3; ++i) S1[T][i] = fp.com[i];
+      S2[T][0] = 0.0; S2[T][1] = 0.0; S2[T][2] = fp.dummy_target_z;
+      w[T] = fp.dummy_comp;
     }
-    if (P.gravity) {
-      for (int i = 0; i < 3; ++i) S1[T][i] = (double)P.com[i];
-      S2[T][0] = 0.0; S2[T][1] = 0.0; S2[T][2] = (double)P.dummy_target_z;
-      w[T] = (double)P.dummy_comp;
-    }
-    double c1[3] = {0, 0, 0}, c2[3] = {0, 0, 0};
+    c1[0] = c1[1] = c1[2] = 0.0;
+    c2[0] = c2[1] = c2[2] = 0.0;
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { c1[j] += S1[i][j]; c2[j] += S2[i][j]; }
     for (int j = 0; j < 3; ++j) { c1[j] /= NP; c2[j] /= NP; }
-    double Pm[NTA + 1][3], Qm[NTA + 1][3];
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { Pm[i][j] = w[i] * (S1[i][j] - c1[j]); Qm[i][j] = w[i] * (S2[i][j] - c2[j]); }
     double H[9];
@@ -281,108 +284,32 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
         for (int i = 0; i < NP; ++i) acc += Pm[i][r] * Qm[i][c];
         H[3 * r + c] = acc;
       }
-    KabschTape tp;
-    double R[9];
-    kabsch_rotation(H, in.noise + k * in.noise_stride, tp, R);
-    o.flip = tp.d < 0 ? 1 : 0;
-    double W = 0.0, num[3] = {0, 0, 0}, RS1[NTA + 1][3];
+    kabsch_rotation(H, noise, tp, R);
+    flip = tp.d < 0 ? 1 : 0;
+    W = 0.0;
+    double num[3] = {0, 0, 0};
     for (int i = 0; i < NP; ++i) {
       W += w[i];
       mat3_vec(R, S1[i], RS1[i]);
       for (int j = 0; j < 3; ++j) num[j] += w[i] * (S2[i][j] - RS1[i][j]);
     }
-    double t[3] = {num[0] / W, num[1] / W, num[2] / W};
-    double diff[NTA][3], dn[NTA], dir[NTA][3], ne[NTA][3];
-    double ang[NTA], mpre[NTA], margin[NTA], fn[NTA], force[NTA][3];
-    double reward = 0.0;
+    for (int j = 0; j < 3; ++j) t[j] = num[j] / W;
+    reward = 0.0;
     for (int f = 0; f < T; ++f) {
-      for (int i = 0; i < 3; ++i) diff[f][i] = RS1[f][i] + t[i] - in.target[3 * f + i];
+      for (int i = 0; i < 3; ++i) diff[f][i] = RS1[f][i] + t[i] - target[3 * f + i];
       dn[f] = sqrt(dot3(diff[f], diff[f]));
-      for (int i = 0; i < 3; ++i) { dir[f][i] = diff[f][i] / dn[f]; force[f][i] = in.comp[f] * (-diff[f][i]); }
+      for (int i = 0; i < 3; ++i) { dir[f][i] = diff[f][i] / dn[f]; force[f][i] = comp[f] * (-diff[f][i]); }
       mat3_vec(R, n[f], ne[f]);
       ang[f] = dot3(dir[f], ne[f]);
-      mpre[f] = ang[f] - cos_mu;
+      mpre[f] = ang[f] - fp.cos_mu;
       margin[f] = mpre[f] < -0.9999 ? -0.9999 : mpre[f];
       fn[f] = sqrt(dot3(force[f], force[f]));
       reward += 0.2 * log(ang[f] + 1) + 0.8 * log(margin[f] + 1);
     }
-    // contact margin (unclamped)
-    double cd[NTA][3], cdn[NTA], cdir[NTA][3], cang[NTA];
-    double creward = 0.0;
-    for (int f = 0; f < T; ++f) {
-      for (int i = 0; i < 3; ++i) cd[f][i] = a[f][i] - in.target[3 * f + i];
-      cdn[f] = sqrt(dot3(cd[f], cd[f]));
-      for (int i = 0; i < 3; ++i) cdir[f][i] = cd[f][i] / cdn[f];
-      cang[f] = dot3(cdir[f], n[f]);
-      creward += 0.1 * log(cang[f] + 1) + 0.9 * log(cang[f] - cos_mu + 1);
-    }
-    // force cost: −Σ clamp(fn·softmin(fn), max=10)
-    double zmax = -fn[0];
-    for (int f = 1; f < T; ++f) zmax = -fn[f] > zmax ? -fn[f] : zmax;
-    double ez[NTA], esum = 0.0;
-    for (int f = 0; f < T; ++f) { ez[f] = exp(-fn[f] - zmax); esum += ez[f]; }
-    double sm[NTA], v[NTA], fcost = 0.0;
-    for (int f = 0; f < T; ++f) {
-      sm[f] = ez[f] / esum;
-      v[f] = fn[f] * sm[f];
-      fcost += v[f] > 10.0 ? 10.0 : v[f];
-    }
-    fcost = -fcost;
-    // variance cost: uncertainty · max_f log(100 std)
-    int fmax = 0;
-    double lmax = log(100 * s[0]);
-    for (int f = 1; f < T; ++f) {
-      const double lv = log(100 * s[f]);
-      if (lv > lmax) { lmax = lv; fmax = f; }
-    }
-    double dcost = 0.0, tcost = 0.0;
-    for (int f = 0; f < T; ++f) { dcost += fabs(d[f]); tcost += td[f]; }
-    const double l = -reward * 200.0 + 1000 * dcost + 20 * tcost + (-creward * 200.0) + fcost + qnorm * 10.0 +
-                     P.uncertainty * lmax;
-    o.l = l;
-    for (int f = 0; f < T; ++f) o.margin[f] = margin[f];
+  }
 
-    // ---- backward of this level with dL/dl = wk
-    double g_a[NTA][3];
-    for (int f = 0; f < T; ++f) g_a[f][0] = g_a[f][1] = g_a[f][2] = 0.0;
-    // dist / tar_dist / variance (GPIS gradients at the query points)
-    for (int f = 0; f < T; ++f) {
-      const GpisPoint& ga = gp(0, u, f);
-      const double sg = d[f] > 0 ? 1.0 : (d[f] < 0 ? -1.0 : 0.0);
-      const double gd = wk * 1000.0 * sg;
-      for (int i = 0; i < 3; ++i) g_a[f][i] += gd * ga.gmean[i];
-      const GpisPoint& gt = gp(1, 0, f);
-      for (int i = 0; i < 3; ++i) o.g_target[f][i] += wk * 20.0 * gt.gmean[i];
-    }
-    {
-      const GpisPoint& ga = gp(0, u, fmax);
-      const double gs = wk * P.uncertainty / s[fmax];
-      for (int i = 0; i < 3; ++i) g_a[fmax][i] += gs * ga.gstd[i];
-    }
-    // force cost
-    double g_fn[NTA], g_sm[NTA];
-    double gsm_dot = 0.0;
-    for (int f = 0; f < T; ++f) {
-      const double gv = v[f] <= 10.0 ? -wk : 0.0;
-      g_fn[f] = gv * sm[f];
-      g_sm[f] = gv * fn[f];
-      gsm_dot += g_sm[f] * sm[f];
-    }
-    for (int f = 0; f < T; ++f) g_fn[f] += -(sm[f] * (g_sm[f] - gsm_dot));
-    // contact margin reward (gain −200·wk)
-    const double g_cr = -200.0 * wk;
-    for (int f = 0; f < T; ++f) {
-      const double gcang = g_cr * (0.1 / (cang[f] + 1) + 0.9 / (cang[f] - cos_mu + 1));
-      double gdir[3] = {gcang * n[f][0], gcang * n[f][1], gcang * n[f][2]};
-      const double pd = dot3(cdir[f], gdir);
-      for (int i = 0; i < 3; ++i) {
-        const double gcd = (gdir[i] - cdir[f][i] * pd) / cdn[f];
-        g_a[f][i] += gcd;
-        o.g_target[f][i] -= gcd;
-      }
-    }
-    // force_eq reward (gain −200·wk) + force norms
-    const double g_rw = -200.0 * wk;
+  CDX_HDM void backward(double g_rw, const double* g_fn, const double* comp, double (*g_tip)[3], double (*g_target)[3],
+                       double* g_comp) const {
     double gR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g_t[3] = {0, 0, 0};
     double g_S1[NTA + 1][3], g_S2[NTA + 1][3], g_w[NTA + 1];
     for (int i = 0; i < NP; ++i) { g_S1[i][0] = g_S1[i][1] = g_S1[i][2] = 0; g_S2[i][0] = g_S2[i][1] = g_S2[i][2] = 0; g_w[i] = 0; }
@@ -395,7 +322,7 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
         double gforce[3];
         for (int i = 0; i < 3; ++i) gforce[i] = g_fn[f] * force[f][i] / fn[f];
         g_w[f] += -dot3(gforce, diff[f]);
-        for (int i = 0; i < 3; ++i) gdiff[i] += -in.comp[f] * gforce[i];
+        for (int i = 0; i < 3; ++i) gdiff[i] += -comp[f] * gforce[i];
       }
       // ang = dir·ne ; ne = R·n (n detached)
       double gdir[3], gne[3];
@@ -405,7 +332,7 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
       const double pd = dot3(dir[f], gdir);
       for (int i = 0; i < 3; ++i) gdiff[i] += (gdir[i] - dir[f][i] * pd) / dn[f];
       // diff = R·S1_f + t − target_f
-      for (int i = 0; i < 3; ++i) { g_t[i] += gdiff[i]; o.g_target[f][i] -= gdiff[i]; }
+      for (int i = 0; i < 3; ++i) { g_t[i] += gdiff[i]; g_target[f][i] -= gdiff[i]; }
       for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) gR[3 * r + c] += gdiff[r] * S1[f][c];
       double rt[3];
@@ -448,18 +375,137 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { g_S1[i][j] += g_c1[j] / NP; g_S2[i][j] += g_c2[j] / NP; }
     for (int f = 0; f < T; ++f) {
-      for (int i = 0; i < 3; ++i) { g_a[f][i] += g_S1[f][i]; o.g_target[f][i] += g_S2[f][i]; }
-      o.g_comp[f] += g_w[f];
-    }
-    // all-tip interpolation a = target + c·(tip − target)
-    for (int f = 0; f < T; ++f) {
-      const double c = (double)P.coeff[k][f];
-      for (int i = 0; i < 3; ++i) {
-        o.g_tip[f][i] = c * g_a[f][i];
-        o.g_target[f][i] += g_a[f][i] - c * g_a[f][i];
-      }
+      for (int i = 0; i < 3; ++i) { g_tip[f][i] += g_S1[f][i]; g_target[f][i] += g_S2[f][i]; }
+      g_comp[f] += g_w[f];
     }
   }
+};
+
+// One pregrasp level of compute_loss (:713-739) for one candidate, forward AND backward with
+// dL/dl_k = w_k: returns l_k, margin_k, the Kabsch mask and the level's gradient w.r.t. the
+// pregrasp tips, targets and compliances.  NT = fingertip count at compile time (0: runtime).
+struct LevelOut {
+  double l;
+  double margin[CDX_MAX_TIPS];
+  double g_tip[CDX_MAX_TIPS][3];
+  double g_target[CDX_MAX_TIPS][3];
+  double g_comp[CDX_MAX_TIPS];
+  int flip;
+};
+
+template <int NT, typename GpisAt>
+CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, const double (*tip)[3], double qnorm,
+                          GpisAt gp, LevelOut& o) {
+  constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
+  const int T = NT > 0 ? NT : P.chain.n_tips;
+  const double cos_mu = (double)P.cos_mu;
+  for (int f = 0; f < T; ++f) {
+    for (int i = 0; i < 3; ++i) { o.g_target[f][i] = 0.0; o.g_tip[f][i] = 0.0; }
+    o.g_comp[f] = 0.0;
+  }
+  const int u = P.level_query[k];
+  const double wk = P.weight[k];
+  // ---- forward of compute_loss for this level
+  double a[NTA][3], d[NTA], s[NTA], n[NTA][3], td[NTA];
+  for (int f = 0; f < T; ++f) {
+    const double c = (double)P.coeff[k][f];
+    for (int i = 0; i < 3; ++i) a[f][i] = in.target[3 * f + i] + c * (tip[f][i] - in.target[3 * f + i]);
+    const GpisPoint& ga = gp(0, u, f);
+    d[f] = ga.mean;
+    s[f] = ga.std;
+    for (int i = 0; i < 3; ++i) n[f][i] = ga.normal[i];
+    td[f] = gp(1, 0, f).mean;
+  }
+  ForceEq<NTA> fe;
+  fe.forward(force_eq_params(P), T, a, in.target, in.comp, n, in.noise + k * in.noise_stride);
+  o.flip = fe.flip;
+  // contact margin (unclamped)
+  double cd[NTA][3], cdn[NTA], cdir[NTA][3], cang[NTA];
+  double creward = 0.0;
+  for (int f = 0; f < T; ++f) {
+    for (int i = 0; i < 3; ++i) cd[f][i] = a[f][i] - in.target[3 * f + i];
+    cdn[f] = sqrt(dot3(cd[f], cd[f]));
+    for (int i = 0; i < 3; ++i) cdir[f][i] = cd[f][i] / cdn[f];
+    cang[f] = dot3(cdir[f], n[f]);
+    creward += 0.1 * log(cang[f] + 1) + 0.9 * log(cang[f] - cos_mu + 1);
+  }
+  // force cost: −Σ clamp(fn·softmin(fn), max=10)
+  const double* fn = fe.fn;
+  double zmax = -fn[0];
+  for (int f = 1; f < T; ++f) zmax = -fn[f] > zmax ? -fn[f] : zmax;
+  double ez[NTA], esum = 0.0;
+  for (int f = 0; f < T; ++f) { ez[f] = exp(-fn[f] - zmax); esum += ez[f]; }
+  double sm[NTA], v[NTA], fcost = 0.0;
+  for (int f = 0; f < T; ++f) {
+    sm[f] = ez[f] / esum;
+    v[f] = fn[f] * sm[f];
+    fcost += v[f] > 10.0 ? 10.0 : v[f];
+  }
+  fcost = -fcost;
+  // variance cost: uncertainty · max_f log(100 std)
+  int fmax = 0;
+  double lmax = log(100 * s[0]);
+  for (int f = 1; f < T; ++f) {
+    const double lv = log(100 * s[f]);
+    if (lv > lmax) { lmax = lv; fmax = f; }
+  }
+  double dcost = 0.0, tcost = 0.0;
+  for (int f = 0; f < T; ++f) { dcost += fabs(d[f]); tcost += td[f]; }
+  const double l = -fe.reward * 200.0 + 1000 * dcost + 20 * tcost + (-creward * 200.0) + fcost + qnorm * 10.0 +
+                   P.uncertainty * lmax;
+  o.l = l;
+  for (int f = 0; f < T; ++f) o.margin[f] = fe.margin[f];
+
+  // ---- backward of this level with dL/dl = wk
+  double g_a[NTA][3];
+  for (int f = 0; f < T; ++f) g_a[f][0] = g_a[f][1] = g_a[f][2] = 0.0;
+  // dist / tar_dist / variance (GPIS gradients at the query points)
+  for (int f = 0; f < T; ++f) {
+    const GpisPoint& ga = gp(0, u, f);
+    const double sg = d[f] > 0 ? 1.0 : (d[f] < 0 ? -1.0 : 0.0);
+    const double gd = wk * 1000.0 * sg;
+    for (int i = 0; i < 3; ++i) g_a[f][i] += gd * ga.gmean[i];
+    const GpisPoint& gt = gp(1, 0, f);
+    for (int i = 0; i < 3; ++i) o.g_target[f][i] += wk * 20.0 * gt.gmean[i];
+  }
+  {
+    const GpisPoint& ga = gp(0, u, fmax);
+    const double gs = wk * P.uncertainty / s[fmax];
+    for (int i = 0; i < 3; ++i) g_a[fmax][i] += gs * ga.gstd[i];
+  }
+  // force cost
+  double g_fn[NTA], g_sm[NTA];
+  double gsm_dot = 0.0;
+  for (int f = 0; f < T; ++f) {
+    const double gv = v[f] <= 10.0 ? -wk : 0.0;
+    g_fn[f] = gv * sm[f];
+    g_sm[f] = gv * fn[f];
+    gsm_dot += g_sm[f] * sm[f];
+  }
+  for (int f = 0; f < T; ++f) g_fn[f] += -(sm[f] * (g_sm[f] - gsm_dot));
+  // contact margin reward (gain −200·wk)
+  const double g_cr = -200.0 * wk;
+  for (int f = 0; f < T; ++f) {
+    const double gcang = g_cr * (0.1 / (cang[f] + 1) + 0.9 / (cang[f] - cos_mu + 1));
+    double gdir[3] = {gcang * n[f][0], gcang * n[f][1], gcang * n[f][2]};
+    const double pd = dot3(cdir[f], gdir);
+    for (int i = 0; i < 3; ++i) {
+      const double gcd = (gdir[i] - cdir[f][i] * pd) / cdn[f];
+      g_a[f][i] += gcd;
+      o.g_target[f][i] -= gcd;
+    }
+  }
+  // force_eq reward (gain −200·wk) + force norms
+  fe.backward(-200.0 * wk, g_fn, in.comp, g_a, o.g_target, o.g_comp);
+  // all-tip interpolation a = target + c·(tip − target)
+  for (int f = 0; f < T; ++f) {
+    const double c = (double)P.coeff[k][f];
+    for (int i = 0; i < 3; ++i) {
+      o.g_tip[f][i] = c * g_a[f][i];
+      o.g_target[f][i] += g_a[f][i] - c * g_a[f][i];
+    }
+  }
+}
 
 // Forward + backward of Σ_levels w_k·l_k − 5·Σ pre_dist + 1/palm_dist for one candidate.
 // gp(kind, level_or_0, finger) returns the GPIS results at the corresponding query.

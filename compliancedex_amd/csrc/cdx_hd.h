@@ -9,8 +9,10 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define CDX_HD __host__ __device__ __forceinline__
+#define CDX_HDM __host__ __device__ __forceinline__  // member functions
 #else
 #define CDX_HD static inline
+#define CDX_HDM inline
 #endif
 
 #include "../../include/cdx.h"

@@ -119,6 +119,35 @@ void cdxh_collision(const cdx_collision* C, int64_t E, const double* q, const do
     cdx::collision_candidate(*C, q + e * D, pp + 3 * e, po + 3 * e, cost[e], g_q + e * D, g_pp + 3 * e, g_po + 3 * e);
 }
 
+void cdxh_force_eq(const cdx_force_eq* p, int64_t B, const double* tip, const double* target, const double* comp,
+                   const double* normal, const double* noise, const double* g_reward, const double* g_fn,
+                   double* reward, double* margin, double* fn, int32_t* flip, double* g_tip, double* g_target,
+                   double* g_comp) {
+  cdx::ForceEqParams fp;
+  fp.cos_mu = (double)p->cos_mu;
+  fp.gravity = p->gravity;
+  for (int i = 0; i < 3; ++i) fp.com[i] = (double)p->com[i];
+  fp.dummy_target_z = (double)p->dummy_target_z;
+  fp.dummy_comp = (double)p->dummy_comp;
+  const int T = p->n_tips;
+  for (int64_t b = 0; b < B; ++b) {
+    double tp[CDX_MAX_TIPS][3], nr[CDX_MAX_TIPS][3];
+    for (int f = 0; f < T; ++f)
+      for (int i = 0; i < 3; ++i) { tp[f][i] = tip[(b * T + f) * 3 + i]; nr[f][i] = normal[(b * T + f) * 3 + i]; }
+    cdx::ForceEq<CDX_MAX_TIPS> fe;
+    fe.forward(fp, T, tp, target + b * T * 3, comp + b * T, nr, noise + b * 9);
+    reward[b] = fe.reward;
+    flip[b] = fe.flip;
+    double gt[CDX_MAX_TIPS][3] = {}, gg[CDX_MAX_TIPS][3] = {}, gc[CDX_MAX_TIPS] = {};
+    for (int f = 0; f < T; ++f) { margin[b * T + f] = fe.margin[f]; fn[b * T + f] = fe.fn[f]; }
+    fe.backward(g_reward[b], g_fn + b * T, comp + b * T, gt, gg, gc);
+    for (int f = 0; f < T; ++f) {
+      for (int i = 0; i < 3; ++i) { g_tip[(b * T + f) * 3 + i] = gt[f][i]; g_target[(b * T + f) * 3 + i] = gg[f][i]; }
+      g_comp[b * T + f] = gc[f];
+    }
+  }
+}
+
 void cdxh_svd3(const double* H, double* U, double* S, double* V) { cdx::svd3(H, U, S, V); }
 
 void cdxh_sdf_forward(const float* points, int64_t P, const float* faces, int64_t F, float* dist, int32_t* sign,

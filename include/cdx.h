@@ -175,6 +175,34 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                 double* g_q, double* g_comp, double* g_target, double* g_palm_pos,
                 double* g_palm_ori, int32_t* flip, cdx_stream_t stream);
 
+/* ------------------------------------------------------------ force_eq_reward ------
+ * Replaces force_eq_reward (optimize_pregrasp.py:73-118) with optimal_transformation_batch
+ * (:49-69) where the SDF / Kin / GPIS / KinGPIS optimisers (:121-513) call it directly, in f64.
+ * Rows are independent: tip, target, normal [B*n_tips*3], comp [B*n_tips]; noise [B*9] is the
+ * rand_like(H) draw (:61), or NULL for the on-device counter-based draw keyed by (seed, row) —
+ * backward must get the same noise / seed as forward.  normal is detached (every caller passes
+ * GPIS/SDF normals without a graph). */
+typedef struct {
+  float cos_mu;          /* sqrt(1/(1+mu²)) in f32 (:111) */
+  int32_t gravity;       /* dummy gravity spring (gravity is not None, :87-97) */
+  float com[3];          /* dummy tip = COM (f32 tensor, :90-91) */
+  float dummy_target_z;  /* -M (:93) */
+  float dummy_comp;      /* gravity·mass/M (f32, :94) */
+  int32_t n_tips;
+} cdx_force_eq;
+
+/* → reward [B], margin [B*n_tips] (clamped, :112), force_norm [B*n_tips], flip [B] (nullable). */
+int cdx_force_eq_forward(const cdx_force_eq* p, int64_t B, const double* tip, const double* target,
+                         const double* comp, const double* normal, const double* noise, uint64_t seed,
+                         double* reward, double* margin, double* force_norm, int32_t* flip,
+                         cdx_stream_t stream);
+/* Vector-Jacobian product: g_reward [B], g_force_norm [B*n_tips] (either nullable = 0) →
+ * g_tip, g_target [B*n_tips*3], g_comp [B*n_tips] (overwritten). */
+int cdx_force_eq_backward(const cdx_force_eq* p, int64_t B, const double* tip, const double* target,
+                          const double* comp, const double* normal, const double* noise, uint64_t seed,
+                          const double* g_reward, const double* g_force_norm, double* g_tip,
+                          double* g_target, double* g_comp, cdx_stream_t stream);
+
 /* ------------------------------------------------------------ collision loss -------
  * Replaces ProbabilisticGraspOptimizer.compute_collision_loss (optimize_pregrasp.py:671-701):
  * anchor links by f32 FK (:674-676), palm transform R(euler XYZ)·a + palm_pos (:677-678), then
@@ -256,9 +284,9 @@ int cdx_profile_enable(int on);
 int cdx_profile_read(double* ms5, int64_t* count5);
 
 /* sizeof(cdx_gpis), sizeof(cdx_body), sizeof(cdx_chain), sizeof(cdx_problem),
- * sizeof(cdx_collision), sizeof(cdx_adam), sizeof(cdx_opt_buffers) — lets a binding verify its
- * struct layouts before the first call. */
-void cdx_abi_sizes(size_t* out7);
+ * sizeof(cdx_collision), sizeof(cdx_adam), sizeof(cdx_opt_buffers), sizeof(cdx_force_eq) — lets
+ * a binding verify its struct layouts before the first call. */
+void cdx_abi_sizes(size_t* out8);
 
 /* Test hook: D[16×16] = A[16×4]·B[4×16] through one v_mfma_f64_16x16x4_f64 (checks the
  * fragment layout the GPIS std kernel relies on). */

@@ -97,3 +97,15 @@ def collision(desc, q, palm):
     g_pp, g_po = np.zeros((E, 3)), np.zeros((E, 3))
     host().cdxh_collision(C.byref(desc), C.c_int64(E), p(q), p(pp), p(po), p(cost), p(g_q), p(g_pp), p(g_po))
     return cost, g_q, np.concatenate([g_pp, g_po], 1)
+
+
+def force_eq(desc, tip, target, comp, normal, noise, g_reward, g_fn):
+    B, T = comp.shape
+    a = [np.ascontiguousarray(x, np.float64) for x in (tip, target, comp, normal, noise, g_reward, g_fn)]
+    reward, margin, fn = np.zeros(B), np.zeros((B, T)), np.zeros((B, T))
+    flip = np.zeros(B, np.int32)
+    g_tip, g_target, g_comp = np.zeros((B, T, 3)), np.zeros((B, T, 3)), np.zeros((B, T))
+    host().cdxh_force_eq(C.byref(desc), C.c_int64(B), *(p(x) for x in a), p(reward), p(margin), p(fn), p(flip),
+                         p(g_tip), p(g_target), p(g_comp))
+    return dict(reward=reward, margin=margin, force_norm=fn, flip=flip, grad_tip=g_tip, grad_target=g_target,
+                grad_comp=g_comp)

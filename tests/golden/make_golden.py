@@ -21,6 +21,10 @@ Fixtures:
   optimize_<case>.npz ProbabilisticGraspOptimizer.optimize (:771-839) for 30 iterations
                       with a replayed noise sequence.
   collision_<hand>.npz compute_collision_loss (:671-701) cost and d(Σ cost)/d(q, palm pose).
+  force_eq_<case>.npz force_eq_reward (:73-118) outputs and input gradients, noise captured.
+  mode_<mode>.npz     GPIS / KinGPIS / SDF / Kin optimisers (:121-511), 12 iterations, E = 6: final
+                      outputs and the per-iteration Σ loss (TorchSDF via the C oracle, whose _C
+                      module the reference lacks).
 """
 from __future__ import annotations
 
@@ -265,6 +269,140 @@ def gen_optimize(ns, name, hand, state, E, seed, iters):
     print("optimize", name)
 
 
+def gen_force_eq(ns, name, B, seed, gravity, mu, mass=0.1, com=(0.0, 0.0, 0.0)):
+    """force_eq_reward (:73-118) on seeded rows: reward, margin, force_norm and
+    d(Σ cr·reward + Σ cf·force_norm)/d(tip, target, compliance); Kabsch noise captured.  Half the
+    rows put the tips close to their targets (near-rank-1 H, as at the optimisers' start)."""
+    torch = ns.torch
+    rng = np.random.default_rng(seed)
+    T = 4
+    target = 0.05 * rng.standard_normal((B, T, 3))
+    tip = target + 0.03 * rng.standard_normal((B, T, 3))
+    tip[: B // 2] = target[: B // 2] + 1e-3 * rng.standard_normal((B // 2, T, 3))
+    comp = rng.uniform(10.0, 200.0, (B, T))
+    normal = rng.standard_normal((B, T, 3))
+    normal /= np.linalg.norm(normal, axis=2, keepdims=True)
+    cr, cf = rng.standard_normal(B), rng.standard_normal((B, T))
+    tt = torch.from_numpy(tip).clone().requires_grad_(True)
+    gt = torch.from_numpy(target).clone().requires_grad_(True)
+    ct = torch.from_numpy(comp).clone().requires_grad_(True)
+    with NoiseTape(torch, seed=seed) as tape:
+        reward, margin, fn = ns.opt.force_eq_reward(tt, gt, ct, mu, torch.from_numpy(normal), mass=mass,
+                                                    gravity=10.0 if gravity else None, COM=list(com))
+    ((reward * torch.from_numpy(cr)).sum() + (fn * torch.from_numpy(cf)).sum()).backward()
+    np.savez_compressed(os.path.join(OUT, f"force_eq_{name}.npz"), tip=tip, target=target, comp=comp, normal=normal,
+                        noise=torch.stack(tape.record).numpy().reshape(B, 9), gravity=gravity, mu=mu, mass=mass,
+                        com=np.asarray(com), cr=cr, cf=cf, reward=reward.detach().numpy(),
+                        margin=margin.detach().numpy(), force_norm=fn.detach().numpy(), grad_tip=tt.grad.numpy(),
+                        grad_target=gt.grad.numpy(), grad_comp=ct.grad.numpy())
+    print("force_eq", name, float(reward.sum()))
+
+
+class _OracleSDF:
+    """CPU compute_sdf for the reference's SDF / Kin optimisers (its CUDA _C module is absent):
+    the C oracle (oracle/sdf_oracle.c, the restatement pinned in tests/test_sdf_cpu.py) forward,
+    backward 2·g·(p − c) as unbatched_triangle_distance_cuda.cu:263-269."""
+
+    def __init__(self, torch):
+        sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+        from tests import _sdf_oracle
+        self.o = _sdf_oracle
+        o = _sdf_oracle
+
+        class Fn(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, points, faces):
+                assert points.dtype == torch.float32 and faces.dtype == torch.float32
+                d, sg, n, c, _ = o.forward(points.detach().numpy(), faces.detach().numpy())
+                c = torch.from_numpy(c)
+                ctx.save_for_backward(points.detach(), c)
+                sg, n = torch.from_numpy(sg), torch.from_numpy(n)
+                ctx.mark_non_differentiable(sg, n, c)
+                return torch.from_numpy(d), sg, n, c
+
+            @staticmethod
+            def backward(ctx, g, *_):
+                p, c = ctx.saved_tensors
+                return torch.from_numpy(o.backward(g.contiguous().numpy(), p.numpy(), c.numpy())), None
+
+        self.fn = Fn
+
+    def __call__(self, points, faces):
+        return self.fn.apply(points, faces)
+
+
+def _loss_trace(text):
+    out = []
+    for line in text.splitlines():
+        if line.startswith("Loss:"):
+            out.append(float(line.split()[1].rstrip(",")))
+    return np.asarray(out)
+
+
+def gen_modes(ns, iters=12, E=6, seed=50):
+    """The four other optimisers (:121-511) for ``iters`` iterations on the banana, noise replayed;
+    final outputs + the per-iteration Σ loss parsed from their verbose prints."""
+    torch = ns.torch
+    from compliancedex_amd.optimizers import TriangleMesh
+    ns.opt.compute_sdf = _OracleSDF(torch)
+    rng = np.random.default_rng(seed)
+    verts = obj_vertices(os.path.join(ns.ref, "assets/banana/banana.obj"))
+    center = 0.5 * (verts.min(0) + verts.max(0))
+    init_tip = np.array([[0.05, 0.05, 0.02], [0.06, -0.0, -0.01], [0.03, -0.04, 0.0], [-0.07, -0.01, 0.02]])
+    tips = center + init_tip + 0.005 * rng.standard_normal((E, 4, 3))
+    target = np.tile(center, (E, 4, 1)) + 0.003 * rng.standard_normal((E, 4, 3))
+    comp = np.tile([10.0, 10.0, 10.0, 20.0], (E, 1))
+    rc = ns.robot_configs["allegro"]
+    q = np.asarray(rc["ref_q"], dtype=np.float64) + 0.05 * rng.standard_normal((E, 16))
+    palm3 = np.array([-0.06 + center[0], 0.015 + center[1], 0.05 + 2 * center[2] + 0.09])
+    bbox = [ns.opt.FINGERTIP_LB, ns.opt.FINGERTIP_UB]
+    links, offs = rc["ee_link_name"], rc["ee_link_offset"].tolist()
+    urdf = os.path.join(ns.ref, _refload.URDFS["allegro"])
+
+    def mesh():
+        vs, fs = [], []
+        for line in open(os.path.join(ns.ref, "assets/banana/banana.obj")):
+            if line.startswith("f "):
+                fs.append([int(t.split("/")[0]) - 1 for t in line.split()[1:4]])
+        return TriangleMesh(verts, fs)
+
+    def run(name, f32, make, call):
+        nonlocal E
+        dt = torch.float32 if f32 else torch.float64
+        gen = torch.Generator().manual_seed(seed)
+        tape = [torch.rand((E, 3, 3), dtype=dt, generator=gen).double() for _ in range(iters)]
+        with NoiseTape(torch, replay=tape) as nt, contextlib.redirect_stdout(io.StringIO()) as buf:
+            o = make()
+            out = call(o, dt)
+        trace = _loss_trace(buf.getvalue())
+        assert len(trace) == iters, (name, len(trace))
+        res = [t.detach().double().numpy() for t in out[:3]]
+        np.savez_compressed(os.path.join(OUT, f"mode_{name}.npz"), mode=name, iters=iters, tips=tips, target=target,
+                            comp=comp, q=q, palm3=palm3, center=center, noise=torch.stack(nt.record).numpy(),
+                            f32=f32, out0=res[0], out1=res[1], out2=res[2], flag=bool(out[3]), loss_trace=trace)
+        print("mode", name, trace[0], trace[-1], bool(out[3]))
+
+    g = load_state(ns, "banana")
+    run("gpis", False, lambda: ns.opt.GPISGraspOptimizer(bbox, num_iters=iters, optimize_target=True),
+        lambda o, dt: o.optimize(torch.from_numpy(tips), torch.from_numpy(target), torch.from_numpy(comp), 1, g))
+    run("kingpis", False,
+        lambda: ns.opt.KinGPISGraspOptimizer(urdf, links, offs, palm_offset=palm3.tolist(), num_iters=iters,
+                                             optimize_target=True, ref_q=rc["ref_q"].tolist(), tip_bounding_box=bbox),
+        lambda o, dt: o.optimize(torch.from_numpy(q), torch.from_numpy(target), torch.from_numpy(comp), 1, g))
+    # SDF / Kin modes: the reference broadcasts tar_sign [E·T] against a [E, T] view (:297, :211), which
+    # only runs for E = 1 — one candidate each
+    E = 1
+    tips, target, comp, q = tips[:1], target[:1], comp[:1], q[:1]
+    run("sdf", True, lambda: ns.opt.SDFGraspOptimizer(bbox, num_iters=iters, optimize_target=True),
+        lambda o, dt: o.optimize(torch.from_numpy(tips).float(), torch.from_numpy(target).float(),
+                                 torch.from_numpy(comp).float(), 1, mesh()))
+    run("kin", True,
+        lambda: ns.opt.KinGraspOptimizer(urdf, links, offs, palm_offset=palm3.tolist(), num_iters=iters,
+                                         optimize_target=True, ref_q=rc["ref_q"].tolist()),
+        lambda o, dt: o.optimize(torch.from_numpy(q).float(), torch.from_numpy(target).float(),
+                                 torch.from_numpy(comp).float(), 1, mesh()))
+
+
 def gen_collision(ns, name, hand, E, seed):
     """compute_collision_loss (:671-701) with its autograd gradient w.r.t. q and the palm pose.
     Joint angles are perturbed hard and palm heights drawn low so the pairwise (< 0.02), anchor
@@ -290,7 +428,7 @@ def main():
     ns = _refload.load()
     torch = ns.torch
     torch.set_num_threads(8)
-    what = sys.argv[1:] or ["gpis", "fk", "closure", "optimize", "collision"]
+    what = sys.argv[1:] or ["gpis", "fk", "closure", "optimize", "collision", "force_eq", "modes"]
     if "gpis" in what:
         gen_gpis(ns)
     if "fk" in what:
@@ -304,6 +442,11 @@ def main():
         gen_closure(ns, "allegro_mug_e16_spread", "allegro", "mug", 16, 15, True)
         g, _ = synthetic_banana(ns)
         gen_closure(ns, "allegro_syn2000_e16_spread", "allegro", "synthetic2000", 16, 16, True, gpis_obj=g)
+    if "modes" in what:
+        gen_modes(ns)
+    if "force_eq" in what:
+        gen_force_eq(ns, "gravity_mu1", 64, 40, True, 1)
+        gen_force_eq(ns, "nogravity_mu05", 64, 41, False, 0.5)
     if "collision" in what:
         gen_collision(ns, "allegro_e64", "allegro", 64, 30)
         gen_collision(ns, "leap_e64", "leap", 64, 31)

@@ -73,3 +73,17 @@ def test_collision_host_vs_reference(name):
     assert rel_err(cost, d["cost"]) < 1e-4
     assert rel_err(g_q, d["grad_q"]) < 1e-4
     assert rel_err(g_palm, d["grad_palm"]) < 1e-4
+
+
+@pytest.mark.parametrize("name", golden_names("force_eq_"))
+def test_force_eq_host_vs_reference(name):
+    """force_eq_reward (:73-118): the ForceEq code shared by the closure and the standalone op."""
+    from compliancedex_amd.force_eq import force_eq_descriptor
+    d = golden(name)
+    desc = force_eq_descriptor(4, float(d["mu"]) if float(d["mu"]) != 1 else 1, float(d["mass"]),
+                               10.0 if bool(d["gravity"]) else None, COM=d["com"].tolist())
+    out = _host.force_eq(desc, d["tip"], d["target"], d["comp"], d["normal"], d["noise"], d["cr"], d["cf"])
+    for k in ("reward", "margin", "force_norm"):
+        assert rel_err(out[k], d[k]) < 1e-9, k
+    for k in ("grad_tip", "grad_target", "grad_comp"):
+        assert rel_err(out[k], d[k]) < 1e-6, (k, rel_err(out[k], d[k]))

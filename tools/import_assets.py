@@ -5,6 +5,7 @@
   compliancedex_amd/data/gpis_states/<obj>_state.npz   stored GPIS states (gpis.py:155-168 format)
   compliancedex_amd/data/meshes/<obj>_faces.npy        face_vertices [F,3,3] float32 (banana mesh,
                                           TorchSDF test models cube / sphere-42)
+  compliancedex_amd/data/meshes/banana_mesh.npz        banana vertices (f64) + triangles
   compliancedex_amd/data/banana_center.npy, partial_pcd_banana.npy
 
 Run: ``python tools/import_assets.py`` (reads /root/reference; the GPU box never needs it).
@@ -88,7 +89,8 @@ def main():
     for name, rel in meshes.items():
         vs, fs = obj_faces(os.path.join(REF, rel))
         np.save(os.path.join(mdir, f"{name}_faces.npy"), vs[fs].astype(np.float32))
-        if name == "banana":
+        if name == "banana":  # f64 vertices + triangles: the SDF optimisers rescale the mesh (:163-164)
+            np.savez_compressed(os.path.join(mdir, f"{name}_mesh.npz"), vertices=vs, triangles=fs.astype(np.int32))
             np.save(os.path.join(PKG, "data", "banana_center.npy"), 0.5 * (vs.min(0) + vs.max(0)))
         print("mesh", name, fs.shape)
     shutil.copyfile(os.path.join(REF, "partial_pcd/banana.npy"), os.path.join(PKG, "data", "partial_pcd_banana.npy"))
