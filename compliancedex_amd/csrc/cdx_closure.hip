@@ -161,11 +161,12 @@ CDX_HD cdx::ForceEqParams force_eq_params(const cdx_force_eq& p) {
   return fp;
 }
 
-template <int NTA>
+template <int NT>
 __device__ __forceinline__ void force_eq_row(const cdx_force_eq& p, int64_t b, const double* tip,
                                              const double* target, const double* comp, const double* normal,
-                                             const double* noise, uint64_t seed, cdx::ForceEq<NTA>& fe) {
-  const int T = p.n_tips;
+                                             const double* noise, uint64_t seed, cdx::ForceEq<NT>& fe) {
+  constexpr int NTA = cdx::ForceEq<NT>::NTA;
+  const int T = NT > 0 ? NT : p.n_tips;
   double tp[NTA][3], nr[NTA][3], nz[9];
   for (int f = 0; f < T; ++f)
     for (int i = 0; i < 3; ++i) { tp[f][i] = tip[(b * T + f) * 3 + i]; nr[f][i] = normal[(b * T + f) * 3 + i]; }
@@ -177,7 +178,7 @@ __device__ __forceinline__ void force_eq_row(const cdx_force_eq& p, int64_t b, c
   fe.forward(force_eq_params(p), T, tp, target + b * T * 3, comp + b * T, nr, nz);
 }
 
-template <int NTA>
+template <int NT>
 __global__ __launch_bounds__(64) void force_eq_forward_kernel(cdx_force_eq p, int64_t B, const double* __restrict__ tip,
                                                               const double* __restrict__ target,
                                                               const double* __restrict__ comp,
@@ -187,15 +188,15 @@ __global__ __launch_bounds__(64) void force_eq_forward_kernel(cdx_force_eq p, in
                                                               double* __restrict__ force_norm, int32_t* __restrict__ flip) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  cdx::ForceEq<NTA> fe;
-  force_eq_row<NTA>(p, b, tip, target, comp, normal, noise, seed, fe);
-  const int T = p.n_tips;
+  cdx::ForceEq<NT> fe;
+  force_eq_row<NT>(p, b, tip, target, comp, normal, noise, seed, fe);
+  const int T = NT > 0 ? NT : p.n_tips;
   reward[b] = fe.reward;
   for (int f = 0; f < T; ++f) { margin[b * T + f] = fe.margin[f]; force_norm[b * T + f] = fe.fn[f]; }
   if (flip) flip[b] = fe.flip;
 }
 
-template <int NTA>
+template <int NT>
 __global__ __launch_bounds__(64) void force_eq_backward_kernel(
     cdx_force_eq p, int64_t B, const double* __restrict__ tip, const double* __restrict__ target,
     const double* __restrict__ comp, const double* __restrict__ normal, const double* __restrict__ noise, uint64_t seed,
@@ -203,9 +204,10 @@ __global__ __launch_bounds__(64) void force_eq_backward_kernel(
     double* __restrict__ g_target, double* __restrict__ g_comp) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  cdx::ForceEq<NTA> fe;
-  force_eq_row<NTA>(p, b, tip, target, comp, normal, noise, seed, fe);
-  const int T = p.n_tips;
+  cdx::ForceEq<NT> fe;
+  force_eq_row<NT>(p, b, tip, target, comp, normal, noise, seed, fe);
+  constexpr int NTA = cdx::ForceEq<NT>::NTA;
+  const int T = NT > 0 ? NT : p.n_tips;
   double gfn[NTA], gt[NTA][3], gg[NTA][3], gc[NTA];
   for (int f = 0; f < T; ++f) {
     gfn[f] = g_force_norm ? g_force_norm[b * T + f] : 0.0;
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(64) void force_eq_backward_kernel(
   }
 }
 
-template <int NT>
+template <int NT, int G>
 __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_t E, const double* __restrict__ q,
                                                            const double* __restrict__ comp,
                                                            const double* __restrict__ target,
@@ -255,7 +257,7 @@ __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_
   GpisView g = gv;
   g.e = e;
   cdx::LevelOut lo;
-  cdx::level_fwd_bwd<NT>(P, k, in, tip, qnorm, g, lo);
+  cdx::level_fwd_bwd<NT, GpisView, G>(P, k, in, tip, qnorm, g, lo);
   double* r = lvl + t * level_record_width(T);
   r[0] = lo.l;
   for (int f = 0; f < T; ++f) {
@@ -464,11 +466,11 @@ int cdx_force_eq_forward(const cdx_force_eq* p, int64_t B, const double* tip, co
   if (!tip || !target || !comp || !normal || !reward || !margin || !force_norm) return CDX_EINVAL;
   const dim3 grid((unsigned)((B + 63) / 64));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (p->n_tips <= 4)
+  if (p->n_tips == 4)
     hipLaunchKernelGGL(force_eq_forward_kernel<4>, grid, dim3(64), 0, s, *p, B, tip, target, comp, normal, noise, seed,
                        reward, margin, force_norm, flip);
   else
-    hipLaunchKernelGGL(force_eq_forward_kernel<CDX_MAX_TIPS>, grid, dim3(64), 0, s, *p, B, tip, target, comp, normal,
+    hipLaunchKernelGGL(force_eq_forward_kernel<0>, grid, dim3(64), 0, s, *p, B, tip, target, comp, normal,
                        noise, seed, reward, margin, force_norm, flip);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
@@ -482,11 +484,11 @@ int cdx_force_eq_backward(const cdx_force_eq* p, int64_t B, const double* tip, c
   if (!tip || !target || !comp || !normal || !g_tip || !g_target || !g_comp) return CDX_EINVAL;
   const dim3 grid((unsigned)((B + 63) / 64));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (p->n_tips <= 4)
+  if (p->n_tips == 4)
     hipLaunchKernelGGL(force_eq_backward_kernel<4>, grid, dim3(64), 0, s, *p, B, tip, target, comp, normal, noise, seed,
                        g_reward, g_force_norm, g_tip, g_target, g_comp);
   else
-    hipLaunchKernelGGL(force_eq_backward_kernel<CDX_MAX_TIPS>, grid, dim3(64), 0, s, *p, B, tip, target, comp, normal,
+    hipLaunchKernelGGL(force_eq_backward_kernel<0>, grid, dim3(64), 0, s, *p, B, tip, target, comp, normal,
                        noise, seed, g_reward, g_force_norm, g_tip, g_target, g_comp);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
@@ -551,12 +553,15 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   {
     const int64_t KE = (int64_t)p->n_levels * E;
     const dim3 lgrid((unsigned)((KE + 63) / 64));
-    if (p->chain.n_tips == 4)
-      hipLaunchKernelGGL(closure_level_kernel<4>, lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X, kabsch_noise,
-                         seed, gv, w.lvl, flip);
+    if (p->chain.n_tips == 4 && p->gravity)
+      hipLaunchKernelGGL((closure_level_kernel<4, 1>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
+                         kabsch_noise, seed, gv, w.lvl, flip);
+    else if (p->chain.n_tips == 4)
+      hipLaunchKernelGGL((closure_level_kernel<4, 0>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
+                         kabsch_noise, seed, gv, w.lvl, flip);
     else
-      hipLaunchKernelGGL(closure_level_kernel<0>, lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X, kabsch_noise,
-                         seed, gv, w.lvl, flip);
+      hipLaunchKernelGGL((closure_level_kernel<0, -1>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
+                         kabsch_noise, seed, gv, w.lvl, flip);
     if (hipGetLastError() != hipSuccess) return CDX_ELAUNCH;
     if (p->chain.n_tips <= 4)
       hipLaunchKernelGGL(closure_combine_kernel<4>, dim3((unsigned)((E * 4 + 255) / 256)), dim3(256), 0, s, *p, E, q,

@@ -245,9 +245,12 @@ CDX_HD ForceEqParams force_eq_params(const cdx_problem& P) {
   return fp;
 }
 
-template <int NTA>
+// NT: fingertip count at compile time (0: runtime, up to CDX_MAX_TIPS); G: gravity spring at
+// compile time (0 / 1; -1: runtime) — with both fixed every loop has a constant trip count.
+template <int NT, int G = -1>
 struct ForceEq {
-  int T, NP;
+  static constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
+  int T_rt, NP_rt;
   double S1[NTA + 1][3], S2[NTA + 1][3], w[NTA + 1], n[NTA][3];
   double c1[3], c2[3], Pm[NTA + 1][3], Qm[NTA + 1][3];
   KabschTape tp;
@@ -259,35 +262,49 @@ struct ForceEq {
 
   CDX_HDM void forward(const ForceEqParams& fp, int T_, const double (*tip)[3], const double* target,
                       const double* comp, const double (*nrm)[3], const double* noise) {
-    T = T_;
-    NP = fp.gravity ? T + 1 : T;
+    T_rt = T_;
+    const int T = NT > 0 ? NT : T_;
+    const bool grav = G >= 0 ? G != 0 : fp.gravity != 0;
+    NP_rt = grav ? T + 1 : T;
+    const int NP = (NT > 0 && G >= 0) ? (G ? NT + 1 : NT) : NP_rt;
+#pragma unroll
     for (int f = 0; f < T; ++f) {
       for (int i = 0; i < 3; ++i) { S1[f][i] = tip[f][i]; S2[f][i] = target[3 * f + i]; n[f][i] = nrm[f][i]; }
       w[f] = comp[f];
     }
-    if (fp.gravity) {
+    if (grav) {
       for (int i = 0; i < 3; ++i) S1[T][i] = fp.com[i];
       S2[T][0] = 0.0; S2[T][1] = 0.0; S2[T][2] = fp.dummy_target_z;
       w[T] = fp.dummy_comp;
     }
     c1[0] = c1[1] = c1[2] = 0.0;
     c2[0] = c2[1] = c2[2] = 0.0;
+#pragma unroll
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { c1[j] += S1[i][j]; c2[j] += S2[i][j]; }
     for (int j = 0; j < 3; ++j) { c1[j] /= NP; c2[j] /= NP; }
+#pragma unroll
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { Pm[i][j] = w[i] * (S1[i][j] - c1[j]); Qm[i][j] = w[i] * (S2[i][j] - c2[j]); }
     double H[9];
     for (int r = 0; r < 3; ++r)
       for (int c = 0; c < 3; ++c) {
         double acc = 0.0;
+#pragma unroll
         for (int i = 0; i < NP; ++i) acc += Pm[i][r] * Qm[i][c];
         H[3 * r + c] = acc;
       }
-    kabsch_rotation(H, noise, tp, R);
+    {
+      // svd3 sorts with data-dependent indices: run it on a separate tape so that only this small
+      // object, not the whole ForceEq, has to live in scratch
+      KabschTape t_;
+      kabsch_rotation(H, noise, t_, R);
+      tp = t_;
+    }
     flip = tp.d < 0 ? 1 : 0;
     W = 0.0;
     double num[3] = {0, 0, 0};
+#pragma unroll
     for (int i = 0; i < NP; ++i) {
       W += w[i];
       mat3_vec(R, S1[i], RS1[i]);
@@ -295,6 +312,7 @@ struct ForceEq {
     }
     for (int j = 0; j < 3; ++j) t[j] = num[j] / W;
     reward = 0.0;
+#pragma unroll
     for (int f = 0; f < T; ++f) {
       for (int i = 0; i < 3; ++i) diff[f][i] = RS1[f][i] + t[i] - target[3 * f + i];
       dn[f] = sqrt(dot3(diff[f], diff[f]));
@@ -310,9 +328,13 @@ struct ForceEq {
 
   CDX_HDM void backward(double g_rw, const double* g_fn, const double* comp, double (*g_tip)[3], double (*g_target)[3],
                        double* g_comp) const {
+    const int T = NT > 0 ? NT : T_rt;
+    const int NP = (NT > 0 && G >= 0) ? (G ? NT + 1 : NT) : NP_rt;
     double gR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g_t[3] = {0, 0, 0};
     double g_S1[NTA + 1][3], g_S2[NTA + 1][3], g_w[NTA + 1];
+#pragma unroll
     for (int i = 0; i < NP; ++i) { g_S1[i][0] = g_S1[i][1] = g_S1[i][2] = 0; g_S2[i][0] = g_S2[i][1] = g_S2[i][2] = 0; g_w[i] = 0; }
+#pragma unroll
     for (int f = 0; f < T; ++f) {
       double gang = g_rw * 0.2 / (ang[f] + 1);
       if (mpre[f] >= -0.9999) gang += g_rw * 0.8 / (margin[f] + 1);
@@ -343,6 +365,7 @@ struct ForceEq {
     {
       double gnum[3] = {g_t[0] / W, g_t[1] / W, g_t[2] / W};
       const double gW = -dot3(g_t, t) / W;
+#pragma unroll
       for (int i = 0; i < NP; ++i) {
         double r_i[3] = {S2[i][0] - RS1[i][0], S2[i][1] - RS1[i][1], S2[i][2] - RS1[i][2]};
         g_w[i] += gW + dot3(gnum, r_i);
@@ -358,6 +381,7 @@ struct ForceEq {
     double gH[9];
     kabsch_rotation_bwd(tp, gR, gH);
     double g_c1[3] = {0, 0, 0}, g_c2[3] = {0, 0, 0};
+#pragma unroll
     for (int i = 0; i < NP; ++i) {
       double gP[3], gQ[3];
       mat3_vec(gH, Qm[i], gP);
@@ -372,8 +396,10 @@ struct ForceEq {
         g_c2[j] -= w[i] * gQ[j];
       }
     }
+#pragma unroll
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { g_S1[i][j] += g_c1[j] / NP; g_S2[i][j] += g_c2[j] / NP; }
+#pragma unroll
     for (int f = 0; f < T; ++f) {
       for (int i = 0; i < 3; ++i) { g_tip[f][i] += g_S1[f][i]; g_target[f][i] += g_S2[f][i]; }
       g_comp[f] += g_w[f];
@@ -393,7 +419,7 @@ struct LevelOut {
   int flip;
 };
 
-template <int NT, typename GpisAt>
+template <int NT, typename GpisAt, int G = -1>
 CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, const double (*tip)[3], double qnorm,
                           GpisAt gp, LevelOut& o) {
   constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
@@ -416,7 +442,7 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
     for (int i = 0; i < 3; ++i) n[f][i] = ga.normal[i];
     td[f] = gp(1, 0, f).mean;
   }
-  ForceEq<NTA> fe;
+  ForceEq<NT, G> fe;
   fe.forward(force_eq_params(P), T, a, in.target, in.comp, n, in.noise + k * in.noise_stride);
   o.flip = fe.flip;
   // contact margin (unclamped)

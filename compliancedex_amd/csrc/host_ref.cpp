@@ -134,7 +134,7 @@ void cdxh_force_eq(const cdx_force_eq* p, int64_t B, const double* tip, const do
     double tp[CDX_MAX_TIPS][3], nr[CDX_MAX_TIPS][3];
     for (int f = 0; f < T; ++f)
       for (int i = 0; i < 3; ++i) { tp[f][i] = tip[(b * T + f) * 3 + i]; nr[f][i] = normal[(b * T + f) * 3 + i]; }
-    cdx::ForceEq<CDX_MAX_TIPS> fe;
+    cdx::ForceEq<0> fe;
     fe.forward(fp, T, tp, target + b * T * 3, comp + b * T, nr, noise + b * 9);
     reward[b] = fe.reward;
     flip[b] = fe.flip;
