@@ -121,9 +121,7 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 //   partials per (column tile, query).
 // VAR = true (std path, whitened): B = L⁻ᵀ (upper triangular), V = K*·L⁻ᵀ = (L⁻¹K*ᵀ)ᵀ, epilogue
 //   Σ V² → 1 partial per (column tile, query).  Column tile nt only needs K-rows j < n0 + ST_BN
-//   (and < N), so tile costs run 1..Nt K-sweeps: tiles are issued heaviest stripe first, and each
-//   XCD takes every eighth query tile of a stripe so all XCDs see the same cost mix while the 32
-//   CUs of one XCD still share the stripe's L⁻ᵀ rows in their L2.
+//   (and < N), so tile costs run 1..Nt K-sweeps: stripes are paired heavy+light per XCD (below).
 template <int KT, bool VAR>
 __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X,
                                                                         int64_t M, double* __restrict__ partial,
@@ -135,11 +133,17 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
   const int b = blockIdx.x;
   int nt, mt;
   if (VAR) {
-    if ((Mt & 7) == 0) {
-      const int per = Mt >> 3, r = b >> 3;
-      nt = Nt - 1 - r / per;
-      mt = (r % per) * 8 + (b & 7);
-    } else {
+    // Stripe nt costs ∝ nt + 1 K-sweeps.  Pair stripes (Nt−1−a, a) — every pair costs Nt + 1 — and
+    // give each pair to X = 16/Nt XCDs (blocks b, b+8, … share an XCD), each XCD taking 1/X of the
+    // pair's query tiles, heavy stripe first: equal work per XCD, and each XCD's L2 holds only its
+    // two stripes of L⁻ᵀ (each stripe is fetched by X XCDs instead of all eight).
+    const int X = 16 / Nt;
+    if (Nt >= 2 && Nt <= 16 && (Nt & (Nt - 1)) == 0 && Mt % X == 0) {
+      const int xcd = b & 7, r = b >> 3, per = Mt / X;
+      const int a = xcd / X, part = xcd % X;
+      nt = r < per ? Nt - 1 - a : a;
+      mt = part * per + (r < per ? r : r - per);
+    } else {  // heaviest stripe first
       nt = Nt - 1 - b / Mt;
       mt = b % Mt;
     }
