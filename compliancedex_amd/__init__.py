@@ -13,6 +13,7 @@ All compute runs in libcdx.so (HIP, gfx950); importing works without a GPU, call
 from .gpis import GPIS  # noqa: F401
 from .optimizer import (EE_OFFSETS, FINGERTIP_LB, FINGERTIP_UB, WRIST_OFFSET,  # noqa: F401
                         ProbabilisticGraspOptimizer, euler_angles_to_matrix)
+from .anneal import PregraspAnnealer  # noqa: F401
 from .force_eq import force_eq_reward  # noqa: F401
 from .optimizers import (GPISGraspOptimizer, KinGPISGraspOptimizer, KinGraspOptimizer,  # noqa: F401
                          SDFGraspOptimizer, TriangleMesh)

@@ -217,11 +217,20 @@ class ProbabilisticGraspOptimizer:
 
     # -------------------------------------------------------------- optimize
     def optimize(self, init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose=True,
-                 noise_tape=None, fused=True):
+                 noise_tape=None, fused=True, init_palm=None):
         """The reference's optimisation loop (:771-839).  ``fused=True`` (default): per iteration
         one cdx_closure + one cdx_optimizer_step (Adam, best iterate, clamps on device, no host
         sync); ``fused=False``: the same loop with torch.optim.Adam.  ``noise_tape``: optional
-        per-iteration Kabsch noise tensors (parity replay)."""
+        per-iteration Kabsch noise tensors (parity replay).  ``init_palm`` [E, 6]: start from these
+        palm poses instead of ``palm_offset`` (the annealing outer loop's proposals)."""
+        if init_palm is not None:
+            saved = self.palm_offset
+            self.palm_offset = init_palm.detach().to(torch.float64)
+            try:
+                return self.optimize(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
+                                     noise_tape, fused)
+            finally:
+                self.palm_offset = saved
         if fused:
             return self._optimize_fused(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
                                         noise_tape)

@@ -10,6 +10,11 @@ c3     config 3 objects (stored states, box fit, dummy for realsense), 4096 cand
 c4     config 4 primitives: iiwa7_allegro FK (23 DOF, 4 tips) fwd+bwd for 16 384 candidates and the
        TorchSDF kernel on the banana mesh (16 384 faces) for the 3 SDF calls of an SDF/Kin-mode iteration
        (tips vs deflated mesh, tips vs mesh, targets vs mesh: 3 × 65 536 points) + SDF backward.
+c4loop config 4 loops: prob closure on the iiwa7_allegro chain (23 DOF) with the collision term fused
+       (collision=True), 16 384 candidates, N = 2000 GPIS; and the SDF/Kin-mode optimiser
+       (KinGraspOptimizer: FK + 3 TorchSDF calls on the banana mesh + force_eq) at 16 384 candidates.
+c5     config 5: annealing outer loop (compliancedex_amd.anneal) over 65 536 candidates on one GPU,
+       3 outer steps × 30 fused inner iterations, N = 2000 GPIS.
 fit    §8f row 2: on-device GPIS fit (R, E11) + factor (Cholesky, E11⁻¹, α) for N = 361 / 1000 / 2000,
        next to torch-CPU fit + inverse (the work the reference does per object) on the host cores.
 """
@@ -142,6 +147,80 @@ def case_c4(dev):
                       "fk_evals_per_s": E / fk_s, "sdf_3calls_fwd_bwd_ms": sdf_s * 1e3,
                       "sdf_point_face_pairs_per_s": pairs / sdf_s, "faces": int(faces.shape[0]),
                       "sdf_evals_per_s": E / sdf_s}), flush=True)
+
+
+def case_c4loop(dev):
+    from compliancedex_amd import KinGraspOptimizer, ProbabilisticGraspOptimizer, TriangleMesh
+    from compliancedex_amd.urdf import load_robot
+    from compliancedex_amd.workloads import prob_inputs, synthetic_banana_gpis
+    E = 16384
+    links = load_robot("iiwa7_allegro")["config"]["ee_link_name"]
+    D = 23
+    ref_q = [0.0] * D
+    offs = [[0.0, -0.04, 0.015]] * 3 + [[0.0, -0.05, -0.015]]
+    g = synthetic_banana_gpis(2000, dev)
+    q, comp, target, _ = prob_inputs(ref_q, E, seed=8, spread=True)
+    q = 0.05 * np.random.default_rng(9).standard_normal((E, D))
+    # the "palm" pose is the arm base here: place it so the fingertips at q = 0 surround the banana
+    from compliancedex_amd import DifferentiableRobotModel
+    tips0 = DifferentiableRobotModel("iiwa7_allegro", device=dev).compute_forward_kinematics(
+        torch.zeros(1, D, device=dev), links, offsets=offs)[0].view(4, 3).double().mean(0).cpu().numpy()
+    center = np.load(os.path.join(REPO, "compliancedex_amd", "data", "banana_center.npy"))
+    rng = np.random.default_rng(8)
+    palm = np.concatenate([center - tips0 + 0.005 * rng.standard_normal((E, 3)), 0.02 * rng.standard_normal((E, 3))], 1)
+    pairs = [[0, 1], [0, 2], [0, 3], [1, 2], [1, 3], [2, 3]]
+    opt = ProbabilisticGraspOptimizer("iiwa7_allegro", links, offs, palm_offset=palm, ref_q=ref_q,
+                                      optimize_target=True, optimize_palm=True, device=dev, anchor_link_names=links,
+                                      anchor_link_offsets=offs, collision_pairs=pairs, collision=True)
+    t = [torch.from_numpy(a).to(dev).requires_grad_(True) for a in (q, comp, target, palm[:, :3], palm[:, 3:])]
+
+    def step():
+        for x in t:
+            x.grad = None
+        opt.closure(*t, 1, g, E)
+    sec = timed(step, 10)
+    print(json.dumps({"case": "config4_closure_iiwa7_collision", "E": E, "n_dofs": D, "n_inducing": 2000,
+                      "ms_per_closure": sec * 1e3, "evals_per_s": E / sec,
+                      "nan_candidates": int((~torch.isfinite(opt.total_loss)).sum())}), flush=True)
+    mesh = TriangleMesh.from_npz(os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_mesh.npz"))
+    iters = 5
+    kin = KinGraspOptimizer("iiwa7_allegro", links, offs, palm_offset=[0.0, 0.0, 0.0], num_iters=iters,
+                            optimize_target=True, ref_q=ref_q)
+    qf = (0.3 * torch.randn(E, D, device=dev)).float()
+    tg = torch.from_numpy(target).to(dev).float()
+    cp = torch.from_numpy(comp).to(dev).float()
+
+    def loop():
+        kin.optimize(qf, tg, cp, 1, TriangleMesh(mesh.vertices, mesh.triangles), verbose=False)
+    sec = timed(loop, 2, warm=1)
+    print(json.dumps({"case": "config4_kin_sdf_loop", "E": E, "iterations": iters, "faces": int(len(mesh.triangles)),
+                      "ms_per_iteration": sec / iters * 1e3, "evals_per_s": E * iters / sec}), flush=True)
+
+
+def case_c5(dev):
+    from compliancedex_amd import PregraspAnnealer, ProbabilisticGraspOptimizer
+    from compliancedex_amd.urdf import load_robot
+    from compliancedex_amd.workloads import prob_inputs, synthetic_banana_gpis
+    E, inner, outer = 65536, 30, 3
+    cfg = load_robot("allegro")["config"]
+    g = synthetic_banana_gpis(2000, dev)
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=9, spread=True)
+    opt = ProbabilisticGraspOptimizer("allegro", cfg["ee_link_name"], cfg["ee_link_offset"], palm_offset=palm,
+                                      ref_q=cfg["ref_q"], optimize_target=True, optimize_palm=True, device=dev,
+                                      num_iters=inner)
+    t = [torch.from_numpy(a).to(dev) for a in (q, target, comp, palm)]
+    ann = PregraspAnnealer(opt, g, seed=1)
+    res = {}
+
+    def run():
+        res["best"] = ann.run(*t, outer_steps=outer)
+    sec = timed(run, 1, warm=1)
+    best = res["best"]
+    surv = int((best["margin"] > 0).all(1).sum())
+    print(json.dumps({"case": "config5_anneal", "E": E, "inner_iterations": inner, "outer_steps": outer,
+                      "seconds": sec, "evals_per_s": E * inner * outer / sec,
+                      "finite_best": int(torch.isfinite(best["loss"]).sum()), "surviving_grasps": surv,
+                      "mean_accepts": float(best["accepted"].double().mean())}), flush=True)
 
 
 def case_fit(dev):
