@@ -150,9 +150,9 @@ def main():
     m_std, m_grad = lq * E * 4, lq * E
     n_ind = args.n_inducing
     # algorithmic flops per launch (unpadded N): V = K*·L⁻ᵀ is triangular, N(N+1)/2 MACs per
-    # query; W = K*·E11⁻¹ at the variance cost's argmax fingertip only, N² MACs per query
+    # query; W = V·L⁻¹ (= (E11⁻¹k)ᵀ) at the variance cost's argmax fingertip only, also triangular
     flops = m_std * float(n_ind) * (n_ind + 1)
-    flops_g = m_grad * 2.0 * n_ind * n_ind
+    flops_g = m_grad * float(n_ind) * (n_ind + 1)
     std_ms, grad_ms = stage_ms["gpis_std_var"], stage_ms["gpis_std_grad"]
     achieved = flops / (std_ms * 1e-3) / 1e12 if std_ms else None
     achieved_g = flops_g / (grad_ms * 1e-3) / 1e12 if grad_ms else None
@@ -175,12 +175,13 @@ def main():
                          "flops_per_launch": flops,
                          "note": f"{m_std} std queries x N(N+1) (triangular whitened form; all-tip queries "
                                  f"deduplicated over the 3 identical pregrasp levels, the reference does 3x)"},
-            "roofline_grad": {"bound": "mfma", "kernel": "gpis_std_kernel<!VAR> (K*·E11⁻¹, ∇std)",
+            "roofline_grad": {"bound": "mfma", "kernel": "gpis_std_kernel<GRADV> (V·L⁻¹ = (E11⁻¹k)ᵀ, ∇std)",
                               "achieved": achieved_g, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": (achieved_g / FP64_MFMA_PEAK_TFLOPS) if achieved_g else None,
                               "traffic": hbm_traffic(E, n_ind, "gpis_grad_bytes_per_launch"),
                               "flops_per_launch": flops_g,
-                              "note": f"{m_grad} queries (the variance cost's argmax fingertip) x 2·N²"},
+                              "note": f"{m_grad} queries (the variance cost's argmax fingertip) x N(N+1), "
+                                      f"from the whitened vectors the std pass keeps"},
             "nan_candidates": nan_candidates,  # reference semantics: unclamped log in :708-709
         }
         if world == 1 and not args.no_cpu_baseline:

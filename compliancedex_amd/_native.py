@@ -21,7 +21,7 @@ ERRORS = {-1: "invalid argument", -2: "unsupported GPIS kernel", -3: "chain exce
 
 class CdxGpis(C.Structure):
     _fields_ = [("X1", C.c_void_p), ("alpha", C.c_void_p), ("Ainv", C.c_void_p), ("Linv_t", C.c_void_p),
-                ("N", C.c_int32),
+                ("Linv", C.c_void_p), ("N", C.c_int32),
                 ("N_pad", C.c_int32), ("kernel", C.c_int32), ("_pad", C.c_int32), ("R", C.c_double),
                 ("sigma", C.c_double), ("bias", C.c_double)]
 
@@ -83,7 +83,7 @@ _SIGS = {
     "cdx_gpis_std": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P, _P]),
     "cdx_gpis_fit": (C.c_int, [_P, C.c_int32, _P, C.c_int32, C.c_double, _P, _P, _P]),
     "cdx_gpis_factor_workspace": (C.c_size_t, [C.c_int32]),
-    "cdx_gpis_factor": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P]),
+    "cdx_gpis_factor": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P, _P]),
     "cdx_fk_forward": (C.c_int, [C.POINTER(CdxChain), _P, _I64, _P, _P, _P]),
     "cdx_fk_backward": (C.c_int, [C.POINTER(CdxChain), _P, _I64, _P, _P, _P]),
     "cdx_force_eq_forward": (C.c_int, [C.POINTER(CdxForceEq), _I64, _P, _P, _P, _P, _P, C.c_uint64, _P, _P, _P, _P,

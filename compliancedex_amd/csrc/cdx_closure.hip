@@ -6,9 +6,9 @@
 //                               (all-tip rows deduplicated over identical coefficient rows,
 //                               targets once, pregrasp tips, palm)      — :657-669, :743-750
 //   2. gpis_mean (cdx_gpis.hip) mean/∇mean/normal at all queries      — gpis.py:43-87
-//   3. gpis std  (cdx_gpis.hip) std at the all-tip queries (whitened, triangular fp64 MFMA),
-//      closure_std_select_kernel (the variance cost's argmax fingertip), ∇std at those
-//      queries only (fp64 MFMA)
+//   3. gpis std  (cdx_gpis.hip) std at the all-tip queries (whitened, triangular fp64 MFMA,
+//      V = L⁻¹k kept), closure_std_select_kernel (the variance cost's argmax fingertip),
+//      ∇std at those queries only: E11⁻¹k = L⁻ᵀv from the kept V (triangular fp64 MFMA)
 //   4. closure_cost_kernel      one thread per candidate: seven cost terms per level,
 //                               Kabsch + SVD backward, FK backward; writes loss, margin
 //                               and the five parameter gradients        — :713-769, :49-118
@@ -375,7 +375,7 @@ bool chain_ok(const cdx_chain* c) {
 size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 struct ClosureWs {
-  double *X, *mean, *gmean, *normal, *std_, *var, *gstd, *Xg, *lvl;
+  double *X, *mean, *gmean, *normal, *std_, *var, *gstd, *Xg, *lvl, *V;
   int64_t* sel;
   void *var_ws, *grad_ws;
   size_t bytes;
@@ -422,6 +422,11 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   w.var_ws = take(cdx::gpis_var_ws_bytes(p->gpis, Ms));
   w.grad_ws = take(cdx::gpis_grad_ws_bytes(p->gpis, Mg));
   w.lvl = (double*)take((size_t)p->n_levels * E * level_record_width(p->chain.n_tips) * sizeof(double));
+#if !defined(CDX_GRAD_EXPLICIT)
+  w.V = (double*)take(cdx::gpis_v_bytes(p->gpis, Ms));
+#else
+  w.V = nullptr;
+#endif
   w.bytes = off;
   return w;
 }
@@ -526,7 +531,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   if (!q || !comp || !target || !palm_pos || !palm_ori || !workspace || !total_loss || !total_margin || !g_q ||
       !g_comp || !g_target || !g_palm_pos || !g_palm_ori)
     return CDX_EINVAL;
-  if (!p->gpis.Ainv || !p->gpis.Linv_t || !p->gpis.X1 || !p->gpis.alpha) return CDX_EINVAL;
+  if (!p->gpis.Ainv || !p->gpis.Linv_t || !p->gpis.Linv || !p->gpis.X1 || !p->gpis.alpha) return CDX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   ClosureWs w = closure_ws_layout(p, E, static_cast<char*>(workspace));
   const int64_t Mq = cdx::n_queries(*p, E);
@@ -539,12 +544,13 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   if (hipGetLastError() != hipSuccess) return CDX_ELAUNCH;
   int rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
   if (rc) return rc;
-  rc = cdx::gpis_var_launch(p->gpis, w.X, Ms, w.std_, w.var, w.var_ws, s);
+  // whitened std at every all-tip query, keeping V = (L⁻¹K*ᵀ)ᵀ for the ∇std pass
+  rc = cdx::gpis_var_launch(p->gpis, w.X, Ms, w.std_, w.var, w.var_ws, s, w.V);
   if (rc) return rc;
   const int64_t Mg = (int64_t)p->n_query_levels * E;
   hipLaunchKernelGGL(closure_std_select_kernel, dim3((unsigned)((Mg + 255) / 256)), dim3(256), 0, s, E,
                      p->chain.n_tips, p->n_query_levels, (const double*)w.std_, (const double*)w.X, w.sel, w.Xg);
-  rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s);
+  rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V);
   if (rc) return rc;
   GpisView gv;
   gv.mean = w.mean; gv.gmean = w.gmean; gv.normal = w.normal; gv.std_ = w.std_; gv.gstd = w.gstd;

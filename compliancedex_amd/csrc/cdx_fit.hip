@@ -258,6 +258,14 @@ __global__ __launch_bounds__(256) void transpose_kernel(const double* __restrict
   }
 }
 
+// Linv = X with rows/columns ≥ N zeroed.
+__global__ __launch_bounds__(256) void pad_copy_kernel(const double* __restrict__ X, int N, int Np,
+                                                       double* __restrict__ Lr) {
+  const int i = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < Np) Lr[(int64_t)i * Np + j] = (i < N && j < N) ? X[(int64_t)i * Np + j] : 0.0;
+}
+
 // out = A y (rows ≥ N zero, columns ≥ N ignored): one wave per row.
 __global__ __launch_bounds__(256) void matvec_kernel(const double* __restrict__ A, const double* __restrict__ y1, int N,
                                                      int Np, double* __restrict__ alpha) {
@@ -300,8 +308,9 @@ size_t cdx_gpis_factor_workspace(int32_t N_pad) {
 }
 
 int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pad, void* ws, double* Ainv,
-                    double* Linv_t, double* alpha, int32_t* info, cdx_stream_t stream) {
-  if (!E11 || !y1 || !ws || !Ainv || !Linv_t || !alpha || !info || N <= 0 || N_pad < N || N_pad % CDX_NPAD_ALIGN ||
+                    double* Linv_t, double* Linv, double* alpha, int32_t* info, cdx_stream_t stream) {
+  if (!E11 || !y1 || !ws || !Ainv || !Linv_t || !Linv || !alpha || !info || N <= 0 || N_pad < N ||
+      N_pad % CDX_NPAD_ALIGN ||
       N_pad > 65535)
     return CDX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -321,6 +330,7 @@ int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pa
     hipLaunchKernelGGL(tri_inv_row_kernel, dim3(i), dim3(256), 0, s, (const double*)M, X, N_pad, i);
   hipLaunchKernelGGL(xtx_kernel, dim3(nb * (nb + 1) / 2), dim3(256), 0, s, (const double*)X, N_pad, N, Ainv);
   hipLaunchKernelGGL(transpose_kernel, dim3(nb, nb), dim3(256), 0, s, (const double*)X, N_pad, N, Linv_t);
+  hipLaunchKernelGGL(pad_copy_kernel, dim3((N_pad + 255) / 256, N_pad), dim3(256), 0, s, (const double*)X, N, N_pad, Linv);
   // α = L⁻ᵀ (L⁻¹ y1): two triangular matvecs (6e-13 from the reference's solve where E11⁻¹·y1
   // with the explicit inverse is 7e-10); M's storage is free again and holds L⁻¹ y1
   hipLaunchKernelGGL(matvec_kernel, dim3((N_pad + 3) / 4), dim3(256), 0, s, (const double*)X, y1, N, N_pad, M);

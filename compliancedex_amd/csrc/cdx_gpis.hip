@@ -117,23 +117,54 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 // v2: 128 queries × ST_BN output columns per workgroup of 2 × ST_WN waves, each wave owning
 // 64×64 = 4×4 v_mfma_f64_16x16x4_f64 tiles; K-step 16, two LDS buffers, one barrier per step.
 //
-// VAR = false (∇std path): B = E11⁻¹, W = K*·E11⁻¹, epilogue Σ W·k and Σ W·kd·(x − x_n) → 4
-//   partials per (column tile, query).
-// VAR = true (std path, whitened): B = L⁻ᵀ (upper triangular), V = K*·L⁻ᵀ = (L⁻¹K*ᵀ)ᵀ, epilogue
-//   Σ V² → 1 partial per (column tile, query).  Column tile nt only needs K-rows j < n0 + ST_BN
-//   (and < N), so tile costs run 1..Nt K-sweeps: stripes are paired heavy+light per XCD (below).
-template <int KT, bool VAR>
+// MODE_GRAD (∇std, explicit inverse): A = K* (generated), B = E11⁻¹, W = K*·E11⁻¹, epilogue
+//   Σ W·k and Σ W·kd·(x − x_n) → 4 partials per (column tile, query).
+// MODE_VAR (std, whitened): A = K* (generated), B = L⁻ᵀ (upper triangular), V = K*·L⁻ᵀ =
+//   (L⁻¹K*ᵀ)ᵀ, epilogue Σ V² → 1 partial per (column tile, query); optionally V itself is stored
+//   (vout, [M_pad, N_pad]).  Column tile nt only needs K-rows j < n0 + ST_BN (and < N).
+// MODE_GRADV (∇std from the stored whitened vector): A = V rows (loaded, row vsel[m] of vin),
+//   B = L⁻¹ (lower triangular), W = V·L⁻¹ = (L⁻ᵀv)ᵀ = (E11⁻¹k)ᵀ, the MODE_GRAD epilogue (linear
+//   in W, so K can be split).  Column tile nt only needs K-rows i ≥ n0: N² flops per query
+//   instead of 2N²; launched split-K over 256-row chunks (Nt(Nt+1)/2 partial slots).
+// The triangular modes' tile costs run 1..Nt K-sweeps: stripes are paired heavy+light per XCD.
+enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2 };
+#if !defined(CDX_GV_SPLIT)
+#define CDX_GV_SPLIT 1
+#endif
+constexpr int GV_SPLIT = CDX_GV_SPLIT;  // GRADV K-chunks per 256-row stripe (2: 0.468 vs 0.423 ms at E = 4096)
+
+template <int KT, int MODE>
 __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X,
                                                                         int64_t M, double* __restrict__ partial,
-                                                                        int64_t M_pad, int Mt, int Nt) {
+                                                                        int64_t M_pad, int Mt, int Nt,
+                                                                        double* __restrict__ vout,
+                                                                        const double* __restrict__ vin,
+                                                                        const int64_t* __restrict__ vsel) {
+  constexpr bool VAR = MODE == MODE_VAR;
+  constexpr bool TRI = MODE != MODE_GRAD;
   __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
   double* xq = smem + 2 * (ST_TILE + ST_BTILE);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = Mt * Nt;
   const int b = blockIdx.x;
-  int nt, mt;
-  if (VAR) {
-    // Stripe nt costs ∝ nt + 1 K-sweeps.  Pair stripes (Nt−1−a, a) — every pair costs Nt + 1 — and
+  int nt, mt, pslot, kbeg_ = 0, kend_ = g.N;
+  if (MODE == MODE_GRADV) {
+    // Split-K: unit = (stripe nt, 256-row K-chunk c ≥ 0) with c < Nt − nt, so every unit costs the
+    // same 16 K-steps (the ∇std pass runs on E·L_q queries only: one workgroup per CU would leave
+    // the light stripes' CUs idle).  Units of one (nt, c) block share their L⁻¹ block: each XCD
+    // takes a contiguous run of blocks over all query tiles.  Partial slot = block index.
+    const int U = Mt * (GV_SPLIT * Nt * (Nt + 1) / 2);
+    const int t = (U & 7) == 0 ? (b & 7) * (U >> 3) + (b >> 3) : b;
+    int blk = t / Mt;
+    mt = t - blk * Mt;
+    pslot = blk;
+    nt = 0;
+    while (blk >= GV_SPLIT * (Nt - nt)) { blk -= GV_SPLIT * (Nt - nt); ++nt; }
+    kbeg_ = nt * ST_BN + blk * (ST_BN / GV_SPLIT);
+    kend_ = min(g.N, kbeg_ + ST_BN / GV_SPLIT);
+  } else if (TRI) {
+    // Stripe nt costs ∝ nt + 1 K-sweeps (VAR; GRADV: Nt − nt, mirrored below).  Pair stripes
+    // (Nt−1−a, a) — every pair costs Nt + 1 — and
     // give each pair to X = 16/Nt XCDs (blocks b, b+8, … share an XCD), each XCD taking 1/X of the
     // pair's query tiles, heavy stripe first: equal work per XCD, and each XCD's L2 holds only its
     // two stripes of L⁻ᵀ (each stripe is fetched by X XCDs instead of all eight).
@@ -147,17 +178,19 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
       nt = Nt - 1 - b / Mt;
       mt = b % Mt;
     }
+    pslot = nt;
   } else {
     // XCD-aware order: blocks b and b+8 share an XCD (round-robin dispatch); give each XCD a
     // contiguous run of n-major tiles so its L2 serves the same E11⁻¹ column stripes.
     const int t = (T & 7) == 0 ? (b & 7) * (T >> 3) + (b >> 3) : b;
     nt = t / Mt;
     mt = t - nt * Mt;
+    pslot = nt;
   }
   const int64_t m0 = (int64_t)mt * ST_BM;
   const int n0 = nt * ST_BN;
   const int Np = g.N_pad;
-  const double* __restrict__ Bop = VAR ? g.Linv_t : g.Ainv;
+  const double* __restrict__ Bop = MODE == MODE_VAR ? g.Linv_t : (MODE == MODE_GRADV ? g.Linv : g.Ainv);
   const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
 
   // K* generation: thread → query row gm, GEN_PER k-columns starting at gk (wave-uniform)
@@ -165,10 +198,12 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
   const int gm = tid & (ST_BM - 1);
   const int gk = __builtin_amdgcn_readfirstlane((tid >> 7) * GEN_PER);
   double qx, qy, qz;
+  const double* vrow = nullptr;  // MODE_GRADV: this thread's row of the stored V
   {
     const int64_t m = min(m0 + gm, M - 1);  // pad rows replicate a valid query
     qx = X[3 * m]; qy = X[3 * m + 1]; qz = X[3 * m + 2];
     if (tid < ST_BM) { xq[3 * tid] = qx; xq[3 * tid + 1] = qy; xq[3 * tid + 2] = qz; }
+    if (MODE == MODE_GRADV) vrow = vin + (vsel ? vsel[m] : m) * (int64_t)Np;
   }
   // E11⁻¹ tile: 16 rows × ST_BN columns, 8 consecutive doubles per thread
   constexpr int A_TPR = ST_BN / 8;                      // threads per row
@@ -181,6 +216,11 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     const dbl2v* src = reinterpret_cast<const dbl2v*>(Bop + (int64_t)(kb + ar) * Np + n0 + ac);
 #pragma unroll
     for (int i = 0; i < 4; ++i) av[i] = src[i];
+    if (MODE == MODE_GRADV) {
+#pragma unroll
+      for (int i = 0; i < GEN_PER; ++i) kv[i] = vrow[kb + gk + i];
+      return;
+    }
     const double* x1 = g.X1 + 3 * (kb + gk);
 #pragma unroll
     for (int i = 0; i < GEN_PER; ++i) {
@@ -205,19 +245,25 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0, 0, 0, 0};
 
-  // B rows ≥ N are zero: stop at the last live K-step (and, for L⁻ᵀ, at the tile's diagonal)
-  const int kend = VAR ? min(g.N, n0 + ST_BN) : g.N;
-  const int nK = (kend + ST_BK - 1) / ST_BK;
-  stage_load(0);
+  // B rows ≥ N are zero: stop at the last live K-step; L⁻ᵀ (VAR) also stops at the tile's
+  // diagonal, L⁻¹ (GRADV) starts there
+  const int kbeg = MODE == MODE_GRADV ? kbeg_ : 0;
+  const int kend = VAR ? min(g.N, n0 + ST_BN) : kend_;
+  const int nK = (kend - kbeg + ST_BK - 1) / ST_BK;
+  stage_load(kbeg);
   stage_write(0);
   __syncthreads();
   for (int s = 0; s < nK; ++s) {
     // Stage s+1 (clamped at the end: the extra stage lands in the buffer nobody reads again).
-    const int kn = (s + 1 < nK ? s + 1 : s) * ST_BK;
+    const int kn = kbeg + (s + 1 < nK ? s + 1 : s) * ST_BK;
     {
       const dbl2v* src = reinterpret_cast<const dbl2v*>(Bop + (int64_t)(kn + ar) * Np + n0 + ac);
 #pragma unroll
       for (int i = 0; i < 4; ++i) av[i] = src[i];
+      if (MODE == MODE_GRADV) {
+#pragma unroll
+        for (int i = 0; i < GEN_PER; ++i) kv[i] = vrow[kn + gk + i];
+      }
     }
     const double* x1 = g.X1 + 3 * (kn + gk);
     const double* Kt = smem + (s & 1) * (ST_TILE + ST_BTILE);
@@ -242,6 +288,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
       // K* of the next stage spread over the four 16-MFMA groups (overlaps the matrix pipe)
 #pragma unroll
       for (int i = kk * GEN_PER / ST_BK; i < (kk + 4) * GEN_PER / ST_BK; ++i) {
+        if (MODE == MODE_GRADV) break;  // loaded, not generated
 #if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
         kv[i] = qx - x1[3 * i];
 #else
@@ -265,7 +312,18 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
 
   if constexpr (VAR) {
     // Epilogue: per owned row Σ V² over this wave's 64 columns, reduced over the 16 lanes of a
-    // row, then over the column waves in LDS.
+    // row, then over the column waves in LDS; V itself to vout when asked (16 lanes of a row write
+    // 128 contiguous bytes).
+    if (vout) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double* vr = vout + (m0 + wr + 16 * i + (lane >> 4) + 4 * r) * (int64_t)Np + n0 + wc + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vr[16 * j] = acc[i][j][r];
+        }
+    }
     double* red = smem;  // [ST_WN][ST_BM]
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -286,7 +344,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
       double v = 0.0;
 #pragma unroll
       for (int w = 0; w < ST_WN; ++w) v += red[w * ST_BM + tid];
-      partial[(int64_t)nt * M_pad + m0 + tid] = v;
+      partial[(int64_t)pslot * M_pad + m0 + tid] = v;
     }
     return;
   }
@@ -348,7 +406,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     double v = 0.0;
 #pragma unroll
     for (int w = 0; w < ST_WN; ++w) v += red[(w * ST_BM + row) * 4 + c];
-    partial[((int64_t)nt * M_pad + m0 + row) * 4 + c] = v;
+    partial[((int64_t)pslot * M_pad + m0 + row) * 4 + c] = v;
   }
 }
 
@@ -595,15 +653,16 @@ size_t gpis_var_ws_bytes(const cdx_gpis& g, int64_t M) {
 }
 
 size_t gpis_grad_ws_bytes(const cdx_gpis& g, int64_t M) {
-  return (size_t)(g.N_pad / ST_BN) * (size_t)round_up(M, ST_BM) * 4 * sizeof(double);
+  const size_t nt = (size_t)(g.N_pad / ST_BN);
+  return GV_SPLIT * nt * (nt + 1) / 2 * (size_t)round_up(M, ST_BM) * 4 * sizeof(double);  // split-K slots
 }
 
 template <int KT>
 static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double* std_out, double* var_out,
-                          double* partial, int64_t M_pad, int Mt, int n_tiles, hipStream_t s) {
+                          double* partial, int64_t M_pad, int Mt, int n_tiles, double* vout, hipStream_t s) {
   prof_mark(PROF_GPIS_STD, true, s);
-  hipLaunchKernelGGL((gpis_std_kernel<KT, true>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g, X, M,
-                     partial, M_pad, Mt, n_tiles);
+  hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g, X,
+                     M, partial, M_pad, Mt, n_tiles, vout, nullptr, nullptr);
   prof_mark(PROF_GPIS_STD, false, s);
   hipLaunchKernelGGL(gpis_var_finalize<KT>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, g, partial, M, M_pad,
                      n_tiles, std_out, var_out);
@@ -611,22 +670,34 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
 
 template <int KT>
 static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const int64_t* sel, const double* var,
-                           double* gstd, double* partial, int64_t M_pad, int Mt, int n_tiles, hipStream_t s) {
+                           double* gstd, double* partial, int64_t M_pad, int Mt, int n_tiles, const double* vin,
+                           hipStream_t s) {
   prof_mark(PROF_GPIS_GRAD, true, s);
+  int n_parts = n_tiles;
+  if (vin) {
+    n_parts = GV_SPLIT * n_tiles * (n_tiles + 1) / 2;  // split-K units (stripe, K-chunk)
+    hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV>), dim3((unsigned)(Mt * n_parts)), dim3(ST_THREADS), 0, s, g,
+                       X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel);
+  } else {
 #if defined(CDX_STD_MFMA4)
-  hipLaunchKernelGGL(gpis_std_kernel4<KT>, dim3((unsigned)(Mt * n_tiles)), dim3(256), 0, s, g, X, M, partial, M_pad,
-                     Mt, n_tiles);
+    hipLaunchKernelGGL(gpis_std_kernel4<KT>, dim3((unsigned)(Mt * n_tiles)), dim3(256), 0, s, g, X, M, partial, M_pad,
+                       Mt, n_tiles);
 #else
-  hipLaunchKernelGGL((gpis_std_kernel<KT, false>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g, X, M,
-                     partial, M_pad, Mt, n_tiles);
+    hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRAD>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g,
+                       X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr);
 #endif
+  }
   prof_mark(PROF_GPIS_GRAD, false, s);
   hipLaunchKernelGGL(gpis_grad_finalize, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, partial, M, M_pad,
-                     n_tiles, sel, var, gstd);
+                     n_parts, sel, var, gstd);
+}
+
+size_t gpis_v_bytes(const cdx_gpis& g, int64_t M) {
+  return (size_t)round_up(M, ST_BM) * (size_t)g.N_pad * sizeof(double);
 }
 
 int gpis_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* std_out, double* var_out, void* ws,
-                    hipStream_t s) {
+                    hipStream_t s, double* vout) {
   if (M <= 0) return CDX_OK;
   const int64_t M_pad = round_up(M, ST_BM);
   const int n_tiles = g.N_pad / ST_BN;
@@ -634,25 +705,26 @@ int gpis_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* std_o
   const int Mt = (int)(M_pad / ST_BM);
   double* partial = static_cast<double*>(ws);
   switch (g.kernel) {
-    case CDX_KERNEL_TPS: var_launch_kt<CDX_KERNEL_TPS>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, s); break;
-    case CDX_KERNEL_RBF: var_launch_kt<CDX_KERNEL_RBF>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, s); break;
-    default: var_launch_kt<CDX_KERNEL_JOINT>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, s); break;
+    case CDX_KERNEL_TPS: var_launch_kt<CDX_KERNEL_TPS>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, vout, s); break;
+    case CDX_KERNEL_RBF: var_launch_kt<CDX_KERNEL_RBF>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, vout, s); break;
+    default: var_launch_kt<CDX_KERNEL_JOINT>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, vout, s); break;
   }
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
 int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_t* sel, const double* var,
-                     double* gstd, void* ws, hipStream_t s) {
+                     double* gstd, void* ws, hipStream_t s, const double* vin) {
+  if (vin && !g.Linv) return CDX_EINVAL;
   if (M <= 0) return CDX_OK;
   const int64_t M_pad = round_up(M, ST_BM);
   const int n_tiles = g.N_pad / ST_BN;
-  if (M_pad / ST_BM * n_tiles > 0x7fffffff) return CDX_EINVAL;
+  if (M_pad / ST_BM * (int64_t)GV_SPLIT * n_tiles * (n_tiles + 1) / 2 > 0x7fffffff) return CDX_EINVAL;
   const int Mt = (int)(M_pad / ST_BM);
   double* partial = static_cast<double*>(ws);
   switch (g.kernel) {
-    case CDX_KERNEL_TPS: grad_launch_kt<CDX_KERNEL_TPS>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, s); break;
-    case CDX_KERNEL_RBF: grad_launch_kt<CDX_KERNEL_RBF>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, s); break;
-    default: grad_launch_kt<CDX_KERNEL_JOINT>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, s); break;
+    case CDX_KERNEL_TPS: grad_launch_kt<CDX_KERNEL_TPS>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s); break;
+    case CDX_KERNEL_RBF: grad_launch_kt<CDX_KERNEL_RBF>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s); break;
+    default: grad_launch_kt<CDX_KERNEL_JOINT>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s); break;
   }
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }

@@ -8,10 +8,15 @@
 namespace cdx {
 size_t gpis_var_ws_bytes(const cdx_gpis& g, int64_t M);
 size_t gpis_grad_ws_bytes(const cdx_gpis& g, int64_t M);
-// std[m] = sqrt|k0 − ‖L⁻¹k(x_m)‖²|, var_out[m] = the signed k0 − ‖L⁻¹k‖² (nullable).
+// Bytes of the stored whitened vectors V = (L⁻¹K*ᵀ)ᵀ of M queries ([round_up(M, 128), N_pad] f64).
+size_t gpis_v_bytes(const cdx_gpis& g, int64_t M);
+// std[m] = sqrt|k0 − ‖L⁻¹k(x_m)‖²|, var_out[m] = the signed k0 − ‖L⁻¹k‖² (nullable); vout
+// (nullable, gpis_v_bytes) receives V.
 int gpis_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* std_out, double* var_out, void* ws,
-                    hipStream_t s);
+                    hipStream_t s, double* vout = nullptr);
 // gstd[sel[m]] = ∇std at X[m] (sel null: identity), scaled by var[sel[m]] from gpis_var_launch.
+// vin null: W = E11⁻¹k (2N² flops per query); vin = the V of gpis_var_launch: W = L⁻ᵀ v from row
+// sel[m] of V (N² flops per query; needs g.Linv).
 int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_t* sel, const double* var,
-                     double* gstd, void* ws, hipStream_t s);
+                     double* gstd, void* ws, hipStream_t s, const double* vin = nullptr);
 }  // namespace cdx

@@ -40,10 +40,11 @@ class _State:
         y1 = y1.to(dev, torch.float64).reshape(-1).contiguous()
         self.Ainv = torch.empty(Np, Np, dtype=torch.float64, device=dev)
         self.Linv_t = torch.empty(Np, Np, dtype=torch.float64, device=dev)
+        self.Linv = torch.empty(Np, Np, dtype=torch.float64, device=dev)
         self.alpha = torch.empty(Np, dtype=torch.float64, device=dev)
         info = torch.zeros(1, dtype=torch.int32, device=dev)
         ws = torch.empty(lib.cdx_gpis_factor_workspace(Np), dtype=torch.uint8, device=dev)
-        N.check(lib.cdx_gpis_factor(N.ptr(E11), N.ptr(y1), n, Np, N.ptr(ws), N.ptr(self.Ainv), N.ptr(self.Linv_t), N.ptr(self.alpha),
+        N.check(lib.cdx_gpis_factor(N.ptr(E11), N.ptr(y1), n, Np, N.ptr(ws), N.ptr(self.Ainv), N.ptr(self.Linv_t), N.ptr(self.Linv), N.ptr(self.alpha),
                                     N.ptr(info), N.stream_ptr(dev)), "cdx_gpis_factor")
         bad = int(info.item())  # one host sync per state build
         del ws
@@ -52,7 +53,7 @@ class _State:
         self.X1 = X1[:1].to(torch.float64).repeat(Np, 1).contiguous()
         self.X1[:n] = X1.to(torch.float64)
         self.desc = N.CdxGpis(X1=self.X1.data_ptr(), alpha=self.alpha.data_ptr(), Ainv=self.Ainv.data_ptr(),
-                              Linv_t=self.Linv_t.data_ptr(), N=n,
+                              Linv_t=self.Linv_t.data_ptr(), Linv=self.Linv.data_ptr(), N=n,
                               N_pad=Np, kernel=N.KERNELS[kernel], R=float(R), sigma=float(sigma), bias=float(bias))
         self.ws = None
 
@@ -214,7 +215,7 @@ class GPIS:
         sub = _State.__new__(_State)
         sub.__dict__.update(st.__dict__)
         sub.alpha = st.alpha * mask
-        sub.desc = N.CdxGpis(X1=st.desc.X1, alpha=sub.alpha.data_ptr(), Ainv=st.desc.Ainv, Linv_t=st.desc.Linv_t, N=st.desc.N,
+        sub.desc = N.CdxGpis(X1=st.desc.X1, alpha=sub.alpha.data_ptr(), Ainv=st.desc.Ainv, Linv_t=st.desc.Linv_t, Linv=st.desc.Linv, N=st.desc.N,
                              N_pad=st.desc.N_pad, kernel=st.desc.kernel, R=st.desc.R, sigma=st.desc.sigma,
                              bias=st.desc.bias)
         _, _, normal = gpis_mean(sub, X, want_grad=False, want_normal=True)

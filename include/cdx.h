@@ -41,6 +41,8 @@ enum {
  *   Linv_t [N_pad*N_pad] (L^{-1})^T for E11 = L L^T (upper triangular), zero-padded; std path:
  *          std² = |k0 - ‖L^{-1} k‖²| (the whitened form: N² flops per query, and 1e-12 from the
  *          reference's per-call solve where k^T E11^{-1} k with an explicit inverse is 1e-7)
+ *   Linv   [N_pad*N_pad] L^{-1} (lower triangular, row-major), zero-padded; closure ∇std path:
+ *          E11^{-1} k = L^{-T} v from the stored whitened vector v = L^{-1} k (N² flops per query)
  * kernel: 0 = thin-plate spline 2r³-3Rr²+R³ (gpis.py:21-26, the default),
  *         1 = RBF exp(-r²/2σ²) (:16-19), 2 = 0.3·RBF + 0.7·TPS (:28-29). */
 enum { CDX_KERNEL_TPS = 0, CDX_KERNEL_RBF = 1, CDX_KERNEL_JOINT = 2 };
@@ -51,6 +53,7 @@ typedef struct {
   const double* alpha;
   const double* Ainv;
   const double* Linv_t;
+  const double* Linv;
   int32_t N;
   int32_t N_pad;      /* multiple of CDX_NPAD_ALIGN (256), >= N */
   int32_t kernel;
@@ -87,12 +90,13 @@ int cdx_gpis_fit(const double* X1, int32_t N, const double* noise, int32_t kerne
 size_t cdx_gpis_factor_workspace(int32_t N_pad);
 
 /* Query state from a fitted E11 (the solve gpis.py:53 repeats on every pred, done once):
- * E11 = L Lᵀ by blocked Cholesky + triangular inverse in f64, then Ainv = E11⁻¹ = L⁻ᵀL⁻¹ and
- * Linv_t = L⁻ᵀ [N_pad*N_pad] zero-padded, alpha = L⁻ᵀ(L⁻¹ y1) [N_pad] zero-padded.
+ * E11 = L Lᵀ by blocked Cholesky + triangular inverse in f64, then Ainv = E11⁻¹ = L⁻ᵀL⁻¹,
+ * Linv_t = L⁻ᵀ and Linv = L⁻¹ [N_pad*N_pad] zero-padded, alpha = L⁻ᵀ(L⁻¹ y1) [N_pad] zero-padded.
  * *info (device int32) = 0, or the 1-based row of the first non-positive pivot (E11 not
  * positive definite; outputs are then undefined). */
 int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pad, void* workspace,
-                    double* Ainv, double* Linv_t, double* alpha, int32_t* info, cdx_stream_t stream);
+                    double* Ainv, double* Linv_t, double* Linv, double* alpha, int32_t* info,
+                    cdx_stream_t stream);
 
 /* ------------------------------------------------------------------ FK ----------
  * Replaces DifferentiableRobotModel.compute_forward_kinematics(q, link_names,

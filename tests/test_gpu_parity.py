@@ -142,6 +142,9 @@ def test_gpis_factor_is_the_inverse(state):
     Lt = Lt[:n, :n]
     assert not np.tril(Lt, -1).any()
     assert np.abs(Lt.T @ E @ Lt - np.eye(n)).max() < 1e-8
+    Lr = st.Linv.cpu().numpy()  # L⁻¹ row-major (the closure's ∇std pass)
+    assert not Lr[n:].any() and not Lr[:, n:].any()
+    assert np.array_equal(Lr[:n, :n], Lt.T)
 
 
 @pytest.mark.parametrize("n", [1, 5, 64, 255, 300])
