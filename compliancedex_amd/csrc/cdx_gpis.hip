@@ -752,7 +752,8 @@ int cdx_gpis_mean(const cdx_gpis* g, const double* X, int64_t M, double* mean, d
 
 size_t cdx_gpis_std_workspace(const cdx_gpis* g, int64_t M) {
   if (!g || M <= 0 || g->N_pad <= 0) return 0;
-  return cdx::gpis_var_ws_bytes(*g, M) + cdx::gpis_grad_ws_bytes(*g, M) + (size_t)round_up(M, 32) * sizeof(double);
+  return cdx::gpis_var_ws_bytes(*g, M) + cdx::gpis_grad_ws_bytes(*g, M) + (size_t)round_up(M, 32) * sizeof(double) +
+         cdx::gpis_v_bytes(*g, M);
 }
 
 int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std_out, double* grad_std, void* workspace,
@@ -765,9 +766,11 @@ int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std_out,
   double* var = reinterpret_cast<double*>(ws);
   void* pv = ws + (size_t)round_up(M, 32) * sizeof(double);
   void* pg = static_cast<char*>(pv) + cdx::gpis_var_ws_bytes(*g, M);
-  int rc = cdx::gpis_var_launch(*g, X, M, std_out, var, pv, s);
+  double* V = reinterpret_cast<double*>(static_cast<char*>(pg) + cdx::gpis_grad_ws_bytes(*g, M));
+  const bool whitened_grad = grad_std && g->Linv;  // ∇std = −L⁻ᵀv·∇k/std from the kept V
+  int rc = cdx::gpis_var_launch(*g, X, M, std_out, var, pv, s, whitened_grad ? V : nullptr);
   if (rc || !grad_std) return rc;
-  return cdx::gpis_grad_launch(*g, X, M, nullptr, var, grad_std, pg, s);
+  return cdx::gpis_grad_launch(*g, X, M, nullptr, var, grad_std, pg, s, whitened_grad ? V : nullptr);
 }
 
 // Test hook: D[16×16] = A[16×4]·B[4×16] through one v_mfma_f64_16x16x4_f64 (layout check).

@@ -74,8 +74,11 @@ int cdx_gpis_mean(const cdx_gpis* g, const double* X, int64_t M, double* mean,
 size_t cdx_gpis_std_workspace(const cdx_gpis* g, int64_t M);
 
 /* Posterior standard deviation sqrt|k(0) - kᵀ E11^{-1} k| (gpis.py:56-59, the value the
- * reference returns as "var") and its gradient -sign·(E11^{-1}k)ᵀ(∂k/∂x)/std.
- * One fp64 MFMA GEMM with K* generated on chip.  std [M]; grad_std [M*3] (nullable). */
+ * reference returns as "var") and its gradient -sign·(E11^{-1}k)ᵀ(∂k/∂x)/std, in the whitened
+ * form: v = L^{-1}k (triangular fp64 MFMA GEMM, K* generated on chip), std² = |k0 − ‖v‖²|, and
+ * for the gradient E11^{-1}k = L^{-T}v (second triangular GEMM on the kept v; needs Linv, else
+ * the explicit Ainv).  std [M]; grad_std [M*3] (nullable).  Workspace holds v: M·N_pad·8 bytes
+ * plus partial sums (cdx_gpis_std_workspace). */
 int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std, double* grad_std,
                  void* workspace, cdx_stream_t stream);
 
