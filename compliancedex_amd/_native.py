@@ -43,7 +43,7 @@ class CdxProblem(C.Structure):
                 ("weight", C.c_double * MAX_LEVELS), ("ref_q", C.c_float * MAX_DOFS), ("cos_mu", C.c_float),
                 ("gravity", C.c_int32), ("optimize_palm", C.c_int32), ("_pad", C.c_int32), ("com", C.c_float * 3),
                 ("dummy_target_z", C.c_float), ("dummy_comp", C.c_float), ("_pad2", C.c_float),
-                ("uncertainty", C.c_double)]
+                ("uncertainty", C.c_double), ("loop", C.c_void_p)]
 
 
 MAX_PAIRS = 28
@@ -72,7 +72,7 @@ OPT_BUFFER_FIELDS = ["q", "comp", "target", "palm_pos", "palm_ori", "g_q", "g_co
 
 
 class CdxOptBuffers(C.Structure):
-    _fields_ = [(n, C.c_void_p) for n in OPT_BUFFER_FIELDS]
+    _fields_ = [(n, C.c_void_p) for n in OPT_BUFFER_FIELDS] + [("loop", C.c_void_p)]
 
 
 _P = C.c_void_p

@@ -77,6 +77,10 @@ __global__ __launch_bounds__(64) void closure_queries_kernel(cdx_problem P, int6
                                                              double* __restrict__ X, double* __restrict__ pre_out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E) return;
+  if (P.loop && e == 0) {  // advance the device loop counters (read by the later kernels)
+    P.loop->seed += 1;
+    P.loop->step += 1;
+  }
   const int T = P.chain.n_tips, D = P.chain.n_dofs, Lq = P.n_query_levels;
   double tip[CDX_MAX_TIPS][3], Rp[9];
   float tl[CDX_MAX_TIPS][3];
@@ -248,7 +252,7 @@ __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_
   if (noise) {
     in.noise = noise + t * 9;
   } else {
-    device_noise(seed, t, nz);
+    device_noise(P.loop ? seed ^ splitmix64(P.loop->seed) : seed, t, nz);
     in.noise = nz;
   }
   in.noise_stride = 0;

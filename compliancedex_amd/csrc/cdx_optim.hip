@@ -24,6 +24,7 @@ __global__ __launch_bounds__(64) void optimizer_step_kernel(cdx_adam cfg, cdx_op
                                                             int s) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E) return;
+  if (b.loop) s = b.loop->step;  // graph-replayable loop: the closure advanced it
   // best iterate (before the step, with the parameters the closure saw)
   if (s > cfg.best_after && b.total_loss[e] < b.opt_value[e]) {
     b.opt_value[e] = b.total_loss[e];

@@ -105,6 +105,7 @@ class ProbabilisticGraspOptimizer:
         self._problem = self._problem_state = self._problem_key = None
         self._ws = None
         self._seed = int(seed)
+        self._graphs = {}
         self.optim = None
 
     # ------------------------------------------------------------------ FK
@@ -150,17 +151,23 @@ class ProbabilisticGraspOptimizer:
             self._problem_key = key
         return self._problem
 
-    def _closure_into(self, p, q, comp, target, pp, po, noise, out):
-        """cdx_closure on contiguous f64 device tensors, writing into the preallocated ``out``."""
+    def _ensure_ws(self, p, E, dev):
+        need = N.load().cdx_closure_workspace(p, E)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
+
+    def _closure_into(self, p, q, comp, target, pp, po, noise, out, seed=None):
+        """cdx_closure on contiguous f64 device tensors, writing into the preallocated ``out``.
+        ``seed``: the Kabsch-noise key (default: the next value of this optimiser's counter)."""
         lib = N.load()
         E = q.shape[0]
-        need = lib.cdx_closure_workspace(p, E)
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=q.device)
-        self._seed += 1
+        self._ensure_ws(p, E, q.device)
+        if seed is None:
+            self._seed += 1
+            seed = self._seed
         stream = N.stream_ptr(q.device)
         N.check(lib.cdx_closure(p, E, N.ptr(q), N.ptr(comp), N.ptr(target), N.ptr(pp), N.ptr(po), N.ptr(noise),
-                                self._seed, N.ptr(self._ws), N.ptr(out["total_loss"]), N.ptr(out["total_margin"]),
+                                seed, N.ptr(self._ws), N.ptr(out["total_loss"]), N.ptr(out["total_margin"]),
                                 N.ptr(out.get("pregrasp_tip")), N.ptr(out["g_q"]), N.ptr(out["g_comp"]),
                                 N.ptr(out["g_target"]), N.ptr(out["g_palm_pos"]), N.ptr(out["g_palm_ori"]),
                                 N.ptr(out.get("flip")), stream), "cdx_closure")
@@ -217,23 +224,24 @@ class ProbabilisticGraspOptimizer:
 
     # -------------------------------------------------------------- optimize
     def optimize(self, init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose=True,
-                 noise_tape=None, fused=True, init_palm=None):
+                 noise_tape=None, fused=True, init_palm=None, graph=False):
         """The reference's optimisation loop (:771-839).  ``fused=True`` (default): per iteration
         one cdx_closure + one cdx_optimizer_step (Adam, best iterate, clamps on device, no host
         sync); ``fused=False``: the same loop with torch.optim.Adam.  ``noise_tape``: optional
         per-iteration Kabsch noise tensors (parity replay).  ``init_palm`` [E, 6]: start from these
-        palm poses instead of ``palm_offset`` (the annealing outer loop's proposals)."""
+        palm poses instead of ``palm_offset`` (the annealing outer loop's proposals).  ``graph=True``
+        (fused only): capture the whole loop once per (E, problem) as a hipGraph and replay it."""
         if init_palm is not None:
             saved = self.palm_offset
             self.palm_offset = init_palm.detach().to(torch.float64)
             try:
                 return self.optimize(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
-                                     noise_tape, fused)
+                                     noise_tape, fused, graph=graph)
             finally:
                 self.palm_offset = saved
         if fused:
             return self._optimize_fused(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
-                                        noise_tape)
+                                        noise_tape, graph)
         joint_angles = init_joint_angles.clone().requires_grad_(True)
         compliance = compliance.clone().requires_grad_(True)
         params_list = [{"params": joint_angles, "lr": 1e-3}, {"params": compliance, "lr": 0.2}]
@@ -293,43 +301,101 @@ class ProbabilisticGraspOptimizer:
         cfg.best_after = 20
         return cfg
 
-    def _optimize_fused(self, init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose, noise_tape):
+    def _optimize_fused(self, init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose, noise_tape,
+                        graph=False):
+        """Device-resident loop: per iteration one cdx_closure + one cdx_optimizer_step, with the
+        Kabsch-noise key and Adam's step count in device loop counters (cdx_loop), so the loop is
+        the same whether launched eagerly or replayed from a captured hipGraph (``graph=True``;
+        captured once per (E, problem), replayed on later calls)."""
         lib = N.load()
         p = self.problem(gpis, friction_mu)
         E = init_joint_angles.shape[0]
         T, D, K = p.chain.n_tips, p.chain.n_dofs, p.n_levels
         dev = init_joint_angles.device
         f64 = dict(dtype=torch.float64, device=dev)
-        q = init_joint_angles.detach().to(**f64).clone()
-        comp = compliance.detach().to(**f64).clone()
-        target = target_pose.detach().to(**f64).clone()
-        pp = self.palm_offset[:, :3].to(**f64).clone()
-        po = self.palm_offset[:, 3:].to(**f64).clone()
-        out = self._outputs(E, T, D, K, dev, with_pre=False)
-        z = torch.zeros_like
-        st = dict(m_q=z(q), v_q=z(q), m_comp=z(comp), v_comp=z(comp), m_target=z(target), v_target=z(target),
-                  m_palm_pos=z(pp), v_palm_pos=z(pp), m_palm_ori=z(po), v_palm_ori=z(po),
-                  opt_value=torch.full((E,), float("inf"), **f64), opt_margin=torch.zeros(E, T, **f64),
-                  opt_q=init_joint_angles.detach().to(**f64).clone(), opt_comp=comp.clone(), opt_target=target.clone(),
-                  opt_palm=self.palm_offset.to(**f64).clone())
-        bufs = N.CdxOptBuffers(q=q.data_ptr(), comp=comp.data_ptr(), target=target.data_ptr(), palm_pos=pp.data_ptr(),
-                               palm_ori=po.data_ptr(), g_q=out["g_q"].data_ptr(), g_comp=out["g_comp"].data_ptr(),
-                               g_target=out["g_target"].data_ptr(), g_palm_pos=out["g_palm_pos"].data_ptr(),
-                               g_palm_ori=out["g_palm_ori"].data_ptr(), total_loss=out["total_loss"].data_ptr(),
-                               total_margin=out["total_margin"].data_ptr(),
-                               **{k: v.data_ptr() for k, v in st.items()})
+        if graph and noise_tape is not None:
+            raise ValueError("graph=True draws the Kabsch noise on device; noise_tape needs graph=False")
+        key = (E, id(self._problem_state), float(friction_mu), self.num_iters)
+        cache = self._graphs.get(key) if graph else None
+        if cache is None:
+            z = torch.zeros
+            cache = dict(q=z(E, D, **f64), comp=z(E, T, **f64), target=z(E, T, 3, **f64), pp=z(E, 3, **f64),
+                         po=z(E, 3, **f64), loop=torch.zeros(2, dtype=torch.int64, device=dev))
+            cache["out"] = self._outputs(E, T, D, K, dev, with_pre=False)
+            for k in ("m_q", "v_q"):
+                cache[k] = z(E, D, **f64)
+            for k in ("m_comp", "v_comp", "opt_margin"):
+                cache[k] = z(E, T, **f64)
+            for k in ("m_target", "v_target"):
+                cache[k] = z(E, T, 3, **f64)
+            for k in ("m_palm_pos", "v_palm_pos", "m_palm_ori", "v_palm_ori"):
+                cache[k] = z(E, 3, **f64)
+            cache.update(opt_value=z(E, **f64), opt_q=z(E, D, **f64), opt_comp=z(E, T, **f64),
+                         opt_target=z(E, T, 3, **f64), opt_palm=z(E, 6, **f64))
+        c, out = cache, cache["out"]
+        # (re)initialise the loop state in place — the captured graph reads these buffers
+        c["q"].copy_(init_joint_angles.detach())
+        c["comp"].copy_(compliance.detach())
+        c["target"].copy_(target_pose.detach())
+        c["pp"].copy_(self.palm_offset[:, :3])
+        c["po"].copy_(self.palm_offset[:, 3:])
+        for k in ("m_q", "v_q", "m_comp", "v_comp", "m_target", "v_target", "m_palm_pos", "v_palm_pos", "m_palm_ori",
+                  "v_palm_ori", "opt_margin"):
+            c[k].zero_()
+        c["opt_value"].fill_(float("inf"))
+        c["opt_q"].copy_(init_joint_angles.detach())
+        c["opt_comp"].copy_(c["comp"])
+        c["opt_target"].copy_(c["target"])
+        c["opt_palm"].copy_(self.palm_offset)
+        c["loop"][0] = self._seed  # fresh noise keys per call, identical eager / replayed
+        c["loop"].view(torch.int32)[2] = -1
+        self._seed += self.num_iters
+        st = {k: c[k] for k in ("m_q", "v_q", "m_comp", "v_comp", "m_target", "v_target", "m_palm_pos", "v_palm_pos",
+                                "m_palm_ori", "v_palm_ori", "opt_value", "opt_margin", "opt_q", "opt_comp",
+                                "opt_target", "opt_palm")}
+        bufs = N.CdxOptBuffers(q=c["q"].data_ptr(), comp=c["comp"].data_ptr(), target=c["target"].data_ptr(),
+                               palm_pos=c["pp"].data_ptr(), palm_ori=c["po"].data_ptr(), g_q=out["g_q"].data_ptr(),
+                               g_comp=out["g_comp"].data_ptr(), g_target=out["g_target"].data_ptr(),
+                               g_palm_pos=out["g_palm_pos"].data_ptr(), g_palm_ori=out["g_palm_ori"].data_ptr(),
+                               total_loss=out["total_loss"].data_ptr(), total_margin=out["total_margin"].data_ptr(),
+                               loop=c["loop"].data_ptr(), **{k: v.data_ptr() for k, v in st.items()})
         cfg = self.adam_config()
-        stream = N.stream_ptr(dev)
-        for s in range(self.num_iters):
-            noise = None
-            if noise_tape is not None:
-                noise = noise_tape[s].to(**f64).contiguous()
-            self._closure_into(p, q, comp, target, pp, po, noise, out)
-            N.check(lib.cdx_optimizer_step(cfg, bufs, E, D, T, s, stream), "cdx_optimizer_step")
+
+        def run_loop():
+            stream = N.stream_ptr(dev)
+            p.loop = c["loop"].data_ptr()
+            try:
+                for s in range(self.num_iters):
+                    noise = None
+                    if noise_tape is not None:
+                        noise = noise_tape[s].to(**f64).contiguous()
+                    self._closure_into(p, c["q"], c["comp"], c["target"], c["pp"], c["po"], noise, out, seed=0)
+                    N.check(lib.cdx_optimizer_step(cfg, bufs, E, D, T, s, stream), "cdx_optimizer_step")
+            finally:
+                p.loop = None
+
+        if not graph:
+            run_loop()
+        elif "graph" in cache:
+            cache["graph"].replay()
+        else:
+            # workspace and library state exist before capture; the first call captures AND runs
+            self._ensure_ws(p, E, dev)
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side):
+                    run_loop()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            cache["graph"] = g
+            self._graphs[key] = cache
+            g.replay()
         if not self.optimize_target and torch.is_tensor(target_pose):
-            target_pose.copy_(target)  # the reference clamps the caller's target in place (:834)
+            target_pose.copy_(c["target"])  # the reference clamps the caller's target in place (:834)
         self.total_loss, self.total_margin = out["total_loss"], out["total_margin"]
-        self.best_loss = st["opt_value"]
+        self.best_loss = st["opt_value"].clone()
         if verbose:
             print("Margin:", st["opt_margin"])
-        return st["opt_q"], st["opt_comp"], st["opt_target"], st["opt_palm"], st["opt_margin"]
+        return (st["opt_q"].clone(), st["opt_comp"].clone(), st["opt_target"].clone(), st["opt_palm"].clone(),
+                st["opt_margin"].clone())

@@ -145,6 +145,17 @@ int cdx_fk_backward(const cdx_chain* chain, const float* q, int64_t B, const flo
  * compute_contact_margin (:703-710), forward_kinematics (:657-669). */
 #define CDX_MAX_LEVELS 4
 
+/* Device-resident loop counters (optional).  When cdx_problem.loop is set, every cdx_closure
+ * first advances seed and step by one on the device, keys its on-device Kabsch noise by
+ * (seed argument ^ loop->seed), and cdx_optimizer_step with cdx_opt_buffers.loop set takes its
+ * iteration from loop->step — so a whole optimise loop can be captured once in a hipGraph and
+ * replayed (fresh noise and Adam bias correction per replayed iteration). */
+typedef struct {
+  uint64_t seed;
+  int32_t step;     /* set to -1 before the first iteration */
+  int32_t _pad;
+} cdx_loop;
+
 typedef struct {
   cdx_chain chain;
   cdx_gpis gpis;
@@ -163,6 +174,7 @@ typedef struct {
   float dummy_comp;                     /* gravity·mass/M (f32, :94) */
   float _pad2;
   double uncertainty;                   /* variance-cost weight (:733) */
+  cdx_loop* loop;                       /* device loop counters (nullable) */
 } cdx_problem;
 
 /* Workspace bytes for E candidates. */
@@ -259,9 +271,10 @@ typedef struct {                       /* all device pointers, candidate-major *
   double *m_palm_pos, *v_palm_pos, *m_palm_ori, *v_palm_ori;
   const double *total_loss, *total_margin;                         /* closure outputs */
   double *opt_value, *opt_margin, *opt_q, *opt_comp, *opt_target, *opt_palm;  /* best iterate */
+  const cdx_loop* loop;                                            /* nullable: iteration from loop->step */
 } cdx_opt_buffers;
 
-/* iteration = 0-based loop index s; Adam's step count is s + 1. */
+/* iteration = 0-based loop index s (ignored when buf->loop is set); Adam's step count is s + 1. */
 int cdx_optimizer_step(const cdx_adam* cfg, const cdx_opt_buffers* buf, int64_t E, int32_t n_dofs,
                        int32_t n_tips, int32_t iteration, cdx_stream_t stream);
 

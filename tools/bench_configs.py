@@ -4,6 +4,7 @@
 
 c1     config 1: banana stored GPIS (N = 361), 64 candidates, Allegro and Leap — closure evals/s
        (launch-bound at this size) next to the oracle on the host cores.
+c1opt  config 1 size through the fused optimise loop, eager vs hipGraph replay.
 c2opt  config 2 with the optimiser: closure + fused Adam/best-iterate/clamp step, iterations/s.
 c3     config 3 objects (stored states, box fit, dummy for realsense), 4096 candidates each — closure
        evals/s per object on one GPU (one object per GPU on a node).
@@ -91,6 +92,22 @@ def case_c1(dev):
                           "cpu_threads": torch.get_num_threads(), "nan_candidates": nan}), flush=True)
 
 
+def case_c1opt(dev):
+    """Config 1 size through the fused optimise loop: eager launches vs one captured hipGraph."""
+    from compliancedex_amd.workloads import prob_inputs, stored_gpis
+    g = stored_gpis("banana", dev)
+    E, iters = 64, 30
+    for hand in ("allegro", "leap"):
+        opt, cfg = make_opt(hand, np.zeros((E, 6)), dev, iters)
+        q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=6, spread=True)
+        opt.palm_offset = torch.from_numpy(palm).to(dev)
+        args = [torch.from_numpy(a).to(dev) for a in (q, target, comp)]
+        for graph in (False, True):
+            sec = timed(lambda: opt.optimize(*args, 1, g, verbose=False, graph=graph), 5, warm=2)
+            print(json.dumps({"case": "config1_optimize", "hand": hand, "graph": graph, "E": E, "iterations": iters,
+                              "ms_per_iteration": sec / iters * 1e3, "evals_per_s": E * iters / sec}), flush=True)
+
+
 def case_c2opt(dev):
     from compliancedex_amd.workloads import prob_inputs, synthetic_banana_gpis
     g = synthetic_banana_gpis(2000, dev)
@@ -99,10 +116,11 @@ def case_c2opt(dev):
     q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=6, spread=True)
     opt.palm_offset = torch.from_numpy(palm).to(dev)
     args = [torch.from_numpy(a).to(dev) for a in (q, target, comp)]
-    for fused in (True, False):
-        sec = timed(lambda: opt.optimize(*args, 1, g, verbose=False, fused=fused), 2, warm=1)
-        print(json.dumps({"case": "config2_optimize", "fused_step": fused, "E": E, "iterations": iters,
-                          "ms_per_iteration": sec / iters * 1e3, "evals_per_s": E * iters / sec}), flush=True)
+    for fused, graph in ((True, False), (True, True), (False, False)):
+        sec = timed(lambda: opt.optimize(*args, 1, g, verbose=False, fused=fused, graph=graph), 2, warm=1)
+        print(json.dumps({"case": "config2_optimize", "fused_step": fused, "graph": graph, "E": E,
+                          "iterations": iters, "ms_per_iteration": sec / iters * 1e3,
+                          "evals_per_s": E * iters / sec}), flush=True)
 
 
 def case_c3(dev):
