@@ -128,18 +128,36 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 //   instead of 2N²; launched split-K over 256-row chunks (Nt(Nt+1)/2 partial slots).
 // The triangular modes' tile costs run 1..Nt K-sweeps: stripes are paired heavy+light per XCD.
 enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2 };
-#if !defined(CDX_GV_SPLIT)
-#define CDX_GV_SPLIT 1
-#endif
-constexpr int GV_SPLIT = CDX_GV_SPLIT;  // GRADV K-chunks per 256-row stripe (2: 0.468 vs 0.423 ms at E = 4096)
 
+
+// K-range [lo, hi) of stripe nt in the triangular modes.
+__device__ __host__ inline void stripe_k_range(int mode, int nt, int N, int& lo, int& hi) {
+  lo = mode == MODE_GRADV ? nt * ST_BN : 0;
+  hi = mode == MODE_GRADV ? N : min(N, nt * ST_BN + ST_BN);
+}
+
+// Split-K units per query tile: stripe nt contributes ceil((hi − lo)/CH) chunks of CH rows.
+__host__ inline int split_units(int mode, int Nt, int N, int CH) {
+  int u = 0;
+  for (int nt = 0; nt < Nt; ++nt) {
+    int lo, hi;
+    stripe_k_range(mode, nt, N, lo, hi);
+    u += hi > lo ? (hi - lo + CH - 1) / CH : 0;
+  }
+  return u;
+}
+
+// ksplit = 0: one workgroup per (query tile, stripe).  ksplit = s > 0 (GRADV): one workgroup per
+// (query tile, stripe, K-chunk of ST_BN/s rows), `upm` units per query tile, one partial slot per
+// unit (summed in a fixed order by the finalize kernel: deterministic).
 template <int KT, int MODE>
 __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X,
                                                                         int64_t M, double* __restrict__ partial,
                                                                         int64_t M_pad, int Mt, int Nt,
                                                                         double* __restrict__ vout,
                                                                         const double* __restrict__ vin,
-                                                                        const int64_t* __restrict__ vsel) {
+                                                                        const int64_t* __restrict__ vsel, int ksplit,
+                                                                        int upm) {
   constexpr bool VAR = MODE == MODE_VAR;
   constexpr bool TRI = MODE != MODE_GRAD;
   __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
@@ -148,20 +166,29 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
   const int T = Mt * Nt;
   const int b = blockIdx.x;
   int nt, mt, pslot, kbeg_ = 0, kend_ = g.N;
-  if (MODE == MODE_GRADV) {
-    // Split-K: unit = (stripe nt, 256-row K-chunk c ≥ 0) with c < Nt − nt, so every unit costs the
-    // same 16 K-steps (the ∇std pass runs on E·L_q queries only: one workgroup per CU would leave
-    // the light stripes' CUs idle).  Units of one (nt, c) block share their L⁻¹ block: each XCD
-    // takes a contiguous run of blocks over all query tiles.  Partial slot = block index.
-    const int U = Mt * (GV_SPLIT * Nt * (Nt + 1) / 2);
+  const bool split = ksplit > 0;
+  if (TRI && split) {
+    // Split-K: unit = (stripe nt, K-chunk c) so units cost about the same (the ∇std pass runs on
+    // E·L_q queries only; small-M std passes would otherwise run few, long workgroups).  Units of
+    // one (nt, c) block share their B block: each XCD takes a contiguous run of blocks over all
+    // query tiles.  Partial slot = block index.
+    const int CH = ST_BN / ksplit;
+    const int U = Mt * upm;
     const int t = (U & 7) == 0 ? (b & 7) * (U >> 3) + (b >> 3) : b;
     int blk = t / Mt;
     mt = t - blk * Mt;
     pslot = blk;
-    nt = 0;
-    while (blk >= GV_SPLIT * (Nt - nt)) { blk -= GV_SPLIT * (Nt - nt); ++nt; }
-    kbeg_ = nt * ST_BN + blk * (ST_BN / GV_SPLIT);
-    kend_ = min(g.N, kbeg_ + ST_BN / GV_SPLIT);
+    for (nt = 0;; ++nt) {
+      int lo, hi;
+      stripe_k_range(MODE, nt, g.N, lo, hi);
+      const int nch = hi > lo ? (hi - lo + CH - 1) / CH : 0;
+      if (blk < nch) {
+        kbeg_ = lo + blk * CH;
+        kend_ = min(hi, kbeg_ + CH);
+        break;
+      }
+      blk -= nch;
+    }
   } else if (TRI) {
     // Stripe nt costs ∝ nt + 1 K-sweeps (VAR; GRADV: Nt − nt, mirrored below).  Pair stripes
     // (Nt−1−a, a) — every pair costs Nt + 1 — and
@@ -247,8 +274,8 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
 
   // B rows ≥ N are zero: stop at the last live K-step; L⁻ᵀ (VAR) also stops at the tile's
   // diagonal, L⁻¹ (GRADV) starts there
-  const int kbeg = MODE == MODE_GRADV ? kbeg_ : 0;
-  const int kend = VAR ? min(g.N, n0 + ST_BN) : kend_;
+  const int kbeg = split ? kbeg_ : 0;
+  const int kend = split ? kend_ : (VAR ? min(g.N, n0 + ST_BN) : g.N);
   const int nK = (kend - kbeg + ST_BK - 1) / ST_BK;
   stage_load(kbeg);
   stage_write(0);
@@ -652,17 +679,30 @@ size_t gpis_var_ws_bytes(const cdx_gpis& g, int64_t M) {
   return (size_t)(g.N_pad / ST_BN) * (size_t)round_up(M, ST_BM) * sizeof(double);
 }
 
+// Split factor: the smallest s ∈ {1, 2, 4, 8, 16} giving ≥ 2 units per CU (256 CUs), else 16.
+static int choose_split(int mode, const cdx_gpis& g, int64_t M) {
+  const int Mt = (int)(round_up(M, ST_BM) / ST_BM), Nt = g.N_pad / ST_BN;
+  int s = 1;
+  while (s < 16 && (int64_t)Mt * split_units(mode, Nt, g.N, ST_BN / s) < 512) s *= 2;
+  return s;
+}
+
 size_t gpis_grad_ws_bytes(const cdx_gpis& g, int64_t M) {
-  const size_t nt = (size_t)(g.N_pad / ST_BN);
-  return GV_SPLIT * nt * (nt + 1) / 2 * (size_t)round_up(M, ST_BM) * 4 * sizeof(double);  // split-K slots
+  if (M <= 0) return 0;
+  const int s = choose_split(MODE_GRADV, g, M);
+  const size_t upm = (size_t)split_units(MODE_GRADV, g.N_pad / ST_BN, g.N, ST_BN / s);
+  const size_t dense = (size_t)(g.N_pad / ST_BN);  // the explicit-inverse pass's partial slots
+  return (upm > dense ? upm : dense) * (size_t)round_up(M, ST_BM) * 4 * sizeof(double);
 }
 
 template <int KT>
 static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double* std_out, double* var_out,
                           double* partial, int64_t M_pad, int Mt, int n_tiles, double* vout, hipStream_t s) {
+  // (no split-K here: Σ V² needs the K-summed V, and summing chunk partials with atomics made the
+  // result depend on arrival order — the std pass stays one workgroup per (query tile, stripe))
   prof_mark(PROF_GPIS_STD, true, s);
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g, X,
-                     M, partial, M_pad, Mt, n_tiles, vout, nullptr, nullptr);
+                     M, partial, M_pad, Mt, n_tiles, vout, nullptr, nullptr, 0, 0);
   prof_mark(PROF_GPIS_STD, false, s);
   hipLaunchKernelGGL(gpis_var_finalize<KT>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, g, partial, M, M_pad,
                      n_tiles, std_out, var_out);
@@ -675,16 +715,17 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
   prof_mark(PROF_GPIS_GRAD, true, s);
   int n_parts = n_tiles;
   if (vin) {
-    n_parts = GV_SPLIT * n_tiles * (n_tiles + 1) / 2;  // split-K units (stripe, K-chunk)
+    const int ks = choose_split(MODE_GRADV, g, M);
+    n_parts = split_units(MODE_GRADV, n_tiles, g.N, ST_BN / ks);  // split-K units (stripe, K-chunk)
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV>), dim3((unsigned)(Mt * n_parts)), dim3(ST_THREADS), 0, s, g,
-                       X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel);
+                       X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel, ks, n_parts);
   } else {
 #if defined(CDX_STD_MFMA4)
     hipLaunchKernelGGL(gpis_std_kernel4<KT>, dim3((unsigned)(Mt * n_tiles)), dim3(256), 0, s, g, X, M, partial, M_pad,
                        Mt, n_tiles);
 #else
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRAD>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g,
-                       X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr);
+                       X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, 0, 0);
 #endif
   }
   prof_mark(PROF_GPIS_GRAD, false, s);
@@ -718,7 +759,7 @@ int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_
   if (M <= 0) return CDX_OK;
   const int64_t M_pad = round_up(M, ST_BM);
   const int n_tiles = g.N_pad / ST_BN;
-  if (M_pad / ST_BM * (int64_t)GV_SPLIT * n_tiles * (n_tiles + 1) / 2 > 0x7fffffff) return CDX_EINVAL;
+  if (M_pad / ST_BM * (int64_t)16 * n_tiles * (n_tiles + 1) / 2 > 0x7fffffff) return CDX_EINVAL;
   const int Mt = (int)(M_pad / ST_BM);
   double* partial = static_cast<double*>(ws);
   switch (g.kernel) {
