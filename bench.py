@@ -34,6 +34,7 @@ def parse():
     ap.add_argument("--hand", default="allegro")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-E", type=int, default=256)
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal on one GPU)")
     return ap.parse_args()
 
 
@@ -88,10 +89,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(torch.cuda.device_count(), 1)  # ranks share a GPU only in gloo rehearsals
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     from compliancedex_amd import ProbabilisticGraspOptimizer
     from compliancedex_amd import _native as N
@@ -137,7 +142,7 @@ def main():
     lib.cdx_profile_enable(0)
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     nan_candidates = int((~torch.isfinite(opt.total_loss)).sum())

@@ -15,6 +15,8 @@
 // only the diagonal is formed.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "cdx_gpis.h"
 #include "cdx_gpis_launch.h"
 #include "cdx_prof.h"
@@ -235,7 +237,11 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
   // E11⁻¹ tile: 16 rows × ST_BN columns, 8 consecutive doubles per thread
   constexpr int A_TPR = ST_BN / 8;                      // threads per row
   const int ar = tid / A_TPR, ac = (tid % A_TPR) * 8;
-  const int wr = (wave / ST_WN) * 64, wc = (wave % ST_WN) * 64;
+  // wave → 64×64 sub-tile.  With 4 column waves, waves w and w+4 share SIMD w%4 (round-robin wave
+  // placement); giving them complementary columns (w, 7−w) lets the triangular modes skip the
+  // all-zero K-steps of the diagonal block per wave without idling a SIMD (see skip_mfma below).
+  const int cwave = ST_WN == 4 ? (wave < 4 ? wave : 7 - wave) : wave % ST_WN;
+  const int wr = (wave / ST_WN) * 64, wc = __builtin_amdgcn_readfirstlane(cwave * 64);
 
   dbl2v av[4];
   double kv[GEN_PER];
@@ -295,44 +301,56 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     const double* x1 = g.X1 + 3 * (kn + gk);
     const double* Kt = smem + (s & 1) * (ST_TILE + ST_BTILE);
     const double* As = Kt + ST_TILE;
+    // This wave's B columns [n0 + wc, n0 + wc + 64) are all zero for the whole K-step when the step
+    // lies past their diagonal (L⁻ᵀ, VAR) or before it (L⁻¹, GRADV): skip the MFMAs, keep the
+    // staging and barriers.  acc + 0·A is acc, so results are bit-identical.
+    const int kb = kbeg + s * ST_BK;
+    const bool skip_mfma = (MODE == MODE_VAR && kb >= n0 + wc + 64) || (MODE == MODE_GRADV && kb + ST_BK <= n0 + wc);
+    auto kstep = [&](auto do_mfma) {
 #pragma unroll
-    for (int kk = 0; kk < ST_BK; kk += 4) {
-      const int kra = (kk + (lane >> 4)) * ST_LD + (lane & 15);
-      const int krb = (kk + (lane >> 4)) * ST_LDB + (lane & 15);
-      double a[4], bb[4];
+      for (int kk = 0; kk < ST_BK; kk += 4) {
+        const int kra = (kk + (lane >> 4)) * ST_LD + (lane & 15);
+        const int krb = (kk + (lane >> 4)) * ST_LDB + (lane & 15);
+        double a[4], bb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { a[i] = Kt[kra + wr + 16 * i]; bb[i] = As[krb + wc + 16 * i]; }
+        for (int i = 0; i < 4; ++i) { a[i] = Kt[kra + wr + 16 * i]; bb[i] = As[krb + wc + 16 * i]; }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < 4; ++j) {
 #if defined(CDX_DIAG_NOMFMA)  // timing-only diagnostic build: outputs are wrong
-          acc[i][j][0] += a[i] * bb[j];
+            acc[i][j][0] += a[i] * bb[j];
 #else
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], bb[j], acc[i][j], 0, 0, 0);
+            if constexpr (decltype(do_mfma)::value)
+              acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], bb[j], acc[i][j], 0, 0, 0);
+#endif
+          }
+        // K* of the next stage spread over the four 16-MFMA groups (overlaps the matrix pipe)
+#pragma unroll
+        for (int i = kk * GEN_PER / ST_BK; i < (kk + 4) * GEN_PER / ST_BK; ++i) {
+          if (MODE == MODE_GRADV) break;  // loaded, not generated
+#if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
+          kv[i] = qx - x1[3 * i];
+#else
+          const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
+          double kd;
+          gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
 #endif
         }
-      // K* of the next stage spread over the four 16-MFMA groups (overlaps the matrix pipe)
-#pragma unroll
-      for (int i = kk * GEN_PER / ST_BK; i < (kk + 4) * GEN_PER / ST_BK; ++i) {
-        if (MODE == MODE_GRADV) break;  // loaded, not generated
-#if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
-        kv[i] = qx - x1[3 * i];
-#else
-        const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
-        double kd;
-        gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
-#endif
-      }
 #if defined(CDX_STD_SCHED)
-      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // fragment reads first
+        if constexpr (decltype(do_mfma)::value) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // fragment reads first
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // then up to four VALU
-      }
+          for (int q = 0; q < 16; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // then up to four VALU
+          }
+        }
 #endif
-    }
+      }
+    };
+    if (skip_mfma) kstep(std::false_type{});
+    else kstep(std::true_type{});
     stage_write((s + 1) & 1);
     __syncthreads();
   }
@@ -363,7 +381,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
         v += __shfl_xor(v, 2);
         v += __shfl_xor(v, 4);
         v += __shfl_xor(v, 8);
-        if ((lane & 15) == 0) red[(wave % ST_WN) * ST_BM + wr + 16 * i + (lane >> 4) + 4 * r] = v;
+        if ((lane & 15) == 0) red[cwave * ST_BM + wr + 16 * i + (lane >> 4) + 4 * r] = v;
       }
     }
     __syncthreads();
@@ -423,7 +441,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
       for (int r = 0; r < 4; ++r) {
         const int row = wr + 16 * i + (lane >> 4) + 4 * r;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) red[((wave % ST_WN) * ST_BM + row) * 4 + c] = ps[r][c];
+        for (int c = 0; c < 4; ++c) red[(cwave * ST_BM + row) * 4 + c] = ps[r][c];
       }
     }
   }
