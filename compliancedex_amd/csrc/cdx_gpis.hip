@@ -102,7 +102,7 @@ __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const
 // ds_read_b64 (rows k, k+1) land on disjoint banks.
 constexpr int ST_BM = 128, ST_BK = 16, ST_LD = 144;
 constexpr int ST_TILE = ST_BK * ST_LD;                          // doubles per staged K* tile
-#if defined(CDX_STD_WN2) || defined(CDX_STD_MFMA4)
+#if defined(CDX_STD_WN2)
 constexpr int ST_WN = 2;                                        // waves along N (2 or 4)
 #else
 constexpr int ST_WN = 4;
@@ -113,6 +113,17 @@ constexpr int ST_THREADS = 128 * ST_WN;                         // 2 row-waves √
 constexpr int ST_LDB = ST_BN + 16;                              // padded E11‚Åª¬π row (‚â° 32 dwords mod 64)
 constexpr int ST_BTILE = ST_BK * ST_LDB;
 constexpr int ST_SMEM = 2 * (ST_TILE + ST_BTILE) + ST_BM * 3;   // 2 buffers √ó (K*, E11‚Åª¬π) + query tile
+
+// T4 layout of the B tile (v_mfma_f64_4x4x4_4b_f64 path, triangular modes): lane l needs
+// B[k = l>>4][wc + 4¬∑cg + (l&3)] for cg = 0..15, so each 64-column wave slice is stored as
+// [j = col&3][cg = col>>2 (16) + 2 pad] (72 doubles) and rows are T4_LDB ‚â° 8 (mod 32) doubles
+// apart: the 16 (k, j) lane groups of a ds_read_b128 then cover all 64 banks (the 4 Œ≤ lanes of a
+// group read the same address: broadcast).
+constexpr int T4_SLICE = 72;
+constexpr int T4_LDB = 4 * T4_SLICE + 8;                          // 296
+constexpr int T4_BTILE = ST_BK * T4_LDB;
+constexpr int T4_SMEM = 2 * (ST_TILE + T4_BTILE) + ST_BM * 3;
+__device__ __forceinline__ int t4_bpos(int c) { return (c >> 6) * T4_SLICE + (c & 3) * 18 + ((c & 63) >> 2); }
 
 typedef double dbl2v __attribute__((ext_vector_type(2)));
 
@@ -130,6 +141,11 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 //   instead of 2N¬≤; launched split-K over 256-row chunks (Nt(Nt+1)/2 partial slots).
 // The triangular modes' tile costs run 1..Nt K-sweeps: stripes are paired heavy+light per XCD.
 enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2 };
+#if defined(CDX_STD_T4) && !defined(CDX_STD_WN2)
+constexpr bool STD_T4 = true;   // triangular passes on v_mfma_f64_4x4x4_4b_f64
+#else
+constexpr bool STD_T4 = false;  // triangular passes on v_mfma_f64_16x16x4_f64
+#endif
 
 
 // K-range [lo, hi) of stripe nt in the triangular modes.
@@ -152,7 +168,7 @@ __host__ inline int split_units(int mode, int Nt, int N, int CH) {
 // ksplit = 0: one workgroup per (query tile, stripe).  ksplit = s > 0 (GRADV): one workgroup per
 // (query tile, stripe, K-chunk of ST_BN/s rows), `upm` units per query tile, one partial slot per
 // unit (summed in a fixed order by the finalize kernel: deterministic).
-template <int KT, int MODE>
+template <int KT, int MODE, bool T4 = false>
 __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X,
                                                                         int64_t M, double* __restrict__ partial,
                                                                         int64_t M_pad, int Mt, int Nt,
@@ -162,8 +178,11 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
                                                                         int upm) {
   constexpr bool VAR = MODE == MODE_VAR;
   constexpr bool TRI = MODE != MODE_GRAD;
-  __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
-  double* xq = smem + 2 * (ST_TILE + ST_BTILE);
+  static_assert(!T4 || (TRI && ST_WN == 4), "the 4x4x4 path covers the triangular modes of the 128x256 tile");
+  constexpr int LDB = T4 ? T4_LDB : ST_LDB;
+  constexpr int BTILE = T4 ? T4_BTILE : ST_BTILE;
+  __shared__ __attribute__((aligned(16))) double smem[T4 ? T4_SMEM : ST_SMEM];
+  double* xq = smem + 2 * (ST_TILE + BTILE);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = Mt * Nt;
   const int b = blockIdx.x;
@@ -263,20 +282,36 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     }
   };
   auto stage_write = [&](int buf) {
-    double* Kt = smem + buf * (ST_TILE + ST_BTILE);
+    double* Kt = smem + buf * (ST_TILE + BTILE);
     double* As = Kt + ST_TILE;
 #pragma unroll
     for (int i = 0; i < GEN_PER; ++i) Kt[(gk + i) * ST_LD + gm] = kv[i];
-    dbl2v* dst = reinterpret_cast<dbl2v*>(As + ar * ST_LDB + ac);
+    if constexpr (T4) {
+      double* row = As + ar * LDB;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dst[i] = av[i];
+      for (int i = 0; i < 4; ++i) {
+        row[t4_bpos(ac + 2 * i)] = av[i].x;
+        row[t4_bpos(ac + 2 * i + 1)] = av[i].y;
+      }
+    } else {
+      dbl2v* dst = reinterpret_cast<dbl2v*>(As + ar * LDB + ac);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dst[i] = av[i];
+    }
   };
 
-  dbl4 acc[4][4];
+  dbl4 acc[4][4];      // 16x16x4 path: [row block][col block] of 16√ó16
+  double acc4[4][16];  // T4 path: [row group rg (16 rows)][col group cg (4 cols)]
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0, 0, 0, 0};
+  if constexpr (T4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc4[i][j] = 0.0;
+  }
 
   // B rows ‚â• N are zero: stop at the last live K-step; L‚Åª·µÄ (VAR) also stops at the tile's
   // diagonal, L‚Åª¬π (GRADV) starts there
@@ -299,13 +334,58 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
       }
     }
     const double* x1 = g.X1 + 3 * (kn + gk);
-    const double* Kt = smem + (s & 1) * (ST_TILE + ST_BTILE);
+    const double* Kt = smem + (s & 1) * (ST_TILE + BTILE);
     const double* As = Kt + ST_TILE;
     // This wave's B columns [n0 + wc, n0 + wc + 64) are all zero for the whole K-step when the step
     // lies past their diagonal (L‚Åª·µÄ, VAR) or before it (L‚Åª¬π, GRADV): skip the MFMAs, keep the
     // staging and barriers.  acc + 0¬∑A is acc, so results are bit-identical.
     const int kb = kbeg + s * ST_BK;
     const bool skip_mfma = (MODE == MODE_VAR && kb >= n0 + wc + 64) || (MODE == MODE_GRADV && kb + ST_BK <= n0 + wc);
+    auto kstep4 = [&](auto do_mfma) {  // v_mfma_f64_4x4x4_4b_f64: 16 rows √ó 4 cols √ó 4 deep per issue
+#pragma unroll
+      for (int kk = 0; kk < ST_BK; kk += 4) {
+        const int kra = (kk + (lane >> 4)) * ST_LD + (lane & 15);
+        double a[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = Kt[kra + wr + 16 * i];
+        const dbl2v* bp = reinterpret_cast<const dbl2v*>(As + (kk + (lane >> 4)) * LDB + cwave * T4_SLICE +
+                                                         (lane & 3) * 18);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // B fragments in two halves of 8 column groups (register budget)
+          double bb[8];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) { const dbl2v v = bp[4 * h + c]; bb[2 * c] = v.x; bb[2 * c + 1] = v.y; }
+          if constexpr (decltype(do_mfma)::value) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                acc4[i][8 * h + j] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[i], bb[j], acc4[i][8 * h + j], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int i = kk * GEN_PER / ST_BK; i < (kk + 4) * GEN_PER / ST_BK; ++i) {
+          if (MODE == MODE_GRADV) break;  // loaded, not generated
+#if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
+          kv[i] = qx - x1[3 * i];
+#else
+          const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
+          double kd;
+          gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
+#endif
+        }
+#if defined(CDX_STD_SCHED)
+        if constexpr (decltype(do_mfma)::value) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // fragment reads first
+#pragma unroll
+          for (int q = 0; q < 64; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // then one VALU
+          }
+        }
+#endif
+      }
+    };
     auto kstep = [&](auto do_mfma) {
 #pragma unroll
       for (int kk = 0; kk < ST_BK; kk += 4) {
@@ -349,8 +429,13 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
 #endif
       }
     };
-    if (skip_mfma) kstep(std::false_type{});
-    else kstep(std::true_type{});
+    if constexpr (T4) {
+      if (skip_mfma) kstep4(std::false_type{});
+      else kstep4(std::true_type{});
+    } else {
+      if (skip_mfma) kstep(std::false_type{});
+      else kstep(std::true_type{});
+    }
     stage_write((s + 1) & 1);
     __syncthreads();
   }
@@ -359,6 +444,37 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     // Epilogue: per owned row Œ£ V¬≤ over this wave's 64 columns, reduced over the 16 lanes of a
     // row, then over the column waves in LDS; V itself to vout when asked (16 lanes of a row write
     // 128 contiguous bytes).
+    double* red = smem;  // [ST_WN][ST_BM]
+    if constexpr (T4) {
+      // lane l holds, for row group rg and column group cg, V[row][col] with
+      // row = wr + 16¬∑rg + 4¬∑((l>>2)&3) + (l>>4), col = wc + 4¬∑cg + (l&3)
+      const int r4 = 4 * ((lane >> 2) & 3) + (lane >> 4);
+      if (vout) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          double* vr = vout + (m0 + wr + 16 * i + r4) * (int64_t)Np + n0 + wc + (lane & 3);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) vr[4 * j] = acc4[i][j];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        double v = 0.0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v = fma(acc4[i][j], acc4[i][j], v);
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        if ((lane & 3) == 0) red[cwave * ST_BM + wr + 16 * i + r4] = v;
+      }
+      __syncthreads();
+      if (tid < ST_BM) {
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < ST_WN; ++w) v += red[w * ST_BM + tid];
+        partial[(int64_t)pslot * M_pad + m0 + tid] = v;
+      }
+      return;
+    }
     if (vout) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -369,7 +485,6 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
           for (int j = 0; j < 4; ++j) vr[16 * j] = acc[i][j][r];
         }
     }
-    double* red = smem;  // [ST_WN][ST_BM]
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -390,6 +505,56 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
 #pragma unroll
       for (int w = 0; w < ST_WN; ++w) v += red[w * ST_BM + tid];
       partial[(int64_t)pslot * M_pad + m0 + tid] = v;
+    }
+    return;
+  }
+
+  if constexpr (T4) {  // GRADV on the 4x4x4 layout (see the VAR epilogue for the lane map)
+    double* red = smem;
+    const int r4 = 4 * ((lane >> 2) & 3) + (lane >> 4);
+    double ps[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ps[i][0] = ps[i][1] = ps[i][2] = ps[i][3] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int n = n0 + wc + 4 * j + (lane & 3);
+      const double nx = g.X1[3 * n], ny = g.X1[3 * n + 1], nz = g.X1[3 * n + 2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wr + 16 * i + r4;
+        const double dx = xq[3 * row] - nx, dy = xq[3 * row + 1] - ny, dz = xq[3 * row + 2] - nz;
+        double k, kd;
+        gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, k, kd);
+        const double w = acc4[i][j];
+        const double wkd = w * kd;
+        ps[i][0] += w * k;
+        ps[i][1] += wkd * dx;
+        ps[i][2] += wkd * dy;
+        ps[i][3] += wkd * dz;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        double v = ps[i][c];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        ps[i][c] = v;
+      }
+    if ((lane & 3) == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) red[(cwave * ST_BM + wr + 16 * i + r4) * 4 + c] = ps[i][c];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < ST_BM * 4; idx += ST_THREADS) {
+      const int row = idx >> 2, c = idx & 3;
+      double v = 0.0;
+#pragma unroll
+      for (int w = 0; w < ST_WN; ++w) v += red[(w * ST_BM + row) * 4 + c];
+      partial[((int64_t)pslot * M_pad + m0 + row) * 4 + c] = v;
     }
     return;
   }
@@ -455,189 +620,6 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
   }
 }
 
-// v3: the same 128√ó128 tile, K-step 16, staging and epilogue contract as gpis_std_kernel, on
-// v_mfma_f64_4x4x4_4b_f64 (measured 72-75 TF/s sustained on MI355X vs 47-49 for 16x16x4;
-// tools/microbench/mfma_f64_peak.hip).  Lane layout (probed, tools/microbench/
-// mfma_f64_4x4_layout.hip): A lane 16k+4Œ≤+i = A_Œ≤[i][k], B lane 16k+4Œ≤+j = B_Œ≤[k][j],
-// D lane 16i+4Œ≤+j = D_Œ≤[i][j].  Œ≤ is used as a 4-row sub-block with B broadcast over Œ≤, so one
-// instruction is a 16-row √ó 4-column √ó 4-deep product.  Each wave owns 64 rows √ó 64 columns:
-// 4 row groups rg √ó 16 column groups cg, one f64 accumulator each.  Row/column maps are chosen so
-// every lane's fragments are contiguous in LDS (2 + 8 ds_read_b128 per 4-deep step):
-//   A (K*):   lane l, group rg ‚Üí row wr + 4¬∑(l&15) + rg,            k = k0 + (l>>4)
-//   B (E11‚Åª¬π): lane l, group cg ‚Üí col wc + 16¬∑(l&3) + cg,            k = k0 + (l>>4)
-//   D:        lane l, (rg, cg) ‚Üí row wr + 4¬∑(4¬∑((l>>2)&3) + (l>>4)) + rg, col wc + 16¬∑(l&3) + cg
-#if defined(CDX_STD_MFMA4)
-template <int KT>
-__global__ __launch_bounds__(256, 2) void gpis_std_kernel4(cdx_gpis g, const double* __restrict__ X, int64_t M,
-                                                           double* __restrict__ partial, int64_t M_pad, int Mt,
-                                                           int Nt) {
-  __shared__ __attribute__((aligned(16))) double smem[4 * ST_TILE + ST_BM * 3];
-  double* xq = smem + 4 * ST_TILE;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int T = Mt * Nt;
-  const int b = blockIdx.x;
-  const int t = (T & 7) == 0 ? (b & 7) * (T >> 3) + (b >> 3) : b;
-  const int nt = t / Mt, mt = t - nt * Mt;
-  const int64_t m0 = (int64_t)mt * ST_BM;
-  const int n0 = nt * ST_BN;
-  const int Np = g.N_pad;
-  const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
-
-  const int gm = tid & (ST_BM - 1);
-  const int gk = __builtin_amdgcn_readfirstlane((tid >> 7) * 8);
-  double qx, qy, qz;
-  {
-    const int64_t m = min(m0 + gm, M - 1);
-    qx = X[3 * m]; qy = X[3 * m + 1]; qz = X[3 * m + 2];
-    if (tid < ST_BM) { xq[3 * tid] = qx; xq[3 * tid + 1] = qy; xq[3 * tid + 2] = qz; }
-  }
-  const int ar = tid >> 4, ac = (tid & 15) * 8;
-  const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
-
-  dbl2v av[4];
-  double kv[8];
-  {
-    const dbl2v* src = reinterpret_cast<const dbl2v*>(g.Ainv + (int64_t)ar * Np + n0 + ac);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) av[i] = src[i];
-    const double* x1 = g.X1 + 3 * gk;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
-      double kd;
-      gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
-    }
-  }
-  auto stage_write = [&](int buf) {
-    double* Kt = smem + buf * 2 * ST_TILE;
-    double* As = Kt + ST_TILE;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) Kt[(gk + i) * ST_LD + gm] = kv[i];
-    dbl2v* dst = reinterpret_cast<dbl2v*>(As + ar * ST_LD + ac);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dst[i] = av[i];
-  };
-
-  double acc[4][16];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc[i][j] = 0.0;
-
-  const int nK = (g.N + ST_BK - 1) / ST_BK;  // E11‚Åª¬π rows ‚â• N are zero: stop at the last live K-step
-  stage_write(0);
-  __syncthreads();
-  const int arow = wr + 4 * (lane & 15);         // + rg
-  const int bcol = wc + 16 * (lane & 3);         // + cg
-  for (int s = 0; s < nK; ++s) {
-    const int kn = (s + 1 < nK ? s + 1 : s) * ST_BK;
-    {
-      const dbl2v* src = reinterpret_cast<const dbl2v*>(g.Ainv + (int64_t)(kn + ar) * Np + n0 + ac);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = src[i];
-    }
-    const double* x1 = g.X1 + 3 * (kn + gk);
-    const double* Kt = smem + (s & 1) * 2 * ST_TILE;
-    const double* As = Kt + ST_TILE;
-#pragma unroll
-    for (int kk = 0; kk < ST_BK; kk += 4) {
-      const int kr = (kk + (lane >> 4)) * ST_LD;
-      const dbl2v* ap = reinterpret_cast<const dbl2v*>(Kt + kr + arow);
-      const dbl2v* bp = reinterpret_cast<const dbl2v*>(As + kr + bcol);
-      const dbl2v a01 = ap[0], a23 = ap[1];
-      const double a[4] = {a01.x, a01.y, a23.x, a23.y};
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {  // B fragments in two halves of 8 columns (register budget)
-        double bb[8];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) { const dbl2v v = bp[4 * h + c]; bb[2 * c] = v.x; bb[2 * c + 1] = v.y; }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-#if defined(CDX_DIAG_NOMFMA)  // timing-only diagnostic build: outputs are wrong
-            acc[i][8 * h + j] += a[i] * bb[j];
-#else
-            acc[i][8 * h + j] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[i], bb[j], acc[i][8 * h + j], 0, 0, 0);
-#endif
-          }
-      }
-#pragma unroll
-      for (int i = kk / 2; i < kk / 2 + 2; ++i) {
-#if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
-        kv[i] = qx - x1[3 * i];
-#else
-        const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
-        double kd;
-        gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
-#endif
-      }
-#if defined(CDX_STD_SCHED)
-      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-#pragma unroll
-      for (int q = 0; q < 64; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-      }
-#endif
-    }
-    stage_write((s + 1) & 1);
-    __syncthreads();
-  }
-
-  // Epilogue: lane's rows: wr + 4¬∑r16 + rg with r16 = 4¬∑((l>>2)&3) + (l>>4); columns
-  // wc + 16¬∑(l&3) + cg.  Row sums over this lane's 16 columns, then over the 4 lanes of a row
-  // (xor 1, 2), then over the two column waves in LDS.
-  double* red = smem;
-  const int r16 = 4 * ((lane >> 2) & 3) + (lane >> 4);
-  double ps[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) ps[i][0] = ps[i][1] = ps[i][2] = ps[i][3] = 0.0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int n = n0 + bcol + j;
-    const double nx = g.X1[3 * n], ny = g.X1[3 * n + 1], nz = g.X1[3 * n + 2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = wr + 4 * r16 + i;
-      const double dx = xq[3 * row] - nx, dy = xq[3 * row + 1] - ny, dz = xq[3 * row + 2] - nz;
-      double k, kd;
-      gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, k, kd);
-      const double w = acc[i][j];
-      const double wkd = w * kd;
-      ps[i][0] += w * k;
-      ps[i][1] += wkd * dx;
-      ps[i][2] += wkd * dy;
-      ps[i][3] += wkd * dz;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      double v = ps[i][c];
-      v += __shfl_xor(v, 1);
-      v += __shfl_xor(v, 2);
-      ps[i][c] = v;
-    }
-  if ((lane & 3) == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = wr + 4 * r16 + i;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) red[((wave & 1) * ST_BM + row) * 4 + c] = ps[i][c];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int idx = tid + 256 * h;
-    const int row = idx >> 2, c = idx & 3;
-    partial[((int64_t)nt * M_pad + m0 + row) * 4 + c] = red[row * 4 + c] + red[(ST_BM + row) * 4 + c];
-  }
-}
-
-#endif  // CDX_STD_MFMA4
 
 
 // std = sqrt|k0 ‚àí Œ£_t V¬≤-partials|; var_out keeps the signed k0 ‚àí ‚ÄñL‚Åª¬πk‚Äñ¬≤ for the ‚àástd scale.
@@ -719,8 +701,8 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
   // (no split-K here: Œ£ V¬≤ needs the K-summed V, and summing chunk partials with atomics made the
   // result depend on arrival order ‚Äî the std pass stays one workgroup per (query tile, stripe))
   prof_mark(PROF_GPIS_STD, true, s);
-  hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g, X,
-                     M, partial, M_pad, Mt, n_tiles, vout, nullptr, nullptr, 0, 0);
+  hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR, STD_T4>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s,
+                     g, X, M, partial, M_pad, Mt, n_tiles, vout, nullptr, nullptr, 0, 0);
   prof_mark(PROF_GPIS_STD, false, s);
   hipLaunchKernelGGL(gpis_var_finalize<KT>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, g, partial, M, M_pad,
                      n_tiles, std_out, var_out);
@@ -735,16 +717,11 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
   if (vin) {
     const int ks = choose_split(MODE_GRADV, g, M);
     n_parts = split_units(MODE_GRADV, n_tiles, g.N, ST_BN / ks);  // split-K units (stripe, K-chunk)
-    hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV>), dim3((unsigned)(Mt * n_parts)), dim3(ST_THREADS), 0, s, g,
-                       X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel, ks, n_parts);
+    hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV, STD_T4>), dim3((unsigned)(Mt * n_parts)), dim3(ST_THREADS), 0,
+                       s, g, X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel, ks, n_parts);
   } else {
-#if defined(CDX_STD_MFMA4)
-    hipLaunchKernelGGL(gpis_std_kernel4<KT>, dim3((unsigned)(Mt * n_tiles)), dim3(256), 0, s, g, X, M, partial, M_pad,
-                       Mt, n_tiles);
-#else
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRAD>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g,
                        X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, 0, 0);
-#endif
   }
   prof_mark(PROF_GPIS_GRAD, false, s);
   hipLaunchKernelGGL(gpis_grad_finalize, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, partial, M, M_pad,

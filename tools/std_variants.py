@@ -16,6 +16,8 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 VARIANTS = {"wn4": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),
+            "t4": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_STD_T4"),
+            "t4_nosched": ("CDX_FAST_SQRT", "CDX_STD_T4"),
             "wn4_nosched": ("CDX_FAST_SQRT",),
             "wn2": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_STD_WN2"),
             "diag_nogen": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOGEN"),
