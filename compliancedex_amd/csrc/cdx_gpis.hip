@@ -141,10 +141,14 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 //   instead of 2N²; launched split-K over 256-row chunks (Nt(Nt+1)/2 partial slots).
 // The triangular modes' tile costs run 1..Nt K-sweeps: stripes are paired heavy+light per XCD.
 enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2 };
+// MFMA shape per pass (profiles/r01x_std_variants.jsonl, r01y_gradv_ab.txt): the whitened std pass
+// runs equally fast on 16x16x4 and 4x4x4_4b (1.30 ms at M = 16 384); the ∇std pass is faster on
+// 4x4x4_4b for contiguous queries (0.37 vs 0.43 ms at M = 4096) but slower on the closure's gathered
+// argmax rows (0.53 vs 0.44 ms): 16x16x4 by default, 4x4x4_4b for both behind -DCDX_STD_T4.
 #if defined(CDX_STD_T4) && !defined(CDX_STD_WN2)
-constexpr bool STD_T4 = true;   // triangular passes on v_mfma_f64_4x4x4_4b_f64
+constexpr bool STD_T4 = true, GRADV_T4 = true;
 #else
-constexpr bool STD_T4 = false;  // triangular passes on v_mfma_f64_16x16x4_f64
+constexpr bool STD_T4 = false, GRADV_T4 = false;
 #endif
 
 
@@ -270,7 +274,13 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     for (int i = 0; i < 4; ++i) av[i] = src[i];
     if (MODE == MODE_GRADV) {
 #pragma unroll
-      for (int i = 0; i < GEN_PER; ++i) kv[i] = vrow[kb + gk + i];
+      for (int i = 0; i < GEN_PER; ++i) {
+#if defined(CDX_DIAG_NOVLOAD)  // timing-only diagnostic build: outputs are wrong
+        kv[i] = qx + i;
+#else
+        kv[i] = vrow[kb + gk + i];
+#endif
+      }
       return;
     }
     const double* x1 = g.X1 + 3 * (kb + gk);
@@ -330,7 +340,13 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
       for (int i = 0; i < 4; ++i) av[i] = src[i];
       if (MODE == MODE_GRADV) {
 #pragma unroll
-        for (int i = 0; i < GEN_PER; ++i) kv[i] = vrow[kn + gk + i];
+        for (int i = 0; i < GEN_PER; ++i) {
+#if defined(CDX_DIAG_NOVLOAD)  // timing-only diagnostic build: outputs are wrong
+          kv[i] = qx + i + kn;
+#else
+          kv[i] = vrow[kn + gk + i];
+#endif
+        }
       }
     }
     const double* x1 = g.X1 + 3 * (kn + gk);
@@ -717,7 +733,7 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
   if (vin) {
     const int ks = choose_split(MODE_GRADV, g, M);
     n_parts = split_units(MODE_GRADV, n_tiles, g.N, ST_BN / ks);  // split-K units (stripe, K-chunk)
-    hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV, STD_T4>), dim3((unsigned)(Mt * n_parts)), dim3(ST_THREADS), 0,
+    hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV, GRADV_T4>), dim3((unsigned)(Mt * n_parts)), dim3(ST_THREADS), 0,
                        s, g, X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel, ks, n_parts);
   } else {
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRAD>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g,

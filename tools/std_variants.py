@@ -21,7 +21,8 @@ VARIANTS = {"wn4": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),
             "wn4_nosched": ("CDX_FAST_SQRT",),
             "wn2": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_STD_WN2"),
             "diag_nogen": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOGEN"),
-            "diag_nomfma": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOMFMA")}
+            "diag_nomfma": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOMFMA"),
+            "diag_novload": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOVLOAD")}
 
 
 def build():
@@ -53,13 +54,23 @@ def child(lib, M, N, ref_path):
     ev[1].record()
     torch.cuda.synchronize()
     ms = ev[0].elapsed_time(ev[1]) / reps
+    # with ∇std: + the GRADV pass (E11⁻¹k = L⁻ᵀv from the kept V) for all M queries
+    for _ in range(2):
+        gpis_std(st, X, want_grad=True)
+    ev[0].record()
+    for _ in range(reps):
+        gpis_std(st, X, want_grad=True)
+    ev[1].record()
+    torch.cuda.synchronize()
+    ms_grad = ev[0].elapsed_time(ev[1]) / reps - ms
     out = std.unsqueeze(1).cpu().numpy()
     if not os.path.exists(ref_path):
         np.save(ref_path, out)
     ref = np.load(ref_path)
     err = float(np.abs(out - ref).max() / np.abs(ref).max())
     tf = M * float(N) * (N + 1) / (ms * 1e-3) / 1e12
-    print(json.dumps({"lib": os.path.basename(lib), "M": M, "N": N, "ms": ms, "TFLOPs": tf, "rel_diff_vs_first": err}))
+    print(json.dumps({"lib": os.path.basename(lib), "M": M, "N": N, "ms": ms, "TFLOPs": tf, "rel_diff_vs_first": err,
+                      "gradv_ms": ms_grad, "gradv_TFLOPs": tf * ms / ms_grad}))
 
 
 def run(M, N):
