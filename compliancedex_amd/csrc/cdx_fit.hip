@@ -9,7 +9,8 @@
 //   1. blocked right-looking Cholesky M = L Lᵀ — per block column k: diag (one workgroup:
 //      unblocked Cholesky of M_kk in LDS + its triangular inverse X_kk = L_kk⁻¹), trsm
 //      (L_ik = M_ik X_kkᵀ), update (M_ij −= L_ik L_jkᵀ for k < j ≤ i);
-//   2. X = L⁻¹ by block rows: X_ik = −X_ii Σ_{j=k}^{i−1} L_ij X_jk (block row i depends on rows < i);
+//   2. X = L⁻¹ by block rows, right-looking: X_ik = −X_ii Σ_{j=k}^{i−1} L_ij X_jk with the sums
+//      accumulated as rows finish (2 launches per block row, (nb−j−1)(j+1) tile GEMMs in the first);
 //   3. E11⁻¹ = Xᵀ X (lower block pairs, mirrored, padding zeroed), Linv_t = Xᵀ (padding
 //      zeroed) and α = Xᵀ (X y1).
 // ≈ N³ flops (N = 2000: 8 GFLOP) in ≈ 4·nb launches; a fit happens once per object.  A non-
@@ -26,19 +27,24 @@ constexpr int NB = 64;        // block size
 constexpr int LDT = NB + 1;   // LDS row pitch (odd: column walks hit distinct banks)
 
 // ------------------------------------------------------------------ fit
+// R = max_ij ‖x_i − x_j‖: one workgroup per row i, block max, one atomic per row.
 __global__ __launch_bounds__(256) void fit_R_kernel(const double* __restrict__ X1, int N,
                                                     unsigned long long* __restrict__ Rbits) {
-  const int i = blockIdx.y;
+  __shared__ double wmax[4];
+  const int i = blockIdx.x;
   double m = 0.0;
   const double xi = X1[3 * i], yi = X1[3 * i + 1], zi = X1[3 * i + 2];
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x) {
+  for (int j = threadIdx.x; j < N; j += blockDim.x) {
     const double dx = xi - X1[3 * j], dy = yi - X1[3 * j + 1], dz = zi - X1[3 * j + 2];
     m = fmax(m, sqrt(dx * dx + dy * dy + dz * dz));
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
   // non-negative doubles order like their bit patterns
-  if ((threadIdx.x & 63) == 0) atomicMax(Rbits, (unsigned long long)__double_as_longlong(m));
+  if (threadIdx.x == 0)
+    atomicMax(Rbits, (unsigned long long)__double_as_longlong(fmax(fmax(wmax[0], wmax[1]), fmax(wmax[2], wmax[3]))));
 }
 
 template <int KT>
@@ -97,46 +103,75 @@ __global__ __launch_bounds__(256) void pad_kernel(const double* __restrict__ E11
   }
 }
 
-// Cholesky of the diagonal block k in LDS; writes L_kk (lower, upper zeroed) and X_kk = L_kk⁻¹.
+// Cholesky of the diagonal block k; writes L_kk (lower, upper zeroed) and X_kk = L_kk⁻¹.
+// Right-looking with the 64×64 block in registers: thread (c = tid & 63, r0 = tid >> 6) owns rows
+// r0 + 4·it (it < 16) of column c.  Step j broadcasts column j through LDS (double-buffered: one
+// barrier per step) and every thread updates its 16 entries — the same operations, in the same
+// order, as the textbook in-place loop, without its per-element LDS round trips.  The inverse runs
+// the same way: V = I, then for j: row j /= L_jj, rows r > j −= L_rj · row j.
 __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ M, double* __restrict__ X, int Np, int k,
                                                         int* __restrict__ info) {
-  __shared__ double T[NB * LDT];
-  __shared__ double V[NB * LDT];
+  __shared__ double col[2][NB];
+  __shared__ double Lc[NB * LDT];
+  const int c = threadIdx.x & (NB - 1), r0 = threadIdx.x >> 6;
   double* Mk = M + (int64_t)k * NB * Np + k * NB;
-  load_tile(T, Mk, Np, false);
-  __syncthreads();
+  double t[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) t[it] = Mk[(int64_t)(r0 + 4 * it) * Np + c];
   for (int j = 0; j < NB; ++j) {
-    const double d = T[j * LDT + j];
+    double* cj = col[j & 1];
+    if (c == j)
+#pragma unroll
+      for (int it = 0; it < 16; ++it) cj[r0 + 4 * it] = t[it];
+    __syncthreads();
+    const double d = cj[j];
     if (threadIdx.x == 0 && !(d > 0.0)) atomicCAS(info, 0, k * NB + j + 1);
-    const double s = sqrt(d);
-    __syncthreads();
-    for (int r = j + 1 + threadIdx.x; r < NB; r += blockDim.x) T[r * LDT + j] /= s;
-    __syncthreads();
-    if (threadIdx.x == 0) T[j * LDT + j] = s;
-    // trailing update of the lower triangle: T[r][c] −= T[r][j]·T[c][j], j < c ≤ r
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-      const int r = e / NB, c = e % NB;
-      if (c > j && c <= r) T[r * LDT + c] -= T[r * LDT + j] * T[c * LDT + j];
+    const double sq = sqrt(d), isq = 1.0 / sq;  // one division per step (f64 division is a long sequence)
+    const double lc = c > j ? cj[c] * isq : (c == j ? sq : 0.0);  // L[c][j]
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int r = r0 + 4 * it;
+      if (r < j) continue;
+      const double lr = r > j ? cj[r] * isq : sq;  // L[r][j]
+      if (c == j) t[it] = lr;
+      else if (c > j && c <= r) t[it] -= lr * lc;
     }
-    __syncthreads();
   }
-  // triangular inverse: column c of V solves L v = e_c (forward substitution)
-  if (threadIdx.x < NB) {
-    const int c = threadIdx.x;
-    for (int r = 0; r < NB; ++r) {
-      if (r < c) { V[r * LDT + c] = 0.0; continue; }
-      double acc = r == c ? 1.0 : 0.0;
-      for (int t = c; t < r; ++t) acc -= T[r * LDT + t] * V[t * LDT + c];
-      V[r * LDT + c] = acc / T[r * LDT + r];
-    }
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int r = r0 + 4 * it;
+    const double l = c <= r ? t[it] : 0.0;
+    Lc[r * LDT + c] = l;
+    Mk[(int64_t)r * Np + c] = l;
   }
   __syncthreads();
-  double* Xk = X + (int64_t)k * NB * Np + k * NB;
-  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-    const int r = e / NB, c = e % NB;
-    Mk[(int64_t)r * Np + c] = c <= r ? T[r * LDT + c] : 0.0;
-    Xk[(int64_t)r * Np + c] = V[r * LDT + c];
+  // V = L_kk⁻¹ (rows r0 + 4·it of column c in registers); reciprocal diagonal staged once
+  __shared__ double idiag[NB];
+  if (threadIdx.x < NB) idiag[threadIdx.x] = 1.0 / Lc[threadIdx.x * LDT + threadIdx.x];
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 16; ++it) t[it] = (r0 + 4 * it == c) ? 1.0 : 0.0;
+  for (int j = 0; j < NB; ++j) {
+    double* rj = col[j & 1];
+    if ((j & 3) == r0) {
+#pragma unroll
+      for (int it = 0; it < 16; ++it)  // (a constant index keeps t[] in registers)
+        if (it == (j >> 2)) {
+          t[it] *= idiag[j];
+          rj[c] = t[it];
+        }
+    }
+    __syncthreads();
+    const double vj = rj[c];
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int r = r0 + 4 * it;
+      if (r > j) t[it] -= Lc[r * LDT + j] * vj;
+    }
   }
+  double* Xk = X + (int64_t)k * NB * Np + k * NB;
+#pragma unroll
+  for (int it = 0; it < 16; ++it) Xk[(int64_t)(r0 + 4 * it) * Np + c] = t[it];
 }
 
 // L_ik = M_ik · X_kkᵀ for block rows i > k (one workgroup each).
@@ -180,37 +215,45 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ M
     for (int b = 0; b < 4; ++b) Mij[(int64_t)(r0 + a) * Np + c0 + b] -= acc[a][b];
 }
 
-// Block row i of X = L⁻¹: X_ik = −X_ii Σ_{j=k}^{i−1} L_ij X_jk, one workgroup per k < i.
-__global__ __launch_bounds__(256) void tri_inv_row_kernel(const double* __restrict__ M, double* __restrict__ X, int Np,
-                                                          int i) {
+// X = L⁻¹ right-looking: S_ik = Σ_{j=k}^{i−1} L_ij X_jk is accumulated in X_ik's storage (zeroed by
+// pad_kernel) as block rows j are finished: step j adds L_ij X_jk for every i > j, k ≤ j (one
+// workgroup per pair), then block row j+1 is finished: X_{j+1,k} = −X_{j+1,j+1} S_{j+1,k}.
+__global__ __launch_bounds__(256) void inv_update_kernel(const double* __restrict__ M, double* __restrict__ X, int Np,
+                                                         int j) {
   __shared__ double P[NB * LDT];
   __shared__ double Q[NB * LDT];
-  const int k = blockIdx.x;
+  const int k = blockIdx.x % (j + 1), i = j + 1 + blockIdx.x / (j + 1);
+  load_tile(P, M + (int64_t)i * NB * Np + j * NB, Np, false);  // L_ij
+  load_tile(Q, X + (int64_t)j * NB * Np + k * NB, Np, false);  // X_jk
+  __syncthreads();
   double acc[4][4] = {};
   int r0, c0;
   owned(r0, c0);
-  for (int j = k; j < i; ++j) {
-    __syncthreads();
-    load_tile(P, M + (int64_t)i * NB * Np + j * NB, Np, false);
-    load_tile(Q, X + (int64_t)j * NB * Np + k * NB, Np, false);
-    __syncthreads();
-    tile_mac(acc, P, Q, r0, c0);
-  }
-  __syncthreads();
-  // P ← X_ii, Q ← the sum S; X_ik = −X_ii S
-  load_tile(P, X + (int64_t)i * NB * Np + i * NB, Np, false);
+  tile_mac(acc, P, Q, r0, c0);
+  double* S = X + (int64_t)i * NB * Np + k * NB;
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) Q[(r0 + a) * LDT + c0 + b] = acc[a][b];
+    for (int b = 0; b < 4; ++b) S[(int64_t)(r0 + a) * Np + c0 + b] += acc[a][b];
+}
+
+__global__ __launch_bounds__(256) void inv_finish_row_kernel(double* __restrict__ X, int Np, int i) {
+  __shared__ double P[NB * LDT];
+  __shared__ double Q[NB * LDT];
+  const int k = blockIdx.x;
+  load_tile(P, X + (int64_t)i * NB * Np + i * NB, Np, false);  // X_ii
+  double* S = X + (int64_t)i * NB * Np + k * NB;
+  load_tile(Q, S, Np, false);
   __syncthreads();
-  double out[4][4] = {};
-  tile_mac(out, P, Q, r0, c0);
-  double* Xik = X + (int64_t)i * NB * Np + k * NB;
+  double acc[4][4] = {};
+  int r0, c0;
+  owned(r0, c0);
+  tile_mac(acc, P, Q, r0, c0);
+  __syncthreads();
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) Xik[(int64_t)(r0 + a) * Np + c0 + b] = -out[a][b];
+    for (int b = 0; b < 4; ++b) S[(int64_t)(r0 + a) * Np + c0 + b] = -acc[a][b];
 }
 
 // A = Xᵀ X: A_ij = Σ_{k ≥ i} X_kiᵀ X_kj for j ≤ i (X lower block-triangular), mirrored to A_ji;
@@ -290,8 +333,7 @@ int cdx_gpis_fit(const double* X1, int32_t N, const double* noise, int32_t kerne
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(R, 0, sizeof(double), s) != hipSuccess) return CDX_ELAUNCH;
   if (kernel != CDX_KERNEL_RBF)
-    hipLaunchKernelGGL(fit_R_kernel, dim3((N + 255) / 256, N), dim3(256), 0, s, X1, N,
-                       reinterpret_cast<unsigned long long*>(R));
+    hipLaunchKernelGGL(fit_R_kernel, dim3(N), dim3(256), 0, s, X1, N, reinterpret_cast<unsigned long long*>(R));
   const dim3 grid((N + 255) / 256, N);
   if (kernel == CDX_KERNEL_TPS)
     hipLaunchKernelGGL(fit_E11_kernel<CDX_KERNEL_TPS>, grid, dim3(256), 0, s, X1, N, noise, sigma, R, E11);
@@ -326,8 +368,11 @@ int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pa
     hipLaunchKernelGGL(chol_trsm_kernel, dim3(m), dim3(256), 0, s, M, (const double*)X, N_pad, k);
     hipLaunchKernelGGL(chol_update_kernel, dim3(m * (m + 1) / 2), dim3(256), 0, s, M, N_pad, k);
   }
-  for (int i = 1; i < nb; ++i)
-    hipLaunchKernelGGL(tri_inv_row_kernel, dim3(i), dim3(256), 0, s, (const double*)M, X, N_pad, i);
+  for (int j = 0; j + 1 < nb; ++j) {
+    hipLaunchKernelGGL(inv_update_kernel, dim3((nb - j - 1) * (j + 1)), dim3(256), 0, s, (const double*)M, X, N_pad,
+                       j);
+    hipLaunchKernelGGL(inv_finish_row_kernel, dim3(j + 1), dim3(256), 0, s, X, N_pad, j + 1);
+  }
   hipLaunchKernelGGL(xtx_kernel, dim3(nb * (nb + 1) / 2), dim3(256), 0, s, (const double*)X, N_pad, N, Ainv);
   hipLaunchKernelGGL(transpose_kernel, dim3(nb, nb), dim3(256), 0, s, (const double*)X, N_pad, N, Linv_t);
   hipLaunchKernelGGL(pad_copy_kernel, dim3((N_pad + 255) / 256, N_pad), dim3(256), 0, s, (const double*)X, N, N_pad, Linv);
