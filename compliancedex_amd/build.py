@@ -56,7 +56,10 @@ def build_device(force=False, defines=DEFAULT_DEFINES, out_name="libcdx.so"):
         flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-pass-failed", "-I",
                  os.path.join(REPO, "include")]
         flags += [f"-D{d}" for d in defines]
-        if src == "cdx_sdf.hip":
+        # no FMA contraction in the per-candidate code (FK, Kabsch, costs) and TorchSDF: the
+        # device then rounds like the reference's CPU float ops and like libcdx_host.so (the
+        # collision cost's 1/d near the floor amplifies a contracted f32 FK to 1e-4)
+        if src in ("cdx_sdf.hip", "cdx_closure.hip"):
             flags.append("-ffp-contract=off")
         _run([HIPCC, *flags, "-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)

@@ -22,29 +22,30 @@
 namespace {
 
 // --------------------------------------------------------------- standalone FK
+// One thread per (row, tip): the tip's path is walked with a running pose (no per-thread arrays).
 __global__ __launch_bounds__(64) void fk_forward_kernel(cdx_chain c, const float* __restrict__ q, int64_t B,
                                                         float* __restrict__ pos, float* __restrict__ quat) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  float qb[CDX_MAX_DOFS];
-  for (int i = 0; i < c.n_dofs; ++i) qb[i] = q[b * c.n_dofs + i];
-  for (int k = 0; k < c.n_tips; ++k) {
-    float p[3], qt[4];
-    cdx::fk_tip(c, k, qb, p, qt);
-    for (int i = 0; i < 3; ++i) pos[(b * c.n_tips + k) * 3 + i] = p[i];
-    if (quat)
-      for (int i = 0; i < 4; ++i) quat[(b * c.n_tips + k) * 4 + i] = qt[i];
-  }
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * c.n_tips) return;
+  const int64_t b = t / c.n_tips;
+  const int k = (int)(t - b * c.n_tips);
+  float p[3], qt[4];
+  cdx::fk_tip(c, k, q + b * c.n_dofs, p, qt);
+  for (int i = 0; i < 3; ++i) pos[t * 3 + i] = p[i];
+  if (quat)
+    for (int i = 0; i < 4; ++i) quat[t * 4 + i] = qt[i];
 }
 
+// One thread per row: the tips' contributions accumulate into the row of grad_q in tip order.
+template <int MAXD>
 __global__ __launch_bounds__(64) void fk_backward_kernel(cdx_chain c, const float* __restrict__ q, int64_t B,
                                                          const float* __restrict__ gpos, float* __restrict__ gq) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  float qb[CDX_MAX_DOFS], g[CDX_MAX_DOFS];
-  for (int i = 0; i < c.n_dofs; ++i) { qb[i] = q[b * c.n_dofs + i]; g[i] = 0.f; }
-  for (int k = 0; k < c.n_tips; ++k) cdx::fk_tip_bwd(c, k, qb, gpos + (b * c.n_tips + k) * 3, g);
-  for (int i = 0; i < c.n_dofs; ++i) gq[b * c.n_dofs + i] = g[i];
+  float* g = gq + b * c.n_dofs;
+  for (int i = 0; i < c.n_dofs; ++i) g[i] = 0.f;
+  for (int k = 0; k < c.n_tips; ++k)
+    cdx::fk_tip_bwd<MAXD>(c, k, q + b * c.n_dofs, gpos + (b * c.n_tips + k) * 3, cdx::GqAdd{g});
 }
 
 // --------------------------------------------------------------- collision loss
@@ -70,40 +71,47 @@ __global__ __launch_bounds__(64) void collision_kernel(cdx_collision C, int64_t 
 }
 
 // --------------------------------------------------------------- closure stages
+// One thread per (candidate, fingertip): the tip's f32 FK, palm transform (pregrasp_tips, same
+// arithmetic), and that fingertip's query points.
 __global__ __launch_bounds__(64) void closure_queries_kernel(cdx_problem P, int64_t E, const double* __restrict__ q,
                                                              const double* __restrict__ target,
                                                              const double* __restrict__ palm_pos,
                                                              const double* __restrict__ palm_ori,
                                                              double* __restrict__ X, double* __restrict__ pre_out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  if (P.loop && e == 0) {  // advance the device loop counters (read by the later kernels)
+  const int T = P.chain.n_tips, D = P.chain.n_dofs, Lq = P.n_query_levels;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= E * T) return;
+  const int64_t e = t / T;
+  const int f = (int)(t - e * T);
+  if (P.loop && t == 0) {  // advance the device loop counters (read by the later kernels)
     P.loop->seed += 1;
     P.loop->step += 1;
   }
-  const int T = P.chain.n_tips, D = P.chain.n_dofs, Lq = P.n_query_levels;
-  double tip[CDX_MAX_TIPS][3], Rp[9];
-  float tl[CDX_MAX_TIPS][3];
-  cdx::pregrasp_tips(P, q + e * D, palm_pos + 3 * e, palm_ori + 3 * e, tip, tl, Rp);
-  const double* tg = target + e * T * 3;
+  double Rp[9];
+  cdx::euler_xyz(palm_ori + 3 * e, Rp, nullptr, nullptr, nullptr);
+  float tl[3];
+  cdx::fk_tip(P.chain, f, cdx::QRowD{q + e * D}, tl, nullptr);
+  double tip[3];
+  {
+    const double v[3] = {(double)tl[0], (double)tl[1], (double)tl[2]};
+    cdx::mat3_vec(Rp, v, tip);
+    for (int i = 0; i < 3; ++i) tip[i] = tip[i] + palm_pos[3 * e + i];
+  }
+  const double* tg = target + (e * T + f) * 3;
   for (int u = 0; u < Lq; ++u) {
     int k = 0;
     while (k < P.n_levels - 1 && P.level_query[k] != u) ++k;
-    for (int f = 0; f < T; ++f) {
-      const double c = (double)P.coeff[k][f];
-      const int64_t qi = cdx::q_alltip(u, e, f, E, T);
-      for (int i = 0; i < 3; ++i) X[3 * qi + i] = tg[3 * f + i] + c * (tip[f][i] - tg[3 * f + i]);
-    }
+    const double c = (double)P.coeff[k][f];
+    const int64_t qi = cdx::q_alltip(u, e, f, E, T);
+    for (int i = 0; i < 3; ++i) X[3 * qi + i] = tg[i] + c * (tip[i] - tg[i]);
   }
-  for (int f = 0; f < T; ++f) {
-    const int64_t qt = cdx::q_target(Lq, e, f, E, T), qp = cdx::q_pre(Lq, e, f, E, T);
-    for (int i = 0; i < 3; ++i) {
-      X[3 * qt + i] = tg[3 * f + i];
-      X[3 * qp + i] = tip[f][i];
-      if (pre_out) pre_out[(e * T + f) * 3 + i] = tip[f][i];
-    }
+  const int64_t qt = cdx::q_target(Lq, e, f, E, T), qp = cdx::q_pre(Lq, e, f, E, T);
+  for (int i = 0; i < 3; ++i) {
+    X[3 * qt + i] = tg[i];
+    X[3 * qp + i] = tip[i];
+    if (pre_out) pre_out[(e * T + f) * 3 + i] = tip[i];
   }
-  if (P.optimize_palm) {
+  if (P.optimize_palm && f == 0) {
     const int64_t qm = cdx::q_palm(Lq, e, E, T);
     for (int i = 0; i < 3; ++i) X[3 * qm + i] = palm_pos[3 * e + i];
   }
@@ -277,22 +285,21 @@ __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_
 
 // Per-candidate group of GS lanes, lane f = fingertip f: sums the levels, adds the pregrasp
 // and palm GPIS terms (:757-763), the palm/euler backward and the fingertip's FK VJP, then
-// reduces the shared gradients (palm, q) across the group with xor-shuffles.
-template <int GS>
-__global__ __launch_bounds__(256) void closure_combine_kernel(cdx_problem P, int64_t E, const double* __restrict__ q,
-                                                              const double* __restrict__ palm_pos,
-                                                              const double* __restrict__ palm_ori, GpisView gv,
-                                                              const double* __restrict__ lvl,
-                                                              double* __restrict__ total_loss,
-                                                              double* __restrict__ total_margin,
-                                                              double* __restrict__ g_q, double* __restrict__ g_comp,
-                                                              double* __restrict__ g_target,
-                                                              double* __restrict__ g_palm_pos,
-                                                              double* __restrict__ g_palm_ori) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// reduces the shared gradients: palm terms with xor-shuffles, the per-DOF FK contributions
+// through LDS ([dof][thread], summed in the same pairwise order over the group's lanes).
+constexpr int COMBINE_BLOCK = 256;
+template <int GS, int MAXD>
+__global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
+    cdx_problem P, int64_t E, const double* __restrict__ q, const double* __restrict__ palm_pos,
+    const double* __restrict__ palm_ori, GpisView gv, const double* __restrict__ lvl, double* __restrict__ total_loss,
+    double* __restrict__ total_margin, double* __restrict__ g_q, double* __restrict__ g_comp,
+    double* __restrict__ g_target, double* __restrict__ g_palm_pos, double* __restrict__ g_palm_ori) {
+  __shared__ float gcon[CDX_MAX_DOFS][COMBINE_BLOCK];
+  const int tid = threadIdx.x;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + tid;
   const int64_t e = gid / GS;
   const int f = (int)(gid % GS);
-  const int T = P.chain.n_tips, D = P.chain.n_dofs, K = P.n_levels, Lq = P.n_query_levels;
+  const int T = P.chain.n_tips, D = P.chain.n_dofs, K = P.n_levels;
   const bool valid = e < E;
   const bool live = valid && f < T;
   const int LW = level_record_width(T);
@@ -312,35 +319,53 @@ __global__ __launch_bounds__(256) void closure_combine_kernel(cdx_problem P, int
     for (int i = 0; i < 3; ++i) gt[i] += -5.0 * gpp.gmean[i];
   }
   // palm transform backward: tip = Rp·tl + palm_pos
-  float qf[CDX_MAX_DOFS];
-  for (int i = 0; i < D; ++i) qf[i] = (float)q[ec * D + i];
-  float tl[3] = {0.f, 0.f, 0.f};
-  if (live) cdx::fk_tip(P.chain, f, qf, tl, nullptr);
   double Rp[9], dRa[9], dRb[9], dRc[9];
   cdx::euler_xyz(palm_ori + 3 * ec, Rp, dRa, dRb, dRc);
+  double gl[3];
+  cdx::mat3t_vec(Rp, gt, gl);
+  const float gtl[3] = {(float)gl[0], (float)gl[1], (float)gl[2]};
+  for (int i = 0; i < D; ++i) gcon[i][tid] = 0.f;
+  float tl[3] = {0.f, 0.f, 0.f};
+  if (live)
+    cdx::fk_tip_bwd<MAXD>(P.chain, f, cdx::QRowD{q + ec * D}, gtl,
+                          [&](int d, float v) { gcon[d][tid] += v; }, tl);
   double red[12];  // g_palm_pos (3) + g_Rp (9)
   for (int i = 0; i < 3; ++i) red[i] = gt[i];
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < 3; ++c) red[3 + 3 * r + c] = gt[r] * (double)tl[c];
-  double gl[3];
-  cdx::mat3t_vec(Rp, gt, gl);
-  float gtl[3] = {(float)gl[0], (float)gl[1], (float)gl[2]};
-  float gqf[CDX_MAX_DOFS];
-  for (int i = 0; i < D; ++i) gqf[i] = 0.f;
-  if (live) cdx::fk_tip_bwd(P.chain, f, qf, gtl, gqf);
-  double gqd[CDX_MAX_DOFS];
-  for (int i = 0; i < D; ++i) gqd[i] = (double)gqf[i];
 #pragma unroll
-  for (int m = 1; m < GS; m <<= 1) {
+  for (int m = 1; m < GS; m <<= 1)
     for (int i = 0; i < 12; ++i) red[i] += __shfl_xor(red[i], m);
-    for (int i = 0; i < D; ++i) gqd[i] += __shfl_xor(gqd[i], m);
+  __syncthreads();
+  if (!valid) return;
+  // g_q = ref-distance term + Σ_lanes FK contributions; lane f takes DOFs f, f + GS, ...
+  double qn2 = 0.0;
+  for (int i = 0; i < D; ++i) {
+    const double dq = q[e * D + i] - (double)P.ref_q[i];
+    qn2 += dq * dq;
+  }
+  const double qnorm = sqrt(qn2);
+  const int base = tid - f;
+  for (int i = f; i < D; i += GS) {
+    double s[GS];
+#pragma unroll
+    for (int j = 0; j < GS; ++j) s[j] = (double)gcon[i][base + j];
+#pragma unroll
+    for (int w = 1; w < GS; w <<= 1)
+#pragma unroll
+      for (int j = 0; j < GS; j += 2 * w) s[j] += s[j + w];
+    const double dq = q[e * D + i] - (double)P.ref_q[i];
+    double v = 0.0;
+    if (qnorm > 0)
+      for (int k = 0; k < K; ++k) v += P.weight[k] * 10.0 * dq / qnorm;
+    g_q[e * D + i] = v + s[0];
   }
   if (live) {
     total_margin[e * T + f] = marg;
     g_comp[e * T + f] = gcomp;
     for (int i = 0; i < 3; ++i) g_target[(e * T + f) * 3 + i] = gtar[i];
   }
-  if (!valid || f != 0) return;
+  if (f != 0) return;
   double total = 0.0;
   for (int k = 0; k < K; ++k) total += P.weight[k] * lvl[((int64_t)k * E + e) * LW];
   double pre_sum = 0.0;
@@ -361,20 +386,22 @@ __global__ __launch_bounds__(256) void closure_combine_kernel(cdx_problem P, int
     go[2] += red[3 + i] * dRc[i];
   }
   for (int i = 0; i < 3; ++i) { g_palm_pos[3 * e + i] = gpp[i]; g_palm_ori[3 * e + i] = go[i]; }
-  double dq[CDX_MAX_DOFS];
-  const double qnorm = cdx::ref_dist(P, q + e * D, dq);
-  for (int i = 0; i < D; ++i) {
-    double v = 0.0;
-    if (qnorm > 0)
-      for (int k = 0; k < K; ++k) v += P.weight[k] * 10.0 * dq[i] / qnorm;
-    g_q[e * D + i] = v + gqd[i];
-  }
 }
 
 bool chain_ok(const cdx_chain* c) {
-  return c && c->n_bodies > 0 && c->n_bodies <= CDX_MAX_BODIES && c->n_dofs >= 0 && c->n_dofs <= CDX_MAX_DOFS &&
-         c->n_tips > 0 && c->n_tips <= CDX_MAX_TIPS;
+  if (!(c && c->n_bodies > 0 && c->n_bodies <= CDX_MAX_BODIES && c->n_dofs >= 0 && c->n_dofs <= CDX_MAX_DOFS &&
+        c->n_tips > 0 && c->n_tips <= CDX_MAX_TIPS))
+    return false;
+  // parents precede children (the FK walks a tip's path in ascending body order), DOFs in range
+  for (int i = 1; i < c->n_bodies; ++i)
+    if (c->bodies[i].parent < 0 || c->bodies[i].parent >= i || c->bodies[i].dof >= c->n_dofs) return false;
+  for (int k = 0; k < c->n_tips; ++k)
+    if (c->tip_body[k] < 0 || c->tip_body[k] >= c->n_bodies) return false;
+  return true;
 }
+
+// fk_tip_bwd register bound for a chain: 8 levels (the hands) or CDX_MAX_DEPTH (arm + hand).
+bool shallow_chain(const cdx_chain& c) { return cdx::chain_max_depth(c) <= 8; }
 
 size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
@@ -452,7 +479,7 @@ int cdx_fk_forward(const cdx_chain* chain, const float* q, int64_t B, float* pos
   if (!chain_ok(chain)) return CDX_ECHAIN;
   if (B < 0 || (B > 0 && (!q || !pos))) return CDX_EINVAL;
   if (B == 0) return CDX_OK;
-  hipLaunchKernelGGL(fk_forward_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0,
+  hipLaunchKernelGGL(fk_forward_kernel, dim3((unsigned)((B * chain->n_tips + 63) / 64)), dim3(64), 0,
                      reinterpret_cast<hipStream_t>(stream), *chain, q, B, pos, quat);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
@@ -462,8 +489,12 @@ int cdx_fk_backward(const cdx_chain* chain, const float* q, int64_t B, const flo
   if (!chain_ok(chain)) return CDX_ECHAIN;
   if (B < 0 || (B > 0 && (!q || !grad_pos || !grad_q))) return CDX_EINVAL;
   if (B == 0) return CDX_OK;
-  hipLaunchKernelGGL(fk_backward_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0,
-                     reinterpret_cast<hipStream_t>(stream), *chain, q, B, grad_pos, grad_q);
+  if (shallow_chain(*chain))
+    hipLaunchKernelGGL(fk_backward_kernel<8>, dim3((unsigned)((B + 63) / 64)), dim3(64), 0,
+                       reinterpret_cast<hipStream_t>(stream), *chain, q, B, grad_pos, grad_q);
+  else
+    hipLaunchKernelGGL(fk_backward_kernel<CDX_MAX_DEPTH>, dim3((unsigned)((B + 63) / 64)), dim3(64), 0,
+                       reinterpret_cast<hipStream_t>(stream), *chain, q, B, grad_pos, grad_q);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
@@ -540,7 +571,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   ClosureWs w = closure_ws_layout(p, E, static_cast<char*>(workspace));
   const int64_t Mq = cdx::n_queries(*p, E);
   const int64_t Ms = (int64_t)p->n_query_levels * E * p->chain.n_tips;
-  const dim3 grid((unsigned)((E + 63) / 64));
+  const dim3 grid((unsigned)((E * p->chain.n_tips + 63) / 64));
   cdx::prof_mark(cdx::PROF_QUERIES, true, s);
   hipLaunchKernelGGL(closure_queries_kernel, grid, dim3(64), 0, s, *p, E, q, target, palm_pos, palm_ori, w.X,
                      pregrasp_tip);
@@ -573,14 +604,25 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
       hipLaunchKernelGGL((closure_level_kernel<0, -1>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
                          kabsch_noise, seed, gv, w.lvl, flip);
     if (hipGetLastError() != hipSuccess) return CDX_ELAUNCH;
-    if (p->chain.n_tips <= 4)
-      hipLaunchKernelGGL(closure_combine_kernel<4>, dim3((unsigned)((E * 4 + 255) / 256)), dim3(256), 0, s, *p, E, q,
-                         palm_pos, palm_ori, gv, w.lvl, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos,
-                         g_palm_ori);
-    else
-      hipLaunchKernelGGL(closure_combine_kernel<8>, dim3((unsigned)((E * 8 + 255) / 256)), dim3(256), 0, s, *p, E, q,
-                         palm_pos, palm_ori, gv, w.lvl, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos,
-                         g_palm_ori);
+    const bool sh = shallow_chain(p->chain);
+    const dim3 cb(COMBINE_BLOCK);
+    if (p->chain.n_tips <= 4) {
+      const dim3 cg((unsigned)((E * 4 + COMBINE_BLOCK - 1) / COMBINE_BLOCK));
+      if (sh)
+        hipLaunchKernelGGL((closure_combine_kernel<4, 8>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv, w.lvl,
+                           total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
+      else
+        hipLaunchKernelGGL((closure_combine_kernel<4, CDX_MAX_DEPTH>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv,
+                           w.lvl, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
+    } else {
+      const dim3 cg((unsigned)((E * 8 + COMBINE_BLOCK - 1) / COMBINE_BLOCK));
+      if (sh)
+        hipLaunchKernelGGL((closure_combine_kernel<8, 8>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv, w.lvl,
+                           total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
+      else
+        hipLaunchKernelGGL((closure_combine_kernel<8, CDX_MAX_DEPTH>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv,
+                           w.lvl, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
+    }
   }
   cdx::prof_mark(cdx::PROF_COST, false, s);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;

@@ -62,7 +62,7 @@ CDX_HD void collision_candidate(const cdx_collision& C, const double* q, const d
     double gl[3];
     mat3t_vec(Rp, ga[k], gl);
     const float gtl[3] = {(float)gl[0], (float)gl[1], (float)gl[2]};
-    fk_tip_bwd(C.chain, k, qf, gtl, gqf);
+    fk_tip_bwd(C.chain, k, qf, gtl, GqAdd{gqf});
   }
   g_po[0] = g_po[1] = g_po[2] = 0.0;
   for (int i = 0; i < 9; ++i) {

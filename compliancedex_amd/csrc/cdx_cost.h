@@ -610,7 +610,7 @@ CDX_HD void closure_candidate(const cdx_problem& P, const CandidateIn& in, GpisA
   // FK backward in float32, then cast (q.float() backward)
   float qf[CDX_MAX_DOFS], gqf[CDX_MAX_DOFS];
   for (int i = 0; i < P.chain.n_dofs; ++i) { qf[i] = (float)in.q[i]; gqf[i] = 0.f; }
-  for (int f = 0; f < T; ++f) fk_tip_bwd(P.chain, f, qf, &gtl[3 * f], gqf);
+  for (int f = 0; f < T; ++f) fk_tip_bwd(P.chain, f, qf, &gtl[3 * f], GqAdd{gqf});
   for (int i = 0; i < P.chain.n_dofs; ++i) out.g_q[i] += (double)gqf[i];
 }
 

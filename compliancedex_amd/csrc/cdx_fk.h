@@ -35,16 +35,31 @@ CDX_HD void axis_rot(int axis, float th, float* A, float* dA) {
 // Longest root→tip path a chain may have (iiwa7_allegro: 13).
 #define CDX_MAX_DEPTH 16
 
-// Path from the root's child down to `body` (root = body 0 is the identity pose).
-CDX_HD int chain_path(const cdx_chain& c, int body, int* path) {
-  int rev[CDX_MAX_DEPTH];
-  int n = 0;
-  while (body > 0 && n < CDX_MAX_DEPTH) { rev[n++] = body; body = c.bodies[body].parent; }
-  for (int i = 0; i < n; ++i) path[i] = rev[n - 1 - i];
-  return n;
+// Bodies on the path from the root's child down to `body` as a bit mask (root = body 0 is the
+// identity pose).  Parents precede children (urdf.py enforces it, chain_ok re-checks it), so
+// ascending bit order is root→tip order: the path is walked without a per-thread array, which
+// on the GPU would live in scratch memory.
+CDX_HD uint32_t chain_path_mask(const cdx_chain& c, int body) {
+  uint32_t m = 0;
+  for (int n = 0; body > 0 && n < CDX_MAX_DEPTH; ++n) {
+    m |= 1u << body;
+    body = c.bodies[body].parent;
+  }
+  return m;
 }
+CDX_HD int low_bit(uint32_t m) { return __builtin_ctz(m); }
+CDX_HD int high_bit(uint32_t m) { return 31 - __builtin_clz(m); }
+CDX_HD int path_depth(uint32_t m) { return __builtin_popcount(m); }
 
-CDX_HD void joint_rot(const cdx_body& b, const float* q, float* Rj) {
+// Joint-angle readers: q[i] as float32 from a float row, or a double row cast like the
+// reference's q.float() (no per-thread copy of the row).
+struct QRowD {
+  const double* p;
+  CDX_HDM float operator[](int i) const { return (float)p[i]; }
+};
+
+template <class Q>
+CDX_HD void joint_rot(const cdx_body& b, const Q& q, float* Rj) {
   if (b.dof < 0) {
     for (int i = 0; i < 9; ++i) Rj[i] = b.F[i];
     return;
@@ -130,33 +145,24 @@ CDX_HD void quat_rotate_bwd(const float* q, const float* v, const float* G, floa
   gq[2] += 2.0f * w * vxG2 + 2.0f * (d * G[2] + Gq * v[2]);
 }
 
-// World pose of every body on `path` (root→tip).  Rs/ts hold n+1 entries, entry 0 = root.
-CDX_HD void chain_forward(const cdx_chain& c, const int* path, int n, const float* q, float (*Rs)[9],
-                          float (*ts)[3]) {
-  for (int i = 0; i < 9; ++i) Rs[0][i] = (i % 4 == 0) ? 1.f : 0.f;
-  ts[0][0] = ts[0][1] = ts[0][2] = 0.f;
-  for (int l = 0; l < n; ++l) {
-    const cdx_body& b = c.bodies[path[l]];
-    float Rj[9], tt[3];
-    joint_rot(b, q, Rj);
-    mat3_vec(Rs[l], b.t, tt);
-    ts[l + 1][0] = tt[0] + ts[l][0];
-    ts[l + 1][1] = tt[1] + ts[l][1];
-    ts[l + 1][2] = tt[2] + ts[l][2];
-    mat3_mul(Rs[l], Rj, Rs[l + 1]);
-  }
+// One step of the world-pose recurrence: t' = R·t_b + t, R' = R·Rj  (robot_model.py:174-194).
+template <class Q>
+CDX_HD void chain_step(const cdx_body& b, const Q& q, const float* R, const float* t, float* Rn, float* tn) {
+  float Rj[9], tt[3];
+  joint_rot(b, q, Rj);
+  mat3_vec(R, b.t, tt);
+  tn[0] = tt[0] + t[0];
+  tn[1] = tt[1] + t[1];
+  tn[2] = tt[2] + t[2];
+  mat3_mul(R, Rj, Rn);
 }
 
-// Tip position (and quaternion) of tip `k`.
-CDX_HD void fk_tip(const cdx_chain& c, int k, const float* q, float* pos, float* quat) {
-  int path[CDX_MAX_DEPTH];
-  float Rs[CDX_MAX_DEPTH + 1][9], ts[CDX_MAX_DEPTH + 1][3];
-  const int n = chain_path(c, c.tip_body[k], path);
-  chain_forward(c, path, n, q, Rs, ts);
+// Tip position (and quaternion) of tip `k` from the final pose (R, t) of its body.
+CDX_HD void tip_from_pose(const cdx_chain& c, int k, const float* R, const float* t, float* pos, float* quat) {
   float raw[4], sc;
-  quat_raw(Rs[n], raw, &sc);
+  quat_raw(R, raw, &sc);
   float qt[4] = {raw[0] * sc, raw[1] * sc, raw[2] * sc, raw[3] * sc};
-  pos[0] = ts[n][0]; pos[1] = ts[n][1]; pos[2] = ts[n][2];
+  pos[0] = t[0]; pos[1] = t[1]; pos[2] = t[2];
   if (c.has_offsets) {
     float o[3];
     quat_rotate(qt, c.tip_offset[k], o);
@@ -165,46 +171,99 @@ CDX_HD void fk_tip(const cdx_chain& c, int k, const float* q, float* pos, float*
   if (quat) for (int i = 0; i < 4; ++i) quat[i] = qt[i];
 }
 
-// g_q += (∂pos_k/∂q)ᵀ·gpos with the reference's gradient semantics.
-CDX_HD void fk_tip_bwd(const cdx_chain& c, int k, const float* q, const float* gpos, float* g_q) {
-  int path[CDX_MAX_DEPTH];
-  float Rs[CDX_MAX_DEPTH + 1][9], ts[CDX_MAX_DEPTH + 1][3];
-  const int n = chain_path(c, c.tip_body[k], path);
-  chain_forward(c, path, n, q, Rs, ts);
+// Tip position (and quaternion) of tip `k`: running pose, no per-level storage.
+template <class Q>
+CDX_HD void fk_tip(const cdx_chain& c, int k, const Q& q, float* pos, float* quat) {
+  float R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f}, t[3] = {0.f, 0.f, 0.f};
+  for (uint32_t m = chain_path_mask(c, c.tip_body[k]); m; m &= m - 1) {
+    float Rn[9], tn[3];
+    chain_step(c.bodies[low_bit(m)], q, R, t, Rn, tn);
+    for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+    for (int i = 0; i < 3; ++i) t[i] = tn[i];
+  }
+  tip_from_pose(c, k, R, t, pos, quat);
+}
+
+// g_q(dof, v) receives (∂pos_k/∂q)ᵀ·gpos, one call per moving joint on the path, with the
+// reference's gradient semantics; pos (nullable) receives the tip position.  The parent poses
+// the backward needs are kept in a register array of MAXD levels (loops unrolled over the
+// bound, guarded by the path depth): MAXD must cover the chain's deepest tip (see
+// chain_max_depth); CDX_MAX_DEPTH covers every chain.
+template <int MAXD = CDX_MAX_DEPTH, class Q, class GQ>
+CDX_HD void fk_tip_bwd(const cdx_chain& c, int k, const Q& q, const float* gpos, GQ&& g_q, float* pos = nullptr) {
+  const uint32_t mask = chain_path_mask(c, c.tip_body[k]);
+  const int n = path_depth(mask);
+  float Rs[MAXD][9];  // Rs[l]: world rotation of level l's parent
+  float R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f}, t[3] = {0.f, 0.f, 0.f};
+  uint32_t m = mask;
+#pragma unroll
+  for (int l = 0; l < MAXD; ++l) {
+    if (l < n) {
+      for (int i = 0; i < 9; ++i) Rs[l][i] = R[i];
+      float Rn[9], tn[3];
+      chain_step(c.bodies[low_bit(m)], q, R, t, Rn, tn);
+      m &= m - 1;
+      for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+      for (int i = 0; i < 3; ++i) t[i] = tn[i];
+    }
+  }
+  if (pos) tip_from_pose(c, k, R, t, pos, nullptr);
   float GR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   float Gt[3] = {gpos[0], gpos[1], gpos[2]};
   if (c.has_offsets) {
     float raw[4], sc;
-    const int br = quat_raw(Rs[n], raw, &sc);
+    const int br = quat_raw(R, raw, &sc);
     float qt[4] = {raw[0] * sc, raw[1] * sc, raw[2] * sc, raw[3] * sc};
     float gq[4] = {0, 0, 0, 0};
     quat_rotate_bwd(qt, c.tip_offset[k], gpos, gq);
     for (int i = 0; i < 4; ++i) gq[i] *= sc;  // scale is detached: only d raw flows
     quat_raw_bwd(br, gq, GR);
   }
-  for (int l = n - 1; l >= 0; --l) {
-    const cdx_body& b = c.bodies[path[l]];
-    float Rj[9], A[9], dA[9];
-    if (b.dof >= 0) {
-      axis_rot(b.axis, b.sign * q[b.dof], A, dA);
-      mat3_mul(b.F, A, Rj);
-      // G_Rj = R_pᵀ·G_R ;  G_A = Fᵀ·G_Rj ; dθ = <G_A, dA>
-      float GRj[9], GA[9];
-      mat3_mul_tn(Rs[l], GR, GRj);
-      mat3_mul_tn(b.F, GRj, GA);
-      float dth = 0.f;
-      for (int i = 0; i < 9; ++i) dth += GA[i] * dA[i];
-      g_q[b.dof] += b.sign * dth;
-    } else {
-      for (int i = 0; i < 9; ++i) Rj[i] = b.F[i];
+  m = mask;
+#pragma unroll
+  for (int l = MAXD - 1; l >= 0; --l) {
+    if (l < n) {
+      const int bi = high_bit(m);
+      m &= ~(1u << bi);
+      const cdx_body& b = c.bodies[bi];
+      float Rj[9], A[9], dA[9];
+      if (b.dof >= 0) {
+        axis_rot(b.axis, b.sign * q[b.dof], A, dA);
+        mat3_mul(b.F, A, Rj);
+        // G_Rj = R_pᵀ·G_R ;  G_A = Fᵀ·G_Rj ; dθ = <G_A, dA>
+        float GRj[9], GA[9];
+        mat3_mul_tn(Rs[l], GR, GRj);
+        mat3_mul_tn(b.F, GRj, GA);
+        float dth = 0.f;
+        for (int i = 0; i < 9; ++i) dth += GA[i] * dA[i];
+        g_q(b.dof, b.sign * dth);
+      } else {
+        for (int i = 0; i < 9; ++i) Rj[i] = b.F[i];
+      }
+      // G_R_p = G_R·Rjᵀ + G_t ⊗ t_b ;  G_t_p = G_t
+      float GRp[9];
+      mat3_mul_nt(GR, Rj, GRp);
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) GRp[3 * i + j] += Gt[i] * b.t[j];
+      for (int i = 0; i < 9; ++i) GR[i] = GRp[i];
     }
-    // G_R_p = G_R·Rjᵀ + G_t ⊗ t_b ;  G_t_p = G_t
-    float GRp[9];
-    mat3_mul_nt(GR, Rj, GRp);
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) GRp[3 * i + j] += Gt[i] * b.t[j];
-    for (int i = 0; i < 9; ++i) GR[i] = GRp[i];
   }
 }
+
+// Deepest tip path of a chain (host: picks the fk_tip_bwd register bound).
+CDX_HD int chain_max_depth(const cdx_chain& c) {
+  int d = 0;
+  for (int k = 0; k < c.n_tips; ++k) {
+    const int n = path_depth(chain_path_mask(c, c.tip_body[k]));
+    d = n > d ? n : d;
+  }
+  return d;
+}
+
+// Array accumulator for fk_tip_bwd: g[dof] += v.
+struct GqAdd {
+  float* g;
+  CDX_HDM void operator()(int d, float v) const { g[d] += v; }
+};
 
 }  // namespace cdx

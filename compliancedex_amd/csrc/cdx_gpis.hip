@@ -28,20 +28,24 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-// Mean kernel: 256-thread workgroups = 64 queries × 4 lanes; each workgroup stages 256
-// inducing points (xyz, α) per step in LDS and every lane sums a quarter of them
-// (broadcast LDS reads: the 16 lanes of a split read one address), then the 4 lanes of a
-// query reduce with xor-shuffles.  4 waves per 64 queries keep ≈3 waves per SIMD resident.
-constexpr int MEAN_Q = 64, MEAN_SPLIT = 4, MEAN_BLOCK = MEAN_Q * MEAN_SPLIT;
+// Mean kernel: 256-thread workgroups = 16 queries × 16 lanes; each workgroup stages 256
+// inducing points (x, y, z, α) per step in LDS and every lane sums a sixteenth of them
+// (the 4 lanes of a split read one address), then the 16 lanes of a query reduce with
+// xor-shuffles.  The closure's 13·E queries (E = 4096) make 3328 workgroups = 13 waves per SIMD
+// over the run: f64-VALU-bound (≈25 f64 ops + one v_rsq_f64 per pair; 0.117 ms for 1.07e8 pairs
+// ≈ 90 % of the 30 T f64-op/s the VALU sustains, profiles/r01z_valu_f64.jsonl).  64 × 4 layouts
+// (1 wave per SIMD) ran at 0.137 ms; one query per lane with per-wave point ranges (scalar or
+// LDS-broadcast reads) at 0.122–0.133 ms (64-query workgroups quantise to 3.25 rounds).
+constexpr int MEAN_Q = 16, MEAN_SPLIT = 16, MEAN_BLOCK = MEAN_Q * MEAN_SPLIT;
 
 template <int KT>
 __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
                                                                double* __restrict__ mean, double* __restrict__ gmean,
                                                                double* __restrict__ normal) {
-  __shared__ double sp[4 * MEAN_BLOCK];  // [point][x, y, z, α]
+  __shared__ dbl4 sp[MEAN_BLOCK];  // [point] = (x, y, z, α)
   const int tid = threadIdx.x;
   const int split = tid & (MEAN_SPLIT - 1);
-  const int64_t m = (int64_t)blockIdx.x * MEAN_Q + (tid >> 2);
+  const int64_t m = (int64_t)blockIdx.x * MEAN_Q + tid / MEAN_SPLIT;
   double x0 = 0, x1 = 0, x2 = 0;
   if (m < M) { x0 = X[3 * m]; x1 = X[3 * m + 1]; x2 = X[3 * m + 2]; }
   const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
@@ -49,23 +53,21 @@ __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const
   for (int j0 = 0; j0 < g.N; j0 += MEAN_BLOCK) {
     const int j = j0 + tid;
     __syncthreads();
+    dbl4 v;
     if (j < g.N) {
-      sp[4 * tid] = g.X1[3 * j];
-      sp[4 * tid + 1] = g.X1[3 * j + 1];
-      sp[4 * tid + 2] = g.X1[3 * j + 2];
-      sp[4 * tid + 3] = g.alpha[j];
+      v.x = g.X1[3 * j]; v.y = g.X1[3 * j + 1]; v.z = g.X1[3 * j + 2]; v.w = g.alpha[j];
     } else {
-      sp[4 * tid] = x0 + 1.0;  // any finite point; α = 0
-      sp[4 * tid + 1] = sp[4 * tid + 2] = 0.0;
-      sp[4 * tid + 3] = 0.0;
+      v.x = x0 + 1.0; v.y = v.z = 0.0; v.w = 0.0;  // any finite point; α = 0
     }
+    sp[tid] = v;
     __syncthreads();
 #pragma unroll 4
     for (int jj = split; jj < MEAN_BLOCK; jj += MEAN_SPLIT) {
-      const double dx = x0 - sp[4 * jj], dy = x1 - sp[4 * jj + 1], dz = x2 - sp[4 * jj + 2];
+      const dbl4 p = sp[jj];
+      const double dx = x0 - p.x, dy = x1 - p.y, dz = x2 - p.z;
       double k, kd;
       gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, k, kd);
-      const double a = sp[4 * jj + 3];
+      const double a = p.w;
       acc += a * k;
       const double ak = a * kd;
       g0 += ak * dx;

@@ -45,7 +45,15 @@ CDX_HD void mat3t_vec(const T* a, const T* v, T* out) {  // out = aᵀ·v
 template <typename T>
 CDX_HD T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
+// float32 sin/cos of the joint angles.  The device rounds the f64 result (correctly rounded f32
+// except on double-rounding ties), as the host's glibc sinf/cosf and the reference's CPU torch
+// ops are: the collision cost's 1/d near contact turns one ulp of an f32 FK anchor into 1e-4.
+#if defined(__HIP_DEVICE_COMPILE__)
+CDX_HD float cdx_sinf(float x) { return (float)sin((double)x); }
+CDX_HD float cdx_cosf(float x) { return (float)cos((double)x); }
+#else
 CDX_HD float cdx_sinf(float x) { return sinf(x); }
 CDX_HD float cdx_cosf(float x) { return cosf(x); }
+#endif
 
 }  // namespace cdx

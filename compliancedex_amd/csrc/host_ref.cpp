@@ -48,7 +48,7 @@ void cdxh_fk_backward(const cdx_chain* c, const float* q, int64_t B, const float
   for (int64_t b = 0; b < B; ++b) {
     float* g = gq + b * c->n_dofs;
     for (int i = 0; i < c->n_dofs; ++i) g[i] = 0.f;
-    for (int k = 0; k < c->n_tips; ++k) cdx::fk_tip_bwd(*c, k, q + b * c->n_dofs, gpos + (b * c->n_tips + k) * 3, g);
+    for (int k = 0; k < c->n_tips; ++k) cdx::fk_tip_bwd(*c, k, q + b * c->n_dofs, gpos + (b * c->n_tips + k) * 3, cdx::GqAdd{g});
   }
 }
 
