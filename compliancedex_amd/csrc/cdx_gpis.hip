@@ -259,9 +259,13 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     if (tid < ST_BM) { xq[3 * tid] = qx; xq[3 * tid + 1] = qy; xq[3 * tid + 2] = qz; }
     if (MODE == MODE_GRADV) vrow = vin + (vsel ? vsel[m] : m) * (int64_t)Np;
   }
-  // E11⁻¹ tile: 16 rows × ST_BN columns, 8 consecutive doubles per thread
+  // B tile: 16 rows × ST_BN columns; thread → row ar, four 2-double pieces at columns ac + i·BSTR.
+  // Interleaved pieces keep each ds_write_b128 conflict-free (16 consecutive lanes cover the 64
+  // banks once; 8 consecutive doubles per thread made it 4-way conflicted, ≈9 % of the K-step)
+  // and each global load a contiguous 16 B × 32 lanes.
   constexpr int A_TPR = ST_BN / 8;                      // threads per row
-  const int ar = tid / A_TPR, ac = (tid % A_TPR) * 8;
+  constexpr int BSTR = 2 * A_TPR;                       // doubles between a thread's pieces
+  const int ar = tid / A_TPR, ac = (tid % A_TPR) * 2;
   // wave → 64×64 sub-tile.  With 4 column waves, waves w and w+4 share SIMD w%4 (round-robin wave
   // placement); giving them complementary columns (w, 7−w) lets the triangular modes skip the
   // all-zero K-steps of the diagonal block per wave without idling a SIMD (see skip_mfma below).
@@ -273,7 +277,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
   auto stage_load = [&](int kb) {
     const dbl2v* src = reinterpret_cast<const dbl2v*>(Bop + (int64_t)(kb + ar) * Np + n0 + ac);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) av[i] = src[i];
+    for (int i = 0; i < 4; ++i) av[i] = src[i * (BSTR / 2)];
     if (MODE == MODE_GRADV) {
 #pragma unroll
       for (int i = 0; i < GEN_PER; ++i) {
@@ -302,13 +306,13 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
       double* row = As + ar * LDB;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        row[t4_bpos(ac + 2 * i)] = av[i].x;
-        row[t4_bpos(ac + 2 * i + 1)] = av[i].y;
+        row[t4_bpos(ac + BSTR * i)] = av[i].x;
+        row[t4_bpos(ac + BSTR * i + 1)] = av[i].y;
       }
     } else {
       dbl2v* dst = reinterpret_cast<dbl2v*>(As + ar * LDB + ac);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dst[i] = av[i];
+      for (int i = 0; i < 4; ++i) dst[i * (BSTR / 2)] = av[i];
     }
   };
 
@@ -339,7 +343,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     {
       const dbl2v* src = reinterpret_cast<const dbl2v*>(Bop + (int64_t)(kn + ar) * Np + n0 + ac);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = src[i];
+      for (int i = 0; i < 4; ++i) av[i] = src[i * (BSTR / 2)];
       if (MODE == MODE_GRADV) {
 #pragma unroll
         for (int i = 0; i < GEN_PER; ++i) {
@@ -404,23 +408,33 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
 #endif
       }
     };
+    // 16x16x4 K-step: four 4-deep substeps of 16 MFMAs; the next substep's 8 fragment reads are
+    // issued ahead of this substep's MFMAs (register double buffer), so only the first substep
+    // after the barrier waits on LDS latency.
     auto kstep = [&](auto do_mfma) {
-#pragma unroll
-      for (int kk = 0; kk < ST_BK; kk += 4) {
+      double fa[2][4], fb[2][4];
+      auto frag = [&](int kk, double* a, double* bb) {
         const int kra = (kk + (lane >> 4)) * ST_LD + (lane & 15);
         const int krb = (kk + (lane >> 4)) * ST_LDB + (lane & 15);
-        double a[4], bb[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) { a[i] = Kt[kra + wr + 16 * i]; bb[i] = As[krb + wc + 16 * i]; }
+      };
+      if constexpr (decltype(do_mfma)::value) frag(0, fa[0], fb[0]);
+#pragma unroll
+      for (int kk = 0; kk < ST_BK; kk += 4) {
+        const int cur = (kk >> 2) & 1;
+        if constexpr (decltype(do_mfma)::value) {
+          if (kk + 4 < ST_BK) frag(kk + 4, fa[cur ^ 1], fb[cur ^ 1]);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
 #if defined(CDX_DIAG_NOMFMA)  // timing-only diagnostic build: outputs are wrong
-            acc[i][j][0] += a[i] * bb[j];
+            acc[i][j][0] += fa[cur][i] * fb[cur][j];
 #else
             if constexpr (decltype(do_mfma)::value)
-              acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], bb[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
 #endif
           }
         // K* of the next stage spread over the four 16-MFMA groups (overlaps the matrix pipe)
@@ -437,7 +451,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
         }
 #if defined(CDX_STD_SCHED)
         if constexpr (decltype(do_mfma)::value) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // fragment reads first
+          if (kk + 4 < ST_BK) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // next substep's reads first
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA

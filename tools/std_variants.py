@@ -22,7 +22,10 @@ VARIANTS = {"wn4": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),
             "wn2": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_STD_WN2"),
             "diag_nogen": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOGEN"),
             "diag_nomfma": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOMFMA"),
-            "diag_novload": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOVLOAD")}
+            "diag_novload": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOVLOAD"),
+            "t4_nosched_nogen": ("CDX_FAST_SQRT", "CDX_STD_T4", "CDX_DIAG_NOGEN")}
+if os.environ.get("CDX_VARIANTS"):  # e.g. CDX_VARIANTS=wn4,t4_nosched
+    VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CDX_VARIANTS"].split(",")}
 
 
 def build():
