@@ -15,6 +15,7 @@
 // only the diagonal is formed.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "cdx_gpis.h"
@@ -92,46 +93,37 @@ __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const
 }
 
 // ------------------------------------------------------------------ std (MFMA)
-// W = K*·E11⁻¹ tile of 128 queries × 256 output columns per 512-thread workgroup (one per CU),
-// K-step 16, two LDS buffers (register-staged: the K* tile is computed, not loaded), one barrier
-// per K-step.  Waves form a 2×4 grid; each owns 64×64 = 4×4 v_mfma_f64_16x16x4_f64 tiles.  The
-// 256-wide tile halves the per-output-column cost of generating K* on chip against the 128-wide
-// tile of 2×2 waves (-DCDX_STD_WN2): 2.41 vs 2.58 ms at M = 16 384, N = 2000.
+// 128 queries × 256 output columns per 512-thread workgroup (one per CU: 160 KB of LDS), K-step 16.
+// Waves form a 2×4 grid; each owns 64×64 = 4×4 v_mfma_f64_16x16x4_f64 tiles (128 accumulator VGPRs).
+// The 256-wide tile halves the per-output-column cost of generating K* on chip against a 128-wide
+// tile of 2×2 waves (2.41 vs 2.58 ms at M = 16 384, N = 2000, round-1 A/B).
+//
+// Three LDS stage buffers: during K-step s the waves multiply out of buffer s%3, stage s+2 is
+// generated (K*) / loaded (B) into registers and written to buffer (s+2)%3 after the third substep,
+// and the last substep prefetches the first fragments of step s+1 from buffer (s+1)%3 (complete
+// since the barrier that ended step s−1).  One barrier per K-step, and nothing waits on LDS right
+// after it: the matrix pipe runs across step boundaries (the two-buffer version wrote at the end
+// of the step and re-read fragments after the barrier, ≈600 idle pipe cycles per 8192).
 // Fragment maps (cdna_hip_programming.md §3, f64 form):
 //   A: lane l holds A[row l&15][k l>>4];  B: B[k l>>4][col l&15]
 //   C/D: reg r of lane l is D[row (l>>4) + 4r][col l&15]
-// LDS rows are padded to 144 doubles (row stride ≡ 32 dwords mod 64): the two half-waves of a
-// ds_read_b64 (rows k, k+1) land on disjoint banks.
+// K* rows are padded to 144 doubles and B rows to 272 (row stride ≡ 32 dwords mod 64): the two
+// half-waves of a ds_read_b64 (rows k, k+1) land on disjoint banks.
 constexpr int ST_BM = 128, ST_BK = 16, ST_LD = 144;
 constexpr int ST_TILE = ST_BK * ST_LD;                          // doubles per staged K* tile
-#if defined(CDX_STD_WN2)
-constexpr int ST_WN = 2;                                        // waves along N (2 or 4)
-#else
-constexpr int ST_WN = 4;
-#endif
+constexpr int ST_WN = 4;                                        // waves along N
 static_assert(CDX_NPAD_ALIGN % (64 * ST_WN) == 0, "N_pad alignment must cover the tile width");
 constexpr int ST_BN = 64 * ST_WN;                               // output columns per workgroup
 constexpr int ST_THREADS = 128 * ST_WN;                         // 2 row-waves × ST_WN column-waves
-constexpr int ST_LDB = ST_BN + 16;                              // padded E11⁻¹ row (≡ 32 dwords mod 64)
+constexpr int ST_LDB = ST_BN + 16;                              // padded B row (≡ 32 dwords mod 64)
 constexpr int ST_BTILE = ST_BK * ST_LDB;
-constexpr int ST_SMEM = 2 * (ST_TILE + ST_BTILE) + ST_BM * 3;   // 2 buffers × (K*, E11⁻¹) + query tile
-
-// T4 layout of the B tile (v_mfma_f64_4x4x4_4b_f64 path, triangular modes): lane l needs
-// B[k = l>>4][wc + 4·cg + (l&3)] for cg = 0..15, so each 64-column wave slice is stored as
-// [j = col&3][cg = col>>2 (16) + 2 pad] (72 doubles) and rows are T4_LDB ≡ 8 (mod 32) doubles
-// apart: the 16 (k, j) lane groups of a ds_read_b128 then cover all 64 banks (the 4 β lanes of a
-// group read the same address: broadcast).
-constexpr int T4_SLICE = 72;
-constexpr int T4_LDB = 4 * T4_SLICE + 8;                          // 296
-constexpr int T4_BTILE = ST_BK * T4_LDB;
-constexpr int T4_SMEM = 2 * (ST_TILE + T4_BTILE) + ST_BM * 3;
-__device__ __forceinline__ int t4_bpos(int c) { return (c >> 6) * T4_SLICE + (c & 3) * 18 + ((c & 63) >> 2); }
+constexpr int ST_NBUF = 3;                                      // stage buffers
+constexpr int ST_XS = 3 * ST_BK;                                // X1 rows of one stage
+constexpr int ST_SMEM = ST_NBUF * (ST_TILE + ST_BTILE) + ST_BM * 3 + 2 * ST_XS;
+static_assert(ST_SMEM * sizeof(double) <= 160 * 1024, "stage buffers exceed the CU's LDS");
 
 typedef double dbl2v __attribute__((ext_vector_type(2)));
 
-// v2: 128 queries × ST_BN output columns per workgroup of 2 × ST_WN waves, each wave owning
-// 64×64 = 4×4 v_mfma_f64_16x16x4_f64 tiles; K-step 16, two LDS buffers, one barrier per step.
-//
 // MODE_GRAD (∇std, explicit inverse): A = K* (generated), B = E11⁻¹, W = K*·E11⁻¹, epilogue
 //   Σ W·k and Σ W·kd·(x − x_n) → 4 partials per (column tile, query).
 // MODE_VAR (std, whitened): A = K* (generated), B = L⁻ᵀ (upper triangular), V = K*·L⁻ᵀ =
@@ -140,18 +132,10 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 // MODE_GRADV (∇std from the stored whitened vector): A = V rows (loaded, row vsel[m] of vin),
 //   B = L⁻¹ (lower triangular), W = V·L⁻¹ = (L⁻ᵀv)ᵀ = (E11⁻¹k)ᵀ, the MODE_GRAD epilogue (linear
 //   in W, so K can be split).  Column tile nt only needs K-rows i ≥ n0: N² flops per query
-//   instead of 2N²; launched split-K over 256-row chunks (Nt(Nt+1)/2 partial slots).
+//   instead of 2N²; launched as equal pieces of each query tile's K-sequence (below).
 // The triangular modes' tile costs run 1..Nt K-sweeps: stripes are paired heavy+light per XCD.
+// (A v_mfma_f64_4x4x4_4b_f64 variant ran no faster — LDS-read-bound, profiles/r01_std_gemm_variants.md.)
 enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2 };
-// MFMA shape per pass (profiles/r01x_std_variants.jsonl, r01y_gradv_ab.txt): the whitened std pass
-// runs equally fast on 16x16x4 and 4x4x4_4b (1.30 ms at M = 16 384); the ∇std pass is faster on
-// 4x4x4_4b for contiguous queries (0.37 vs 0.43 ms at M = 4096) but slower on the closure's gathered
-// argmax rows (0.53 vs 0.44 ms): 16x16x4 by default, 4x4x4_4b for both behind -DCDX_STD_T4.
-#if defined(CDX_STD_T4) && !defined(CDX_STD_WN2)
-constexpr bool STD_T4 = true, GRADV_T4 = true;
-#else
-constexpr bool STD_T4 = false, GRADV_T4 = false;
-#endif
 
 
 // K-range [lo, hi) of stripe nt in the triangular modes.
@@ -160,97 +144,67 @@ __device__ __host__ inline void stripe_k_range(int mode, int nt, int N, int& lo,
   hi = mode == MODE_GRADV ? N : min(N, nt * ST_BN + ST_BN);
 }
 
-// Split-K units per query tile: stripe nt contributes ceil((hi − lo)/CH) chunks of CH rows.
-__host__ inline int split_units(int mode, int Nt, int N, int CH) {
-  int u = 0;
-  for (int nt = 0; nt < Nt; ++nt) {
-    int lo, hi;
-    stripe_k_range(mode, nt, N, lo, hi);
-    u += hi > lo ? (hi - lo + CH - 1) / CH : 0;
-  }
-  return u;
+// K-steps of stripe nt's range in the ∇std pass (rows [nt·ST_BN, N)).
+__device__ __host__ inline int gradv_ksteps(int nt, int N) {
+  const int lo = nt * ST_BN;
+  return N > lo ? (N - lo + ST_BK - 1) / ST_BK : 0;
 }
 
-// ksplit = 0: one workgroup per (query tile, stripe).  ksplit = s > 0 (GRADV): one workgroup per
-// (query tile, stripe, K-chunk of ST_BN/s rows), `upm` units per query tile, one partial slot per
-// unit (summed in a fixed order by the finalize kernel: deterministic).
-template <int KT, int MODE, bool T4 = false>
-__global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X,
-                                                                        int64_t M, double* __restrict__ partial,
-                                                                        int64_t M_pad, int Mt, int Nt,
-                                                                        double* __restrict__ vout,
-                                                                        const double* __restrict__ vin,
-                                                                        const int64_t* __restrict__ vsel, int ksplit,
-                                                                        int upm) {
+#if defined(CDX_DIAG_WGTIME)
+// timing-only diagnostic: per-workgroup [start, end] (s_memrealtime, 100 MHz), HW_ID, XCC_ID, stripe,
+// K-steps of the whitened pass (read back by cdx_diag_wgtime)
+__device__ unsigned long long cdx_wgtime[16384][4];
+#endif
+
+// VAR, GRAD: one workgroup per (query tile, stripe), partial slot = stripe.  GRADV: a query tile's
+// work is the concatenated K-step sequence of its stripes (Σ_nt gradv_ksteps(nt)); it is cut into
+// `parts` equal contiguous pieces, one workgroup each, and a piece runs one segment per stripe it
+// touches (epilogue per segment, partial slot p + nt: unique, < parts + Nt; the caller zeroes the
+// slots and the finalize kernel sums them in a fixed order — deterministic).  Equal pieces keep
+// every CU equally busy whatever the query count (the closure's 4096 ∇std queries: 32 tiles ×
+// 8 pieces = one workgroup of 69 K-steps per CU).
+template <int KT, int MODE>
+__global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
+                                                                double* __restrict__ partial, int64_t M_pad, int Mt,
+                                                                int Nt, double* __restrict__ vout,
+                                                                const double* __restrict__ vin,
+                                                                const int64_t* __restrict__ vsel, int parts) {
   constexpr bool VAR = MODE == MODE_VAR;
   constexpr bool TRI = MODE != MODE_GRAD;
-  static_assert(!T4 || (TRI && ST_WN == 4), "the 4x4x4 path covers the triangular modes of the 128x256 tile");
-  constexpr int LDB = T4 ? T4_LDB : ST_LDB;
-  constexpr int BTILE = T4 ? T4_BTILE : ST_BTILE;
-  __shared__ __attribute__((aligned(16))) double smem[T4 ? T4_SMEM : ST_SMEM];
-  double* xq = smem + 2 * (ST_TILE + BTILE);
+  constexpr bool GEN = MODE != MODE_GRADV;  // A tile generated on chip (else loaded from vin)
+  __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
+  double* xq = smem + ST_NBUF * (ST_TILE + ST_BTILE);
+  double* xs = xq + ST_BM * 3;  // [2][ST_XS]: X1 rows of the stage generated next
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int T = Mt * Nt;
+#if defined(CDX_DIAG_WGTIME)
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   const int b = blockIdx.x;
-  int nt, mt, pslot, kbeg_ = 0, kend_ = g.N;
-  const bool split = ksplit > 0;
-  if (TRI && split) {
-    // Split-K: unit = (stripe nt, K-chunk c) so units cost about the same (the ∇std pass runs on
-    // E·L_q queries only; small-M std passes would otherwise run few, long workgroups).  Units of
-    // one (nt, c) block share their B block: each XCD takes a contiguous run of blocks over all
-    // query tiles.  Partial slot = block index.
-    const int CH = ST_BN / ksplit;
-    const int U = Mt * upm;
-    const int t = (U & 7) == 0 ? (b & 7) * (U >> 3) + (b >> 3) : b;
-    int blk = t / Mt;
-    mt = t - blk * Mt;
-    pslot = blk;
-    for (nt = 0;; ++nt) {
-      int lo, hi;
-      stripe_k_range(MODE, nt, g.N, lo, hi);
-      const int nch = hi > lo ? (hi - lo + CH - 1) / CH : 0;
-      if (blk < nch) {
-        kbeg_ = lo + blk * CH;
-        kend_ = min(hi, kbeg_ + CH);
-        break;
-      }
-      blk -= nch;
-    }
-  } else if (TRI) {
-    // Stripe nt costs ∝ nt + 1 K-sweeps (VAR; GRADV: Nt − nt, mirrored below).  Pair stripes
-    // (Nt−1−a, a) — every pair costs Nt + 1 — and
-    // give each pair to X = 16/Nt XCDs (blocks b, b+8, … share an XCD), each XCD taking 1/X of the
-    // pair's query tiles, heavy stripe first: equal work per XCD, and each XCD's L2 holds only its
-    // two stripes of L⁻ᵀ (each stripe is fetched by X XCDs instead of all eight).
-    const int X = 16 / Nt;
-    if (Nt >= 2 && Nt <= 16 && (Nt & (Nt - 1)) == 0 && Mt % X == 0) {
-      const int xcd = b & 7, r = b >> 3, per = Mt / X;
-      const int a = xcd / X, part = xcd % X;
-      nt = r < per ? Nt - 1 - a : a;
-      mt = part * per + (r < per ? r : r - per);
-    } else {  // heaviest stripe first
-      nt = Nt - 1 - b / Mt;
-      mt = b % Mt;
-    }
-    pslot = nt;
-  } else {
-    // XCD-aware order: blocks b and b+8 share an XCD (round-robin dispatch); give each XCD a
-    // contiguous run of n-major tiles so its L2 serves the same E11⁻¹ column stripes.
-    const int t = (T & 7) == 0 ? (b & 7) * (T >> 3) + (b >> 3) : b;
-    nt = t / Mt;
-    mt = t - nt * Mt;
-    pslot = nt;
-  }
-  const int64_t m0 = (int64_t)mt * ST_BM;
-  const int n0 = nt * ST_BN;
+  const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
   const int Np = g.N_pad;
   const double* __restrict__ Bop = MODE == MODE_VAR ? g.Linv_t : (MODE == MODE_GRADV ? g.Linv : g.Ainv);
-  const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
-
   // K* generation: thread → query row gm, GEN_PER k-columns starting at gk (wave-uniform)
-  constexpr int GEN_PER = ST_BM * ST_BK / ST_THREADS;  // 8 (2 col-waves) or 4 (4 col-waves)
+  constexpr int GEN_PER = ST_BM * ST_BK / ST_THREADS;  // 4
+  static_assert(GEN_PER == 4, "the substep schedule below spreads 4 generated entries over 3 substeps");
   const int gm = tid & (ST_BM - 1);
   const int gk = __builtin_amdgcn_readfirstlane((tid >> 7) * GEN_PER);
+  // B tile: 16 rows × ST_BN columns; thread → row ar, four 2-double pieces at columns ac + i·BSTR.
+  // Interleaved pieces keep each ds_write_b128 conflict-free (16 consecutive lanes cover the 64
+  // banks once; 8 consecutive doubles per thread made it 4-way conflicted, ≈9 % of the K-step)
+  // and each global load a contiguous 16 B × 32 lanes.
+  constexpr int A_TPR = ST_BN / 8;                      // threads per row
+  constexpr int BSTR = 2 * A_TPR;                       // doubles between a thread's pieces
+  const int ar = tid / A_TPR, ac = (tid % A_TPR) * 2;
+  // wave → 64×64 sub-tile.  Waves w and w+4 share SIMD w%4 (round-robin wave placement); giving
+  // them complementary columns (w, 7−w) lets the triangular modes skip the all-zero K-steps of the
+  // diagonal block per wave without idling a SIMD (see skip_mfma below).
+  const int cwave = wave < 4 ? wave : 7 - wave;
+  const int wr = (wave / ST_WN) * 64, wc = __builtin_amdgcn_readfirstlane(cwave * 64);
+
+  // One (query tile mt, stripe nt, K-rows [kbeg, kend)) product and its epilogue into slot pslot.
+  auto tile = [&](int mt, int nt, int kbeg, int kend, int pslot) {
+  const int64_t m0 = (int64_t)mt * ST_BM;
+  const int n0 = nt * ST_BN;
   double qx, qy, qz;
   const double* vrow = nullptr;  // MODE_GRADV: this thread's row of the stored V
   {
@@ -259,199 +213,123 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     if (tid < ST_BM) { xq[3 * tid] = qx; xq[3 * tid + 1] = qy; xq[3 * tid + 2] = qz; }
     if (MODE == MODE_GRADV) vrow = vin + (vsel ? vsel[m] : m) * (int64_t)Np;
   }
-  // B tile: 16 rows × ST_BN columns; thread → row ar, four 2-double pieces at columns ac + i·BSTR.
-  // Interleaved pieces keep each ds_write_b128 conflict-free (16 consecutive lanes cover the 64
-  // banks once; 8 consecutive doubles per thread made it 4-way conflicted, ≈9 % of the K-step)
-  // and each global load a contiguous 16 B × 32 lanes.
-  constexpr int A_TPR = ST_BN / 8;                      // threads per row
-  constexpr int BSTR = 2 * A_TPR;                       // doubles between a thread's pieces
-  const int ar = tid / A_TPR, ac = (tid % A_TPR) * 2;
-  // wave → 64×64 sub-tile.  With 4 column waves, waves w and w+4 share SIMD w%4 (round-robin wave
-  // placement); giving them complementary columns (w, 7−w) lets the triangular modes skip the
-  // all-zero K-steps of the diagonal block per wave without idling a SIMD (see skip_mfma below).
-  const int cwave = ST_WN == 4 ? (wave < 4 ? wave : 7 - wave) : wave % ST_WN;
-  const int wr = (wave / ST_WN) * 64, wc = __builtin_amdgcn_readfirstlane(cwave * 64);
+  // B rows ≥ N are zero: stop at the last live K-step; L⁻ᵀ (VAR) also stops at the tile's
+  // diagonal, L⁻¹ (GRADV) starts there
+  const int nK = (kend - kbeg + ST_BK - 1) / ST_BK;
+  // first row of stage t, clamped at the last stage (the extra stages land in buffers nobody reads)
+  auto stage_row = [&](int t) { return kbeg + (t < nK ? t : nK - 1) * ST_BK; };
 
   dbl2v av[4];
   double kv[GEN_PER];
-  auto stage_load = [&](int kb) {
+  auto load_stage = [&](int kb) {  // B rows (and GRADV's V entries) of the stage at row kb
     const dbl2v* src = reinterpret_cast<const dbl2v*>(Bop + (int64_t)(kb + ar) * Np + n0 + ac);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) av[i] = src[i * (BSTR / 2)];
+    for (int i = 0; i < 4; ++i) {
+#if defined(CDX_DIAG_NOBLOAD)  // timing-only diagnostic build: outputs are wrong
+      av[i] = dbl2v{qx + kb, qy + i};
+#else
+      av[i] = src[i * (BSTR / 2)];
+#endif
+    }
     if (MODE == MODE_GRADV) {
 #pragma unroll
-      for (int i = 0; i < GEN_PER; ++i) {
-#if defined(CDX_DIAG_NOVLOAD)  // timing-only diagnostic build: outputs are wrong
-        kv[i] = qx + i;
-#else
-        kv[i] = vrow[kb + gk + i];
-#endif
-      }
-      return;
-    }
-    const double* x1 = g.X1 + 3 * (kb + gk);
-#pragma unroll
-    for (int i = 0; i < GEN_PER; ++i) {
-      const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
-      double kd;
-      gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
+      for (int i = 0; i < GEN_PER; ++i) kv[i] = vrow[kb + gk + i];
     }
   };
+  auto gen = [&](const double* x1, int i) {  // K* entry (gm, gk + i) from the X1 rows at x1
+#if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
+    kv[i] = qx - x1[3 * i];
+#else
+    const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
+    double kd;
+    gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
+#endif
+  };
   auto stage_write = [&](int buf) {
-    double* Kt = smem + buf * (ST_TILE + BTILE);
+    double* Kt = smem + buf * (ST_TILE + ST_BTILE);
     double* As = Kt + ST_TILE;
 #pragma unroll
     for (int i = 0; i < GEN_PER; ++i) Kt[(gk + i) * ST_LD + gm] = kv[i];
-    if constexpr (T4) {
-      double* row = As + ar * LDB;
+    dbl2v* dst = reinterpret_cast<dbl2v*>(As + ar * ST_LDB + ac);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        row[t4_bpos(ac + BSTR * i)] = av[i].x;
-        row[t4_bpos(ac + BSTR * i + 1)] = av[i].y;
-      }
-    } else {
-      dbl2v* dst = reinterpret_cast<dbl2v*>(As + ar * LDB + ac);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dst[i * (BSTR / 2)] = av[i];
-    }
+    for (int i = 0; i < 4; ++i) dst[i * (BSTR / 2)] = av[i];
   };
 
-  dbl4 acc[4][4];      // 16x16x4 path: [row block][col block] of 16×16
-  double acc4[4][16];  // T4 path: [row group rg (16 rows)][col group cg (4 cols)]
+  dbl4 acc[4][4];  // [row block][col block] of 16×16
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0, 0, 0, 0};
-  if constexpr (T4) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc4[i][j] = 0.0;
-  }
 
-  // B rows ≥ N are zero: stop at the last live K-step; L⁻ᵀ (VAR) also stops at the tile's
-  // diagonal, L⁻¹ (GRADV) starts there
-  const int kbeg = split ? kbeg_ : 0;
-  const int kend = split ? kend_ : (VAR ? min(g.N, n0 + ST_BN) : g.N);
-  const int nK = (kend - kbeg + ST_BK - 1) / ST_BK;
-  stage_load(kbeg);
-  stage_write(0);
-  __syncthreads();
-  for (int s = 0; s < nK; ++s) {
-    // Stage s+1 (clamped at the end: the extra stage lands in the buffer nobody reads again).
-    const int kn = kbeg + (s + 1 < nK ? s + 1 : s) * ST_BK;
-    {
-      const dbl2v* src = reinterpret_cast<const dbl2v*>(Bop + (int64_t)(kn + ar) * Np + n0 + ac);
+  // Prologue: stages 0 and 1 into buffers 0 and 1 (X1 straight from global memory), the X1 rows of
+  // stage 2 into xs[0].
 #pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = src[i * (BSTR / 2)];
-      if (MODE == MODE_GRADV) {
+  for (int t = 0; t < 2; ++t) {
+    const int kb = stage_row(t);
+    load_stage(kb);
+    if (GEN) {
 #pragma unroll
-        for (int i = 0; i < GEN_PER; ++i) {
-#if defined(CDX_DIAG_NOVLOAD)  // timing-only diagnostic build: outputs are wrong
-          kv[i] = qx + i + kn;
-#else
-          kv[i] = vrow[kn + gk + i];
-#endif
-        }
-      }
+      for (int i = 0; i < GEN_PER; ++i) gen(g.X1 + 3 * (kb + gk), i);
     }
-    const double* x1 = g.X1 + 3 * (kn + gk);
-    const double* Kt = smem + (s & 1) * (ST_TILE + BTILE);
+    stage_write(t);
+  }
+  if (GEN && tid < ST_XS / 2)
+    reinterpret_cast<dbl2v*>(xs)[tid] = reinterpret_cast<const dbl2v*>(g.X1 + 3 * stage_row(2))[tid];
+  __syncthreads();
+
+  double fa[2][4], fb[2][4];  // fragment double buffer (substep parity)
+  auto frag = [&](int buf, int kk, double* a, double* bb) {
+    const double* Kt = smem + buf * (ST_TILE + ST_BTILE);
     const double* As = Kt + ST_TILE;
+    const int kra = (kk + (lane >> 4)) * ST_LD + (lane & 15);
+    const int krb = (kk + (lane >> 4)) * ST_LDB + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { a[i] = Kt[kra + wr + 16 * i]; bb[i] = As[krb + wc + 16 * i]; }
+  };
+  frag(0, 0, fa[0], fb[0]);
+  int cb = 0;  // buffer of step s: s % 3
+  for (int s = 0; s < nK; ++s) {
+    const int nb = cb == ST_NBUF - 1 ? 0 : cb + 1, wb = nb == ST_NBUF - 1 ? 0 : nb + 1;
+    load_stage(stage_row(s + 2));
+    // X1 rows of stage s+3 (staged through LDS by the first 24 lanes: the generation then issues no
+    // scalar loads, whose lgkmcnt waits would also drain the fragment reads in flight)
+    dbl2v xl = dbl2v{0, 0};
+    if (GEN && tid < ST_XS / 2) xl = reinterpret_cast<const dbl2v*>(g.X1 + 3 * stage_row(s + 3))[tid];
+    const double* x1 = xs + (s & 1) * ST_XS + 3 * gk;
     // This wave's B columns [n0 + wc, n0 + wc + 64) are all zero for the whole K-step when the step
     // lies past their diagonal (L⁻ᵀ, VAR) or before it (L⁻¹, GRADV): skip the MFMAs, keep the
     // staging and barriers.  acc + 0·A is acc, so results are bit-identical.
     const int kb = kbeg + s * ST_BK;
     const bool skip_mfma = (MODE == MODE_VAR && kb >= n0 + wc + 64) || (MODE == MODE_GRADV && kb + ST_BK <= n0 + wc);
-    auto kstep4 = [&](auto do_mfma) {  // v_mfma_f64_4x4x4_4b_f64: 16 rows × 4 cols × 4 deep per issue
-#pragma unroll
-      for (int kk = 0; kk < ST_BK; kk += 4) {
-        const int kra = (kk + (lane >> 4)) * ST_LD + (lane & 15);
-        double a[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = Kt[kra + wr + 16 * i];
-        const dbl2v* bp = reinterpret_cast<const dbl2v*>(As + (kk + (lane >> 4)) * LDB + cwave * T4_SLICE +
-                                                         (lane & 3) * 18);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {  // B fragments in two halves of 8 column groups (register budget)
-          double bb[8];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) { const dbl2v v = bp[4 * h + c]; bb[2 * c] = v.x; bb[2 * c + 1] = v.y; }
-          if constexpr (decltype(do_mfma)::value) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int j = 0; j < 8; ++j)
-                acc4[i][8 * h + j] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[i], bb[j], acc4[i][8 * h + j], 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int i = kk * GEN_PER / ST_BK; i < (kk + 4) * GEN_PER / ST_BK; ++i) {
-          if (MODE == MODE_GRADV) break;  // loaded, not generated
-#if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
-          kv[i] = qx - x1[3 * i];
-#else
-          const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
-          double kd;
-          gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
-#endif
-        }
-#if defined(CDX_STD_SCHED)
-        if constexpr (decltype(do_mfma)::value) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // fragment reads first
-#pragma unroll
-          for (int q = 0; q < 64; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // then one VALU
-          }
-        }
-#endif
-      }
-    };
-    // 16x16x4 K-step: four 4-deep substeps of 16 MFMAs; the next substep's 8 fragment reads are
-    // issued ahead of this substep's MFMAs (register double buffer), so only the first substep
-    // after the barrier waits on LDS latency.
     auto kstep = [&](auto do_mfma) {
-      double fa[2][4], fb[2][4];
-      auto frag = [&](int kk, double* a, double* bb) {
-        const int kra = (kk + (lane >> 4)) * ST_LD + (lane & 15);
-        const int krb = (kk + (lane >> 4)) * ST_LDB + (lane & 15);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { a[i] = Kt[kra + wr + 16 * i]; bb[i] = As[krb + wc + 16 * i]; }
-      };
-      if constexpr (decltype(do_mfma)::value) frag(0, fa[0], fb[0]);
 #pragma unroll
       for (int kk = 0; kk < ST_BK; kk += 4) {
         const int cur = (kk >> 2) & 1;
+        // next substep's fragments; the last substep reads step s+1's first ones
+        if (kk + 4 < ST_BK) frag(cb, kk + 4, fa[cur ^ 1], fb[cur ^ 1]);
+        else frag(nb, 0, fa[cur ^ 1], fb[cur ^ 1]);
         if constexpr (decltype(do_mfma)::value) {
-          if (kk + 4 < ST_BK) frag(kk + 4, fa[cur ^ 1], fb[cur ^ 1]);
-        }
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < 4; ++j) {
 #if defined(CDX_DIAG_NOMFMA)  // timing-only diagnostic build: outputs are wrong
-            acc[i][j][0] += fa[cur][i] * fb[cur][j];
+              acc[i][j][0] += fa[cur][i] * fb[cur][j];
 #else
-            if constexpr (decltype(do_mfma)::value)
               acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
 #endif
-          }
-        // K* of the next stage spread over the four 16-MFMA groups (overlaps the matrix pipe)
-#pragma unroll
-        for (int i = kk * GEN_PER / ST_BK; i < (kk + 4) * GEN_PER / ST_BK; ++i) {
-          if (MODE == MODE_GRADV) break;  // loaded, not generated
-#if defined(CDX_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
-          kv[i] = qx - x1[3 * i];
-#else
-          const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
-          double kd;
-          gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
-#endif
+            }
         }
+        // stage s+2: K* entries over substeps 0–2 (2, 1, 1), written after substep 2's MFMAs
+        if (GEN) {
+          if (kk == 0) { gen(x1, 0); gen(x1, 1); }
+          if (kk == 4) gen(x1, 2);
+          if (kk == 8) gen(x1, 3);
+        }
+        if (kk == 8) stage_write(wb);
 #if defined(CDX_STD_SCHED)
         if constexpr (decltype(do_mfma)::value) {
-          if (kk + 4 < ST_BK) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // next substep's reads first
+          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // next fragments first
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
@@ -461,14 +339,10 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
 #endif
       }
     };
-    if constexpr (T4) {
-      if (skip_mfma) kstep4(std::false_type{});
-      else kstep4(std::true_type{});
-    } else {
-      if (skip_mfma) kstep(std::false_type{});
-      else kstep(std::true_type{});
-    }
-    stage_write((s + 1) & 1);
+    if (skip_mfma) kstep(std::false_type{});
+    else kstep(std::true_type{});
+    if (GEN && tid < ST_XS / 2) reinterpret_cast<dbl2v*>(xs + ((s + 1) & 1) * ST_XS)[tid] = xl;
+    cb = nb;
     __syncthreads();
   }
 
@@ -477,36 +351,6 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     // row, then over the column waves in LDS; V itself to vout when asked (16 lanes of a row write
     // 128 contiguous bytes).
     double* red = smem;  // [ST_WN][ST_BM]
-    if constexpr (T4) {
-      // lane l holds, for row group rg and column group cg, V[row][col] with
-      // row = wr + 16·rg + 4·((l>>2)&3) + (l>>4), col = wc + 4·cg + (l&3)
-      const int r4 = 4 * ((lane >> 2) & 3) + (lane >> 4);
-      if (vout) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          double* vr = vout + (m0 + wr + 16 * i + r4) * (int64_t)Np + n0 + wc + (lane & 3);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) vr[4 * j] = acc4[i][j];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        double v = 0.0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v = fma(acc4[i][j], acc4[i][j], v);
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        if ((lane & 3) == 0) red[cwave * ST_BM + wr + 16 * i + r4] = v;
-      }
-      __syncthreads();
-      if (tid < ST_BM) {
-        double v = 0.0;
-#pragma unroll
-        for (int w = 0; w < ST_WN; ++w) v += red[w * ST_BM + tid];
-        partial[(int64_t)pslot * M_pad + m0 + tid] = v;
-      }
-      return;
-    }
     if (vout) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -538,61 +382,21 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
       for (int w = 0; w < ST_WN; ++w) v += red[w * ST_BM + tid];
       partial[(int64_t)pslot * M_pad + m0 + tid] = v;
     }
+#if defined(CDX_DIAG_WGTIME)
+    if (tid == 0 && b < 16384) {
+      cdx_wgtime[b][0] = t_start;
+      cdx_wgtime[b][1] = __builtin_amdgcn_s_memrealtime();
+      cdx_wgtime[b][2] = ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32) |
+                         (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+      cdx_wgtime[b][3] = ((unsigned long long)nt << 32) | (unsigned)nK;
+    }
+#endif
     return;
   }
 
-  if constexpr (T4) {  // GRADV on the 4x4x4 layout (see the VAR epilogue for the lane map)
-    double* red = smem;
-    const int r4 = 4 * ((lane >> 2) & 3) + (lane >> 4);
-    double ps[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ps[i][0] = ps[i][1] = ps[i][2] = ps[i][3] = 0.0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int n = n0 + wc + 4 * j + (lane & 3);
-      const double nx = g.X1[3 * n], ny = g.X1[3 * n + 1], nz = g.X1[3 * n + 2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wr + 16 * i + r4;
-        const double dx = xq[3 * row] - nx, dy = xq[3 * row + 1] - ny, dz = xq[3 * row + 2] - nz;
-        double k, kd;
-        gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, k, kd);
-        const double w = acc4[i][j];
-        const double wkd = w * kd;
-        ps[i][0] += w * k;
-        ps[i][1] += wkd * dx;
-        ps[i][2] += wkd * dy;
-        ps[i][3] += wkd * dz;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        double v = ps[i][c];
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        ps[i][c] = v;
-      }
-    if ((lane & 3) == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) red[(cwave * ST_BM + wr + 16 * i + r4) * 4 + c] = ps[i][c];
-    }
-    __syncthreads();
-    for (int idx = tid; idx < ST_BM * 4; idx += ST_THREADS) {
-      const int row = idx >> 2, c = idx & 3;
-      double v = 0.0;
-#pragma unroll
-      for (int w = 0; w < ST_WN; ++w) v += red[(w * ST_BM + row) * 4 + c];
-      partial[((int64_t)pslot * M_pad + m0 + row) * 4 + c] = v;
-    }
-    return;
-  }
-
-  // Epilogue: per owned row, s = Σ_n W k and g = Σ_n W kd (x_m − x_n) over this wave's 64 columns,
-  // reduced over the 16 lanes of a row (xor-shuffles), then over the column waves in LDS.
+  // Epilogue: per owned row g = Σ_n W kd (x_m − x_n) over this wave's 64 columns (slot 0 of the
+  // 4-double partial stays 0), reduced over the 16 lanes of a row (xor-shuffles), then over the
+  // column waves in LDS.
   double* red = smem;  // [ST_WN][ST_BM][4], reuses the staging buffers (loop ended on a barrier)
   double nxs[4][3];
 #pragma unroll
@@ -614,9 +418,7 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
         const double dx = mx - nxs[j][0], dy = my - nxs[j][1], dz = mz - nxs[j][2];
         double k, kd;
         gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, k, kd);
-        const double w = acc[i][j][r];
-        const double wkd = w * kd;
-        ps[r][0] += w * k;
+        const double wkd = acc[i][j][r] * kd;
         ps[r][1] += wkd * dx;
         ps[r][2] += wkd * dy;
         ps[r][3] += wkd * dz;
@@ -650,6 +452,54 @@ __global__ __launch_bounds__(ST_THREADS, 8 / ST_WN) void gpis_std_kernel(cdx_gpi
     for (int w = 0; w < ST_WN; ++w) v += red[(w * ST_BM + row) * 4 + c];
     partial[((int64_t)pslot * M_pad + m0 + row) * 4 + c] = v;
   }
+  };  // tile
+
+  if (MODE == MODE_GRADV) {
+    const int U = Mt * parts;
+    const int t = (U & 7) == 0 ? (b & 7) * (U >> 3) + (b >> 3) : b;  // each XCD: one K-range, many tiles
+    const int p = t / Mt, mt = t - p * Mt;
+    int W = 0;
+    for (int nt = 0; nt < Nt; ++nt) W += gradv_ksteps(nt, g.N);
+    const int q0 = (int)((int64_t)W * p / parts), q1 = (int)((int64_t)W * (p + 1) / parts);
+    bool first = true;
+    for (int nt = 0, s0 = 0; nt < Nt; ++nt) {
+      const int s1 = s0 + gradv_ksteps(nt, g.N);
+      const int a = max(q0, s0), e = min(q1, s1);
+      if (a < e) {
+        if (!first) __syncthreads();  // the previous segment's epilogue used the stage buffers
+        first = false;
+        tile(mt, nt, nt * ST_BN + (a - s0) * ST_BK, min(g.N, nt * ST_BN + (e - s0) * ST_BK), p + nt);
+      }
+      s0 = s1;
+    }
+    return;
+  }
+  int nt, mt;
+  if (TRI) {
+    // Stripe nt costs ∝ nt + 1 K-sweeps.  Pair stripes (Nt−1−a, a) — every pair costs Nt + 1 — and
+    // give each pair to X = 16/Nt XCDs (blocks b, b+8, … share an XCD), each XCD taking 1/X of the
+    // pair's query tiles, heavy stripe first: equal work per XCD, and each XCD's L2 holds only its
+    // two stripes of L⁻ᵀ (each stripe is fetched by X XCDs instead of all eight).
+    const int X = 16 / Nt;
+    if (Nt >= 2 && Nt <= 16 && (Nt & (Nt - 1)) == 0 && Mt % X == 0) {
+      const int xcd = b & 7, r = b >> 3, per = Mt / X;
+      const int a = xcd / X, part = xcd % X;
+      nt = r < per ? Nt - 1 - a : a;
+      mt = part * per + (r < per ? r : r - per);
+    } else {  // heaviest stripe first
+      nt = Nt - 1 - b / Mt;
+      mt = b % Mt;
+    }
+  } else {
+    // XCD-aware order: blocks b and b+8 share an XCD (round-robin dispatch); give each XCD a
+    // contiguous run of n-major tiles so its L2 serves the same E11⁻¹ column stripes.
+    const int T = Mt * Nt;
+    const int t = (T & 7) == 0 ? (b & 7) * (T >> 3) + (b >> 3) : b;
+    nt = t / Mt;
+    mt = t - nt * Mt;
+  }
+  // B rows ≥ N are zero: stop at the last live K-step; L⁻ᵀ (VAR) also stops at the tile's diagonal
+  tile(mt, nt, 0, VAR ? min(g.N, nt * ST_BN + ST_BN) : g.N, nt);
 }
 
 
@@ -711,20 +561,20 @@ size_t gpis_var_ws_bytes(const cdx_gpis& g, int64_t M) {
   return (size_t)(g.N_pad / ST_BN) * (size_t)round_up(M, ST_BM) * sizeof(double);
 }
 
-// Split factor: the smallest s ∈ {1, 2, 4, 8, 16} giving ≥ 2 units per CU (256 CUs), else 16.
-static int choose_split(int mode, const cdx_gpis& g, int64_t M) {
-  const int Mt = (int)(round_up(M, ST_BM) / ST_BM), Nt = g.N_pad / ST_BN;
-  int s = 1;
-  while (s < 16 && (int64_t)Mt * split_units(mode, Nt, g.N, ST_BN / s) < 512) s *= 2;
-  return s;
+// Pieces per query tile of the ∇std pass: one round of workgroups over the 256 CUs when the query
+// tiles alone do not fill it (pieces of ≥ 8 K-steps), else one piece per tile.
+static int gradv_parts(const cdx_gpis& g, int Mt) {
+  int W = 0;
+  for (int nt = 0; nt < g.N_pad / ST_BN; ++nt) W += gradv_ksteps(nt, g.N);
+  int p = Mt >= 256 ? 1 : (256 + Mt - 1) / Mt;
+  return std::max(1, std::min(p, W / 8));
 }
 
 size_t gpis_grad_ws_bytes(const cdx_gpis& g, int64_t M) {
   if (M <= 0) return 0;
-  const int s = choose_split(MODE_GRADV, g, M);
-  const size_t upm = (size_t)split_units(MODE_GRADV, g.N_pad / ST_BN, g.N, ST_BN / s);
-  const size_t dense = (size_t)(g.N_pad / ST_BN);  // the explicit-inverse pass's partial slots
-  return (upm > dense ? upm : dense) * (size_t)round_up(M, ST_BM) * 4 * sizeof(double);
+  const int Mt = (int)(round_up(M, ST_BM) / ST_BM), Nt = g.N_pad / ST_BN;
+  const size_t slots = (size_t)std::max(gradv_parts(g, Mt) + Nt, Nt);  // GRADV pieces + stripes; GRAD: stripes
+  return slots * (size_t)round_up(M, ST_BM) * 4 * sizeof(double);
 }
 
 template <int KT>
@@ -733,8 +583,8 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
   // (no split-K here: Σ V² needs the K-summed V, and summing chunk partials with atomics made the
   // result depend on arrival order — the std pass stays one workgroup per (query tile, stripe))
   prof_mark(PROF_GPIS_STD, true, s);
-  hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR, STD_T4>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s,
-                     g, X, M, partial, M_pad, Mt, n_tiles, vout, nullptr, nullptr, 0, 0);
+  hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s,
+                     g, X, M, partial, M_pad, Mt, n_tiles, vout, nullptr, nullptr, 0);
   prof_mark(PROF_GPIS_STD, false, s);
   hipLaunchKernelGGL(gpis_var_finalize<KT>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, g, partial, M, M_pad,
                      n_tiles, std_out, var_out);
@@ -745,19 +595,20 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
                            double* gstd, double* partial, int64_t M_pad, int Mt, int n_tiles, const double* vin,
                            hipStream_t s) {
   prof_mark(PROF_GPIS_GRAD, true, s);
-  int n_parts = n_tiles;
+  int n_slots = n_tiles;
   if (vin) {
-    const int ks = choose_split(MODE_GRADV, g, M);
-    n_parts = split_units(MODE_GRADV, n_tiles, g.N, ST_BN / ks);  // split-K units (stripe, K-chunk)
-    hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV, GRADV_T4>), dim3((unsigned)(Mt * n_parts)), dim3(ST_THREADS), 0,
-                       s, g, X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel, ks, n_parts);
+    const int parts = gradv_parts(g, Mt);
+    n_slots = parts + n_tiles;  // slot p + nt per (piece, stripe) segment; unused slots stay zero
+    (void)hipMemsetAsync(partial, 0, (size_t)n_slots * M_pad * 4 * sizeof(double), s);
+    hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV>), dim3((unsigned)(Mt * parts)), dim3(ST_THREADS), 0,
+                       s, g, X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel, parts);
   } else {
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRAD>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g,
-                       X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, 0, 0);
+                       X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, 0);
   }
   prof_mark(PROF_GPIS_GRAD, false, s);
   hipLaunchKernelGGL(gpis_grad_finalize, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, partial, M, M_pad,
-                     n_parts, sel, var, gstd);
+                     n_slots, sel, var, gstd);
 }
 
 size_t gpis_v_bytes(const cdx_gpis& g, int64_t M) {
@@ -786,7 +637,7 @@ int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_
   if (M <= 0) return CDX_OK;
   const int64_t M_pad = round_up(M, ST_BM);
   const int n_tiles = g.N_pad / ST_BN;
-  if (M_pad / ST_BM * (int64_t)16 * n_tiles * (n_tiles + 1) / 2 > 0x7fffffff) return CDX_EINVAL;
+  if (M_pad / ST_BM * (int64_t)(256 + n_tiles) > 0x7fffffff) return CDX_EINVAL;
   const int Mt = (int)(M_pad / ST_BM);
   double* partial = static_cast<double*>(ws);
   switch (g.kernel) {
@@ -840,6 +691,13 @@ int cdx_gpis_std(const cdx_gpis* g, const double* X, int64_t M, double* std_out,
   if (rc || !grad_std) return rc;
   return cdx::gpis_grad_launch(*g, X, M, nullptr, var, grad_std, pg, s, whitened_grad ? V : nullptr);
 }
+
+#if defined(CDX_DIAG_WGTIME)
+int cdx_diag_wgtime(void* host_out, int n) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(cdx_wgtime), (size_t)n * 32, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? CDX_OK : CDX_ELAUNCH;
+}
+#endif
 
 // Test hook: D[16×16] = A[16×4]·B[4×16] through one v_mfma_f64_16x16x4_f64 (layout check).
 int cdx_selftest_mfma_f64(const double* A, const double* B, double* D, cdx_stream_t stream) {

@@ -97,6 +97,35 @@ def test_gpis_large_batch_vs_oracle_chunk():
     assert rel_err(Xt.grad.cpu().numpy()[idx], ref["gstd"]) < 1e-9
 
 
+@pytest.mark.parametrize("state", ["banana", "synthetic2000"])
+def test_gpis_std_explicit_inverse_path(state):
+    """A C-ABI state without L⁻¹ (cdx_gpis.Linv = NULL) takes the explicit-inverse ∇std pass
+    (W = K*·E11⁻¹, 2N² per query, the dense MODE_GRAD GEMM) instead of the whitened one."""
+    from compliancedex_amd import _native as N
+    from compliancedex_amd.gpis import _State, gpis_std
+    from tests._helpers import oracle_gpis_at
+    g = _gpis(state)
+    st = g.native_state()
+    sub = _State.__new__(_State)
+    sub.__dict__.update(st.__dict__)
+    sub.ws = None
+    sub.desc = N.CdxGpis(X1=st.desc.X1, alpha=st.desc.alpha, Ainv=st.desc.Ainv, Linv_t=st.desc.Linv_t, Linv=None,
+                         N=st.desc.N, N_pad=st.desc.N_pad, kernel=st.desc.kernel, R=st.desc.R, sigma=st.desc.sigma,
+                         bias=st.desc.bias)
+    rng = np.random.default_rng(17)
+    X1 = g.X1.cpu().numpy()
+    X = X1.min(0) - 0.02 + (np.ptp(X1, 0) + 0.04) * rng.random((1000, 3))
+    Xt = torch.from_numpy(X).to(DEV)
+    std_w, gstd_w = gpis_std(st, Xt)
+    std_e, gstd_e = gpis_std(sub, Xt)
+    torch.cuda.synchronize()
+    assert torch.equal(std_w, std_e)  # std is the whitened pass either way
+    ref = oracle_gpis_at(oracle_gpis(state), X[:100], with_std=True)
+    # explicit inverse: ∇std carries E11⁻¹'s rounding (cond up to 1.1e7): 1.3e-8 measured on MI355X
+    assert rel_err(gstd_e[:100].cpu().numpy(), ref["gstd"]) < 1e-6
+    assert rel_err(gstd_e.cpu().numpy(), gstd_w.cpu().numpy()) < 1e-6
+
+
 @pytest.mark.parametrize("kernel", ["tps", "rbf", "joint"])
 def test_gpis_fit_vs_oracle(kernel):
     """cdx_gpis_fit (R, E11) and the factored state vs the oracle's fit + solve (gpis.py:33-59)."""

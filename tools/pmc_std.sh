@@ -10,7 +10,8 @@ i=0
 for G in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_F64" \
          "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS" \
          "SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
-         "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY"; do
+         "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY" \
+         "TCC_HIT_sum TCC_MISS_sum SQ_INSTS_VMEM_RD SQ_INSTS_SALU"; do
   i=$((i + 1))
   timeout -k 10 200 rocprofv3 --pmc $G --output-format csv -d "$OUT/p$i" -o run -- \
     python3 tools/std_variants.py child "$PWD/compliancedex_amd/lib/libcdx_$LIB.so" 16384 2000 "$OUT/ref.npy" \

@@ -12,6 +12,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 from collections import defaultdict
@@ -54,9 +55,11 @@ def main():
         w = sum(write.get(k, [0])) / max(len(write.get(k, [])), 1)
         summary["kernels"][short(k)] = {"FETCH_SIZE_kB": f, "WRITE_SIZE_kB": w, "hbm_bytes": (2 * f + w) * 1024,
                                         "dispatches": len(fetch.get(k, []))}
-        if "gpis_std_kernel" in k:
-            key = "gpis_var_bytes_per_launch" if "true>" in k else "gpis_grad_bytes_per_launch"
-            summary[key] = (2 * f + w) * 1024
+        m = re.search(r"gpis_std_kernel<\d+, (\d)", k)
+        if m:  # template <KT, MODE, T4>: MODE 1 = whitened std pass (VAR), 2 = ∇std pass (GRADV)
+            key = {"1": "gpis_var_bytes_per_launch", "2": "gpis_grad_bytes_per_launch"}.get(m.group(1))
+            if key:
+                summary[key] = (2 * f + w) * 1024
     json.dump(summary, open(os.path.join(REPO, "profiles", f"{tag}_pmc.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
 

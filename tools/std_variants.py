@@ -15,15 +15,14 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-VARIANTS = {"wn4": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),
-            "t4": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_STD_T4"),
-            "t4_nosched": ("CDX_FAST_SQRT", "CDX_STD_T4"),
+VARIANTS = {"wn4": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),               # default build
             "wn4_nosched": ("CDX_FAST_SQRT",),
-            "wn2": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_STD_WN2"),
+            "old2buf": None,                                       # prebuilt older library, not rebuilt
             "diag_nogen": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOGEN"),
             "diag_nomfma": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOMFMA"),
-            "diag_novload": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOVLOAD"),
-            "t4_nosched_nogen": ("CDX_FAST_SQRT", "CDX_STD_T4", "CDX_DIAG_NOGEN")}
+            "diag_nobload": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOBLOAD"),
+            "diag_wgtime": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_WGTIME"),
+            "diag_nobload_nogen": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_DIAG_NOBLOAD", "CDX_DIAG_NOGEN")}
 if os.environ.get("CDX_VARIANTS"):  # e.g. CDX_VARIANTS=wn4,t4_nosched
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CDX_VARIANTS"].split(",")}
 
@@ -31,6 +30,8 @@ if os.environ.get("CDX_VARIANTS"):  # e.g. CDX_VARIANTS=wn4,t4_nosched
 def build():
     from compliancedex_amd.build import build_device
     for name, defs in VARIANTS.items():
+        if defs is None:
+            continue
         build_device(force=True, defines=defs, out_name=f"libcdx_{name}.so")
 
 
@@ -67,6 +68,16 @@ def child(lib, M, N, ref_path):
     torch.cuda.synchronize()
     ms_grad = ev[0].elapsed_time(ev[1]) / reps - ms
     out = std.unsqueeze(1).cpu().numpy()
+    if "wgtime" in lib:  # per-workgroup timeline of one whitened pass (CDX_DIAG_WGTIME builds)
+        import ctypes
+        from compliancedex_amd import _native
+        gpis_std(st, X, want_grad=False)
+        torch.cuda.synchronize()
+        n = 16384
+        buf = np.zeros((n, 4), dtype=np.uint64)
+        _native.load().cdx_diag_wgtime.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        assert _native.load().cdx_diag_wgtime(buf.ctypes.data, n) == 0
+        np.save(os.path.join(REPO, "gpurun_out", f"wgtime_{M}_{N}.npy"), buf)
     if not os.path.exists(ref_path):
         np.save(ref_path, out)
     ref = np.load(ref_path)
