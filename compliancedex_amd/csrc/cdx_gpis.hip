@@ -144,6 +144,12 @@ __device__ __host__ inline void stripe_k_range(int mode, int nt, int N, int& lo,
   hi = mode == MODE_GRADV ? N : min(N, nt * ST_BN + ST_BN);
 }
 
+// K-steps of stripe nt's range in the whitened pass (rows [0, min(N, (nt+1)·ST_BN))).
+__device__ __host__ inline int var_ksteps(int nt, int N) {
+  const int hi = min(N, (nt + 1) * ST_BN);
+  return (hi + ST_BK - 1) / ST_BK;
+}
+
 // K-steps of stripe nt's range in the ∇std pass (rows [nt·ST_BN, N)).
 __device__ __host__ inline int gradv_ksteps(int nt, int N) {
   const int lo = nt * ST_BN;
@@ -349,8 +355,21 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   if constexpr (VAR) {
     // Epilogue: per owned row Σ V² over this wave's 64 columns, reduced over the 16 lanes of a
     // row, then over the column waves in LDS; V itself to vout when asked (16 lanes of a row write
-    // 128 contiguous bytes).
+    // 128 contiguous bytes).  Split-K launches (parts > 0) store their K-chunk's partial V tile to
+    // partial[pslot = chunk][M_pad][N_pad] instead; gpis_var_splitk_finalize sums the chunks.
     double* red = smem;  // [ST_WN][ST_BM]
+    if (parts > 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double* vr = partial + ((int64_t)pslot * M_pad + m0 + wr + 16 * i + (lane >> 4) + 4 * r) * Np + n0 + wc +
+                       (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vr[16 * j] = acc[i][j][r];
+        }
+      return;
+    }
     if (vout) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -475,6 +494,20 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     return;
   }
   int nt, mt;
+  if (VAR && parts > 0) {
+    // Split-K (few query tiles): unit = (stripe nt, K-chunk c of `parts` K-steps, query tile); the
+    // units of one (nt, c) block are consecutive, block-major.
+    int blk = b / Mt;
+    mt = b - blk * Mt;
+    for (nt = 0;; ++nt) {
+      const int nch = (var_ksteps(nt, g.N) + parts - 1) / parts;
+      if (blk < nch) break;
+      blk -= nch;
+    }
+    const int k0 = blk * parts * ST_BK;
+    tile(mt, nt, k0, min(min(g.N, nt * ST_BN + ST_BN), k0 + parts * ST_BK), blk);
+    return;
+  }
   if (TRI) {
     // Stripe nt costs ∝ nt + 1 K-sweeps.  Pair stripes (Nt−1−a, a) — every pair costs Nt + 1 — and
     // give each pair to X = 16/Nt XCDs (blocks b, b+8, … share an XCD), each XCD taking 1/X of the
@@ -518,6 +551,37 @@ __global__ __launch_bounds__(256) void gpis_var_finalize(cdx_gpis g, const doubl
   if (var_out) var_out[m] = v;
 }
 
+// Split-K whitened pass: V[m, col] = Σ_c chunk partials (fixed order), stored to vout when asked,
+// std = sqrt|k0 − Σ_col V²| — one 256-thread block per query row, tree-reduced (deterministic).
+template <int KT>
+__global__ __launch_bounds__(256) void gpis_var_splitk_finalize(cdx_gpis g, const double* __restrict__ vpart,
+                                                                int64_t M_pad, int chunk, double* __restrict__ vout,
+                                                                double* __restrict__ std_out,
+                                                                double* __restrict__ var_out) {
+  __shared__ double red[256];
+  const int64_t m = blockIdx.x;
+  const int Np = g.N_pad;
+  double s = 0;
+  for (int col = threadIdx.x; col < Np; col += 256) {
+    const int nch = (var_ksteps(col / ST_BN, g.N) + chunk - 1) / chunk;
+    double v = 0;
+    for (int c = 0; c < nch; ++c) v += vpart[((int64_t)c * M_pad + m) * Np + col];
+    if (vout) vout[m * Np + col] = v;
+    s = fma(v, v, s);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double v = gpis_k0<KT>(g.R) - red[0];
+    std_out[m] = sqrt(fabs(v));
+    if (var_out) var_out[m] = v;
+  }
+}
+
 // ∇std = −sign(v)·(Σ_n W kd (x − x_n))/sqrt|v| at query m, written to row sel[m] (identity when
 // sel is null) with v = var[sel[m]] from the whitened pass.
 __global__ __launch_bounds__(256) void gpis_grad_finalize(const double* __restrict__ partial, int64_t M,
@@ -557,17 +621,40 @@ int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
 namespace cdx {
 
+// Split-K chunk (K-steps) of the whitened pass, 0 = one workgroup per (query tile, stripe).  Used
+// when those workgroups do not fill the 256 CUs (config 1: 4 workgroups of up to 23 serial K-steps):
+// the largest power-of-two chunk ≥ 2 K-steps giving ≥ 256 units, within 256 MB of chunk partials.
+static int var_chunk(const cdx_gpis& g, int64_t M) {
+  const int Mt = (int)(round_up(M, ST_BM) / ST_BM), Nt = g.N_pad / ST_BN;
+  if ((int64_t)Mt * Nt >= 256) return 0;
+  auto units = [&](int c) {
+    int u = 0;
+    for (int nt = 0; nt < Nt; ++nt) u += (var_ksteps(nt, g.N) + c - 1) / c;
+    return (int64_t)Mt * u;
+  };
+  int c = 64;
+  while (c > 2 && units(c) < 256) c >>= 1;
+  const int64_t maxch = (var_ksteps(Nt - 1, g.N) + c - 1) / c;
+  if (maxch * round_up(M, ST_BM) * g.N_pad * (int64_t)sizeof(double) > ((int64_t)256 << 20)) return 0;
+  return c;
+}
+
 size_t gpis_var_ws_bytes(const cdx_gpis& g, int64_t M) {
+  const int c = var_chunk(g, M);
+  if (c > 0) {
+    const int Nt = g.N_pad / ST_BN;
+    return (size_t)((var_ksteps(Nt - 1, g.N) + c - 1) / c) * (size_t)round_up(M, ST_BM) * g.N_pad * sizeof(double);
+  }
   return (size_t)(g.N_pad / ST_BN) * (size_t)round_up(M, ST_BM) * sizeof(double);
 }
 
 // Pieces per query tile of the ∇std pass: one round of workgroups over the 256 CUs when the query
-// tiles alone do not fill it (pieces of ≥ 8 K-steps), else one piece per tile.
+// tiles alone do not fill it (pieces of ≥ 4 K-steps), else one piece per tile.
 static int gradv_parts(const cdx_gpis& g, int Mt) {
   int W = 0;
   for (int nt = 0; nt < g.N_pad / ST_BN; ++nt) W += gradv_ksteps(nt, g.N);
   int p = Mt >= 256 ? 1 : (256 + Mt - 1) / Mt;
-  return std::max(1, std::min(p, W / 8));
+  return std::max(1, std::min(p, W / 4));
 }
 
 size_t gpis_grad_ws_bytes(const cdx_gpis& g, int64_t M) {
@@ -580,8 +667,20 @@ size_t gpis_grad_ws_bytes(const cdx_gpis& g, int64_t M) {
 template <int KT>
 static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double* std_out, double* var_out,
                           double* partial, int64_t M_pad, int Mt, int n_tiles, double* vout, hipStream_t s) {
-  // (no split-K here: Σ V² needs the K-summed V, and summing chunk partials with atomics made the
-  // result depend on arrival order — the std pass stays one workgroup per (query tile, stripe))
+  // Σ V² needs the K-summed V: a split-K launch (few query tiles) stores per-chunk V tiles and a
+  // second kernel sums them in a fixed order (no atomics: deterministic).
+  const int chunk = var_chunk(g, M);
+  if (chunk > 0) {
+    int units = 0;
+    for (int nt = 0; nt < n_tiles; ++nt) units += (var_ksteps(nt, g.N) + chunk - 1) / chunk;
+    prof_mark(PROF_GPIS_STD, true, s);
+    hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * units)), dim3(ST_THREADS), 0, s,
+                       g, X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, chunk);
+    hipLaunchKernelGGL(gpis_var_splitk_finalize<KT>, dim3((unsigned)M), dim3(256), 0, s, g, partial, M_pad, chunk,
+                       vout, std_out, var_out);
+    prof_mark(PROF_GPIS_STD, false, s);
+    return;
+  }
   prof_mark(PROF_GPIS_STD, true, s);
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s,
                      g, X, M, partial, M_pad, Mt, n_tiles, vout, nullptr, nullptr, 0);

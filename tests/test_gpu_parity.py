@@ -126,6 +126,27 @@ def test_gpis_std_explicit_inverse_path(state):
     assert rel_err(gstd_e.cpu().numpy(), gstd_w.cpu().numpy()) < 1e-6
 
 
+@pytest.mark.parametrize("n_small", [1, 300, 2000])
+def test_gpis_std_split_k_matches_stripe_path(n_small):
+    """Few query tiles take the split-K whitened pass (per-chunk V tiles summed in a fixed order by
+    gpis_var_splitk_finalize); the same queries inside a large batch take one workgroup per
+    (query tile, stripe).  The two differ only in summation order; the ∇std pass reads the V
+    either one stores."""
+    from compliancedex_amd.gpis import gpis_std
+    g = _gpis("synthetic2000")
+    st = g.native_state()
+    rng = np.random.default_rng(21)
+    X1 = g.X1.cpu().numpy()
+    X = X1.min(0) - 0.02 + (np.ptp(X1, 0) + 0.04) * rng.random((8192, 3))  # 64 tiles × 8 stripes: stripe path
+    Xt = torch.from_numpy(X).to(DEV)
+    std_big, g_big = gpis_std(st, Xt)
+    std_small, g_small = gpis_std(st, Xt[:n_small].contiguous())  # ≤ 16 tiles × 8 stripes: split-K
+    torch.cuda.synchronize()
+    # cond(E11) = 1.1e7: k0 − ‖L⁻¹k‖² cancels ~7 digits, so reordered sums move std by ~1e-12
+    assert rel_err(std_small.cpu(), std_big[:n_small].cpu()) < 1e-10
+    assert rel_err(g_small.cpu(), g_big[:n_small].cpu()) < 1e-8
+
+
 @pytest.mark.parametrize("kernel", ["tps", "rbf", "joint"])
 def test_gpis_fit_vs_oracle(kernel):
     """cdx_gpis_fit (R, E11) and the factored state vs the oracle's fit + solve (gpis.py:33-59)."""
