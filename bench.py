@@ -27,8 +27,9 @@ FP64_MFMA_PEAK_TFLOPS = 78.6  # gfx950 vendor spec; MI355X_MICROAR
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    # the GPU clock ramps over the first ~10 closures (1.92 → 1.77 ms, tools/clock_ramp.py): warm past it
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--E", type=int, default=4096, help="candidates per GPU")
     ap.add_argument("--n-inducing", type=int, default=2000)
     ap.add_argument("--hand", default="allegro")

@@ -7,7 +7,7 @@ cd "$ROOT"
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
 TAG=${1:-r01}
-STEPS=${STEPS:-20}
+STEPS=${STEPS:-50}
 
 stop_if_fault() { if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "GPU step failed hard (rc=$1): stopping"; exit "$1"; fi; }
 
@@ -20,12 +20,12 @@ timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 rc=$?; echo "smoke rc=$rc"; tail -2 "$OUT/smoke_$TAG.log"; stop_if_fault $rc
 
 echo "== bench"; date
-timeout -k 10 300 python bench.py --steps "$STEPS" --warmup 3 > "$OUT/bench_$TAG.log" 2>&1
+timeout -k 10 300 python bench.py --steps "$STEPS" --warmup 20 > "$OUT/bench_$TAG.log" 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 "$OUT/bench_$TAG.log"; stop_if_fault $rc
 
 echo "== rocprofv3 kernel trace"; date
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/rocprof_$TAG.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- python3 "$ROOT/bench.py" --steps 30 --warmup 20 --no-cpu-baseline > "$OUT/rocprof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -2 "$OUT/rocprof_$TAG.log"
 find "$OUT/prof_$TAG" -name "*stats*" | head
 date

@@ -44,6 +44,21 @@ def main():
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
     for f in glob.glob(os.path.join(out, f"prof_{tag}", "**", "*kernel_stats.csv"), recursive=True):
         shutil.copyfile(f, os.path.join(REPO, "profiles", f"{tag}_kernel_stats.csv"))
+    # steady state: the last `timed` dispatches of each kernel in the trace (the stats CSV averages
+    # over the warm-up dispatches too, while the GPU clock is still ramping)
+    timed = int(os.environ.get("TIMED_STEPS", "30"))
+    for f in glob.glob(os.path.join(out, f"prof_{tag}", "**", "*kernel_trace.csv"), recursive=True):
+        per = defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            per[short(r["Kernel_Name"])].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        steady = {}
+        for k, v in per.items():
+            v.sort()
+            d = [(e - b) / 1e3 for b, e in v[-timed:]]
+            steady[k] = {"dispatches_total": len(v), "last_n": len(d), "avg_us": sum(d) / len(d),
+                         "min_us": min(d), "max_us": max(d)}
+        json.dump({"tag": tag, "what": f"rocprofv3 kernel trace, mean over the last {timed} dispatches per kernel",
+                   "kernels": steady}, open(os.path.join(REPO, "profiles", f"{tag}_kernel_steady.json"), "w"), indent=1)
     fetch = counters(os.path.join(out, f"pmc_FETCH_SIZE_{tag}"), "FETCH_SIZE")
     write = counters(os.path.join(out, f"pmc_WRITE_SIZE_{tag}"), "WRITE_SIZE")
     summary = {"tag": tag, "E": E, "n_inducing": N, "unit": "bytes per dispatch",
