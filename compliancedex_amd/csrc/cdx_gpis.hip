@@ -144,9 +144,16 @@ __device__ __host__ inline void stripe_k_range(int mode, int nt, int N, int& lo,
   hi = mode == MODE_GRADV ? N : min(N, nt * ST_BN + ST_BN);
 }
 
-// K-steps of stripe nt's range in the whitened pass (rows [0, min(N, (nt+1)·ST_BN))).
-__device__ __host__ inline int var_ksteps(int nt, int N) {
-  const int hi = min(N, (nt + 1) * ST_BN);
+// Column shift of the whitened pass: V column j of the pass is L⁻ᵀ column j − var_shift (columns
+// below the shift read as zero), i.e. the N_pad − N padding columns (rounded down to whole 16-column
+// blocks) sit in front of stripe 0, the lightest stripe (rows [0, 256 − shift)), instead of at the
+// end of the heaviest one (all N rows).  N = 2000: 48 columns, stripe pair costs 144 → 138 K-steps.
+// The stored V (vout) uses the shifted columns; the ∇std pass reads them back at k + var_shift.
+__device__ __host__ inline int var_shift(int N, int Np) { return (Np - N) / ST_BK * ST_BK; }
+
+// K-steps of stripe nt's range in the whitened pass (rows [0, min(N, (nt+1)·ST_BN − shift))).
+__device__ __host__ inline int var_ksteps(int nt, int N, int Np) {
+  const int hi = min(N, (nt + 1) * ST_BN - var_shift(N, Np));
   return (hi + ST_BK - 1) / ST_BK;
 }
 
@@ -188,6 +195,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   const int b = blockIdx.x;
   const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
   const int Np = g.N_pad;
+  const int vsh = MODE == MODE_GRAD ? 0 : var_shift(g.N, Np);  // VAR: B column shift; GRADV: V column shift
   const double* __restrict__ Bop = MODE == MODE_VAR ? g.Linv_t : (MODE == MODE_GRADV ? g.Linv : g.Ainv);
   // K* generation: thread → query row gm, GEN_PER k-columns starting at gk (wave-uniform)
   constexpr int GEN_PER = ST_BM * ST_BK / ST_THREADS;  // 4
@@ -228,18 +236,19 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   dbl2v av[4];
   double kv[GEN_PER];
   auto load_stage = [&](int kb) {  // B rows (and GRADV's V entries) of the stage at row kb
-    const dbl2v* src = reinterpret_cast<const dbl2v*>(Bop + (int64_t)(kb + ar) * Np + n0 + ac);
+    const dbl2v* src = reinterpret_cast<const dbl2v*>(Bop + (int64_t)(kb + ar) * Np + n0 + ac - (VAR ? vsh : 0));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #if defined(CDX_DIAG_NOBLOAD)  // timing-only diagnostic build: outputs are wrong
       av[i] = dbl2v{qx + kb, qy + i};
 #else
-      av[i] = src[i * (BSTR / 2)];
+      // VAR: the shifted-in columns of stripe 0 are zero (pieces are whole: the shift is a multiple of 16)
+      av[i] = (!VAR || n0 != 0 || ac + i * BSTR >= vsh) ? src[i * (BSTR / 2)] : dbl2v{0.0, 0.0};
 #endif
     }
     if (MODE == MODE_GRADV) {
 #pragma unroll
-      for (int i = 0; i < GEN_PER; ++i) kv[i] = vrow[kb + gk + i];
+      for (int i = 0; i < GEN_PER; ++i) kv[i] = vrow[kb + gk + i + vsh];
     }
   };
   auto gen = [&](const double* x1, int i) {  // K* entry (gm, gk + i) from the X1 rows at x1
@@ -306,7 +315,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     // lies past their diagonal (L⁻ᵀ, VAR) or before it (L⁻¹, GRADV): skip the MFMAs, keep the
     // staging and barriers.  acc + 0·A is acc, so results are bit-identical.
     const int kb = kbeg + s * ST_BK;
-    const bool skip_mfma = (MODE == MODE_VAR && kb >= n0 + wc + 64) || (MODE == MODE_GRADV && kb + ST_BK <= n0 + wc);
+    const bool skip_mfma = (MODE == MODE_VAR && kb >= n0 + wc + 64 - vsh) || (MODE == MODE_GRADV && kb + ST_BK <= n0 + wc);
     auto kstep = [&](auto do_mfma) {
 #pragma unroll
       for (int kk = 0; kk < ST_BK; kk += 4) {
@@ -500,12 +509,12 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     int blk = b / Mt;
     mt = b - blk * Mt;
     for (nt = 0;; ++nt) {
-      const int nch = (var_ksteps(nt, g.N) + parts - 1) / parts;
+      const int nch = (var_ksteps(nt, g.N, g.N_pad) + parts - 1) / parts;
       if (blk < nch) break;
       blk -= nch;
     }
     const int k0 = blk * parts * ST_BK;
-    tile(mt, nt, k0, min(min(g.N, nt * ST_BN + ST_BN), k0 + parts * ST_BK), blk);
+    tile(mt, nt, k0, min(min(g.N, nt * ST_BN + ST_BN - vsh), k0 + parts * ST_BK), blk);
     return;
   }
   if (TRI) {
@@ -532,7 +541,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     mt = t - nt * Mt;
   }
   // B rows ≥ N are zero: stop at the last live K-step; L⁻ᵀ (VAR) also stops at the tile's diagonal
-  tile(mt, nt, 0, VAR ? min(g.N, nt * ST_BN + ST_BN) : g.N, nt);
+  tile(mt, nt, 0, VAR ? min(g.N, nt * ST_BN + ST_BN - vsh) : g.N, nt);
 }
 
 
@@ -563,7 +572,7 @@ __global__ __launch_bounds__(256) void gpis_var_splitk_finalize(cdx_gpis g, cons
   const int Np = g.N_pad;
   double s = 0;
   for (int col = threadIdx.x; col < Np; col += 256) {
-    const int nch = (var_ksteps(col / ST_BN, g.N) + chunk - 1) / chunk;
+    const int nch = (var_ksteps(col / ST_BN, g.N, Np) + chunk - 1) / chunk;
     double v = 0;
     for (int c = 0; c < nch; ++c) v += vpart[((int64_t)c * M_pad + m) * Np + col];
     if (vout) vout[m * Np + col] = v;
@@ -629,12 +638,12 @@ static int var_chunk(const cdx_gpis& g, int64_t M) {
   if ((int64_t)Mt * Nt >= 256) return 0;
   auto units = [&](int c) {
     int u = 0;
-    for (int nt = 0; nt < Nt; ++nt) u += (var_ksteps(nt, g.N) + c - 1) / c;
+    for (int nt = 0; nt < Nt; ++nt) u += (var_ksteps(nt, g.N, g.N_pad) + c - 1) / c;
     return (int64_t)Mt * u;
   };
   int c = 64;
   while (c > 2 && units(c) < 256) c >>= 1;
-  const int64_t maxch = (var_ksteps(Nt - 1, g.N) + c - 1) / c;
+  const int64_t maxch = (var_ksteps(Nt - 1, g.N, g.N_pad) + c - 1) / c;
   if (maxch * round_up(M, ST_BM) * g.N_pad * (int64_t)sizeof(double) > ((int64_t)256 << 20)) return 0;
   return c;
 }
@@ -643,7 +652,7 @@ size_t gpis_var_ws_bytes(const cdx_gpis& g, int64_t M) {
   const int c = var_chunk(g, M);
   if (c > 0) {
     const int Nt = g.N_pad / ST_BN;
-    return (size_t)((var_ksteps(Nt - 1, g.N) + c - 1) / c) * (size_t)round_up(M, ST_BM) * g.N_pad * sizeof(double);
+    return (size_t)((var_ksteps(Nt - 1, g.N, g.N_pad) + c - 1) / c) * (size_t)round_up(M, ST_BM) * g.N_pad * sizeof(double);
   }
   return (size_t)(g.N_pad / ST_BN) * (size_t)round_up(M, ST_BM) * sizeof(double);
 }
@@ -672,7 +681,7 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
   const int chunk = var_chunk(g, M);
   if (chunk > 0) {
     int units = 0;
-    for (int nt = 0; nt < n_tiles; ++nt) units += (var_ksteps(nt, g.N) + chunk - 1) / chunk;
+    for (int nt = 0; nt < n_tiles; ++nt) units += (var_ksteps(nt, g.N, g.N_pad) + chunk - 1) / chunk;
     prof_mark(PROF_GPIS_STD, true, s);
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * units)), dim3(ST_THREADS), 0, s,
                        g, X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, chunk);
