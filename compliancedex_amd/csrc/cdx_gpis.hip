@@ -172,8 +172,8 @@ __device__ unsigned long long cdx_wgtime[16384][4];
 // VAR, GRAD: one workgroup per (query tile, stripe), partial slot = stripe.  GRADV: a query tile's
 // work is the concatenated K-step sequence of its stripes (Σ_nt gradv_ksteps(nt)); it is cut into
 // `parts` equal contiguous pieces, one workgroup each, and a piece runs one segment per stripe it
-// touches (epilogue per segment, partial slot p + nt: unique, < parts + Nt; the caller zeroes the
-// slots and the finalize kernel sums them in a fixed order — deterministic).  Equal pieces keep
+// touches (epilogue per segment, partial slot p + nt: unique, < parts + Nt; the finalize kernel
+// recomputes which slots were written and sums them in a fixed order — deterministic).  Equal pieces keep
 // every CU equally busy whatever the query count (the closure's 4096 ∇std queries: 32 tiles ×
 // 8 pieces = one workgroup of 69 K-steps per CU).
 template <int KT, int MODE>
@@ -303,7 +303,8 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   };
   frag(0, 0, fa[0], fb[0]);
   int cb = 0;  // buffer of step s: s % 3
-  for (int s = 0; s < nK; ++s) {
+  // The steps of one K-sweep; this wave's MFMA block range [JLO, JHI) per step (see kstep).
+  auto step = [&](int s, auto jlo_s, auto jhi_s) {
     const int nb = cb == ST_NBUF - 1 ? 0 : cb + 1, wb = nb == ST_NBUF - 1 ? 0 : nb + 1;
     load_stage(stage_row(s + 2));
     // X1 rows of stage s+3 (staged through LDS by the first 24 lanes: the generation then issues no
@@ -311,30 +312,29 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     dbl2v xl = dbl2v{0, 0};
     if (GEN && tid < ST_XS / 2) xl = reinterpret_cast<const dbl2v*>(g.X1 + 3 * stage_row(s + 3))[tid];
     const double* x1 = xs + (s & 1) * ST_XS + 3 * gk;
-    // This wave's B columns [n0 + wc, n0 + wc + 64) are all zero for the whole K-step when the step
-    // lies past their diagonal (L⁻ᵀ, VAR) or before it (L⁻¹, GRADV): skip the MFMAs, keep the
-    // staging and barriers.  acc + 0·A is acc, so results are bit-identical.
-    const int kb = kbeg + s * ST_BK;
-    const bool skip_mfma = (MODE == MODE_VAR && kb >= n0 + wc + 64 - vsh) || (MODE == MODE_GRADV && kb + ST_BK <= n0 + wc);
-    auto kstep = [&](auto do_mfma) {
+    // This wave's B columns (true columns [c0, c0 + 64)) are all zero for the whole K-step when the
+    // step lies past their diagonal (L⁻ᵀ, VAR) or before it (L⁻¹, GRADV): skip the MFMAs, keep the
+    // staging and barriers.  Inside the diagonal block (K-step t = 0..3 of it) the 16-column blocks
+    // j < t (VAR) or j > t (GRADV) are zero too: those variants issue only the live blocks' MFMAs
+    // (compile-time block ranges, no per-block predicate).  acc + 0·A is acc: bit-identical.
+    auto kstep = [&](auto jlo_c, auto jhi_c) {
+      constexpr int JLO = decltype(jlo_c)::value, JHI = decltype(jhi_c)::value;  // live blocks [JLO, JHI)
 #pragma unroll
       for (int kk = 0; kk < ST_BK; kk += 4) {
         const int cur = (kk >> 2) & 1;
         // next substep's fragments; the last substep reads step s+1's first ones
         if (kk + 4 < ST_BK) frag(cb, kk + 4, fa[cur ^ 1], fb[cur ^ 1]);
         else frag(nb, 0, fa[cur ^ 1], fb[cur ^ 1]);
-        if constexpr (decltype(do_mfma)::value) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+          for (int j = JLO; j < JHI; ++j) {
 #if defined(CDX_DIAG_NOMFMA)  // timing-only diagnostic build: outputs are wrong
-              acc[i][j][0] += fa[cur][i] * fb[cur][j];
+            acc[i][j][0] += fa[cur][i] * fb[cur][j];
 #else
-              acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
 #endif
-            }
-        }
+          }
         // stage s+2: K* entries over substeps 0–2 (2, 1, 1), written after substep 2's MFMAs
         if (GEN) {
           if (kk == 0) { gen(x1, 0); gen(x1, 1); }
@@ -343,10 +343,10 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
         }
         if (kk == 8) stage_write(wb);
 #if defined(CDX_STD_SCHED)
-        if constexpr (decltype(do_mfma)::value) {
+        if constexpr (JHI > JLO) {
           __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // next fragments first
 #pragma unroll
-          for (int q = 0; q < 16; ++q) {
+          for (int q = 0; q < 4 * (JHI - JLO); ++q) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // then up to four VALU
           }
@@ -354,11 +354,42 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
 #endif
       }
     };
-    if (skip_mfma) kstep(std::false_type{});
-    else kstep(std::true_type{});
+    kstep(jlo_s, jhi_s);
     if (GEN && tid < ST_XS / 2) reinterpret_cast<dbl2v*>(xs + ((s + 1) & 1) * ST_XS)[tid] = xl;
     cb = nb;
     __syncthreads();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  // K-step s sits at dt = s + d0 relative to this wave's 64-row diagonal block (true columns
+  // [c0, c0 + 64)); the diagonal variants run in their own straight-line calls, so each loop keeps
+  // one fragment schedule (a per-step dispatch inside one loop made the allocator spill).
+  const int c0 = n0 + wc - (VAR ? vsh : 0);
+  const int d0 = (kbeg - c0) >> 4;  // kbeg − c0 is a multiple of 16; wave-uniform
+  int s = 0;
+  if constexpr (MODE == MODE_VAR) {
+    for (const int e = min(nK, max(0, 1 - d0)); s < e; ++s) step(s, I0{}, I4{});
+#if !defined(CDX_STD_NODIAG)
+    if (s < nK && s + d0 == 1) step(s++, I1{}, I4{});
+    if (s < nK && s + d0 == 2) step(s++, I2{}, I4{});
+    if (s < nK && s + d0 == 3) step(s++, I3{}, I4{});
+#else
+    for (const int e = min(nK, max(0, 4 - d0)); s < e; ++s) step(s, I0{}, I4{});
+#endif
+    for (; s < nK; ++s) step(s, I0{}, I0{});
+  } else if constexpr (MODE == MODE_GRADV) {
+    for (const int e = min(nK, max(0, -d0)); s < e; ++s) step(s, I0{}, I0{});
+#if !defined(CDX_STD_NODIAG)
+    if (s < nK && s + d0 == 0) step(s++, I0{}, I1{});
+    if (s < nK && s + d0 == 1) step(s++, I0{}, I2{});
+    if (s < nK && s + d0 == 2) step(s++, I0{}, I3{});
+#endif
+    for (; s < nK; ++s) step(s, I0{}, I4{});
+  } else {
+    for (; s < nK; ++s) step(s, I0{}, I4{});
   }
 
   if constexpr (VAR) {
@@ -592,16 +623,32 @@ __global__ __launch_bounds__(256) void gpis_var_splitk_finalize(cdx_gpis g, cons
 }
 
 // ∇std = −sign(v)·(Σ_n W kd (x − x_n))/sqrt|v| at query m, written to row sel[m] (identity when
-// sel is null) with v = var[sel[m]] from the whitened pass.
+// sel is null) with v = var[sel[m]] from the whitened pass.  GRADV launches (parts > 0) sum only the
+// slots p + nt their pieces wrote, in increasing slot order (no memset of the others).
 __global__ __launch_bounds__(256) void gpis_grad_finalize(const double* __restrict__ partial, int64_t M,
                                                           int64_t M_pad, int n_tiles, const int64_t* __restrict__ sel,
-                                                          const double* __restrict__ var, double* __restrict__ gstd) {
+                                                          const double* __restrict__ var, double* __restrict__ gstd,
+                                                          int parts, int Nt, int N) {
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
   double g0 = 0, g1 = 0, g2 = 0;
-  for (int t = 0; t < n_tiles; ++t) {
+  auto add = [&](int t) {
     const double* p = partial + ((int64_t)t * M_pad + m) * 4;
     g0 += p[1]; g1 += p[2]; g2 += p[3];
+  };
+  if (parts > 0) {
+    int W = 0;
+    for (int nt = 0; nt < Nt; ++nt) W += gradv_ksteps(nt, N);
+    for (int p = 0; p < parts; ++p) {  // the segments gpis_std_kernel<MODE_GRADV> runs for piece p
+      const int q0 = (int)((int64_t)W * p / parts), q1 = (int)((int64_t)W * (p + 1) / parts);
+      for (int nt = 0, s0 = 0; nt < Nt; ++nt) {
+        const int s1 = s0 + gradv_ksteps(nt, N);
+        if (max(q0, s0) < min(q1, s1)) add(p + nt);
+        s0 = s1;
+      }
+    }
+  } else {
+    for (int t = 0; t < n_tiles; ++t) add(t);
   }
   const int64_t o = sel ? sel[m] : m;
   const double v = var[o];
@@ -703,11 +750,11 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
                            double* gstd, double* partial, int64_t M_pad, int Mt, int n_tiles, const double* vin,
                            hipStream_t s) {
   prof_mark(PROF_GPIS_GRAD, true, s);
-  int n_slots = n_tiles;
+  int n_slots = n_tiles, gparts = 0;
   if (vin) {
     const int parts = gradv_parts(g, Mt);
-    n_slots = parts + n_tiles;  // slot p + nt per (piece, stripe) segment; unused slots stay zero
-    (void)hipMemsetAsync(partial, 0, (size_t)n_slots * M_pad * 4 * sizeof(double), s);
+    n_slots = parts + n_tiles;  // slot p + nt per (piece, stripe) segment; the finalize reads only those
+    gparts = parts;
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV>), dim3((unsigned)(Mt * parts)), dim3(ST_THREADS), 0,
                        s, g, X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel, parts);
   } else {
@@ -716,7 +763,7 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
   }
   prof_mark(PROF_GPIS_GRAD, false, s);
   hipLaunchKernelGGL(gpis_grad_finalize, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, partial, M, M_pad,
-                     n_slots, sel, var, gstd);
+                     n_slots, sel, var, gstd, gparts, n_tiles, g.N);
 }
 
 size_t gpis_v_bytes(const cdx_gpis& g, int64_t M) {

@@ -76,6 +76,21 @@ def test_gpis_large_inducing_set():
     assert rel_err(Xt.grad.cpu().numpy()[idx], r["gstd"]) < 1e-6
 
 
+@pytest.mark.parametrize("n", [1800, 2000, 2047])
+def test_gpis_whitened_column_shift_stripe_path(n):
+    """≥ 4096 queries: one workgroup per (query tile, stripe), not split-K, with the whitened pass's
+    padding columns shifted in front of stripe 0 (N_pad − N = 248 → 240, 48, 1 → 0)."""
+    g, ref, X1 = _random_gpis(n, seed=20 + n)
+    X = 0.08 * np.random.default_rng(21).standard_normal((4200, 3))
+    idx = np.random.default_rng(22).choice(4200, 50, replace=False)
+    Xt = torch.from_numpy(X).to(DEV).requires_grad_(True)
+    mean, std = g.pred(Xt)
+    std.sum().backward()
+    r = oracle_gpis_at(ref, X[idx], with_std=True)
+    assert rel_err(std.detach().cpu().numpy()[idx], r["std"]) < 1e-7
+    assert rel_err(Xt.grad.cpu().numpy()[idx], r["gstd"]) < 1e-6
+
+
 def test_gpis_queries_on_and_far_from_training_points():
     g, ref, X1 = _random_gpis(500, seed=5)
     X = np.vstack([X1[:50], X1[50:100] + 1e-9, 5.0 * np.ones((3, 3)), -5.0 * np.ones((3, 3))])
