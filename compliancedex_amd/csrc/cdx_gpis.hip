@@ -137,6 +137,18 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 // (A v_mfma_f64_4x4x4_4b_f64 variant ran no faster — LDS-read-bound, profiles/r01_std_gemm_variants.md.)
 enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2 };
 
+// Whitened pass A operand: K* generated on chip per stripe (default), or read from a buffer
+// gpis_kstar_kernel wrote (CDX_VAR_KLOAD).  On chip, each K* entry is regenerated by every stripe
+// that needs its row (Σ_nt K-steps = 4.4× the unique ones at N = 2000) and its ≈ 16 f64 VALU ops
+// share the DP pipe with the f64 MFMA.  Measured (profiles/r01zi_var_kload_ab.jsonl): the buffer
+// makes the std kernel 3 % faster (1.185 → 1.152 ms) but the closure 3 % slower (2.35 → 2.27 M
+// evals/s): the 268 MB K* write plus its re-reads slow the K* kernel, mean and ∇std passes more.
+#if defined(CDX_VAR_KLOAD)
+constexpr bool VAR_KLOAD = true;
+#else
+constexpr bool VAR_KLOAD = false;
+#endif
+
 
 // K-range [lo, hi) of stripe nt in the triangular modes.
 __device__ __host__ inline void stripe_k_range(int mode, int nt, int N, int& lo, int& hi) {
@@ -184,7 +196,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
                                                                 const int64_t* __restrict__ vsel, int parts) {
   constexpr bool VAR = MODE == MODE_VAR;
   constexpr bool TRI = MODE != MODE_GRAD;
-  constexpr bool GEN = MODE != MODE_GRADV;  // A tile generated on chip (else loaded from vin)
+  constexpr bool GEN = MODE == MODE_GRAD || (VAR && !VAR_KLOAD);  // A tile generated on chip (else loaded from vin)
   __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
   double* xq = smem + ST_NBUF * (ST_TILE + ST_BTILE);
   double* xs = xq + ST_BM * 3;  // [2][ST_XS]: X1 rows of the stage generated next
@@ -225,7 +237,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     const int64_t m = min(m0 + gm, M - 1);  // pad rows replicate a valid query
     qx = X[3 * m]; qy = X[3 * m + 1]; qz = X[3 * m + 2];
     if (tid < ST_BM) { xq[3 * tid] = qx; xq[3 * tid + 1] = qy; xq[3 * tid + 2] = qz; }
-    if (MODE == MODE_GRADV) vrow = vin + (vsel ? vsel[m] : m) * (int64_t)Np;
+    if (!GEN) vrow = vin + (vsel ? vsel[m] : m) * (int64_t)Np;
   }
   // B rows ≥ N are zero: stop at the last live K-step; L⁻ᵀ (VAR) also stops at the tile's
   // diagonal, L⁻¹ (GRADV) starts there
@@ -246,9 +258,9 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
       av[i] = (!VAR || n0 != 0 || ac + i * BSTR >= vsh) ? src[i * (BSTR / 2)] : dbl2v{0.0, 0.0};
 #endif
     }
-    if (MODE == MODE_GRADV) {
+    if (!GEN) {  // GRADV: V at shifted columns; VAR: K* rows
 #pragma unroll
-      for (int i = 0; i < GEN_PER; ++i) kv[i] = vrow[kb + gk + i + vsh];
+      for (int i = 0; i < GEN_PER; ++i) kv[i] = vrow[kb + gk + i + (VAR ? 0 : vsh)];
     }
   };
   auto gen = [&](const double* x1, int i) {  // K* entry (gm, gk + i) from the X1 rows at x1
@@ -577,6 +589,36 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
 
 
 
+// K*[m][j] = k(x_m, x_j) for j < N, 0 for N ≤ j < N_pad: the whitened pass's A operand
+// ([M][N_pad], row-major).  Each 256-thread block covers KS_ROWS query rows: a thread keeps one
+// inducing point per column step and writes KS_ROWS rows (coalesced along j); X1 is read once
+// per block.  Write-bound: 8·N_pad bytes per query.
+constexpr int KS_ROWS = 16;
+template <int KT>
+__global__ __launch_bounds__(256) void gpis_kstar_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
+                                                         double* __restrict__ out) {
+  __shared__ double xq[3 * KS_ROWS];
+  const int64_t m0 = (int64_t)blockIdx.x * KS_ROWS;
+  const int Np = g.N_pad, N = g.N;
+  if (threadIdx.x < 3 * KS_ROWS) {
+    const int64_t m = min(m0 + threadIdx.x / 3, M - 1);
+    xq[threadIdx.x] = X[3 * m + threadIdx.x % 3];
+  }
+  __syncthreads();
+  const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
+  const int nr = (int)min((int64_t)KS_ROWS, M - m0);
+  for (int j = threadIdx.x; j < Np; j += 256) {
+    const bool live = j < N;
+    const double px = live ? g.X1[3 * j] : 0.0, py = live ? g.X1[3 * j + 1] : 0.0, pz = live ? g.X1[3 * j + 2] : 0.0;
+    for (int r = 0; r < nr; ++r) {
+      const double dx = xq[3 * r] - px, dy = xq[3 * r + 1] - py, dz = xq[3 * r + 2] - pz;
+      double k, kd;
+      gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, k, kd);
+      out[(m0 + r) * Np + j] = live ? k : 0.0;
+    }
+  }
+}
+
 // std = sqrt|k0 − Σ_t V²-partials|; var_out keeps the signed k0 − ‖L⁻¹k‖² for the ∇std scale.
 template <int KT>
 __global__ __launch_bounds__(256) void gpis_var_finalize(cdx_gpis g, const double* __restrict__ partial, int64_t M,
@@ -695,13 +737,21 @@ static int var_chunk(const cdx_gpis& g, int64_t M) {
   return c;
 }
 
-size_t gpis_var_ws_bytes(const cdx_gpis& g, int64_t M) {
+// Chunk/stripe partials, then (VAR_KLOAD) the K* buffer at a 256-byte aligned offset.
+static size_t var_partial_bytes(const cdx_gpis& g, int64_t M) {
   const int c = var_chunk(g, M);
+  size_t b;
   if (c > 0) {
     const int Nt = g.N_pad / ST_BN;
-    return (size_t)((var_ksteps(Nt - 1, g.N, g.N_pad) + c - 1) / c) * (size_t)round_up(M, ST_BM) * g.N_pad * sizeof(double);
+    b = (size_t)((var_ksteps(Nt - 1, g.N, g.N_pad) + c - 1) / c) * (size_t)round_up(M, ST_BM) * g.N_pad * sizeof(double);
+  } else {
+    b = (size_t)(g.N_pad / ST_BN) * (size_t)round_up(M, ST_BM) * sizeof(double);
   }
-  return (size_t)(g.N_pad / ST_BN) * (size_t)round_up(M, ST_BM) * sizeof(double);
+  return (b + 255) / 256 * 256;
+}
+
+size_t gpis_var_ws_bytes(const cdx_gpis& g, int64_t M) {
+  return var_partial_bytes(g, M) + (VAR_KLOAD ? (size_t)M * g.N_pad * sizeof(double) : 0);
 }
 
 // Pieces per query tile of the ∇std pass: one round of workgroups over the 256 CUs when the query
@@ -726,12 +776,18 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
   // Σ V² needs the K-summed V: a split-K launch (few query tiles) stores per-chunk V tiles and a
   // second kernel sums them in a fixed order (no atomics: deterministic).
   const int chunk = var_chunk(g, M);
+  double* kstar = nullptr;
+  if (VAR_KLOAD) {
+    kstar = reinterpret_cast<double*>(reinterpret_cast<char*>(partial) + var_partial_bytes(g, M));
+    hipLaunchKernelGGL(gpis_kstar_kernel<KT>, dim3((unsigned)((M + KS_ROWS - 1) / KS_ROWS)), dim3(256), 0, s, g, X, M,
+                       kstar);
+  }
   if (chunk > 0) {
     int units = 0;
     for (int nt = 0; nt < n_tiles; ++nt) units += (var_ksteps(nt, g.N, g.N_pad) + chunk - 1) / chunk;
     prof_mark(PROF_GPIS_STD, true, s);
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * units)), dim3(ST_THREADS), 0, s,
-                       g, X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, chunk);
+                       g, X, M, partial, M_pad, Mt, n_tiles, nullptr, kstar, nullptr, chunk);
     hipLaunchKernelGGL(gpis_var_splitk_finalize<KT>, dim3((unsigned)M), dim3(256), 0, s, g, partial, M_pad, chunk,
                        vout, std_out, var_out);
     prof_mark(PROF_GPIS_STD, false, s);
@@ -739,7 +795,7 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
   }
   prof_mark(PROF_GPIS_STD, true, s);
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s,
-                     g, X, M, partial, M_pad, Mt, n_tiles, vout, nullptr, nullptr, 0);
+                     g, X, M, partial, M_pad, Mt, n_tiles, vout, kstar, nullptr, 0);
   prof_mark(PROF_GPIS_STD, false, s);
   hipLaunchKernelGGL(gpis_var_finalize<KT>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, g, partial, M, M_pad,
                      n_tiles, std_out, var_out);
