@@ -664,33 +664,26 @@ __global__ __launch_bounds__(256) void gpis_var_splitk_finalize(cdx_gpis g, cons
   }
 }
 
+// Partial slots a ∇std launch wrote, in increasing order (host-computed, passed by value).
+constexpr int GRAD_MAX_SLOTS = 512;
+struct GradSlots {
+  int n;
+  unsigned short t[GRAD_MAX_SLOTS];
+};
+
 // ∇std = −sign(v)·(Σ_n W kd (x − x_n))/sqrt|v| at query m, written to row sel[m] (identity when
-// sel is null) with v = var[sel[m]] from the whitened pass.  GRADV launches (parts > 0) sum only the
-// slots p + nt their pieces wrote, in increasing slot order (no memset of the others).
+// sel is null) with v = var[sel[m]] from the whitened pass.  Sums the listed slots in order: all
+// stripes (GRAD), or only the slots p + nt the GRADV pieces wrote (no memset of the others).
 __global__ __launch_bounds__(256) void gpis_grad_finalize(const double* __restrict__ partial, int64_t M,
-                                                          int64_t M_pad, int n_tiles, const int64_t* __restrict__ sel,
-                                                          const double* __restrict__ var, double* __restrict__ gstd,
-                                                          int parts, int Nt, int N) {
+                                                          int64_t M_pad, const GradSlots slots,
+                                                          const int64_t* __restrict__ sel,
+                                                          const double* __restrict__ var, double* __restrict__ gstd) {
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
   double g0 = 0, g1 = 0, g2 = 0;
-  auto add = [&](int t) {
-    const double* p = partial + ((int64_t)t * M_pad + m) * 4;
+  for (int i = 0; i < slots.n; ++i) {
+    const double* p = partial + ((int64_t)slots.t[i] * M_pad + m) * 4;
     g0 += p[1]; g1 += p[2]; g2 += p[3];
-  };
-  if (parts > 0) {
-    int W = 0;
-    for (int nt = 0; nt < Nt; ++nt) W += gradv_ksteps(nt, N);
-    for (int p = 0; p < parts; ++p) {  // the segments gpis_std_kernel<MODE_GRADV> runs for piece p
-      const int q0 = (int)((int64_t)W * p / parts), q1 = (int)((int64_t)W * (p + 1) / parts);
-      for (int nt = 0, s0 = 0; nt < Nt; ++nt) {
-        const int s1 = s0 + gradv_ksteps(nt, N);
-        if (max(q0, s0) < min(q1, s1)) add(p + nt);
-        s0 = s1;
-      }
-    }
-  } else {
-    for (int t = 0; t < n_tiles; ++t) add(t);
   }
   const int64_t o = sel ? sel[m] : m;
   const double v = var[o];
@@ -806,20 +799,31 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
                            double* gstd, double* partial, int64_t M_pad, int Mt, int n_tiles, const double* vin,
                            hipStream_t s) {
   prof_mark(PROF_GPIS_GRAD, true, s);
-  int n_slots = n_tiles, gparts = 0;
+  GradSlots slots;
+  slots.n = 0;
   if (vin) {
     const int parts = gradv_parts(g, Mt);
-    n_slots = parts + n_tiles;  // slot p + nt per (piece, stripe) segment; the finalize reads only those
-    gparts = parts;
+    // slot p + nt per (piece, stripe) segment the kernel runs (same cut as gpis_std_kernel<GRADV>)
+    int W = 0;
+    for (int nt = 0; nt < n_tiles; ++nt) W += gradv_ksteps(nt, g.N);
+    for (int p = 0; p < parts; ++p) {
+      const int q0 = (int)((int64_t)W * p / parts), q1 = (int)((int64_t)W * (p + 1) / parts);
+      for (int nt = 0, s0 = 0; nt < n_tiles; ++nt) {
+        const int s1 = s0 + gradv_ksteps(nt, g.N);
+        if (std::max(q0, s0) < std::min(q1, s1) && slots.n < GRAD_MAX_SLOTS) slots.t[slots.n++] = (unsigned short)(p + nt);
+        s0 = s1;
+      }
+    }
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV>), dim3((unsigned)(Mt * parts)), dim3(ST_THREADS), 0,
                        s, g, X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel, parts);
   } else {
+    for (int nt = 0; nt < n_tiles && nt < GRAD_MAX_SLOTS; ++nt) slots.t[slots.n++] = (unsigned short)nt;
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRAD>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g,
                        X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, 0);
   }
   prof_mark(PROF_GPIS_GRAD, false, s);
   hipLaunchKernelGGL(gpis_grad_finalize, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, partial, M, M_pad,
-                     n_slots, sel, var, gstd, gparts, n_tiles, g.N);
+                     slots, sel, var, gstd);
 }
 
 size_t gpis_v_bytes(const cdx_gpis& g, int64_t M) {
@@ -849,6 +853,7 @@ int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_
   const int64_t M_pad = round_up(M, ST_BM);
   const int n_tiles = g.N_pad / ST_BN;
   if (M_pad / ST_BM * (int64_t)(256 + n_tiles) > 0x7fffffff) return CDX_EINVAL;
+  if (256 + n_tiles > GRAD_MAX_SLOTS) return CDX_EINVAL;  // finalize slot list (N_pad ≤ 65 536)
   const int Mt = (int)(M_pad / ST_BM);
   double* partial = static_cast<double*>(ws);
   switch (g.kernel) {
