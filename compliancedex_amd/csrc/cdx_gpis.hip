@@ -161,7 +161,8 @@ __device__ __host__ inline void stripe_k_range(int mode, int nt, int N, int& lo,
 // blocks) sit in front of stripe 0, the lightest stripe (rows [0, 256 − shift)), instead of at the
 // end of the heaviest one (all N rows).  N = 2000: 48 columns, stripe pair costs 144 → 138 K-steps.
 // The stored V (vout) uses the shifted columns; the ∇std pass reads them back at k + var_shift.
-__device__ __host__ inline int var_shift(int N, int Np) { return (Np - N) / ST_BK * ST_BK; }
+// Capped below one stripe so stripe 0 keeps ≥ 1 live K-step when a caller pads N_pad by ≥ 256.
+__device__ __host__ inline int var_shift(int N, int Np) { return min((Np - N) / ST_BK * ST_BK, ST_BN - ST_BK); }
 
 // K-steps of stripe nt's range in the whitened pass (rows [0, min(N, (nt+1)·ST_BN − shift))).
 __device__ __host__ inline int var_ksteps(int nt, int N, int Np) {

@@ -91,6 +91,24 @@ def test_gpis_whitened_column_shift_stripe_path(n):
     assert rel_err(Xt.grad.cpu().numpy()[idx], r["gstd"]) < 1e-6
 
 
+@pytest.mark.parametrize("m", [300, 16500])
+def test_gpis_oversized_padding(monkeypatch, m):
+    """A C-ABI state padded by ≥ 256 (N = 200, N_pad = 512): the whitened pass's column shift is
+    capped below one stripe; split-K (300 queries) and stripe (16 500 queries) paths."""
+    from compliancedex_amd import _native as N
+    monkeypatch.setattr(N, "NPAD_ALIGN", 512)
+    g, ref, X1 = _random_gpis(200, seed=31)
+    assert g.native_state().desc.N_pad == 512
+    X = 0.08 * np.random.default_rng(32).standard_normal((m, 3))
+    idx = np.random.default_rng(33).choice(m, 50, replace=False)
+    Xt = torch.from_numpy(X).to(DEV).requires_grad_(True)
+    mean, std = g.pred(Xt)
+    std.sum().backward()
+    r = oracle_gpis_at(ref, X[idx], with_std=True)
+    assert rel_err(std.detach().cpu().numpy()[idx], r["std"]) < 1e-7
+    assert rel_err(Xt.grad.cpu().numpy()[idx], r["gstd"]) < 1e-6
+
+
 def test_gpis_queries_on_and_far_from_training_points():
     g, ref, X1 = _random_gpis(500, seed=5)
     X = np.vstack([X1[:50], X1[50:100] + 1e-9, 5.0 * np.ones((3, 3)), -5.0 * np.ones((3, 3))])
