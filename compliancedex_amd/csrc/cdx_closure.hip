@@ -636,7 +636,7 @@ namespace cdx {
 namespace {
 constexpr int PROF_POOL = 4096;
 struct Prof {
-  bool on = false;
+  unsigned mask = 0;  // stages recorded
   hipEvent_t ev[PROF_STAGES][PROF_POOL][2];
   int n[PROF_STAGES] = {};
   bool created = false;
@@ -644,7 +644,7 @@ struct Prof {
 }  // namespace
 
 void prof_mark(int stage, bool begin, hipStream_t s) {
-  if (!g_prof.on) return;
+  if (!((g_prof.mask >> stage) & 1u)) return;
   const int i = g_prof.n[stage];
   if (i >= PROF_POOL) return;
   (void)hipEventRecord(g_prof.ev[stage][i][begin ? 0 : 1], s);
@@ -652,8 +652,9 @@ void prof_mark(int stage, bool begin, hipStream_t s) {
 }
 }  // namespace cdx
 
-extern "C" int cdx_profile_enable(int on) {
+extern "C" int cdx_profile_enable(int stages) {
   using cdx::g_prof;
+  const unsigned on = (unsigned)stages & ((1u << cdx::PROF_STAGES) - 1);
   if (on && !g_prof.created) {
     for (int st = 0; st < cdx::PROF_STAGES; ++st)
       for (int i = 0; i < cdx::PROF_POOL; ++i)
@@ -661,7 +662,7 @@ extern "C" int cdx_profile_enable(int on) {
           if (hipEventCreate(&g_prof.ev[st][i][j]) != hipSuccess) return CDX_ELAUNCH;
     g_prof.created = true;
   }
-  g_prof.on = on != 0;
+  g_prof.mask = on;
   for (int st = 0; st < cdx::PROF_STAGES; ++st) g_prof.n[st] = 0;
   return CDX_OK;
 }

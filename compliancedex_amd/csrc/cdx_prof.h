@@ -1,6 +1,6 @@
 // Optional per-stage HIP-event timing of the closure pipeline (bench.py reads it through
 // cdx_profile_enable / cdx_profile_read).  Events are recorded on the launch stream
-// around each kernel, so they time exactly what runs; disabled by default.
+// around each kernel of the enabled stages, so they time exactly what runs; disabled by default.
 #pragma once
 #include <hip/hip_runtime.h>
 
