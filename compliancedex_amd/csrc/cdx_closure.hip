@@ -659,7 +659,9 @@ extern "C" int cdx_profile_enable(int stages) {
     for (int st = 0; st < cdx::PROF_STAGES; ++st)
       for (int i = 0; i < cdx::PROF_POOL; ++i)
         for (int j = 0; j < 2; ++j)
-          if (hipEventCreate(&g_prof.ev[st][i][j]) != hipSuccess) return CDX_ELAUNCH;
+          // timing-only events: no system-scope fence (L2 writeback) at each record
+          if (hipEventCreateWithFlags(&g_prof.ev[st][i][j], hipEventDisableSystemFence) != hipSuccess)
+            return CDX_ELAUNCH;
     g_prof.created = true;
   }
   g_prof.mask = on;
