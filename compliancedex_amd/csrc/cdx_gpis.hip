@@ -185,8 +185,8 @@ __device__ unsigned long long cdx_wgtime[16384][4];
 // VAR, GRAD: one workgroup per (query tile, stripe), partial slot = stripe.  GRADV: a query tile's
 // work is the concatenated K-step sequence of its stripes (Σ_nt gradv_ksteps(nt)); it is cut into
 // `parts` equal contiguous pieces, one workgroup each, and a piece runs one segment per stripe it
-// touches (epilogue per segment, partial slot p + nt: unique, < parts + Nt; the finalize kernel
-// recomputes which slots were written and sums them in a fixed order — deterministic).  Equal pieces keep
+// touches (epilogue per segment, partial slot p + nt: unique, < parts + Nt; the launch lists the
+// written slots on the host and the finalize kernel sums them in that fixed order — deterministic).  Equal pieces keep
 // every CU equally busy whatever the query count (the closure's 4096 ∇std queries: 32 tiles ×
 // 8 pieces = one workgroup of 69 K-steps per CU).
 template <int KT, int MODE>
