@@ -7,7 +7,7 @@
 //                               targets once, pregrasp tips, palm)      — :657-669, :743-750
 //   2. gpis_mean (cdx_gpis.hip) mean/∇mean/normal at all queries      — gpis.py:43-87
 //   3. gpis std  (cdx_gpis.hip) std at the all-tip queries (whitened, triangular fp64 MFMA,
-//      V = L⁻¹k kept), closure_std_select_kernel (the variance cost's argmax fingertip),
+//      V = L⁻¹k kept; the finalize also selects the variance cost's argmax fingertip),
 //      ∇std at those queries only: E11⁻¹k = L⁻ᵀv from the kept V (triangular fp64 MFMA)
 //   4. closure_cost_kernel      one thread per candidate: seven cost terms per level,
 //                               Kabsch + SVD backward, FK backward; writes loss, margin
@@ -413,26 +413,8 @@ struct ClosureWs {
 };
 
 // The variance cost takes max_f log(100·std_f) (:730), so ∇std is only ever needed at one
-// fingertip per (distinct level, candidate): pick it exactly as level_fwd_bwd does (first
-// maximum of log(100·s)) and gather its query for the ∇std GEMM.
-__global__ __launch_bounds__(256) void closure_std_select_kernel(int64_t E, int T, int Lq,
-                                                                 const double* __restrict__ std_,
-                                                                 const double* __restrict__ X,
-                                                                 int64_t* __restrict__ sel, double* __restrict__ Xg) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)Lq * E) return;
-  const int u = (int)(t / E);
-  const int64_t e = t - (int64_t)u * E;
-  int fmax = 0;
-  double lmax = log(100 * std_[cdx::q_alltip(u, e, 0, E, T)]);
-  for (int f = 1; f < T; ++f) {
-    const double lv = log(100 * std_[cdx::q_alltip(u, e, f, E, T)]);
-    if (lv > lmax) { lmax = lv; fmax = f; }
-  }
-  const int64_t qi = cdx::q_alltip(u, e, fmax, E, T);
-  sel[t] = qi;
-  for (int i = 0; i < 3; ++i) Xg[3 * t + i] = X[3 * qi + i];
-}
+// fingertip per (distinct level, candidate): the std finalize picks it exactly as level_fwd_bwd
+// does (first maximum of log(100·s), cdx::VarSelect) and gathers its query for the ∇std GEMM.
 
 ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   ClosureWs w;
@@ -580,11 +562,12 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   int rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
   if (rc) return rc;
   // whitened std at every all-tip query, keeping V = (L⁻¹K*ᵀ)ᵀ for the ∇std pass
-  rc = cdx::gpis_var_launch(p->gpis, w.X, Ms, w.std_, w.var, w.var_ws, s, w.V);
+  // … and the ∇std fingertip of each (distinct level, candidate): the all-tip rows q_alltip(u, e, f)
+  // = (u·E + e)·T + f form groups of T, selected in the std finalize
+  const cdx::VarSelect vs{p->chain.n_tips, w.sel, w.Xg};
+  rc = cdx::gpis_var_launch(p->gpis, w.X, Ms, w.std_, w.var, w.var_ws, s, w.V, &vs);
   if (rc) return rc;
   const int64_t Mg = (int64_t)p->n_query_levels * E;
-  hipLaunchKernelGGL(closure_std_select_kernel, dim3((unsigned)((Mg + 255) / 256)), dim3(256), 0, s, E,
-                     p->chain.n_tips, p->n_query_levels, (const double*)w.std_, (const double*)w.X, w.sel, w.Xg);
   rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V);
   if (rc) return rc;
   GpisView gv;

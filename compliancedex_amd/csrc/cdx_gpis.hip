@@ -634,6 +634,60 @@ __global__ __launch_bounds__(256) void gpis_var_finalize(cdx_gpis g, const doubl
   if (var_out) var_out[m] = v;
 }
 
+// argmax over the T rows of group t of log(100·std) (first maximum), as level_fwd_bwd picks it.
+__device__ inline void group_select(int64_t t, int T, const double* __restrict__ std_, const double* __restrict__ X,
+                                    int64_t* __restrict__ sel, double* __restrict__ Xg) {
+  int fmax = 0;
+  double lmax = log(100 * std_[t * T]);
+  for (int f = 1; f < T; ++f) {
+    const double lv = log(100 * std_[t * T + f]);
+    if (lv > lmax) { lmax = lv; fmax = f; }
+  }
+  const int64_t qi = t * T + fmax;
+  sel[t] = qi;
+  for (int i = 0; i < 3; ++i) Xg[3 * t + i] = X[3 * qi + i];
+}
+
+// gpis_var_finalize (one thread per row), then each group's selection by its first row's thread
+// from the block's LDS copy of log(100·std) (T divides the 256-row block: groups never straddle).
+template <int KT>
+__global__ __launch_bounds__(256) void gpis_var_finalize_select(cdx_gpis g, const double* __restrict__ partial,
+                                                                int64_t M, int T, int64_t M_pad, int n_tiles,
+                                                                double* __restrict__ std_out,
+                                                                double* __restrict__ var_out,
+                                                                const double* __restrict__ X,
+                                                                int64_t* __restrict__ sel, double* __restrict__ Xg) {
+  __shared__ double lg[256];
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < M) {
+    double s = 0;
+    for (int t = 0; t < n_tiles; ++t) s += partial[(int64_t)t * M_pad + m];
+    const double v = gpis_k0<KT>(g.R) - s;
+    const double sd = sqrt(fabs(v));
+    std_out[m] = sd;
+    if (var_out) var_out[m] = v;
+    lg[threadIdx.x] = log(100 * sd);
+  }
+  __syncthreads();
+  if (m >= M || m % T != 0) return;
+  int fmax = 0;
+  double lmax = lg[threadIdx.x];
+  for (int f = 1; f < T; ++f) {
+    const double lv = lg[threadIdx.x + f];
+    if (lv > lmax) { lmax = lv; fmax = f; }
+  }
+  const int64_t t = m / T, qi = m + fmax;
+  sel[t] = qi;
+  for (int i = 0; i < 3; ++i) Xg[3 * t + i] = X[3 * qi + i];
+}
+
+__global__ __launch_bounds__(256) void gpis_select_kernel(int64_t G, int T, const double* __restrict__ std_,
+                                                          const double* __restrict__ X, int64_t* __restrict__ sel,
+                                                          double* __restrict__ Xg) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < G) group_select(t, T, std_, X, sel, Xg);
+}
+
 // Split-K whitened pass: V[m, col] = Σ_c chunk partials (fixed order), stored to vout when asked,
 // std = sqrt|k0 − Σ_col V²| — one 256-thread block per query row, tree-reduced (deterministic).
 template <int KT>
@@ -766,7 +820,9 @@ size_t gpis_grad_ws_bytes(const cdx_gpis& g, int64_t M) {
 
 template <int KT>
 static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double* std_out, double* var_out,
-                          double* partial, int64_t M_pad, int Mt, int n_tiles, double* vout, hipStream_t s) {
+                          double* partial, int64_t M_pad, int Mt, int n_tiles, double* vout, hipStream_t s,
+                          const VarSelect* vs) {
+  const int64_t G = vs ? M / vs->T : 0;
   // Σ V² needs the K-summed V: a split-K launch (few query tiles) stores per-chunk V tiles and a
   // second kernel sums them in a fixed order (no atomics: deterministic).
   const int chunk = var_chunk(g, M);
@@ -785,14 +841,25 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
     hipLaunchKernelGGL(gpis_var_splitk_finalize<KT>, dim3((unsigned)M), dim3(256), 0, s, g, partial, M_pad, chunk,
                        vout, std_out, var_out);
     prof_mark(PROF_GPIS_STD, false, s);
+    if (vs)
+      hipLaunchKernelGGL(gpis_select_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, G, vs->T,
+                         (const double*)std_out, X, vs->sel, vs->Xg);
     return;
   }
   prof_mark(PROF_GPIS_STD, true, s);
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s,
                      g, X, M, partial, M_pad, Mt, n_tiles, vout, kstar, nullptr, 0);
   prof_mark(PROF_GPIS_STD, false, s);
+  if (vs && 256 % vs->T == 0) {
+    hipLaunchKernelGGL(gpis_var_finalize_select<KT>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, g, partial,
+                       M, vs->T, M_pad, n_tiles, std_out, var_out, X, vs->sel, vs->Xg);
+    return;
+  }
   hipLaunchKernelGGL(gpis_var_finalize<KT>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, g, partial, M, M_pad,
                      n_tiles, std_out, var_out);
+  if (vs)
+    hipLaunchKernelGGL(gpis_select_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, G, vs->T,
+                       (const double*)std_out, X, vs->sel, vs->Xg);
 }
 
 template <int KT>
@@ -832,17 +899,18 @@ size_t gpis_v_bytes(const cdx_gpis& g, int64_t M) {
 }
 
 int gpis_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* std_out, double* var_out, void* ws,
-                    hipStream_t s, double* vout) {
+                    hipStream_t s, double* vout, const VarSelect* vs) {
   if (M <= 0) return CDX_OK;
+  if (vs && (vs->T <= 0 || M % vs->T != 0 || !vs->sel || !vs->Xg)) return CDX_EINVAL;
   const int64_t M_pad = round_up(M, ST_BM);
   const int n_tiles = g.N_pad / ST_BN;
   if (M_pad / ST_BM * n_tiles > 0x7fffffff) return CDX_EINVAL;
   const int Mt = (int)(M_pad / ST_BM);
   double* partial = static_cast<double*>(ws);
   switch (g.kernel) {
-    case CDX_KERNEL_TPS: var_launch_kt<CDX_KERNEL_TPS>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, vout, s); break;
-    case CDX_KERNEL_RBF: var_launch_kt<CDX_KERNEL_RBF>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, vout, s); break;
-    default: var_launch_kt<CDX_KERNEL_JOINT>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, vout, s); break;
+    case CDX_KERNEL_TPS: var_launch_kt<CDX_KERNEL_TPS>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, vout, s, vs); break;
+    case CDX_KERNEL_RBF: var_launch_kt<CDX_KERNEL_RBF>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, vout, s, vs); break;
+    default: var_launch_kt<CDX_KERNEL_JOINT>(g, X, M, std_out, var_out, partial, M_pad, Mt, n_tiles, vout, s, vs); break;
   }
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }

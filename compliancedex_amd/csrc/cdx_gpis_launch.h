@@ -10,10 +10,18 @@ size_t gpis_var_ws_bytes(const cdx_gpis& g, int64_t M);
 size_t gpis_grad_ws_bytes(const cdx_gpis& g, int64_t M);
 // Bytes of the stored whitened vectors V = (L⁻¹K*ᵀ)ᵀ of M queries ([round_up(M, 128), N_pad] f64).
 size_t gpis_v_bytes(const cdx_gpis& g, int64_t M);
+// Per-group argmax selection fused into the std finalize: rows [t·T, t·T + T) form group t; sel[t]
+// = the row of the first maximum of log(100·std) in the group (optimize_pregrasp.py:730's max),
+// Xg[t] = X[sel[t]].
+struct VarSelect {
+  int T;
+  int64_t* sel;
+  double* Xg;
+};
 // std[m] = sqrt|k0 − ‖L⁻¹k(x_m)‖²|, var_out[m] = the signed k0 − ‖L⁻¹k‖² (nullable); vout
-// (nullable, gpis_v_bytes) receives V.
+// (nullable, gpis_v_bytes) receives V; vs (nullable; M a multiple of vs->T) selects per group.
 int gpis_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* std_out, double* var_out, void* ws,
-                    hipStream_t s, double* vout = nullptr);
+                    hipStream_t s, double* vout = nullptr, const VarSelect* vs = nullptr);
 // gstd[sel[m]] = ∇std at X[m] (sel null: identity), scaled by var[sel[m]] from gpis_var_launch.
 // vin null: W = E11⁻¹k (2N² flops per query); vin = the V of gpis_var_launch: W = L⁻ᵀ v from row
 // sel[m] of V (N² flops per query; needs g.Linv).
