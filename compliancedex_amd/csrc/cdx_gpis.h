@@ -29,17 +29,34 @@ CDX_HD double sqrt_r2(double x) {
 #endif
 }
 
-template <int KT>
+// sqrt_r2 without its final Newton correction (≤ 1 ulp from the rounded root): the whitened
+// pass's on-chip K* generation (CDX_GEN_SQRT_FULL keeps the full sequence there).
+CDX_HD double sqrt_r2_gen(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(CDX_FAST_SQRT) && !defined(CDX_GEN_SQRT_FULL)
+  x = fmax(x, 1e-200);
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double e = fma(-h, g, 0.5);
+  g = fma(g, e, g);
+  h = fma(h, e, h);
+  const double d = fma(-g, g, x);
+  return fma(d, h, g);
+#else
+  return sqrt_r2(x);
+#endif
+}
+
+template <int KT, bool GENSQRT = false>
 CDX_HD void gpis_k(double r2, double R, double inv_s2, double& k, double& kd) {
   if (KT == CDX_KERNEL_TPS) {
-    const double r = sqrt_r2(r2);
+    const double r = GENSQRT ? sqrt_r2_gen(r2) : sqrt_r2(r2);
     k = 2.0 * (r2 * r) - 3.0 * R * r2 + R * R * R;
     kd = 6.0 * r - 6.0 * R;
   } else if (KT == CDX_KERNEL_RBF) {
     k = exp(-0.5 * r2 * inv_s2);
     kd = -k * inv_s2;
   } else {
-    const double r = sqrt_r2(r2);
+    const double r = GENSQRT ? sqrt_r2_gen(r2) : sqrt_r2(r2);
     const double kr = exp(-0.5 * r2 * inv_s2);
     k = 0.3 * kr + 0.7 * (2.0 * (r2 * r) - 3.0 * R * r2 + R * R * R);
     kd = 0.3 * (-kr * inv_s2) + 0.7 * (6.0 * r - 6.0 * R);

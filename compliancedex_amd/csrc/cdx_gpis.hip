@@ -270,7 +270,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
 #else
     const double dx = qx - x1[3 * i], dy = qy - x1[3 * i + 1], dz = qz - x1[3 * i + 2];
     double kd;
-    gpis_k<KT>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
+    gpis_k<KT, true>(dx * dx + dy * dy + dz * dz, R, inv_s2, kv[i], kd);
 #endif
   };
   auto stage_write = [&](int buf) {

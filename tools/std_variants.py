@@ -17,6 +17,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 VARIANTS = {"wn4": ("CDX_FAST_SQRT", "CDX_STD_SCHED"),               # default build
             "wn4_nosched": ("CDX_FAST_SQRT",),
+            "gensqrtfull": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_GEN_SQRT_FULL"),  # full sqrt in K* generation
             "kload": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_VAR_KLOAD"),  # whitened pass reads a K* buffer
             "nodiag": ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_STD_NODIAG"),  # no diagonal-block MFMA trimming
             "old2buf": None,                                       # prebuilt older library, not rebuilt
