@@ -128,7 +128,7 @@ def main():
     # HIP events only around the two roofline kernels inside the timed region (each event record
     # costs ≈ 5 µs of stream time); the other stages are timed in a separate pass afterwards
     PROF_TIMED = (1 << 2) | (1 << 4)  # gpis_std_var, gpis_std_grad
-    lib.cdx_profile_enable(PROF_TIMED)
+    N.check(lib.cdx_profile_enable(PROF_TIMED), "cdx_profile_enable")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -146,7 +146,7 @@ def main():
     # stage split (informational): every stage timed over a short extra pass, outside the timed region
     ms_all = (ctypes.c_double * 5)()
     cnt_all = (ctypes.c_int64 * 5)()
-    lib.cdx_profile_enable(0x1F)
+    N.check(lib.cdx_profile_enable(0x1F), "cdx_profile_enable")
     for _ in range(min(10, args.steps)):
         step()
     torch.cuda.synchronize()

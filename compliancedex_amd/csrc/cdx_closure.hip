@@ -14,6 +14,8 @@
 //                               and the five parameter gradients        — :713-769, :49-118
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "cdx_collision.h"
 #include "cdx_cost.h"
 #include "cdx_gpis_launch.h"
@@ -639,12 +641,17 @@ extern "C" int cdx_profile_enable(int stages) {
   using cdx::g_prof;
   const unsigned on = (unsigned)stages & ((1u << cdx::PROF_STAGES) - 1);
   if (on && !g_prof.created) {
+    // timing-only events: no system-scope fence (L2 writeback) at each record; CDX_PROF_EVENT_FLAGS
+    // (hex) overrides the flags for A/B runs
+    unsigned flags = hipEventDisableSystemFence;
+    if (const char* f = getenv("CDX_PROF_EVENT_FLAGS")) flags = (unsigned)strtoul(f, nullptr, 16);
     for (int st = 0; st < cdx::PROF_STAGES; ++st)
       for (int i = 0; i < cdx::PROF_POOL; ++i)
         for (int j = 0; j < 2; ++j)
-          // timing-only events: no system-scope fence (L2 writeback) at each record
-          if (hipEventCreateWithFlags(&g_prof.ev[st][i][j], hipEventDisableSystemFence) != hipSuccess)
-            return CDX_ELAUNCH;
+          if (hipEventCreateWithFlags(&g_prof.ev[st][i][j], flags) != hipSuccess) {
+            (void)hipGetLastError();  // not left pending for the caller's next launch check
+            return CDX_EINVAL;
+          }
     g_prof.created = true;
   }
   g_prof.mask = on;
