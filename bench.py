@@ -1,13 +1,21 @@
-"""Benchmark: candidate-grasp cost+grad evals/sec (BASELINE.json metric), config 2.
+"""Benchmark: candidate-grasp cost+grad evals/sec (BASELINE.json metric), configs 2 and 3.
 
 One step = one prob-mode closure (forward + backward, optimize_pregrasp.py:741-769) over
-E candidates per GPU on the N = 2000 synthetic banana GPIS with the Allegro hand — the
-whole hot path (FK → GPIS mean/normal/std → cost + analytic backward) through the C ABI.
+E candidates per GPU with the Allegro hand — the whole hot path (FK → GPIS mean/normal/std →
+cost + analytic backward) through the C ABI.
+
+Workload = config 3 as north_star states it, which at one GPU is config 2: rank r owns object r
+of workloads.CONFIG3_OBJECTS (banana, mug, mug2, hammer, lego, coffeebottle, box, realsense
+stand-in), each an N = 2000 GPIS fitted with the config-2 recipe (rank 0's banana IS config 2's
+synthetic state), E = 4096 candidates around the object.  No collective inside the steps; the
+timed region ends with the path's one exchange step: every rank packs its surviving grasps (all
+four margins > 0) into fixed-capacity records and one all_gather (RCCL over xGMI) gives every
+rank all objects' survivors (distributed.py).  Per-GPU work is fixed as N grows
+(weak scaling).
 
   python bench.py [--gpus N --steps K --warmup W --E 4096 --n-inducing 2000]
   N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
-Each rank evaluates its own E candidates (weak scaling, no data-path collective;
-SURVEY §8e).  Rank 0 prints one JSON line.
+Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -39,8 +47,21 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_quota():
+    """CPUs this process may use: the cgroup quota (cpu.max) if set, else the affinity mask."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    return len(os.sched_getaffinity(0))
+
+
 def cpu_baseline(args, ref_q, cfg):
-    """Oracle (CPU restatement of the reference path) on a bounded sample of the same workload."""
+    """Oracle (CPU restatement of the reference path) on a bounded sample of the same workload,
+    with torch's intra-op threads = the CPUs this job may use (the GPU box allots 16 per GPU:
+    os.cpu_count() reports the whole machine, whose other cores run other jobs)."""
     import numpy as np
     import torch
 
@@ -52,6 +73,8 @@ def cpu_baseline(args, ref_q, cfg):
     prob = OracleProblem(OracleChain(load_robot(args.hand)["bodies"]), cfg["ee_link_name"], cfg["ee_link_offset"],
                          ref_q, OracleGPIS.fit(X1, y, noise, bias=1.0))
     E = args.cpu_E
+    threads = cpu_quota()
+    torch.set_num_threads(threads)
     q, comp, target, palm = prob_inputs(ref_q, E, seed=99, spread=True)
     kn = np.random.default_rng(98).random((3 * E, 3, 3))
     times = []
@@ -63,7 +86,8 @@ def cpu_baseline(args, ref_q, cfg):
     return {"value": E / med, "unit": "evals/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"oracle/cdx_oracle.py closure (reference algorithm incl. per-call LU solve and M×M "
                       f"posterior), E={E} candidates, N={args.n_inducing} GPIS, {args.hand}; median of 3 after "
-                      f"1 warm-up; host os.cpu_count()={os.cpu_count()}"}
+                      f"1 warm-up; torch threads = the job's CPU quota ({threads}); host "
+                      f"os.cpu_count()={os.cpu_count()} (whole machine)"}
 
 
 def hbm_traffic(E, n, key="gpis_var_bytes_per_launch"):
@@ -79,6 +103,9 @@ def hbm_traffic(E, n, key="gpis_var_bytes_per_launch"):
         if d.get("E") == E and d.get("n_inducing") == n and key in d:
             best = d[key]
     return best
+
+
+CONFIG3 = ["banana", "mug", "mug2", "hammer", "lego", "coffeebottle", "box", "realsense"]
 
 
 def main():
@@ -101,14 +128,16 @@ def main():
 
     from compliancedex_amd import ProbabilisticGraspOptimizer
     from compliancedex_amd import _native as N
+    from compliancedex_amd import distributed as D
     from compliancedex_amd.urdf import load_robot
-    from compliancedex_amd.workloads import prob_inputs, synthetic_banana_gpis
+    from compliancedex_amd.workloads import config3_gpis, prob_inputs, surface_center
 
     cfg = load_robot(args.hand)["config"]
     ref_q = cfg["ref_q"]
     E = args.E
-    gpis = synthetic_banana_gpis(args.n_inducing, dev)
-    q, comp, target, palm = prob_inputs(ref_q, E, seed=1000 + rank, spread=True)
+    obj, gpis = config3_gpis(rank, dev, n_total=args.n_inducing)
+    center = None if obj == "banana" else surface_center(gpis)  # banana: config 2's mesh centre
+    q, comp, target, palm = prob_inputs(ref_q, E, seed=1000 + rank, spread=True, center=center)
     opt = ProbabilisticGraspOptimizer(args.hand, cfg["ee_link_name"], cfg["ee_link_offset"], palm_offset=palm,
                                       ref_q=ref_q, optimize_target=True, optimize_palm=True, device=dev, seed=rank << 32)
     qt = torch.from_numpy(q).to(dev).requires_grad_(True)
@@ -121,8 +150,20 @@ def main():
         qt.grad = ct.grad = tt.grad = pp.grad = po.grad = None
         opt.closure(qt, ct, tt, pp, po, 1, gpis, E)
 
+    def exchange():
+        """Surviving grasps of this rank's object → one all_gather of fixed-capacity records
+        (capacity E on every rank; the header keeps the true count)."""
+        buf = D.pack_survivors(E, rank, rank, 0, opt.total_loss, opt.total_margin, qt.detach(), ct.detach(),
+                               tt.detach(), torch.cat([pp, po], 1).detach())
+        if world > 1:
+            records, bufs = D.all_gather_survivors(buf if args.backend == "nccl" else buf.cpu(), return_buffers=True)
+        else:
+            records, bufs = D.unpack_records([buf]), [buf]
+        return buf, records, bufs
+
     for _ in range(args.warmup):
         step()
+    exchange()  # warms the pack kernels and the communicator (RCCL sets up its rings on first use)
     lib = N.load()
     import ctypes
     # HIP events only around the two roofline kernels inside the timed region (each event record
@@ -137,6 +178,11 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
+    tg0 = time.perf_counter()
+    buf, records, bufs = exchange()
+    n_records = int(records.shape[0])
+    torch.cuda.synchronize()
+    t1g = time.perf_counter()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
@@ -155,11 +201,11 @@ def main():
     for i in range(5):
         if not cnt[i]:
             ms[i], cnt[i] = ms_all[i], cnt_all[i]
-    elapsed = t1 - t0
+    elapsed, gather_s = t1 - t0, t1g - tg0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed, gather_s], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+        elapsed, gather_s = float(t[0]), float(t[1])
     nan_candidates = int((~torch.isfinite(opt.total_loss)).sum())
 
     ms_per_step = 1e3 * elapsed / args.steps
@@ -183,10 +229,18 @@ def main():
             "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"prob-mode closure fwd+bwd, banana GPIS N={n_ind} (in-repo fit recipe), "
-                                   f"{E} candidates/GPU, {args.hand} FK (f32), 3 pregrasp levels",
+            "config": {"workload": (f"config {'2' if world == 1 else '3'}: prob-mode closure fwd+bwd, "
+                                    f"{E} candidates/GPU, {args.hand} FK (f32), 3 pregrasp levels; one object per GPU "
+                                    f"({', '.join(CONFIG3[:world])}), each an N={n_ind} GPIS (in-repo fit recipe; "
+                                    f"rank 0 = config 2's banana); ends with one all_gather of surviving grasps"),
                        "candidates_per_gpu": E, "n_inducing": n_ind, "hand": args.hand,
-                       "parallelism": f"candidates sharded over {world} GPU(s), GPIS replicated"},
+                       "parallelism": f"one object per GPU over {world} GPU(s), survivors all-gathered"},
+            "exchange": {"collective": "all_gather" if world > 1 else None,
+                         "backend": (args.backend if world > 1 else None), "ms": gather_s * 1e3,
+                         "bytes_per_rank": int(buf.numel() * 8), "records_gathered": n_records,
+                         "overflow": D.overflow(bufs),
+                         "note": "pack (nonzero + gather of surviving rows) + all_gather + unpack, inside the timed "
+                                 "region after the last step"},
             "stage_ms": stage_ms,
             "stage_ms_note": "gpis_std_var / gpis_std_grad: HIP events over the timed steps; the other "
                               "stages from a 10-step all-stage pass after the timed region",

@@ -81,7 +81,7 @@ def anneal_sharded(annealer, q, target, comp, palm, outer_steps=4, object_id=0, 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     lo, hi = D.shard_range(q.shape[0], rank, world)
     best = annealer.run(q[lo:hi], target[lo:hi], comp[lo:hi], palm[lo:hi], outer_steps)
-    buf = D.pack_survivors(capacity or (hi - lo), object_id, rank, lo, best["loss"], best["margin"], best["q"],
+    buf = D.pack_survivors(capacity or D.default_capacity(q.shape[0], world), object_id, rank, lo, best["loss"], best["margin"], best["q"],
                            best["comp"], best["target"], best["palm"])
     if world == 1:
         return best, D.unpack_records([buf])

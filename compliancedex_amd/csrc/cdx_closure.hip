@@ -645,13 +645,14 @@ extern "C" int cdx_profile_enable(int stages) {
     // (hex) overrides the flags for A/B runs
     unsigned flags = hipEventDisableSystemFence;
     if (const char* f = getenv("CDX_PROF_EVENT_FLAGS")) flags = (unsigned)strtoul(f, nullptr, 16);
-    for (int st = 0; st < cdx::PROF_STAGES; ++st)
-      for (int i = 0; i < cdx::PROF_POOL; ++i)
-        for (int j = 0; j < 2; ++j)
-          if (hipEventCreateWithFlags(&g_prof.ev[st][i][j], flags) != hipSuccess) {
-            (void)hipGetLastError();  // not left pending for the caller's next launch check
-            return CDX_EINVAL;
-          }
+    const int total = cdx::PROF_STAGES * cdx::PROF_POOL * 2;
+    hipEvent_t* evs = &g_prof.ev[0][0][0];
+    for (int e = 0; e < total; ++e)
+      if (hipEventCreateWithFlags(&evs[e], flags) != hipSuccess) {
+        (void)hipGetLastError();  // not left pending for the caller's next launch check
+        for (int k = 0; k < e; ++k) (void)hipEventDestroy(evs[k]);  // no partial pool is kept
+        return CDX_EINVAL;
+      }
     g_prof.created = true;
   }
   g_prof.mask = on;

@@ -12,6 +12,11 @@ xGMI under the ``nccl`` backend; gloo on CPU in tests) gives every rank the glob
 
 Record layout (float64, RECORD_FIELDS + D + 5·T entries, ≈ 344 B for Allegro):
   [object_id, rank, candidate_id, best_loss, survive, margin[T], q[D], comp[T], target[T·3], palm[6]]
+Row 0 of a rank's buffer is the header: [stored count, true survivor count, capacity, 0, …]; the
+two counts differ when more candidates survived than the buffer holds (``overflow``).
+
+Every rank must pass an equal-shaped buffer to ``all_gather`` (RCCL sizes its receive buffers from
+the local one), so the default capacity is the same on every rank: ⌈total / world⌉.
 """
 from __future__ import annotations
 
@@ -32,18 +37,26 @@ def record_width(n_dofs, n_tips):
     return RECORD_FIELDS + n_tips + n_dofs + n_tips + 3 * n_tips + 6
 
 
+def default_capacity(total, world):
+    """Records per rank: the largest shard (⌈total / world⌉), identical on every rank."""
+    return -(-int(total) // int(world))
+
+
 def pack_survivors(capacity, object_id, rank, cand_offset, best_loss, margin, q, comp, target, palm):
-    """[capacity + 1, W] float64 buffer; row 0 = count header, rows 1.. = surviving candidates
-    in candidate order (truncated to ``capacity``)."""
+    """[capacity + 1, W] float64 buffer; row 0 = header [stored, survived, capacity], rows 1.. =
+    surviving candidates in candidate order (the first ``capacity`` of them)."""
     E, T = margin.shape
     D = q.shape[1]
     W = record_width(D, T)
     dev = margin.device
     survive = (margin > 0).all(dim=1)
-    idx = torch.nonzero(survive).flatten()[:capacity]
+    all_idx = torch.nonzero(survive).flatten()
+    idx = all_idx[:capacity]
     buf = torch.zeros(capacity + 1, W, dtype=torch.float64, device=dev)
     n = idx.numel()
     buf[0, 0] = n
+    buf[0, 1] = all_idx.numel()
+    buf[0, 2] = capacity
     if n:
         cols = [torch.full((n, 1), float(object_id), dtype=torch.float64, device=dev),
                 torch.full((n, 1), float(rank), dtype=torch.float64, device=dev),
@@ -62,20 +75,32 @@ def unpack_records(gathered):
     return torch.cat(rows, dim=0) if rows else gathered[0][1:1]
 
 
-def all_gather_survivors(buf, group=None):
-    """One collective: every rank receives every rank's fixed-capacity buffer."""
+def overflow(gathered):
+    """Per-rank count of survivors that did not fit the buffer (0 everywhere = nothing lost)."""
+    return [int(g[0, 1]) - int(g[0, 0]) for g in gathered]
+
+
+def all_gather_survivors(buf, group=None, return_buffers=False):
+    """One collective: every rank receives every rank's fixed-capacity buffer (all ranks must
+    pass the same shape — see ``default_capacity``)."""
     world = dist.get_world_size(group)
     out = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(out, buf.contiguous(), group=group)
-    return unpack_records(out)
+    return (unpack_records(out), out) if return_buffers else unpack_records(out)
 
 
-def optimize_sharded(optimizer, gpis, q, target, comp, friction_mu, object_id=0, capacity=None, group=None):
+def optimize_sharded(optimizer, gpis, q, target, comp, friction_mu, object_id=0, capacity=None, group=None,
+                     shard=True):
     """Each rank optimises its shard of the global candidate arrays (already resident on
-    its GPU), then all ranks exchange surviving grasps.  Returns (local results, records)."""
+    its GPU), then all ranks exchange surviving grasps.  Returns (local results, records).
+    ``shard=False`` (config 3, one object per rank): the arrays are this rank's own object's
+    candidates, optimised whole; every rank must then hold the same candidate count."""
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    lo, hi = shard_range(q.shape[0], rank, world)
+    if shard:
+        lo, hi = shard_range(q.shape[0], rank, world)
+    else:
+        lo, hi = 0, q.shape[0]
     palm_all = optimizer.palm_offset
     optimizer.palm_offset = palm_all[lo:hi]
     try:
@@ -85,8 +110,8 @@ def optimize_sharded(optimizer, gpis, q, target, comp, friction_mu, object_id=0,
     opt_q, opt_comp, opt_target, opt_palm, opt_margin = res
     best = optimizer.best_loss if hasattr(optimizer, "best_loss") else torch.zeros(hi - lo, dtype=torch.float64,
                                                                                   device=q.device)
-    buf = pack_survivors(capacity or (hi - lo), object_id, rank, lo, best, opt_margin, opt_q, opt_comp, opt_target,
-                         opt_palm)
+    cap = capacity or (default_capacity(q.shape[0], world) if shard else q.shape[0])
+    buf = pack_survivors(cap, object_id, rank, lo, best, opt_margin, opt_q, opt_comp, opt_target, opt_palm)
     if world == 1:
         return res, unpack_records([buf])
     return res, all_gather_survivors(buf, group)

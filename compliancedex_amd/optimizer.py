@@ -156,18 +156,21 @@ class ProbabilisticGraspOptimizer:
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
 
-    def _closure_into(self, p, q, comp, target, pp, po, noise, out, seed=None):
+    def _closure_into(self, p, q, comp, target, pp, po, noise, out, seed=None, ws=None):
         """cdx_closure on contiguous f64 device tensors, writing into the preallocated ``out``.
-        ``seed``: the Kabsch-noise key (default: the next value of this optimiser's counter)."""
+        ``seed``: the Kabsch-noise key (default: the next value of this optimiser's counter).
+        ``ws``: a caller-owned workspace (a captured hipGraph's own), else the optimiser's."""
         lib = N.load()
         E = q.shape[0]
-        self._ensure_ws(p, E, q.device)
+        if ws is None:
+            self._ensure_ws(p, E, q.device)
+            ws = self._ws
         if seed is None:
             self._seed += 1
             seed = self._seed
         stream = N.stream_ptr(q.device)
         N.check(lib.cdx_closure(p, E, N.ptr(q), N.ptr(comp), N.ptr(target), N.ptr(pp), N.ptr(po), N.ptr(noise),
-                                seed, N.ptr(self._ws), N.ptr(out["total_loss"]), N.ptr(out["total_margin"]),
+                                seed, N.ptr(ws), N.ptr(out["total_loss"]), N.ptr(out["total_margin"]),
                                 N.ptr(out.get("pregrasp_tip")), N.ptr(out["g_q"]), N.ptr(out["g_comp"]),
                                 N.ptr(out["g_target"]), N.ptr(out["g_palm_pos"]), N.ptr(out["g_palm_ori"]),
                                 N.ptr(out.get("flip")), stream), "cdx_closure")
@@ -315,6 +318,9 @@ class ProbabilisticGraspOptimizer:
         f64 = dict(dtype=torch.float64, device=dev)
         if graph and noise_tape is not None:
             raise ValueError("graph=True draws the Kabsch noise on device; noise_tape needs graph=False")
+        # A captured graph replays raw device pointers: each cache entry owns its workspace and
+        # holds the GPIS state it captured (so neither is freed or reused while the entry lives;
+        # the id() in the key cannot be recycled while the entry references the object).
         key = (E, id(self._problem_state), float(friction_mu), self.num_iters)
         cache = self._graphs.get(key) if graph else None
         if cache is None:
@@ -332,6 +338,9 @@ class ProbabilisticGraspOptimizer:
                 cache[k] = z(E, 3, **f64)
             cache.update(opt_value=z(E, **f64), opt_q=z(E, D, **f64), opt_comp=z(E, T, **f64),
                          opt_target=z(E, T, 3, **f64), opt_palm=z(E, 6, **f64))
+            if graph:
+                cache["ws"] = torch.empty(lib.cdx_closure_workspace(p, E), dtype=torch.uint8, device=dev)
+                cache["state"], cache["problem"] = self._problem_state, p
         c, out = cache, cache["out"]
         # (re)initialise the loop state in place — the captured graph reads these buffers
         c["q"].copy_(init_joint_angles.detach())
@@ -369,7 +378,8 @@ class ProbabilisticGraspOptimizer:
                     noise = None
                     if noise_tape is not None:
                         noise = noise_tape[s].to(**f64).contiguous()
-                    self._closure_into(p, c["q"], c["comp"], c["target"], c["pp"], c["po"], noise, out, seed=0)
+                    self._closure_into(p, c["q"], c["comp"], c["target"], c["pp"], c["po"], noise, out, seed=0,
+                                       ws=c.get("ws"))
                     N.check(lib.cdx_optimizer_step(cfg, bufs, E, D, T, s, stream), "cdx_optimizer_step")
             finally:
                 p.loop = None
@@ -380,7 +390,6 @@ class ProbabilisticGraspOptimizer:
             cache["graph"].replay()
         else:
             # workspace and library state exist before capture; the first call captures AND runs
-            self._ensure_ws(p, E, dev)
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             g = torch.cuda.CUDAGraph()
@@ -389,6 +398,8 @@ class ProbabilisticGraspOptimizer:
                     run_loop()
             torch.cuda.current_stream(dev).wait_stream(side)
             cache["graph"] = g
+            if len(self._graphs) >= 8:  # bound the graphs (and the states/workspaces they pin)
+                self._graphs.pop(next(iter(self._graphs)))
             self._graphs[key] = cache
             g.replay()
         if not self.optimize_target and torch.is_tensor(target_pose):

@@ -18,31 +18,43 @@ import torch
 DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 
 
-def synthetic_banana_arrays(n_total=2000):
-    pcd = np.load(os.path.join(DATA, "partial_pcd_banana.npy"))
-    center = 0.5 * (pcd.min(0) + pcd.max(0))
-    n_ext, n_int = 14, 50
-    n_surf = n_total - n_ext - n_int
-    surf = pcd[np.random.default_rng(0).permutation(len(pcd))[:n_surf]]
-    bound = 0.15
-    ext = np.array([[-1, -1, -1], [1, -1, -1], [-1, 1, -1], [1, 1, -1], [-1, -1, 1], [1, -1, 1], [-1, 1, 1],
-                    [1, 1, 1], [-1, 0, 0], [0, -1, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1], [0, 0, -1]],
-                   dtype=np.float64) * bound + center
-    w = torch.rand(n_int, n_surf, generator=torch.Generator().manual_seed(0)).double()
-    internal = (torch.softmax(w * 30, dim=1) @ torch.from_numpy(surf)).numpy()
+EXTERNAL_DIRS = np.array([[-1, -1, -1], [1, -1, -1], [-1, 1, -1], [1, 1, -1], [-1, -1, 1], [1, -1, 1], [-1, 1, 1],
+                          [1, 1, 1], [-1, 0, 0], [0, -1, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1], [0, 0, -1]],
+                         dtype=np.float64)
+
+
+def recipe_arrays(surf, center, n_int=50, bound=0.15, seed=0):
+    """The in-repo fit recipe (optimize_pregrasp.py:904-922) on given surface points: 14 external
+    points at ±``bound`` around ``center`` (y = +bound, noise 0.2), the surface (y = 0, noise
+    0.005), ``n_int`` internal points = softmax(30·U)·surface (y = −bound, noise 0.1)."""
+    n_surf = len(surf)
+    ext = EXTERNAL_DIRS * bound + center
+    w = torch.rand(n_int, n_surf, generator=torch.Generator().manual_seed(seed)).double()
+    internal = (torch.softmax(w * 30, dim=1) @ torch.from_numpy(np.ascontiguousarray(surf))).numpy()
     X1 = np.vstack([ext, surf, internal])
-    y = np.concatenate([np.full(n_ext, bound), np.zeros(n_surf), np.full(n_int, -bound)])[:, None]
-    noise = np.concatenate([np.full(n_ext, 0.2), np.full(n_surf, 0.005), np.full(n_int, 0.1)])
+    y = np.concatenate([np.full(len(ext), bound), np.zeros(n_surf), np.full(n_int, -bound)])[:, None]
+    noise = np.concatenate([np.full(len(ext), 0.2), np.full(n_surf, 0.005), np.full(n_int, 0.1)])
     return X1, y, noise
 
 
-def synthetic_banana_gpis(n_total=2000, device="cuda"):
+def synthetic_banana_arrays(n_total=2000):
+    pcd = np.load(os.path.join(DATA, "partial_pcd_banana.npy"))
+    center = 0.5 * (pcd.min(0) + pcd.max(0))
+    surf = pcd[np.random.default_rng(0).permutation(len(pcd))[:n_total - 14 - 50]]
+    return recipe_arrays(surf, center)
+
+
+def fitted_gpis(X1, y, noise, device="cuda"):
+    """GPIS(0.08, 1.0) fitted on the device with bias 1 (the recipe's ``gpis.bias``)."""
     from .gpis import GPIS
-    X1, y, noise = synthetic_banana_arrays(n_total)
     g = GPIS(0.08, 1.0)
     g.fit(torch.from_numpy(X1).to(device), torch.from_numpy(y).to(device), noise=torch.from_numpy(noise).to(device))
     g.bias = torch.tensor(1.0, dtype=torch.float64, device=device)
     return g
+
+
+def synthetic_banana_gpis(n_total=2000, device="cuda"):
+    return fitted_gpis(*synthetic_banana_arrays(n_total), device=device)
 
 
 def stored_gpis(name, device="cuda"):
@@ -84,11 +96,8 @@ def prob_inputs(ref_q, E, seed=0, spread=True, center=None):
     return q, comp, target, palm
 
 
-def box_gpis(side=0.065, n_surface=400, device="cuda", seed=0):
-    """Config 3's "box": the 0.065 m cube of assets/cube_visualization.urdf:7 (no stored state),
-    fitted with the same recipe as the synthetic banana: surface samples (y = 0, noise 0.005),
-    14 external points at ±0.15 (y = +0.15, noise 0.2), 50 internal points (y = −0.15, noise 0.1)."""
-    from .gpis import GPIS
+def box_surface(side=0.065, n_surface=400, seed=0):
+    """Uniform samples on the faces of the 0.065 m cube of assets/cube_visualization.urdf:7."""
     rng = np.random.default_rng(seed)
     h = side / 2
     face = rng.integers(0, 6, n_surface)
@@ -99,24 +108,76 @@ def box_gpis(side=0.065, n_surface=400, device="cuda", seed=0):
         p = [u, v]
         p.insert(ax, sgn * h)
         surf[i] = p
+    return surf, rng
+
+
+def box_arrays(side=0.065, n_surface=400, seed=0):
+    """Config 3's "box" (no stored state), reduced size: ``n_surface`` cube-face samples (y = 0,
+    noise 0.005), 14 external points at ±0.15 (y = +0.15, noise 0.2), 50 internal points uniform
+    in the inner 60 % of the cube (y = −0.15, noise 0.1).  Returns numpy (X1, y, noise)."""
+    surf, rng = box_surface(side, n_surface, seed)
+    h = side / 2
     bound = 0.15
-    ext = np.array([[-1, -1, -1], [1, -1, -1], [-1, 1, -1], [1, 1, -1], [-1, -1, 1], [1, -1, 1], [-1, 1, 1],
-                    [1, 1, 1], [-1, 0, 0], [0, -1, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1], [0, 0, -1]], float) * bound
+    ext = EXTERNAL_DIRS * bound
     internal = rng.uniform(-0.6 * h, 0.6 * h, (50, 3))
     X1 = np.vstack([ext, surf, internal])
     y = np.concatenate([np.full(14, bound), np.zeros(n_surface), np.full(50, -bound)])[:, None]
     noise = np.concatenate([np.full(14, 0.2), np.full(n_surface, 0.005), np.full(50, 0.1)])
-    g = GPIS(0.08, 1.0)
-    g.fit(torch.from_numpy(X1).to(device), torch.from_numpy(y).to(device), noise=torch.from_numpy(noise).to(device))
-    g.bias = torch.tensor(1.0, dtype=torch.float64, device=device)
-    return g
+    return X1, y, noise
 
 
-# config 3: one object per GPU; "realsense" (fit on the fly from an absent point cloud) is
-# stood in for by the stored dummy state, "box" by box_gpis.
+def box_gpis(side=0.065, n_surface=400, device="cuda", seed=0):
+    """GPIS(0.08, 1.0) fitted on ``box_arrays`` (bias 1, as the synthetic banana)."""
+    return fitted_gpis(*box_arrays(side, n_surface, seed), device=device)
+
+
+# Config 3: one object per GPU.  Two sources per object:
+#   "fit" (default, bench and scaling): an N = 2000 GPIS per object with the config-2 recipe —
+#     banana = config 2's synthetic state itself (so the 1-GPU run IS config 2); hammer, lego, mug,
+#     mug2 from 1 936 points sampled on their meshes, coffeebottle from its observed point cloud
+#     (data/config3_surface.npz, tools/import_assets.py); box from its cube; "realsense" (fitted on
+#     the fly in the reference from an absent point cloud) from the stored dummy state's surface
+#     points, resampled with 1 mm jitter.  Every rank then does config 2's per-GPU work.
+#   "stored": the reference's stored states (N = 196…401), the 400-point box, dummy for realsense.
 CONFIG3_OBJECTS = ["banana", "mug", "mug2", "hammer", "lego", "coffeebottle", "box", "dummy"]
 
 
-def config3_gpis(rank, device="cuda"):
+def config3_arrays(name, n_total=2000):
+    """numpy (X1, y, noise) of config 3's N = ``n_total`` GPIS for one object."""
+    if name == "banana":
+        return synthetic_banana_arrays(n_total)
+    n_surf = n_total - 14 - 50
+    rng = np.random.default_rng(CONFIG3_OBJECTS.index(name))
+    if name == "box":
+        surf, _ = box_surface(n_surface=n_surf, seed=1)
+    elif name == "dummy":
+        d = np.load(os.path.join(DATA, "gpis_states", "dummy_state.npz"))
+        y1 = d["y1"].reshape(-1)
+        pts = d["X1"][y1 == -1.0]
+        surf = pts[rng.integers(0, len(pts), n_surf)] + 1e-3 * rng.standard_normal((n_surf, 3))
+    else:
+        surf = np.load(os.path.join(DATA, "config3_surface.npz"))[name][:n_surf]
+    return recipe_arrays(surf, 0.5 * (surf.min(0) + surf.max(0)))
+
+
+def config3_gpis(rank, device="cuda", source="fit", n_total=2000):
+    """(name, GPIS) of rank ``rank``'s object (see CONFIG3_OBJECTS for the two sources)."""
     name = CONFIG3_OBJECTS[rank % len(CONFIG3_OBJECTS)]
+    if source == "fit":
+        return name, fitted_gpis(*config3_arrays(name, n_total), device=device)
     return name, (box_gpis(device=device) if name == "box" else stored_gpis(name, device))
+
+
+def surface_center(gpis):
+    """AABB centre of a GPIS's surface points (the most frequent label, y1 = −bias: 0-level set),
+    the object centre ``__main__`` derives from the mesh (:885-888)."""
+    X1 = gpis.X1.detach().cpu().numpy()
+    y1 = gpis.y1.detach().cpu().numpy().reshape(-1)
+    vals, counts = np.unique(y1, return_counts=True)
+    surf = X1[y1 == vals[np.argmax(counts)]]
+    return 0.5 * (surf.min(0) + surf.max(0))
+
+
+def config3_inputs(gpis, ref_q, E, seed):
+    """Config 3's per-object candidates: ``prob_inputs`` around the object's surface centre."""
+    return prob_inputs(ref_q, E, seed=seed, spread=True, center=surface_center(gpis))

@@ -95,6 +95,23 @@ class OracleGPIS:
             return n.view(shape)
         return n.view(shape), weight.sum()
 
+    def compute_multinormals(self, X2, num_normal_samples):
+        """Normals of nested inducing-point subsets (gpis.py:89-111): fractions linspace(0.8, 1)
+        of the leading points, all points, then ranges from ``int(1 − fraction)`` (= 0: the
+        reference's index quirk makes the trailing half full sets)."""
+        n = len(self.X1)
+        frac = torch.linspace(0.8, 1, num_normal_samples // 2)
+        idx = [list(range(int(frac[i] * n))) for i in range(num_normal_samples // 2)]
+        idx.append(list(range(n)))
+        idx += [list(range(int(1 - frac[-i - 1]), n)) for i in range(num_normal_samples // 2)]
+        normals, weights = [], []
+        for ix in idx:
+            nrm, w = self.compute_normal(X2, ix)
+            normals.append(nrm)
+            weights.append(w)
+        weights = torch.hstack(weights)
+        return torch.stack(normals, dim=1), weights / weights.sum()
+
 
 # ------------------------------------------------------------------------------- FK
 def _axis_rot(axis, ang):
@@ -370,6 +387,29 @@ class OracleProblem:
         loss = total_loss.sum()
         loss.backward()
         return loss.detach(), total_loss.detach(), total_margin.detach(), pre.detach(), flip
+
+
+def collision_loss(chain, anchor_links, anchor_offsets, pairs, q, palm, threshold=0.02, optimize_palm=True):
+    """compute_collision_loss (optimize_pregrasp.py:671-701): anchor FK (f32) in world, 1/d for
+    anchor pairs closer than ``threshold``, 0.1/z for anchors below z = 0.02, 1/z for a palm
+    below z = 0.02 (when the palm is optimised).  Masked terms are multiplied by 0 (so a NaN
+    or inf there stays NaN, as in the reference's ``*= 0.0``)."""
+    L = len(anchor_links)
+    a = chain.forward_kinematics(q.float(), anchor_links, anchor_offsets)[0].double().view(-1, L, 3)
+    R = euler_xyz(palm[:, 3:])
+    a = torch.bmm(R, a.transpose(1, 2)).transpose(1, 2) + palm[:, :3].unsqueeze(1)
+    pr = torch.as_tensor(pairs).long()
+    dist = torch.norm(a[:, pr[:, 0]] - a[:, pr[:, 1]], dim=2)
+    inv = 1.0 / dist
+    inv = torch.where(dist < threshold, inv, inv * 0.0)
+    cost = inv.sum(dim=1)
+    z = a[:, :, 2]
+    zc = 1 / z * 0.1
+    cost = cost + torch.where(z < 0.02, zc, zc * 0.0).sum(dim=1)
+    if optimize_palm:
+        pz = 1 / palm[:, 2]
+        cost = cost + torch.where(palm[:, 2] < 0.02, pz, pz * 0.0)
+    return cost
 
 
 def closure_with_grads(problem, q, comp, target, palm, noise):

@@ -1,13 +1,13 @@
 /* ORACLE — test infrastructure only.  Plain-C restatement of the TorchSDF forward and
  * backward kernels (thirdparty/TorchSDF/torchsdf/csrc/unbatched_triangle_distance_cuda.cu),
  * used to check the gfx950 kernel bit-for-bit on integer outputs (sign, argmin face) and
- * floats.  Build: see oracle/build_oracle.py (gcc -O2 -ffp-contract=off).
+ * floats.  Build: compliancedex_amd/build.py build_oracle() (gcc -O2 -ffp-contract=off).
  *
  * Parity pinning: the reference kernel cannot run here (its _C.so is a missing blob and it
  * is CUDA-only, unbatched_triangle_distance.cpp:48-53) and its own tests compare against
  * Kaolin, which is absent, so value/sign parity vs the reference is UNPINNED; the one
  * self-contained reference invariant, tests/normal.py:36-39 (normals·2·sqrt(d) equals the
- * autograd gradient, atol 5e-7), is checked in tests/test_sdf.py.
+ * autograd gradient, atol 5e-7), is checked in tests/test_sdf_cpu.py and tests/test_gpu_parity.py.
  *
  * Deliberate restatement choices:
  *   - rsqrt(x) is computed as 1.0f/sqrtf(x) (correctly rounded).  CUDA's rsqrtf is a

@@ -25,6 +25,16 @@ Fixtures:
   mode_<mode>.npz     GPIS / KinGPIS / SDF / Kin optimisers (:121-511), 12 iterations, E = 6: final
                       outputs and the per-iteration Σ loss (TorchSDF via the C oracle, whose _C
                       module the reference lacks).
+  gpis_box.npz        as gpis_<state> for config 3's box object (no stored state: fitted by the
+                      reference GPIS.fit on compliancedex_amd.workloads.box_arrays; X1/y/noise saved).
+  normals_<state>.npz compute_normal(X, index) (gpis.py:63-87, index branch: normals + Σ weights)
+                      for three index sets, and compute_multinormals (:89-111) for 3 and 5 samples,
+                      2-D and 3-D query batches.
+  closure_iiwa7_*.npz the prob closure on the 23-DOF iiwa7_allegro chain (config 4) plus
+                      compute_collision_loss (:671-701) on the same inputs (the reference closure has
+                      it commented out at :765; the build's collision=True adds it).
+  results_<exp>.npz   the reference's own optimiser outputs data/{contact,target,wrist,compliance,
+                      joint_angle}_<exp>.npy (writer :1016-1020), copied as data for the FK/format check.
 """
 from __future__ import annotations
 
@@ -257,6 +267,14 @@ def gen_optimize(ns, name, hand, state, E, seed, iters):
     o = make_optimizer(ns, hand, inp["palm"], iters)
     gen = torch.Generator().manual_seed(seed)
     tape = [torch.rand((3 * E, 3, 3), dtype=torch.float64, generator=gen) for _ in range(iters)]
+    trace = []
+    closure = o.closure
+
+    def traced(*a, **k):  # per-iteration total_loss: the input of the best-iterate update_flag (:821-829)
+        r = closure(*a, **k)
+        trace.append(o.total_loss.detach().clone())
+        return r
+    o.closure = traced
     with NoiseTape(torch, replay=tape), contextlib.redirect_stdout(io.StringIO()):
         out = o.optimize(torch.from_numpy(inp["q"]), torch.from_numpy(inp["target"]),
                          torch.from_numpy(inp["comp"]), 1, g)
@@ -265,7 +283,7 @@ def gen_optimize(ns, name, hand, state, E, seed, iters):
         os.path.join(OUT, f"optimize_{name}.npz"),
         hand=hand, state=state, iters=iters, q=inp["q"], comp=inp["comp"], target=inp["target"],
         palm=inp["palm"], noise=torch.stack(tape).numpy(), opt_q=opt_q, opt_comp=opt_comp,
-        opt_target=opt_target, opt_palm=opt_palm, opt_margin=opt_margin)
+        opt_target=opt_target, opt_palm=opt_palm, opt_margin=opt_margin, loss_trace=torch.stack(trace).numpy())
     print("optimize", name)
 
 
@@ -424,11 +442,136 @@ def gen_collision(ns, name, hand, E, seed):
     print("collision", name, int((cost.detach() != 0).sum()), "of", E, "non-zero")
 
 
+def gen_gpis_box(ns):
+    """Config 3's box GPIS: the reference GPIS.fit on the build's box recipe, pred/normal at
+    seeded queries (same fields as gen_gpis, X1/y/noise saved as syn_*)."""
+    torch = ns.torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from compliancedex_amd.workloads import box_arrays
+    X1, y, noise = box_arrays()
+    g = ns.gpis.GPIS(0.08, 1.0)
+    g.fit(torch.from_numpy(X1), torch.from_numpy(y), noise=torch.from_numpy(noise))
+    g.bias = torch.tensor(1.0, dtype=torch.float64)
+    rng = np.random.default_rng(5)
+    M = 96
+    lo, hi = X1.min(0) - 0.03, X1.max(0) + 0.03
+    Xq = lo + (hi - lo) * rng.random((M, 3))
+    # near the cube faces: where the variance cost and the closure's queries live
+    Xq[:48] = X1[14 + rng.integers(0, 400, 48)] + 2e-3 * rng.standard_normal((48, 3))
+    X = torch.from_numpy(Xq).requires_grad_(True)
+    mean, std = g.pred(X)
+    cm, cs = rng.standard_normal(M), rng.standard_normal(M)
+    (mean * torch.from_numpy(cm)).sum().add((std * torch.from_numpy(cs)).sum()).backward()
+    normal = g.compute_normal(torch.from_numpy(Xq))
+    mean3, std3 = g.pred(torch.from_numpy(Xq).view(-1, 4, 3))
+    np.savez_compressed(os.path.join(OUT, "gpis_box.npz"), X=Xq, mean=mean.detach().numpy(), std=std.detach().numpy(),
+                        cm=cm, cs=cs, grad_X=X.grad.numpy(), normal=normal.numpy(), mean3=mean3.detach().numpy(),
+                        std3=std3.detach().numpy(), R=float(g.R), bias=float(g.bias), syn_X1=X1, syn_y=y,
+                        syn_noise=noise)
+    print("gpis box", len(X1))
+
+
+def gen_normals(ns):
+    """compute_normal(X, index) and compute_multinormals on stored states (fresh GPIS object per
+    multinormals call: the reference caches ``fraction``/``indices`` from the first call)."""
+    torch = ns.torch
+    for name, seed in (("banana", 60), ("mug", 61)):
+        rng = np.random.default_rng(seed)
+        g = load_state(ns, name)
+        X1 = g.X1.numpy()
+        n = len(X1)
+        Xq = X1[rng.integers(0, n, 48)] + 5e-3 * rng.standard_normal((48, 3))
+        idx_sets = [list(range(int(0.8 * n))), sorted(rng.choice(n, n // 2, replace=False).tolist()),
+                    list(range(n // 3, n))]
+        out = dict(X=Xq)
+        for i, idx in enumerate(idx_sets):
+            nrm, w = g.compute_normal(torch.from_numpy(Xq), idx)
+            out[f"index{i}"] = np.asarray(idx)
+            out[f"normal_index{i}"] = nrm.numpy()
+            out[f"weight_index{i}"] = float(w)
+        for S in (3, 5):
+            for dim in (2, 3):
+                gs = load_state(ns, name)
+                X = torch.from_numpy(Xq) if dim == 2 else torch.from_numpy(Xq).view(-1, 4, 3)
+                nrms, ws = gs.compute_multinormals(X, S)
+                out[f"multi{S}_{dim}d_normals"] = nrms.numpy()
+                out[f"multi{S}_{dim}d_weights"] = ws.numpy()
+        np.savez_compressed(os.path.join(OUT, f"normals_{name}.npz"), **out)
+        print("normals", name, n)
+
+
+IIWA7_TIPS = ["link_3.0_tip", "link_7.0_tip", "link_11.0_tip", "link_15.0_tip"]
+IIWA7_PAIRS = [[0, 1], [0, 2], [0, 3], [1, 2], [1, 3], [2, 3]]
+
+
+def gen_closure_iiwa7(ns, name, E, seed, gpis_name="banana"):
+    """Config 4's chain: the prob closure on iiwa7_allegro (23 DOF; the arm base is the "palm"
+    pose, placed so the fingertips at q = 0 surround the banana), fingertips as the collision
+    anchors with all six pairs, then compute_collision_loss on the same inputs."""
+    torch = ns.torch
+    urdf = os.path.join(ns.ref, _refload.URDFS["iiwa7_allegro"])
+    offs = [list(o) for o in ns.opt.EE_OFFSETS]
+    D = 23
+    model = ns.rm.DifferentiableRobotModel(urdf)
+    with contextlib.redirect_stdout(io.StringIO()):
+        tips0 = model.compute_forward_kinematics(torch.zeros(1, D), IIWA7_TIPS, offsets=offs,
+                                                 recursive=False)[0].view(4, 3).double().mean(0).numpy()
+    verts = obj_vertices(os.path.join(ns.ref, "assets/banana/banana.obj"))
+    center = 0.5 * (verts.min(0) + verts.max(0))
+    rng = np.random.default_rng(seed)
+    q = 0.3 * rng.standard_normal((E, D))
+    q[:, :7] *= 0.1  # the 7 arm joints: small, so the fingertips stay around the object
+    palm = np.concatenate([center - tips0 + 0.01 * rng.standard_normal((E, 3)), 0.05 * rng.standard_normal((E, 3))], 1)
+    target = np.tile(center, (E, 4, 1)) + 0.01 * rng.standard_normal((E, 4, 3))
+    comp = np.tile(np.array([10.0, 10.0, 10.0, 20.0]), (E, 1))
+    g = load_state(ns, gpis_name)
+    with contextlib.redirect_stdout(io.StringIO()):
+        o = ns.opt.ProbabilisticGraspOptimizer(
+            urdf, ee_link_names=IIWA7_TIPS, ee_link_offsets=offs, anchor_link_names=IIWA7_TIPS,
+            anchor_link_offsets=offs, collision_pairs=IIWA7_PAIRS,
+            tip_bounding_box=[ns.opt.FINGERTIP_LB, ns.opt.FINGERTIP_UB], ref_q=[0.0] * D, optimize_target=True,
+            optimize_palm=True, num_iters=1, palm_offset=palm, mass=0.1, com=[0.0, 0.0, 0.0], gravity=True,
+            uncertainty=20.0)
+    qt = torch.from_numpy(q).clone().requires_grad_(True)
+    ct = torch.from_numpy(comp).clone().requires_grad_(True)
+    tt = torch.from_numpy(target).clone().requires_grad_(True)
+    pp = torch.from_numpy(palm[:, :3]).clone().requires_grad_(True)
+    po = torch.from_numpy(palm[:, 3:]).clone().requires_grad_(True)
+    o.optim = torch.optim.Adam([qt, ct, tt, pp, po])
+    with NoiseTape(torch, seed=seed) as tape, contextlib.redirect_stdout(io.StringIO()):
+        loss = o.closure(qt, ct, tt, pp, po, 1, g, E)
+    noise = torch.stack(tape.record).numpy()
+    qc = torch.from_numpy(q).clone().requires_grad_(True)
+    pc = torch.from_numpy(palm).clone().requires_grad_(True)
+    with contextlib.redirect_stdout(io.StringIO()):
+        cost = o.compute_collision_loss(qc, pc)
+    cost.sum().backward()
+    np.savez_compressed(
+        os.path.join(OUT, f"closure_{name}.npz"),
+        hand="iiwa7_allegro", state=gpis_name, q=q, comp=comp, target=target, palm=palm, center=center, noise=noise,
+        loss=float(loss), total_loss=o.total_loss.detach().numpy(), total_margin=o.total_margin.detach().numpy(),
+        pregrasp_tip=o.pregrasp_tip_pose.detach().numpy(), grad_q=qt.grad.numpy(), grad_comp=ct.grad.numpy(),
+        grad_target=tt.grad.numpy(), grad_palm_pos=pp.grad.numpy(), grad_palm_ori=po.grad.numpy(),
+        links=np.array(IIWA7_TIPS), offsets=np.asarray(offs), pairs=np.asarray(IIWA7_PAIRS),
+        coll_cost=cost.detach().numpy(), coll_grad_q=qc.grad.numpy(), coll_grad_palm=pc.grad.numpy())
+    print("closure", name, float(loss), "collision non-zero", int((cost.detach() != 0).sum()), "of", E)
+
+
+def gen_results(ns):
+    """The reference's own optimiser outputs (data/*_<exp>.npy), as data for the results check."""
+    for exp in ("lego", "realsense"):
+        arrs = {k: np.load(os.path.join(ns.ref, "data", f"{k}_{exp}.npy"))
+                for k in ("contact", "target", "wrist", "compliance", "joint_angle")}
+        np.savez_compressed(os.path.join(OUT, f"results_{exp}.npz"), **arrs)
+        print("results", exp, {k: v.shape for k, v in arrs.items()})
+
+
 def main():
     ns = _refload.load()
     torch = ns.torch
     torch.set_num_threads(8)
-    what = sys.argv[1:] or ["gpis", "fk", "closure", "optimize", "collision", "force_eq", "modes"]
+    what = sys.argv[1:] or ["gpis", "fk", "closure", "optimize", "collision", "force_eq", "modes", "box", "normals",
+                            "iiwa7", "results"]
     if "gpis" in what:
         gen_gpis(ns)
     if "fk" in what:
@@ -452,6 +595,15 @@ def main():
         gen_collision(ns, "leap_e64", "leap", 64, 31)
     if "optimize" in what:
         gen_optimize(ns, "allegro_banana_e6", "allegro", "banana", 6, 20, 30)
+    if "box" in what:
+        gen_gpis_box(ns)
+    if "normals" in what:
+        gen_normals(ns)
+    if "iiwa7" in what:
+        gen_closure_iiwa7(ns, "iiwa7_banana_e16", 16, 70)
+        gen_closure_iiwa7(ns, "iiwa7_mug_e16", 16, 71, gpis_name="mug")
+    if "results" in what:
+        gen_results(ns)
 
 
 if __name__ == "__main__":

@@ -8,8 +8,11 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from compliancedex_amd.distributed import (all_gather_survivors, pack_survivors, record_width, shard_range,
-                                           unpack_records)
+import numpy as np
+
+from compliancedex_amd.anneal import PregraspAnnealer, anneal_sharded
+from compliancedex_amd.distributed import (all_gather_survivors, default_capacity, optimize_sharded, overflow,
+                                           pack_survivors, record_width, shard_range, unpack_records)
 
 
 def test_shard_range_covers_exactly():
@@ -78,8 +81,105 @@ def test_all_gather_survivors_gloo_world2():
         d = _local(r)
         lo, _ = shard_range(20, r, 2)
         expect.append(unpack_records([pack_survivors(16, 7, r, lo, **d)]).numpy())
-    import numpy as np
     full = np.concatenate(expect)
     for r in range(2):
         assert np.array_equal(res[r], full)
     assert set(full[:, 1]) <= {0.0, 1.0}
+
+
+def test_pack_header_counts_overflow():
+    d = _local(0, E=40)
+    n_surv = int((d["margin"] > 0).all(1).sum())
+    assert n_surv > 3
+    buf = pack_survivors(3, 0, 0, 0, **d)
+    assert int(buf[0, 0]) == 3 and int(buf[0, 1]) == n_surv and int(buf[0, 2]) == 3
+    assert overflow([buf]) == [n_surv - 3]
+    assert unpack_records([buf]).shape[0] == 3
+    full = pack_survivors(40, 0, 0, 0, **d)
+    assert overflow([full]) == [0]
+
+
+def test_default_capacity_is_rank_independent():
+    for total in (1, 21, 4096, 65537):
+        for world in (1, 2, 3, 8):
+            cap = default_capacity(total, world)
+            assert all(cap >= b - a for a, b in (shard_range(total, r, world) for r in range(world)))
+            assert cap == max(b - a for a, b in (shard_range(total, r, world) for r in range(world)))
+
+
+class _ScriptedOpt:
+    """Duck-typed inner optimiser whose result depends on each candidate's own row only."""
+    num_iters = 30
+
+    def __init__(self, palm):
+        self.palm_offset = palm
+        self.seen_palm = None
+
+    def optimize(self, q, target, comp, mu, gpis, verbose=False, init_palm=None):
+        palm = init_palm if init_palm is not None else self.palm_offset
+        self.seen_palm = palm.clone()
+        margin = torch.stack([q[:, 0] - 0.3, q[:, 1] - 0.2, q[:, 2] + 1, q[:, 3] + 1], 1)
+        self.best_loss = q.sum(1)
+        return q + 1, comp * 2, target, palm.clone(), margin
+
+
+TOTAL = 21  # odd: shards of 11 and 10 candidates
+
+
+def _global_inputs():
+    g = torch.Generator().manual_seed(5)
+    f64 = dict(dtype=torch.float64)
+    return dict(q=torch.rand(TOTAL, 16, generator=g, **f64), target=torch.rand(TOTAL, 4, 3, generator=g, **f64),
+                comp=torch.rand(TOTAL, 4, generator=g, **f64), palm=torch.arange(TOTAL * 6, **f64).view(TOTAL, 6))
+
+
+def _run_sharded(kind):
+    x = _global_inputs()
+    if kind == "optimize":
+        opt = _ScriptedOpt(x["palm"])
+        res, rec = optimize_sharded(opt, None, x["q"], x["target"], x["comp"], 1, object_id=2)
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        lo, hi = shard_range(TOTAL, rank, world)
+        assert torch.equal(opt.palm_offset, x["palm"])            # restored after the call
+        assert torch.equal(opt.seen_palm, x["palm"][lo:hi])       # the rank's own palm rows
+        return rec
+    ann = PregraspAnnealer(_ScriptedOpt(x["palm"]), None, q_sigma=0.0, palm_pos_sigma=0.0, palm_ori_sigma=0.0)
+    best, rec = anneal_sharded(ann, x["q"], x["target"], x["comp"], x["palm"], outer_steps=1, object_id=4)
+    return rec
+
+
+def _sharded_worker(rank, world, port, q, kind):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _run_sharded(kind).numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["optimize", "anneal"])
+def test_sharded_gloo_world2_equals_world1(kind):
+    """optimize_sharded / anneal_sharded over 2 gloo ranks with an odd candidate count (unequal
+    shards, equal buffers): every rank gathers exactly the world-1 records (candidate ids are
+    global, palm rows the candidate's own)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, q, kind)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _run_sharded(kind).numpy()
+    assert ref.shape[0] > 3
+    x = _global_inputs()
+    cand = ref[:, 2].astype(int)
+    assert np.array_equal(ref[:, -6:], x["palm"].numpy()[cand])
+    for r in range(2):
+        # the rank column differs (world 1 has only rank 0); every other field is identical
+        assert np.array_equal(np.delete(res[r], 1, axis=1), np.delete(ref, 1, axis=1))
+        lo, _ = shard_range(TOTAL, 1, 2)
+        assert np.array_equal(res[r][:, 1], (res[r][:, 2] >= lo).astype(float))

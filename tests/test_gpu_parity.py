@@ -11,14 +11,20 @@ import numpy as np
 import pytest
 import torch
 
-from tests._helpers import DATA, golden, golden_names, oracle_gpis, oracle_problem, rel_err
+from tests._helpers import DATA, assert_rel, golden, golden_names, oracle_gpis, oracle_problem, rel_err
 
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
 GPIS_CASES = [n[len("gpis_"):-4] for n in golden_names("gpis_")]
 FK_CASES = golden_names("fk_")
-CLOSURE_CASES = golden_names("closure_")
+CLOSURE_CASES = [n for n in golden_names("closure_") if not n.startswith("closure_iiwa7")]  # → test_gpu_configs
+GRADS = ("grad_q", "grad_comp", "grad_target", "grad_palm_pos", "grad_palm_ori")
+# ~10× the errors measured on MI355X (tools/parity_report.py, profiles/r02c_parity_errors.txt), capped at
+# north_star's 1e-4: vs the reference fixtures the gradients reach 1.7e-5 (Leap: f32 FK through the
+# detached-scale quaternion branch), so they stay at the bar
+TOL_CLOSURE_REF = dict(total_loss=1e-5, total_margin=2e-6, **{g: 1e-4 for g in GRADS})   # 7.7e-7, 1.6e-7, ≤ 1.7e-5
+TOL_CLOSURE_ORACLE = dict(total_loss=2e-7, total_margin=2e-6, **{g: 1e-5 for g in GRADS})  # 1.4e-8, 1.4e-7, ≤ 7.0e-7
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -30,7 +36,9 @@ def _gpu():
 
 
 def _gpis(state):
-    from compliancedex_amd.workloads import stored_gpis, synthetic_banana_gpis
+    from compliancedex_amd.workloads import box_gpis, stored_gpis, synthetic_banana_gpis
+    if state == "box":
+        return box_gpis(device=DEV)
     return synthetic_banana_gpis(2000, DEV) if state == "synthetic2000" else stored_gpis(state, DEV)
 
 
@@ -64,8 +72,8 @@ def test_gpis_pred_normal_vs_reference(state):
     X = torch.from_numpy(d["X"]).to(DEV).requires_grad_(True)
     mean, std = g.pred(X)
     ((mean * torch.from_numpy(d["cm"]).to(DEV)).sum() + (std * torch.from_numpy(d["cs"]).to(DEV)).sum()).backward()
-    # the synthetic state is refit on the device (cond(E11) ~ 1e7), stored states are loaded as is
-    tm = 1e-6 if state == "synthetic2000" else 1e-8
+    # the synthetic and box states are refit on the device (cond(E11) ~ 1e7), stored states are loaded as is
+    tm = 1e-6 if state in ("synthetic2000", "box") else 1e-8
     assert rel_err(mean.detach().cpu(), d["mean"]) < tm
     assert rel_err(std.detach().cpu(), d["std"]) < 1e-6
     assert rel_err(X.grad.cpu(), d["grad_X"]) < 1e-6
@@ -271,7 +279,7 @@ def test_closure_vs_reference(name):
     assert rel_err(out["pregrasp_tip"], d["pregrasp_tip"]) < 1e-6
     assert abs(out["loss"] - float(d["loss"])) <= 1e-4 * abs(float(d["loss"]))
     for k in ("total_loss", "total_margin", "grad_q", "grad_comp", "grad_target", "grad_palm_pos", "grad_palm_ori"):
-        assert rel_err(out[k], d[k]) < 1e-4, (k, rel_err(out[k], d[k]))
+        assert_rel(out[k], d[k], TOL_CLOSURE_REF[k], k)
     # bit-exact integer outputs vs the oracle: Kabsch det<0 mask and success flags
     from oracle.cdx_oracle import closure_with_grads
     ref = closure_with_grads(oracle_problem(str(d["hand"]), str(d["state"])), d["q"], d["comp"], d["target"],
@@ -303,7 +311,7 @@ def test_closure_large_batch_vs_oracle_chunk():
     assert ok.sum() >= 12
     for k in ("total_loss", "total_margin", "grad_q", "grad_comp", "grad_target", "grad_palm_pos", "grad_palm_ori"):
         a, b = out[k][sl][ok], ref[k][ok]
-        assert rel_err(a, b) < 1e-4, (k, rel_err(a, b))
+        assert_rel(a, b, TOL_CLOSURE_ORACLE[k], k)
     assert np.array_equal(out["flip"].reshape(3, E)[:, sl].reshape(-1).astype(bool), ref["flip"])
 
 
@@ -324,18 +332,56 @@ def test_closure_device_noise_is_deterministic_and_in_range():
     assert rel_err(outs[0], d["total_loss"]) < 1e-3  # different noise draw: only ~1e-5 effect
 
 
+def update_flags(trace, after=20):
+    """The reference's best-iterate masks (optimize_pregrasp.py:821-829): at step s > ``after``,
+    update_flag = total_loss_s < opt_value, opt_value ← where(update_flag, total_loss_s, opt_value).
+    (update_flag is computed at every step against the still-infinite opt_value, but only used
+    for s > 20.)  → bool [iters, E]."""
+    trace = np.asarray(trace)
+    best = np.full(trace.shape[1], np.inf)
+    flags = np.zeros(trace.shape, dtype=bool)
+    for s_, loss in enumerate(trace):
+        f = loss < best
+        if s_ > after:
+            best = np.where(f, loss, best)
+            flags[s_] = f
+    return flags
+
+
 @pytest.mark.parametrize("fused", [True, False])
 def test_optimize_vs_reference(fused):
+    """30 reference iterations with the replayed noise: final outputs 1e-4, and the best-iterate
+    update_flag of every iteration bit-exact (derived from each side's own per-iteration losses)."""
     d = golden("optimize_allegro_banana_e6.npz")
     iters = int(d["iters"])
     opt = _opt(str(d["hand"]), d["palm"], iters)
     g = _gpis(str(d["state"]))
     tape = [torch.from_numpy(n).to(DEV) for n in d["noise"]]
+    trace = []
+    if fused:
+        inner = opt._closure_into
+
+        def traced(*a, **k):
+            inner(*a, **k)
+            trace.append(a[7]["total_loss"].clone())
+        opt._closure_into = traced
+    else:
+        inner = opt.closure
+
+        def traced(*a, **k):
+            r = inner(*a, **k)
+            trace.append(opt.total_loss.clone())
+            return r
+        opt.closure = traced
     out = opt.optimize(torch.from_numpy(d["q"]).to(DEV), torch.from_numpy(d["target"]).to(DEV),
                        torch.from_numpy(d["comp"]).to(DEV), 1, g, verbose=False, noise_tape=tape, fused=fused)
     names = ["opt_q", "opt_comp", "opt_target", "opt_palm", "opt_margin"]
     for name, t in zip(names, out):
-        assert rel_err(t.detach().cpu().numpy(), d[name]) < 1e-4, (name, rel_err(t.detach().cpu().numpy(), d[name]))
+        assert_rel(t.detach().cpu().numpy(), d[name], 5e-6, name)  # measured ≤ 3.7e-7 (opt_target)
+    ours = torch.stack(trace).cpu().numpy()
+    assert ours.shape == d["loss_trace"].shape
+    assert_rel(ours, d["loss_trace"], 1e-6, "loss_trace")  # measured 5.0e-8
+    assert np.array_equal(update_flags(ours), update_flags(d["loss_trace"]))
 
 
 def _bitwise_equal_nan_aware(a, b):
@@ -442,9 +488,9 @@ def test_collision_vs_reference(name):
     c = cost.detach().cpu().numpy()
     assert np.array_equal(c != 0, d["cost"] != 0)
     # f32 FK anchors, 1/z and 1/d amplify last-ulp differences near the floor: north-star 1e-4 bar
-    assert rel_err(c, d["cost"]) < 1e-4
-    assert rel_err(q.grad.cpu(), d["grad_q"]) < 1e-4
-    assert rel_err(palm.grad.cpu(), d["grad_palm"]) < 1e-4
+    assert_rel(c, d["cost"], 5e-5, "cost")  # measured 3.9e-6
+    assert_rel(q.grad.cpu(), d["grad_q"], 1e-4, "grad_q")  # measured 6.4e-6
+    assert_rel(palm.grad.cpu(), d["grad_palm"], 1e-4, "grad_palm")  # measured 1.2e-5
 
 
 def test_closure_with_collision_adds_the_collision_term():
@@ -506,7 +552,7 @@ def test_force_eq_device_noise_replays_in_backward():
     reward.sum().backward()
     g_dev = tip.grad.clone()
     # the same rows with the reference's noise land within the 1e-6·noise perturbation
-    assert rel_err(reward.detach().cpu(), d["reward"]) < 1e-4
+    assert_rel(reward.detach().cpu(), d["reward"], 1e-4, "reward")
     assert torch.isfinite(g_dev).all()
 
 
@@ -578,3 +624,30 @@ def test_optimize_graph_replay_matches_eager():
         for x, y in zip(a, b):
             assert torch.equal(torch.nan_to_num(x, nan=7.0), torch.nan_to_num(y, nan=7.0))
     assert torch.isfinite(outs["graph"][1][5]).sum() > E // 2
+
+
+def test_graph_replay_survives_workspace_growth_and_new_state():
+    """A cached hipGraph owns its workspace and pins the GPIS state it captured: a closure with a
+    larger E (which regrows the optimiser's own workspace) and a switch to another GPIS between
+    capture and replay leave the replay bit-identical to the same call sequence run eagerly."""
+    from compliancedex_amd.workloads import prob_inputs
+    from compliancedex_amd.urdf import load_robot
+    cfg = load_robot("allegro")["config"]
+    E = 64
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=23, spread=True)
+    t = [torch.from_numpy(a).to(DEV) for a in (q, target, comp)]
+    g, g_mug = _gpis("banana"), _gpis("mug")
+    big = 4 * E
+    qb, cb, tb, pb = prob_inputs(cfg["ref_q"], big, seed=24, spread=True)
+    outs = {}
+    for mode in ("eager", "graph"):
+        opt = _opt("allegro", palm, iters=25)
+        opt.optimize(*t, 1, g, verbose=False, graph=(mode == "graph"))          # graph: capture
+        opt.palm_offset, saved = torch.from_numpy(pb).to(DEV), opt.palm_offset
+        xs = [torch.from_numpy(a).to(DEV).requires_grad_(True) for a in (qb, cb, tb, pb[:, :3], pb[:, 3:])]
+        opt.closure(*xs, 1, g_mug, big)                 # regrows opt._ws, switches the problem's state
+        opt.palm_offset = saved
+        torch.cuda.synchronize()
+        outs[mode] = opt.optimize(*t, 1, g, verbose=False, graph=(mode == "graph"))  # graph: replay
+    for a, b in zip(outs["eager"], outs["graph"]):
+        assert torch.equal(torch.nan_to_num(a, nan=7.0), torch.nan_to_num(b, nan=7.0))

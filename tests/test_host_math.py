@@ -44,7 +44,7 @@ def test_svd3_accuracy():
 @pytest.mark.parametrize("name", CLOSURE_CASES)
 def test_closure_host_vs_reference(name):
     d = golden(name)
-    prob = host_problem(str(d["hand"]))
+    prob = host_problem(str(d["hand"]), d)
     X = _host.closure_queries(prob, d["q"], d["target"], d["palm"])
     E, T = d["q"].shape[0], prob.chain.n_tips
     pre = X[(prob.n_query_levels + 1) * E * T:(prob.n_query_levels + 2) * E * T].reshape(E, T, 3)

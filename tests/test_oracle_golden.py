@@ -9,6 +9,7 @@ from tests._helpers import golden, golden_names, oracle_chain, oracle_gpis, orac
 GPIS_CASES = [n[len("gpis_"):-4] for n in golden_names("gpis_")]
 FK_CASES = golden_names("fk_")
 CLOSURE_CASES = golden_names("closure_")
+NORMAL_CASES = golden_names("normals_")
 
 
 @pytest.mark.parametrize("state", GPIS_CASES)
@@ -45,10 +46,71 @@ def test_fk(name):
 def test_closure(name):
     from oracle.cdx_oracle import closure_with_grads
     d = golden(name)
-    prob = oracle_problem(str(d["hand"]), str(d["state"]))
+    prob = oracle_problem(str(d["hand"]), str(d["state"]), d)
     out = closure_with_grads(prob, d["q"], d["comp"], d["target"], d["palm"], d["noise"][0])
     assert rel_err(out["pregrasp_tip"], d["pregrasp_tip"]) < 1e-9
     assert rel_err(out["total_loss"], d["total_loss"]) < 1e-8
     assert rel_err(out["total_margin"], d["total_margin"]) < 1e-8
     for k in ("grad_q", "grad_comp", "grad_target", "grad_palm_pos", "grad_palm_ori"):
         assert rel_err(out[k], d[k]) < 1e-6, k
+
+
+@pytest.mark.parametrize("name", [n for n in CLOSURE_CASES if n.startswith("closure_iiwa7")])
+def test_collision_iiwa7(name):
+    """compute_collision_loss on the 23-DOF chain, fingertip anchors, all six pairs (:671-701)."""
+    from oracle.cdx_oracle import collision_loss
+    d = golden(name)
+    chain, _ = oracle_chain("iiwa7_allegro")
+    q = torch.from_numpy(d["q"]).requires_grad_(True)
+    palm = torch.from_numpy(d["palm"]).requires_grad_(True)
+    cost = collision_loss(chain, [str(s) for s in d["links"]], d["offsets"].tolist(), d["pairs"], q, palm)
+    cost.sum().backward()
+    assert rel_err(cost.detach(), d["coll_cost"]) < 1e-12
+    assert rel_err(q.grad, d["coll_grad_q"]) < 1e-6  # f32 FK backward: 6e-8 measured
+    assert rel_err(palm.grad, d["coll_grad_palm"]) < 1e-12
+
+
+@pytest.mark.parametrize("name", golden_names("collision_"))
+def test_collision(name):
+    from oracle.cdx_oracle import collision_loss
+    d = golden(name)
+    hand = str(d["hand"])
+    chain, c = oracle_chain(hand)
+    cfg = c["config"]
+    q = torch.from_numpy(d["q"]).requires_grad_(True)
+    palm = torch.from_numpy(d["palm"]).requires_grad_(True)
+    cost = collision_loss(chain, cfg["collision_links"], cfg["collision_offsets"], cfg["collision_pairs"], q, palm)
+    cost.sum().backward()
+    assert rel_err(cost.detach(), d["cost"]) < 1e-12
+    assert rel_err(q.grad, d["grad_q"]) < 1e-6
+    assert rel_err(palm.grad, d["grad_palm"]) < 1e-12
+
+
+@pytest.mark.parametrize("name", NORMAL_CASES)
+def test_normals_index_and_multinormals(name):
+    """compute_normal(X, index) and compute_multinormals (gpis.py:63-111)."""
+    d = golden(name)
+    g = oracle_gpis(name[len("normals_"):-4])
+    X = torch.from_numpy(d["X"])
+    for i in range(3):
+        nrm, w = g.compute_normal(X, d[f"index{i}"].tolist())
+        assert rel_err(nrm, d[f"normal_index{i}"]) < 1e-12
+        assert abs(float(w) - float(d[f"weight_index{i}"])) <= 1e-9 * abs(float(d[f"weight_index{i}"]))
+    for S in (3, 5):
+        for dim in (2, 3):
+            Xd = X if dim == 2 else X.view(-1, 4, 3)
+            nrms, ws = g.compute_multinormals(Xd, S)
+            assert nrms.shape == d[f"multi{S}_{dim}d_normals"].shape
+            assert rel_err(nrms, d[f"multi{S}_{dim}d_normals"]) < 1e-12
+            assert rel_err(ws, d[f"multi{S}_{dim}d_weights"]) < 1e-9
+
+
+@pytest.mark.parametrize("exp", ["lego", "realsense"])
+def test_reference_results_are_allegro_fk(exp):
+    """The reference's own saved outputs: contact = forward_kinematics(joint_angle, wrist) with the
+    Allegro config offsets (optimize_pregrasp.py:1009, :1016-1020).  The files were written by the
+    reference on a CUDA device: f32 FK rounding, 1.0e-7 relative measured → 1e-6."""
+    d = golden(f"results_{exp}.npz")
+    prob = oracle_problem("allegro", "banana")
+    out = prob.forward_kinematics(torch.from_numpy(d["joint_angle"]), torch.from_numpy(d["wrist"]))
+    assert rel_err(out.detach(), d["contact"]) < 1e-6

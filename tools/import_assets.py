@@ -7,6 +7,10 @@
                                           TorchSDF test models cube / sphere-42)
   compliancedex_amd/data/meshes/banana_mesh.npz        banana vertices (f64) + triangles
   compliancedex_amd/data/banana_center.npy, partial_pcd_banana.npy
+  compliancedex_amd/data/config3_surface.npz           config 3's N = 2000 GPIS surfaces: 1 936 points per
+                                          object sampled area-weighted from assets/<obj>/<obj>.obj
+                                          (hammer, lego, mug, mug2) or drawn from the observed point
+                                          cloud (assets/coffeebottle/completed_pcd.npz), seeded
 
 Run: ``python tools/import_assets.py`` (reads /root/reference; the GPU box never needs it).
 """
@@ -63,7 +67,33 @@ def obj_faces(path):
     return vs, fs
 
 
+def sample_surface(vs, fs, n, rng):
+    """Area-weighted uniform samples on a triangle mesh."""
+    tri = vs[fs]
+    area = 0.5 * np.linalg.norm(np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]), axis=1)
+    pick = rng.choice(len(fs), n, p=area / area.sum())
+    u, v = rng.random(n), rng.random(n)
+    flip = u + v > 1
+    u[flip], v[flip] = 1 - u[flip], 1 - v[flip]
+    t = tri[pick]
+    return t[:, 0] + u[:, None] * (t[:, 1] - t[:, 0]) + v[:, None] * (t[:, 2] - t[:, 0])
+
+
+def config3_surfaces(n=1936):
+    rng = np.random.default_rng(3)
+    out = {}
+    for obj in ("hammer", "lego", "mug", "mug2"):
+        vs, fs = obj_faces(os.path.join(REF, "assets", obj, f"{obj}.obj"))
+        out[obj] = sample_surface(vs, fs, n, rng)
+    obs = np.load(os.path.join(REF, "assets/coffeebottle/completed_pcd.npz"))["observed"]
+    out["coffeebottle"] = obs[rng.choice(len(obs), n, replace=False)].astype(np.float64)
+    np.savez_compressed(os.path.join(PKG, "data", "config3_surface.npz"), **out)
+    print("config3 surfaces", {k: v.shape for k, v in out.items()})
+
+
 def main():
+    if sys.argv[1:] == ["config3"]:
+        return config3_surfaces()
     os.makedirs(os.path.join(PKG, "robots"), exist_ok=True)
     for robot, rel in URDFS.items():
         chain = parse_urdf(os.path.join(REF, rel))
@@ -94,6 +124,7 @@ def main():
             np.save(os.path.join(PKG, "data", "banana_center.npy"), 0.5 * (vs.min(0) + vs.max(0)))
         print("mesh", name, fs.shape)
     shutil.copyfile(os.path.join(REF, "partial_pcd/banana.npy"), os.path.join(PKG, "data", "partial_pcd_banana.npy"))
+    config3_surfaces()
 
 
 if __name__ == "__main__":
