@@ -186,12 +186,12 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    ms = (ctypes.c_double * 5)()
-    cnt = (ctypes.c_int64 * 5)()
+    ms = (ctypes.c_double * N.PROF_STAGES)()
+    cnt = (ctypes.c_int64 * N.PROF_STAGES)()
     N.check(lib.cdx_profile_read(ms, cnt), "cdx_profile_read")
     # stage split (informational): every stage timed over a short extra pass, outside the timed region
-    ms_all = (ctypes.c_double * 5)()
-    cnt_all = (ctypes.c_int64 * 5)()
+    ms_all = (ctypes.c_double * N.PROF_STAGES)()
+    cnt_all = (ctypes.c_int64 * N.PROF_STAGES)()
     N.check(lib.cdx_profile_enable(0x1F), "cdx_profile_enable")
     for _ in range(min(10, args.steps)):
         step()

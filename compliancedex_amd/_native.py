@@ -15,6 +15,7 @@ LIB_DIR = os.path.join(_HERE, "lib")
 MAX_BODIES, MAX_TIPS, MAX_DOFS, MAX_LEVELS = 32, 8, 32, 4
 KERNELS = {"tps": 0, "rbf": 1, "joint": 2}
 NPAD_ALIGN = 256  # CDX_NPAD_ALIGN
+PROF_STAGES = 6   # cdx_profile_read array length
 ERRORS = {-1: "invalid argument", -2: "unsupported GPIS kernel", -3: "chain exceeds descriptor capacity",
           -10: "HIP launch failed"}
 
@@ -23,7 +24,7 @@ class CdxGpis(C.Structure):
     _fields_ = [("X1", C.c_void_p), ("alpha", C.c_void_p), ("Ainv", C.c_void_p), ("Linv_t", C.c_void_p),
                 ("Linv", C.c_void_p), ("N", C.c_int32),
                 ("N_pad", C.c_int32), ("kernel", C.c_int32), ("_pad", C.c_int32), ("R", C.c_double),
-                ("sigma", C.c_double), ("bias", C.c_double)]
+                ("sigma", C.c_double), ("bias", C.c_double), ("screen", C.c_void_p), ("screen_delta", C.c_double)]
 
 
 class CdxBody(C.Structure):
@@ -81,6 +82,10 @@ _SIGS = {
     "cdx_gpis_mean": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P, _P]),
     "cdx_gpis_std_workspace": (C.c_size_t, [C.POINTER(CdxGpis), _I64]),
     "cdx_gpis_std": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P, _P]),
+    "cdx_gpis_screen_bytes": (C.c_size_t, [C.c_int32]),
+    "cdx_gpis_screen_prepare": (C.c_int, [C.POINTER(CdxGpis), _P, _P]),
+    "cdx_gpis_screen_workspace": (C.c_size_t, [C.POINTER(CdxGpis), _I64]),
+    "cdx_gpis_screen_var": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P]),
     "cdx_gpis_fit": (C.c_int, [_P, C.c_int32, _P, C.c_int32, C.c_double, _P, _P, _P]),
     "cdx_gpis_factor_workspace": (C.c_size_t, [C.c_int32]),
     "cdx_gpis_factor": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P, _P]),
@@ -92,6 +97,7 @@ _SIGS = {
                                         _P, _P]),
     "cdx_collision_loss": (C.c_int, [C.POINTER(CdxCollision), _I64, _P, _P, _P, _P, _P, _P, _P, C.c_int32, _P]),
     "cdx_closure_workspace": (C.c_size_t, [C.POINTER(CdxProblem), _I64]),
+    "cdx_closure_screen_stats": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, C.POINTER(C.c_int32)]),
     "cdx_closure": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, _P, _P, _P, _P, _P, C.c_uint64, _P,
                               _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cdx_sdf_forward": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),

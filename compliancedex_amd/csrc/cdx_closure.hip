@@ -20,6 +20,7 @@
 #include "cdx_cost.h"
 #include "cdx_gpis_launch.h"
 #include "cdx_prof.h"
+#include "cdx_screen.h"
 
 namespace {
 
@@ -411,8 +412,22 @@ struct ClosureWs {
   double *X, *mean, *gmean, *normal, *std_, *var, *gstd, *Xg, *lvl, *V;
   int64_t* sel;
   void *var_ws, *grad_ws;
+  // split-precision screening (screen_on): estimates, list positions, the kept-row list, per-group
+  // keep masks, stats [refined extra rows, bound misses], ∇std V rows, screen / refine scratch
+  double* sv2;
+  int *vpos, *rows, *stats;
+  unsigned char* keep;
+  int64_t* vrow;
+  void *screen_ws, *refine_ws;
   size_t bytes;
 };
+
+// The closure screens the all-tip rows with the bf16 estimate when the GPIS state carries a
+// calibrated screen (cdx_gpis_screen_prepare + screen_delta) and CDX_NO_SCREEN is unset.
+bool screen_on(const cdx_problem* p) {
+  static const bool off = getenv("CDX_NO_SCREEN") != nullptr;
+  return !off && p->gpis.screen && p->gpis.screen_delta > 0 && p->chain.n_tips <= CDX_MAX_TIPS;
+}
 
 // The variance cost takes max_f log(100·std_f) (:730), so ∇std is only ever needed at one
 // fingertip per (distinct level, candidate): the std finalize picks it exactly as level_fwd_bwd
@@ -434,8 +449,17 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   w.gstd = (double*)take(Ms * 3 * sizeof(double));
   w.sel = (int64_t*)take(Mg * sizeof(int64_t));
   w.Xg = (double*)take(Mg * 3 * sizeof(double));
-  w.var_ws = take(cdx::gpis_var_ws_bytes(p->gpis, Ms));
+  const bool scr = screen_on(p);
+  w.var_ws = scr ? nullptr : take(cdx::gpis_var_ws_bytes(p->gpis, Ms));
   w.grad_ws = take(cdx::gpis_grad_ws_bytes(p->gpis, Mg));
+  w.sv2 = scr ? (double*)take(Ms * sizeof(double)) : nullptr;
+  w.vpos = scr ? (int*)take(Ms * sizeof(int)) : nullptr;
+  w.rows = scr ? (int*)take(Ms * sizeof(int)) : nullptr;
+  w.stats = scr ? (int*)take(4 * sizeof(int)) : nullptr;
+  w.keep = scr ? (unsigned char*)take(Mg) : nullptr;
+  w.vrow = scr ? (int64_t*)take(Mg * sizeof(int64_t)) : nullptr;
+  w.screen_ws = scr ? take(cdx::screen_ws_bytes(p->gpis, Ms)) : nullptr;
+  w.refine_ws = scr ? take(cdx::gpis_refine_ws_bytes(p->gpis, Ms)) : nullptr;
   w.lvl = (double*)take((size_t)p->n_levels * E * level_record_width(p->chain.n_tips) * sizeof(double));
 #if !defined(CDX_GRAD_EXPLICIT)
   w.V = (double*)take(cdx::gpis_v_bytes(p->gpis, Ms));
@@ -566,11 +590,29 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   // whitened std at every all-tip query, keeping V = (L⁻¹K*ᵀ)ᵀ for the ∇std pass
   // … and the ∇std fingertip of each (distinct level, candidate): the all-tip rows q_alltip(u, e, f)
   // = (u·E + e)·T + f form groups of T, selected in the std finalize
-  const cdx::VarSelect vs{p->chain.n_tips, w.sel, w.Xg};
-  rc = cdx::gpis_var_launch(p->gpis, w.X, Ms, w.std_, w.var, w.var_ws, s, w.V, &vs);
-  if (rc) return rc;
   const int64_t Mg = (int64_t)p->n_query_levels * E;
-  rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V);
+  if (screen_on(p)) {
+    // bf16 screen of every all-tip row → exact whitened fp64 pass for the fingertips that can still
+    // be their group's maximum (≈ 1 per group) → ∇std at the group's maximum from its kept V row
+    const int T = p->chain.n_tips;
+    cdx::prof_mark(cdx::PROF_SCREEN, true, s);
+    rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.stats, s);
+    cdx::prof_mark(cdx::PROF_SCREEN, false, s);
+    if (rc) return rc;
+    double* rpart = nullptr;
+    int64_t rpad = 0;
+    rc = cdx::gpis_refine_launch(p->gpis, w.X, w.rows, w.stats, (int)Mg, Ms, w.refine_ws, w.V, s, &rpart, &rpad);
+    if (rc) return rc;
+    rc = cdx::refine_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.sv2, w.vpos, w.std_, w.var, w.sel, w.Xg,
+                                   w.vrow, w.stats, s);
+    if (rc) return rc;
+    rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V, w.vrow);
+  } else {
+    const cdx::VarSelect vs{p->chain.n_tips, w.sel, w.Xg};
+    rc = cdx::gpis_var_launch(p->gpis, w.X, Ms, w.std_, w.var, w.var_ws, s, w.V, &vs);
+    if (rc) return rc;
+    rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V);
+  }
   if (rc) return rc;
   GpisView gv;
   gv.mean = w.mean; gv.gmean = w.gmean; gv.normal = w.normal; gv.std_ = w.std_; gv.gstd = w.gstd;
@@ -611,6 +653,21 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   }
   cdx::prof_mark(cdx::PROF_COST, false, s);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+int cdx_closure_screen_stats(const cdx_problem* p, int64_t E, const void* workspace, int32_t* out) {
+  if (!problem_ok(p) || E <= 0 || !workspace || !out) return CDX_EINVAL;
+  if (!screen_on(p)) {
+    out[0] = out[1] = out[2] = -1;
+    return CDX_OK;
+  }
+  ClosureWs w = closure_ws_layout(p, E, static_cast<char*>(const_cast<void*>(workspace)));
+  int st[2] = {0, 0};
+  if (hipMemcpy(st, w.stats, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess) return CDX_ELAUNCH;
+  out[0] = (int32_t)((int64_t)p->n_query_levels * E + st[0]);  // rows of the exact pass
+  out[1] = st[1];                                                // estimates off by more than Δ
+  out[2] = (int32_t)((int64_t)p->n_query_levels * E * p->chain.n_tips);  // all-tip rows screened
+  return CDX_OK;
 }
 
 const char* cdx_version(void) { return "compliancedex_amd 0.1 gfx950"; }

@@ -135,7 +135,20 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 //   instead of 2N²; launched as equal pieces of each query tile's K-sequence (below).
 // The triangular modes' tile costs run 1..Nt K-sweeps: stripes are paired heavy+light per XCD.
 // (A v_mfma_f64_4x4x4_4b_f64 variant ran no faster — LDS-read-bound, profiles/r01_std_gemm_variants.md.)
-enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2 };
+// MODE_VARL (the closure's refine pass behind the split-precision screen): MODE_VAR over a device-
+//   side row list (rows rl.rows[0 .. G + *rl.extra) of X; V row / partial row = list position),
+//   cut into gridDim.x equal pieces of the concatenated K-sequence of all (query tile, stripe)
+//   pairs: a piece's segments that cover a whole stripe finish their epilogue in place, a stripe
+//   cut by piece boundaries leaves partial V tiles in rl.slots (slot 0: the piece's first segment,
+//   1: its last) that gpis_var_merge sums in piece order.
+enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2, MODE_VARL = 3 };
+
+struct RefineList {
+  const int* rows;    // query index per list position
+  const int* extra;   // device count of positions past the G primary ones
+  int G;
+  double* slots;      // [gridDim.x][2][ST_BM][ST_BN] partial V tiles of cut stripes
+};
 
 // Whitened pass A operand: K* generated on chip per stripe (default), or read from a buffer
 // gpis_kstar_kernel wrote (CDX_VAR_KLOAD).  On chip, each K* entry is regenerated by every stripe
@@ -194,14 +207,17 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
                                                                 double* __restrict__ partial, int64_t M_pad, int Mt,
                                                                 int Nt, double* __restrict__ vout,
                                                                 const double* __restrict__ vin,
-                                                                const int64_t* __restrict__ vsel, int parts) {
-  constexpr bool VAR = MODE == MODE_VAR;
+                                                                const int64_t* __restrict__ vsel, int parts,
+                                                                RefineList rl) {
+  constexpr bool LIST = MODE == MODE_VARL;
+  constexpr bool VAR = MODE == MODE_VAR || LIST;
   constexpr bool TRI = MODE != MODE_GRAD;
   constexpr bool GEN = MODE == MODE_GRAD || (VAR && !VAR_KLOAD);  // A tile generated on chip (else loaded from vin)
   __shared__ __attribute__((aligned(16))) double smem[ST_SMEM];
   double* xq = smem + ST_NBUF * (ST_TILE + ST_BTILE);
   double* xs = xq + ST_BM * 3;  // [2][ST_XS]: X1 rows of the stage generated next
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t Mrows = LIST ? (int64_t)rl.G + *rl.extra : M;  // rows of this launch (list: device count)
 #if defined(CDX_DIAG_WGTIME)
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -209,7 +225,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
   const int Np = g.N_pad;
   const int vsh = MODE == MODE_GRAD ? 0 : var_shift(g.N, Np);  // VAR: B column shift; GRADV: V column shift
-  const double* __restrict__ Bop = MODE == MODE_VAR ? g.Linv_t : (MODE == MODE_GRADV ? g.Linv : g.Ainv);
+  const double* __restrict__ Bop = VAR ? g.Linv_t : (MODE == MODE_GRADV ? g.Linv : g.Ainv);
   // K* generation: thread → query row gm, GEN_PER k-columns starting at gk (wave-uniform)
   constexpr int GEN_PER = ST_BM * ST_BK / ST_THREADS;  // 4
   static_assert(GEN_PER == 4, "the substep schedule below spreads 4 generated entries over 3 substeps");
@@ -229,13 +245,14 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   const int wr = (wave / ST_WN) * 64, wc = __builtin_amdgcn_readfirstlane(cwave * 64);
 
   // One (query tile mt, stripe nt, K-rows [kbeg, kend)) product and its epilogue into slot pslot.
-  auto tile = [&](int mt, int nt, int kbeg, int kend, int pslot) {
+  auto tile = [&](int mt, int nt, int kbeg, int kend, int pslot, bool full = true) {
   const int64_t m0 = (int64_t)mt * ST_BM;
   const int n0 = nt * ST_BN;
   double qx, qy, qz;
   const double* vrow = nullptr;  // MODE_GRADV: this thread's row of the stored V
   {
-    const int64_t m = min(m0 + gm, M - 1);  // pad rows replicate a valid query
+    int64_t m = min(m0 + gm, Mrows - 1);  // pad rows replicate a valid query
+    if (LIST) m = rl.rows[m];
     qx = X[3 * m]; qy = X[3 * m + 1]; qz = X[3 * m + 2];
     if (tid < ST_BM) { xq[3 * tid] = qx; xq[3 * tid + 1] = qy; xq[3 * tid + 2] = qz; }
     if (!GEN) vrow = vin + (vsel ? vsel[m] : m) * (int64_t)Np;
@@ -383,7 +400,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   const int c0 = n0 + wc - (VAR ? vsh : 0);
   const int d0 = (kbeg - c0) >> 4;  // kbeg − c0 is a multiple of 16; wave-uniform
   int s = 0;
-  if constexpr (MODE == MODE_VAR) {
+  if constexpr (VAR) {
     for (const int e = min(nK, max(0, 1 - d0)); s < e; ++s) step(s, I0{}, I4{});
 #if !defined(CDX_STD_NODIAG)
     if (s < nK && s + d0 == 1) step(s++, I1{}, I4{});
@@ -411,7 +428,18 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     // 128 contiguous bytes).  Split-K launches (parts > 0) store their K-chunk's partial V tile to
     // partial[pslot = chunk][M_pad][N_pad] instead; gpis_var_splitk_finalize sums the chunks.
     double* red = smem;  // [ST_WN][ST_BM]
-    if (parts > 0) {
+    if (LIST && !full) {  // a cut stripe: this segment's partial V tile to its slot
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double* vr = rl.slots + ((int64_t)pslot * ST_BM + wr + 16 * i + (lane >> 4) + 4 * r) * ST_BN + wc + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vr[16 * j] = acc[i][j][r];
+        }
+      return;
+    }
+    if (!LIST && parts > 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -526,6 +554,31 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   }
   };  // tile
 
+  if constexpr (LIST) {
+    // pieces of the concatenated K-sequence of all (query tile, stripe) pairs, tile-major
+    const int MtL = (int)((Mrows + ST_BM - 1) / ST_BM);
+    int W = 0;
+    for (int t = 0; t < Nt; ++t) W += var_ksteps(t, g.N, Np);
+    const int64_t total = (int64_t)MtL * W;
+    const int64_t q0 = total * b / gridDim.x, q1 = total * (b + 1) / gridDim.x;
+    bool first = true;
+    for (int64_t q = q0; q < q1;) {
+      const int mt = (int)(q / W);
+      const int r = (int)(q - (int64_t)mt * W);
+      int nt = 0, s0 = 0;
+      while (s0 + var_ksteps(nt, g.N, Np) <= r) s0 += var_ksteps(nt++, g.N, Np);
+      const int s1 = s0 + var_ksteps(nt, g.N, Np);
+      const int64_t e = min(q1, (int64_t)mt * W + s1);
+      const int hi = min(g.N, nt * ST_BN + ST_BN - vsh);
+      const int kbeg = (r - s0) * ST_BK, kend = min(hi, (int)(e - (int64_t)mt * W - s0) * ST_BK);
+      const bool full = r == s0 && e == (int64_t)mt * W + s1;
+      if (!first) __syncthreads();  // the previous segment's epilogue used the stage buffers
+      first = false;
+      tile(mt, nt, kbeg, kend, full ? nt : 2 * b + (q == q0 ? 0 : 1), full);
+      q = e;
+    }
+    return;
+  }
   if (MODE == MODE_GRADV) {
     const int U = Mt * parts;
     const int t = (U & 7) == 0 ? (b & 7) * (U >> 3) + (b >> 3) : b;  // each XCD: one K-range, many tiles
@@ -719,6 +772,56 @@ __global__ __launch_bounds__(256) void gpis_var_splitk_finalize(cdx_gpis g, cons
   }
 }
 
+// Refine pass (MODE_VARL), cut stripes: workgroup p finishes the stripe whose K-range ends inside
+// piece p after starting in an earlier one — V = its partial tiles summed in piece order, stored at
+// the list positions, and Σ V² per row into partial[nt][position] (4 waves, 4 columns per lane).
+__global__ __launch_bounds__(256) void gpis_var_merge(cdx_gpis g, RefineList rl, int64_t M_pad,
+                                                      double* __restrict__ partial, double* __restrict__ vout) {
+  const int Np = g.N_pad, Nt = Np / ST_BN;
+  const int64_t Mrows = (int64_t)rl.G + *rl.extra;
+  const int MtL = (int)((Mrows + ST_BM - 1) / ST_BM);
+  int W = 0;
+  for (int t = 0; t < Nt; ++t) W += var_ksteps(t, g.N, Np);
+  const int64_t total = (int64_t)MtL * W;
+  const int pieces = gridDim.x, p = blockIdx.x;
+  auto qof = [&](int pp) { return total * pp / pieces; };
+  const int64_t q0 = qof(p), q1 = qof(p + 1);
+  if (q0 >= q1 || q0 >= total) return;
+  const int mt = (int)(q0 / W);
+  const int r = (int)(q0 - (int64_t)mt * W);
+  int nt = 0, s0 = 0;
+  while (s0 + var_ksteps(nt, g.N, Np) <= r) s0 += var_ksteps(nt++, g.N, Np);
+  const int64_t S0 = (int64_t)mt * W + s0, S1 = S0 + var_ksteps(nt, g.N, Np);
+  if (!(S0 < q0 && S1 <= q1)) return;
+  int pf = p;
+  while (pf > 0 && qof(pf) > S0) --pf;  // the stripe's first piece (possibly an empty one before it)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int row = wave; row < ST_BM; row += 4) {
+    double v[4] = {0, 0, 0, 0};
+    for (int pp = pf; pp <= p; ++pp) {
+      // this stripe's segment in piece pp (empty pieces — fewer K-steps than pieces — hold none);
+      // slot 0 if it is the piece's first segment, else 1 (gpis_std_kernel<VARL>'s rule)
+      const int64_t a = max(qof(pp), S0), e = min(qof(pp + 1), S1);
+      if (a >= e) continue;
+      const int slot = 2 * pp + (a == qof(pp) ? 0 : 1);
+      const double* src = rl.slots + ((int64_t)slot * ST_BM + row) * ST_BN + 4 * lane;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] += src[c];
+    }
+    const int64_t pos = (int64_t)mt * ST_BM + row;
+    double* dst = vout + pos * Np + nt * ST_BN + 4 * lane;
+    double sq = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      dst[c] = v[c];
+      sq = fma(v[c], v[c], sq);
+    }
+#pragma unroll
+    for (int w = 1; w < 64; w <<= 1) sq += __shfl_xor(sq, w);
+    if (lane == 0) partial[(int64_t)nt * M_pad + pos] = sq;
+  }
+}
+
 // Partial slots a ∇std launch wrote, in increasing order (host-computed, passed by value).
 constexpr int GRAD_MAX_SLOTS = 512;
 struct GradSlots {
@@ -837,7 +940,7 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
     for (int nt = 0; nt < n_tiles; ++nt) units += (var_ksteps(nt, g.N, g.N_pad) + chunk - 1) / chunk;
     prof_mark(PROF_GPIS_STD, true, s);
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * units)), dim3(ST_THREADS), 0, s,
-                       g, X, M, partial, M_pad, Mt, n_tiles, nullptr, kstar, nullptr, chunk);
+                       g, X, M, partial, M_pad, Mt, n_tiles, nullptr, kstar, nullptr, chunk, RefineList{});
     hipLaunchKernelGGL(gpis_var_splitk_finalize<KT>, dim3((unsigned)M), dim3(256), 0, s, g, partial, M_pad, chunk,
                        vout, std_out, var_out);
     prof_mark(PROF_GPIS_STD, false, s);
@@ -848,7 +951,7 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
   }
   prof_mark(PROF_GPIS_STD, true, s);
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VAR>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s,
-                     g, X, M, partial, M_pad, Mt, n_tiles, vout, kstar, nullptr, 0);
+                     g, X, M, partial, M_pad, Mt, n_tiles, vout, kstar, nullptr, 0, RefineList{});
   prof_mark(PROF_GPIS_STD, false, s);
   if (vs && 256 % vs->T == 0) {
     hipLaunchKernelGGL(gpis_var_finalize_select<KT>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, g, partial,
@@ -865,7 +968,7 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
 template <int KT>
 static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const int64_t* sel, const double* var,
                            double* gstd, double* partial, int64_t M_pad, int Mt, int n_tiles, const double* vin,
-                           hipStream_t s) {
+                           hipStream_t s, const int64_t* vrow) {
   prof_mark(PROF_GPIS_GRAD, true, s);
   GradSlots slots;
   slots.n = 0;
@@ -883,11 +986,11 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
       }
     }
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV>), dim3((unsigned)(Mt * parts)), dim3(ST_THREADS), 0,
-                       s, g, X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, sel, parts);
+                       s, g, X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, vrow ? vrow : sel, parts, RefineList{});
   } else {
     for (int nt = 0; nt < n_tiles && nt < GRAD_MAX_SLOTS; ++nt) slots.t[slots.n++] = (unsigned short)nt;
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRAD>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g,
-                       X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, 0);
+                       X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, 0, RefineList{});
   }
   prof_mark(PROF_GPIS_GRAD, false, s);
   hipLaunchKernelGGL(gpis_grad_finalize, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, partial, M, M_pad,
@@ -916,7 +1019,7 @@ int gpis_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* std_o
 }
 
 int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_t* sel, const double* var,
-                     double* gstd, void* ws, hipStream_t s, const double* vin) {
+                     double* gstd, void* ws, hipStream_t s, const double* vin, const int64_t* vrow) {
   if (vin && !g.Linv) return CDX_EINVAL;
   if (M <= 0) return CDX_OK;
   const int64_t M_pad = round_up(M, ST_BM);
@@ -926,10 +1029,46 @@ int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_
   const int Mt = (int)(M_pad / ST_BM);
   double* partial = static_cast<double*>(ws);
   switch (g.kernel) {
-    case CDX_KERNEL_TPS: grad_launch_kt<CDX_KERNEL_TPS>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s); break;
-    case CDX_KERNEL_RBF: grad_launch_kt<CDX_KERNEL_RBF>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s); break;
-    default: grad_launch_kt<CDX_KERNEL_JOINT>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s); break;
+    case CDX_KERNEL_TPS: grad_launch_kt<CDX_KERNEL_TPS>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s, vrow); break;
+    case CDX_KERNEL_RBF: grad_launch_kt<CDX_KERNEL_RBF>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s, vrow); break;
+    default: grad_launch_kt<CDX_KERNEL_JOINT>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s, vrow); break;
   }
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+// Pieces of the refine pass: one per CU.
+constexpr int REFINE_PIECES = 256;
+
+size_t gpis_refine_ws_bytes(const cdx_gpis& g, int64_t Mcap) {
+  const size_t part = (size_t)(g.N_pad / ST_BN) * (size_t)round_up(Mcap, ST_BM) * sizeof(double);
+  const size_t slots = (size_t)REFINE_PIECES * 2 * ST_BM * ST_BN * sizeof(double);
+  return (part + 255) / 256 * 256 + slots;
+}
+
+template <int KT>
+static void refine_launch_kt(const cdx_gpis& g, const double* X, int64_t Mcap, const RefineList& rl, double* partial,
+                             int64_t M_pad, double* vout, hipStream_t s) {
+  hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VARL>), dim3(REFINE_PIECES), dim3(ST_THREADS), 0, s, g, X, Mcap, partial,
+                     M_pad, 0, g.N_pad / ST_BN, vout, nullptr, nullptr, 0, rl);
+  hipLaunchKernelGGL(gpis_var_merge, dim3(REFINE_PIECES), dim3(256), 0, s, g, rl, M_pad, partial, vout);
+}
+
+int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
+                       void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out) {
+  if (Mcap <= 0 || G <= 0 || G > Mcap) return CDX_EINVAL;
+  const int64_t M_pad = round_up(Mcap, ST_BM);
+  double* partial = static_cast<double*>(ws);
+  const size_t part = (size_t)(g.N_pad / ST_BN) * (size_t)M_pad * sizeof(double);
+  RefineList rl{rows, extra, G, reinterpret_cast<double*>(static_cast<char*>(ws) + (part + 255) / 256 * 256)};
+  prof_mark(PROF_GPIS_STD, true, s);
+  switch (g.kernel) {
+    case CDX_KERNEL_TPS: refine_launch_kt<CDX_KERNEL_TPS>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
+    case CDX_KERNEL_RBF: refine_launch_kt<CDX_KERNEL_RBF>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
+    default: refine_launch_kt<CDX_KERNEL_JOINT>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
+  }
+  prof_mark(PROF_GPIS_STD, false, s);
+  if (partial_out) *partial_out = partial;
+  if (M_pad_out) *M_pad_out = M_pad;
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 

@@ -25,6 +25,15 @@ int gpis_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* std_o
 // gstd[sel[m]] = ∇std at X[m] (sel null: identity), scaled by var[sel[m]] from gpis_var_launch.
 // vin null: W = E11⁻¹k (2N² flops per query); vin = the V of gpis_var_launch: W = L⁻ᵀ v from row
 // sel[m] of V (N² flops per query; needs g.Linv).
+// vrow (nullable): the V row of query m is vrow[m] instead of sel[m] (the refine pass's list positions).
 int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_t* sel, const double* var,
-                     double* gstd, void* ws, hipStream_t s, const double* vin = nullptr);
+                     double* gstd, void* ws, hipStream_t s, const double* vin = nullptr,
+                     const int64_t* vrow = nullptr);
+// Refine pass behind the split-precision screen: the whitened fp64 pass (V = K*·L⁻ᵀ, Σ V²) for the
+// rows rows[0 .. G + *extra) of X (device-side count, at most Mcap), cut into equal pieces (one per
+// CU) whatever the count; V rows go to vout at the list positions ([round_up(Mcap, 128), N_pad]),
+// Σ V² per (stripe, position) to the returned partial [N_pad/256][*M_pad_out].
+size_t gpis_refine_ws_bytes(const cdx_gpis& g, int64_t Mcap);
+int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
+                       void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out);
 }  // namespace cdx

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 namespace cdx {
-enum ProfStage { PROF_QUERIES = 0, PROF_GPIS_MEAN = 1, PROF_GPIS_STD = 2, PROF_COST = 3, PROF_GPIS_GRAD = 4, PROF_STAGES = 5 };
+enum ProfStage { PROF_QUERIES = 0, PROF_GPIS_MEAN = 1, PROF_GPIS_STD = 2, PROF_COST = 3, PROF_GPIS_GRAD = 4, PROF_SCREEN = 5,
+                 PROF_STAGES = 6 };
 void prof_mark(int stage, bool begin, hipStream_t s);  // defined in cdx_closure.hip
 }  // namespace cdx

@@ -1,0 +1,59 @@
+// Layout of a GPIS state's screen buffer (cdx_gpis.screen, built by cdx_gpis_screen_prepare) and
+// the launchers of the split-precision variance screen (cdx_screen.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "cdx.h"
+
+namespace cdx {
+
+constexpr int SC_BK = 16;   // K rows per stage (one v_mfma_f32_32x32x16_bf16 deep)
+constexpr int SC_BN = 256;  // columns per stripe (= CDX_NPAD_ALIGN)
+
+// Column shift of the whitened products (the fp64 pass's var_shift): the N_pad − N padding
+// columns, in whole 16-column blocks, sit in front of stripe 0.
+__device__ __host__ inline int screen_shift(int N, int Np) { return std::min((Np - N) / 16 * 16, 256 - 16); }
+
+__device__ __host__ inline size_t screen_align(size_t b) { return (b + 255) / 256 * 256; }
+
+// [L: N_pad/16 × 3 slices × 2 k-halves × N_pad columns × 8 bf16][csum: N_pad f64][X1f: N_pad float4][centre: 4 f64]
+inline size_t screen_bytes(int Np) {
+  return screen_align((size_t)Np * Np * 6) + screen_align((size_t)Np * 8) + screen_align((size_t)Np * 16) + 256;
+}
+
+struct ScreenView {
+  const void* L;
+  const double* csum;
+  const float4* X1f;
+  const double* center;
+};
+
+__device__ __host__ inline ScreenView screen_view(const cdx_gpis& g) {
+  const char* p = static_cast<const char*>(g.screen);
+  const size_t Np = (size_t)g.N_pad;
+  const size_t oL = 0, oc = oL + screen_align(Np * Np * 6), ox = oc + screen_align(Np * 8),
+               oz = ox + screen_align(Np * 16);
+  return ScreenView{p + oL, reinterpret_cast<const double*>(p + oc), reinterpret_cast<const float4*>(p + ox),
+                    reinterpret_cast<const double*>(p + oz)};
+}
+
+// partials [N_pad/256][round_up(M, 256)] f64
+size_t screen_ws_bytes(const cdx_gpis& g, int64_t M);
+// var[m] = estimate of k0 − ‖L⁻¹k(x_m)‖² (g.screen prepared)
+int screen_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* var, void* ws, hipStream_t s);
+
+// Closure screening of the all-tip rows (G groups of T, M = G·T): screen partials in ws
+// (screen_ws_bytes(g, M)), per-row estimate sv2, rows kept for the exact pass listed in rows[0 .. G +
+// stats[0]) (the G group leaders first, at position = group), vpos[q] = list position or −1 (then
+// std_[q] = the estimate), keep [G] scratch.
+int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, void* ws, double* sv2, double* std_,
+                         int* vpos, int* rows, unsigned char* keep, int* stats, hipStream_t s);
+// After the refine pass (gpis_refine_launch): exact std/var of the kept rows, then per group the ∇std
+// row (sel = query, Xg = point, vrow = V row); stats[1] = kept rows whose estimate missed by > Δ.
+int refine_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, const double* rpartial, int64_t M_pad,
+                         const double* sv2, const int* vpos, double* std_, double* var, int64_t* sel, double* Xg,
+                         int64_t* vrow, int* stats, hipStream_t s);
+
+}  // namespace cdx

@@ -21,6 +21,10 @@ import torch
 from . import _native as N
 
 _PKG_STATES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "gpis_states")
+# Closure screening margin Δ = SCREEN_MARGIN × the calibrated max error of the bf16 estimate of std²
+# (cdx_gpis.screen_delta); CDX_SCREEN_MARGIN overrides it, 0 disables screening.
+SCREEN_MARGIN = float(os.environ.get("CDX_SCREEN_MARGIN", "32"))
+CALIB_QUERIES = 8192
 
 
 def _require_cuda(t, what):
@@ -55,7 +59,50 @@ class _State:
         self.desc = N.CdxGpis(X1=self.X1.data_ptr(), alpha=self.alpha.data_ptr(), Ainv=self.Ainv.data_ptr(),
                               Linv_t=self.Linv_t.data_ptr(), Linv=self.Linv.data_ptr(), N=n,
                               N_pad=Np, kernel=N.KERNELS[kernel], R=float(R), sigma=float(sigma), bias=float(bias))
+        # split-precision variance screen (bf16 slices of L⁻ᵀ): built once per state
+        self.screen = torch.empty(lib.cdx_gpis_screen_bytes(Np), dtype=torch.uint8, device=dev)
+        N.check(lib.cdx_gpis_screen_prepare(self.desc, N.ptr(self.screen), N.stream_ptr(dev)), "cdx_gpis_screen_prepare")
+        self.desc.screen = self.screen.data_ptr()
+        self.desc.screen_delta = 0.0
         self.ws = None
+        self.screen_ws = None
+        self.screen_err = self._calibrate_screen(X1[:n].to(torch.float64), R, kernel)
+        # the closure keeps every fingertip whose estimate is within 2Δ of its group's leader
+        k0 = {"tps": float(R) ** 3, "rbf": 1.0, "joint": 0.3 + 0.7 * float(R) ** 3}[kernel]
+        self.desc.screen_delta = max(SCREEN_MARGIN * self.screen_err, 2.0 ** -40 * k0) if SCREEN_MARGIN > 0 else 0.0
+
+    def _calibrate_screen(self, X1, R, kernel):
+        """max |estimate − exact| of k0 − ‖L⁻¹k‖² over calibration queries around this state:
+        the inducing points displaced by 0–3 cm and uniform points in their bounding box ± 5 cm
+        (one host sync).  The closure's screening margin is SCREEN_MARGIN × this."""
+        dev = X1.device
+        gen = torch.Generator(device="cpu").manual_seed(0)
+        n = X1.shape[0]
+        pts = [X1 + sc * torch.randn(n, 3, generator=gen, dtype=torch.float64).to(dev)
+               for sc in (0.0, 0.002, 0.005, 0.01, 0.03)]
+        lo, hi = X1.min(0).values - 0.05, X1.max(0).values + 0.05
+        pts.append(lo + (hi - lo) * torch.rand(2 * n, 3, generator=gen, dtype=torch.float64).to(dev))
+        Xc = torch.cat(pts)
+        if Xc.shape[0] > CALIB_QUERIES:
+            Xc = Xc[torch.randperm(Xc.shape[0], generator=gen)[:CALIB_QUERIES].to(dev)]
+        Xc = Xc.contiguous()
+        est = self.screen_var(Xc)
+        exact = exact_var(self, Xc)
+        return float((est - exact).abs().max())
+
+    def screen_var(self, X):
+        """Split-precision estimate of k0 − ‖L⁻¹k‖² at X [M, 3] (cdx_gpis_screen_var)."""
+        lib = N.load()
+        X = X.contiguous()
+        M = X.shape[0]
+        out = torch.empty(M, dtype=torch.float64, device=X.device)
+        if M:
+            need = lib.cdx_gpis_screen_workspace(self.desc, M)
+            if self.screen_ws is None or self.screen_ws.numel() < need:
+                self.screen_ws = torch.empty(need, dtype=torch.uint8, device=X.device)
+            N.check(lib.cdx_gpis_screen_var(self.desc, N.ptr(X), M, N.ptr(out), N.ptr(self.screen_ws),
+                                            N.stream_ptr(X.device)), "cdx_gpis_screen_var")
+        return out
 
     def workspace(self, M):
         need = N.load().cdx_gpis_std_workspace(self.desc, M)
@@ -74,6 +121,13 @@ def gpis_mean(state, X, want_grad=True, want_normal=False):
     N.check(lib.cdx_gpis_mean(state.desc, N.ptr(X), M, N.ptr(mean), N.ptr(gmean), N.ptr(normal),
                               N.stream_ptr(X.device)), "cdx_gpis_mean")
     return mean, gmean, normal
+
+
+def exact_var(state, X):
+    """The signed fp64 k0 − ‖L⁻¹k‖² at X (cdx_gpis_std keeps it at the head of its workspace)."""
+    M = X.shape[0]
+    gpis_std(state, X, want_grad=False)
+    return state.ws[:M * 8].view(torch.float64).clone()
 
 
 def gpis_std(state, X, want_grad=True):

@@ -151,6 +151,18 @@ class ProbabilisticGraspOptimizer:
             self._problem_key = key
         return self._problem
 
+    def screen_stats(self, gpis, E, friction_mu=1):
+        """Screening of the last closure over E candidates (cdx_closure_screen_stats): dict of the
+        all-tip rows that ran the exact fp64 pass, the rows whose bf16 estimate missed its bound,
+        and the rows screened — or None when the closure ran the full fp64 pass."""
+        import ctypes
+        out = (ctypes.c_int32 * 3)()
+        N.check(N.load().cdx_closure_screen_stats(self.problem(gpis, friction_mu), E, N.ptr(self._ws), out),
+                "cdx_closure_screen_stats")
+        if out[0] < 0:
+            return None
+        return {"exact_rows": out[0], "bound_misses": out[1], "screened_rows": out[2]}
+
     def _ensure_ws(self, p, E, dev):
         need = N.load().cdx_closure_workspace(p, E)
         if self._ws is None or self._ws.numel() < need:

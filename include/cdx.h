@@ -61,6 +61,9 @@ typedef struct {
   double R;           /* TPS radius = max pairwise training distance */
   double sigma;       /* RBF length scale */
   double bias;
+  const void* screen; /* nullable: split-precision variance screen (cdx_gpis_screen_prepare) */
+  double screen_delta;/* absolute bound on the screen's |Δstd²| (calibrated per state); the closure
+                         screens only when screen != NULL and screen_delta > 0 */
 } cdx_gpis;
 
 /* Posterior mean and its spatial gradient at M query points (gpis.py:43-55 mean part,
@@ -100,6 +103,22 @@ size_t cdx_gpis_factor_workspace(int32_t N_pad);
 int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pad, void* workspace,
                     double* Ainv, double* Linv_t, double* Linv, double* alpha, int32_t* info,
                     cdx_stream_t stream);
+
+/* Split-precision variance screen (bf16 matrix cores).  Estimates std² = k0 − ‖L⁻¹k‖² (gpis.py:56-59)
+ * as k0 − ‖Ã·L⁻ᵀ + k0·colsum(L⁻ᵀ)‖² with Ã = K* − k0 generated in fp32 and both operands split into
+ * three bf16 slices (six slice products, fp32 accumulation): fp32-level accuracy at 2.1× the fp64
+ * MFMA flop rate.  The closure uses it to skip the fp64 pass for fingertips that cannot be the
+ * variance cost's maximum; alone it is a throughput estimate with no parity claim.
+ * cdx_gpis_screen_bytes: size of the per-state screen buffer (≈ 6·N_pad² bytes);
+ * cdx_gpis_screen_prepare: fills it from g->Linv_t and g->X1 (the descriptor's own screen field is
+ *   ignored; point it at the buffer afterwards);
+ * cdx_gpis_screen_var: var [M] = the estimate of k0 − ‖L⁻¹k‖² (signed), workspace
+ *   cdx_gpis_screen_workspace bytes. */
+size_t cdx_gpis_screen_bytes(int32_t N_pad);
+int cdx_gpis_screen_prepare(const cdx_gpis* g, void* screen, cdx_stream_t stream);
+size_t cdx_gpis_screen_workspace(const cdx_gpis* g, int64_t M);
+int cdx_gpis_screen_var(const cdx_gpis* g, const double* X, int64_t M, double* var, void* workspace,
+                        cdx_stream_t stream);
 
 /* ------------------------------------------------------------------ FK ----------
  * Replaces DifferentiableRobotModel.compute_forward_kinematics(q, link_names,
@@ -193,6 +212,12 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                 double* total_loss, double* total_margin, double* pregrasp_tip,
                 double* g_q, double* g_comp, double* g_target, double* g_palm_pos,
                 double* g_palm_ori, int32_t* flip, cdx_stream_t stream);
+
+/* Screening statistics of the last cdx_closure on this workspace (one device→host copy): out[0] =
+ * all-tip rows that ran the exact fp64 whitened pass, out[1] = rows whose split-precision estimate
+ * missed the exact value by more than screen_delta (0 expected: the calibration bound), out[2] =
+ * all-tip rows screened; all −1 when the closure did not screen (no screen / CDX_NO_SCREEN set). */
+int cdx_closure_screen_stats(const cdx_problem* p, int64_t E, const void* workspace, int32_t* out3);
 
 /* ------------------------------------------------------------ force_eq_reward ------
  * Replaces force_eq_reward (optimize_pregrasp.py:73-118) with optimal_transformation_batch
@@ -296,14 +321,15 @@ int cdx_sdf_backward(const float* grad_dist, const float* points, const float* c
 const char* cdx_version(void);
 
 /* Per-stage kernel timing with HIP events recorded on the launch stream (off by default).
- * Stages: 0 closure query generation, 1 GPIS mean, 2 GPIS std (whitened K*·L⁻ᵀ GEMM only),
- * 3 closure cost+backward, 4 GPIS ∇std (K*·E11⁻¹ GEMM only).  cdx_profile_read syncs on the
- * recorded events, returns the summed milliseconds and launch counts per stage (arrays of 5),
- * and clears the pool (4096 launches per stage).  `stages` is a bit mask (bit s = stage s; 0x1f
+ * Stages: 0 closure query generation, 1 GPIS mean, 2 GPIS std (whitened K*·L⁻ᵀ fp64 GEMM only; in a
+ * screened closure the refine pass and its merge), 3 closure cost+backward, 4 GPIS ∇std GEMM only,
+ * 5 the closure's split-precision screen (bf16 GEMM + selection).  cdx_profile_read syncs on the
+ * recorded events, returns the summed milliseconds and launch counts per stage (arrays of 6),
+ * and clears the pool (4096 launches per stage).  `stages` is a bit mask (bit s = stage s; 0x3f
  * all, 0 off): each event record costs ≈ 5 µs of stream time, so a throughput run times only
  * the stages it reports. */
 int cdx_profile_enable(int stages);
-int cdx_profile_read(double* ms5, int64_t* count5);
+int cdx_profile_read(double* ms6, int64_t* count6);
 
 /* sizeof(cdx_gpis), sizeof(cdx_body), sizeof(cdx_chain), sizeof(cdx_problem),
  * sizeof(cdx_collision), sizeof(cdx_adam), sizeof(cdx_opt_buffers), sizeof(cdx_force_eq) — lets

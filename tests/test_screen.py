@@ -1,0 +1,141 @@
+"""Split-precision variance screen (cdx_screen.hip) and the screened closure.
+
+The closure estimates std² of every all-tip row with the bf16 screen and runs the exact fp64
+whitened pass only for the fingertips that can still be their group's maximum (the variance cost
+reads max_f log(100·std_f), optimize_pregrasp.py:733).  Parity bar: the screened closure equals the
+unscreened fp64 closure (itself pinned to the reference fixtures by test_gpu_parity) to the rounding
+of the refine pass's K-split (measured ≤ 1e-13 relative; asserted 1e-10), with identical NaN
+positions and Kabsch masks, and no kept row's estimate outside the calibrated bound.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests._helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+OUTS = ("total_loss", "total_margin", "grad_q", "grad_comp", "grad_target", "grad_palm_pos", "grad_palm_ori")
+TOL_EQ = 1e-10  # screened vs unscreened closure (same fp64 arithmetic, K-split rounding only)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.fixture(scope="module")
+def banana2000():
+    from compliancedex_amd.workloads import synthetic_banana_gpis
+    return synthetic_banana_gpis(2000, device=DEV)
+
+
+def _opt(hand="allegro"):
+    from compliancedex_amd import ProbabilisticGraspOptimizer
+    from compliancedex_amd.urdf import load_robot
+    cfg = load_robot(hand)["config"]
+    return cfg, ProbabilisticGraspOptimizer(hand, cfg["ee_link_name"], cfg["ee_link_offset"], ref_q=cfg["ref_q"],
+                                            optimize_target=True, optimize_palm=True, device=DEV)
+
+
+def _closure(opt, gpis, inputs, screen=True):
+    q, comp, target, palm = inputs
+    p = opt.problem(gpis, 1)
+    delta = p.gpis.screen_delta
+    if not screen:
+        p.gpis.screen_delta = 0.0
+    try:
+        t = [torch.from_numpy(np.ascontiguousarray(a)).to(DEV).requires_grad_(True)
+             for a in (q, comp, target, palm[:, :3], palm[:, 3:])]
+        noise = torch.from_numpy(np.random.default_rng(7).random((3 * q.shape[0], 3, 3))).to(DEV)
+        opt.closure(*t, 1, gpis, q.shape[0], kabsch_noise=noise)
+        torch.cuda.synchronize()
+        out = dict(total_loss=opt.total_loss.cpu().numpy(), total_margin=opt.total_margin.cpu().numpy(),
+                   flip=opt.kabsch_flip.cpu().numpy())
+        for k, x in zip(OUTS[2:], t):
+            out[k] = x.grad.cpu().numpy()
+        stats = opt.screen_stats(gpis, q.shape[0])
+    finally:
+        p.gpis.screen_delta = delta
+    return out, stats
+
+
+def _all_tip_queries(cfg, E, seed, center=None):
+    from compliancedex_amd.workloads import prob_inputs
+    from oracle.cdx_oracle import OracleChain, OracleProblem
+    from compliancedex_amd.urdf import load_robot
+    prob = OracleProblem(OracleChain(load_robot("allegro")["bodies"]), cfg["ee_link_name"], cfg["ee_link_offset"],
+                         cfg["ref_q"], None)
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=seed, spread=True, center=center)
+    with torch.no_grad():
+        pre = prob.forward_kinematics(torch.from_numpy(q), torch.from_numpy(palm)).double()
+    tgt = torch.from_numpy(target)
+    return (tgt + 0.8 * (pre - tgt)).reshape(-1, 3)
+
+
+def test_screen_estimate_within_bound(banana2000):
+    """The bf16 estimate of k0 − ‖L⁻¹k‖² against the fp64 pass on the bench's 16 384 all-tip rows:
+    inside an eighth of the closure's margin Δ (= 32× the state's calibrated error; measured ≈ 3e-6·k0
+    against a calibrated 2-4e-6·k0)."""
+    from compliancedex_amd.gpis import exact_var
+    cfg, _ = _opt()
+    st = banana2000.native_state()
+    X = _all_tip_queries(cfg, 4096, 1000).to(DEV)
+    est = st.screen_var(X)
+    ex = exact_var(st, X)
+    err = float((est - ex).abs().max())
+    k0 = float(banana2000.R) ** 3
+    assert np.isfinite(est.cpu().numpy()).all()
+    assert st.desc.screen_delta > 0
+    assert err <= st.desc.screen_delta / 8, (err / k0, st.desc.screen_delta / k0)
+
+
+def test_screen_var_c_abi_edges(banana2000):
+    """M = 0 is a no-op; a null workspace / unprepared descriptor is rejected before any launch."""
+    from compliancedex_amd import _native as N
+    lib = N.load()
+    st = banana2000.native_state()
+    X = torch.zeros(4, 3, dtype=torch.float64, device=DEV)
+    out = torch.zeros(4, dtype=torch.float64, device=DEV)
+    assert lib.cdx_gpis_screen_var(st.desc, N.ptr(X), 0, N.ptr(out), None, None) == 0
+    assert lib.cdx_gpis_screen_var(st.desc, N.ptr(X), 4, N.ptr(out), None, None) == -1
+    bare = N.CdxGpis(X1=st.desc.X1, alpha=st.desc.alpha, Linv_t=st.desc.Linv_t, N=st.desc.N, N_pad=st.desc.N_pad)
+    assert lib.cdx_gpis_screen_var(bare, N.ptr(X), 4, N.ptr(out), N.ptr(out), None) == -1
+
+
+@pytest.mark.parametrize("case", ["config2_E4096", "stored_banana_E64", "config3_mug_E4096"])
+def test_screened_closure_equals_fp64_closure(case, banana2000):
+    """Screened vs unscreened closure on the same inputs: equal to TOL_EQ, NaNs and Kabsch masks
+    identical; the exact pass ran for ≤ 1.25 fingertips per group and no kept estimate left its bound."""
+    from compliancedex_amd.workloads import config3_gpis, prob_inputs, stored_gpis, surface_center
+    cfg, opt = _opt()
+    if case == "config2_E4096":
+        gpis, E, center = banana2000, 4096, None
+    elif case == "stored_banana_E64":
+        gpis, E, center = stored_gpis("banana", DEV), 64, None
+    else:
+        _, gpis = config3_gpis(1, DEV)
+        E, center = 4096, surface_center(gpis)
+    inputs = prob_inputs(cfg["ref_q"], E, seed=321, spread=True, center=center)
+    a, st = _closure(opt, gpis, inputs, screen=True)
+    b, st0 = _closure(opt, gpis, inputs, screen=False)
+    assert st0 is None and st is not None
+    assert st["bound_misses"] == 0
+    assert st["screened_rows"] == 4 * E
+    assert E <= st["exact_rows"] <= 1.25 * E, st
+    assert np.array_equal(a["flip"], b["flip"])
+    for k in OUTS:
+        assert rel_err(a[k], b[k]) <= TOL_EQ, (k, rel_err(a[k], b[k]))
+
+
+def test_screened_closure_deterministic(banana2000):
+    """Two screened closures on the same inputs and noise are bit-identical (the kept-row list is
+    compacted in group order, not by atomics)."""
+    from compliancedex_amd.workloads import prob_inputs
+    cfg, opt = _opt()
+    inputs = prob_inputs(cfg["ref_q"], 2048, seed=5, spread=True)
+    a, _ = _closure(opt, banana2000, inputs)
+    b, _ = _closure(opt, banana2000, inputs)
+    for k in OUTS:
+        assert np.array_equal(a[k], b[k], equal_nan=True), k
