@@ -30,6 +30,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6  # gfx950 vendor spec; MI355X_MICROARCH.md has no f64 row
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md § Matrix cores)
 
 
 def parse():
@@ -168,7 +169,7 @@ def main():
     import ctypes
     # HIP events only around the two roofline kernels inside the timed region (each event record
     # costs ≈ 5 µs of stream time); the other stages are timed in a separate pass afterwards
-    PROF_TIMED = (1 << 2) | (1 << 4)  # gpis_std_var, gpis_std_grad
+    PROF_TIMED = (1 << 2) | (1 << 4) | (1 << 5)  # gpis_std_var (refine), gpis_std_grad, gpis_screen
     N.check(lib.cdx_profile_enable(PROF_TIMED), "cdx_profile_enable")
     torch.cuda.synchronize()
     if world > 1:
@@ -192,13 +193,13 @@ def main():
     # stage split (informational): every stage timed over a short extra pass, outside the timed region
     ms_all = (ctypes.c_double * N.PROF_STAGES)()
     cnt_all = (ctypes.c_int64 * N.PROF_STAGES)()
-    N.check(lib.cdx_profile_enable(0x1F), "cdx_profile_enable")
+    N.check(lib.cdx_profile_enable((1 << N.PROF_STAGES) - 1), "cdx_profile_enable")
     for _ in range(min(10, args.steps)):
         step()
     torch.cuda.synchronize()
     N.check(lib.cdx_profile_read(ms_all, cnt_all), "cdx_profile_read")
     lib.cdx_profile_enable(0)
-    for i in range(5):
+    for i in range(N.PROF_STAGES):
         if not cnt[i]:
             ms[i], cnt[i] = ms_all[i], cnt_all[i]
     elapsed, gather_s = t1 - t0, t1g - tg0
@@ -210,18 +211,22 @@ def main():
 
     ms_per_step = 1e3 * elapsed / args.steps
     value = E * world / (elapsed / args.steps)
-    stage_names = ["queries", "gpis_mean", "gpis_std_var", "cost_bwd", "gpis_std_grad"]
+    stage_names = ["queries", "gpis_mean", "gpis_std_var", "cost_bwd", "gpis_std_grad", "gpis_screen"]
     stage_ms = {n: (ms[i] / cnt[i] if cnt[i] else None) for i, n in enumerate(stage_names)}
     lq = opt.problem(gpis, 1).n_query_levels
     m_std, m_grad = lq * E * 4, lq * E
+    scr = opt.screen_stats(gpis, E)  # rows of the exact fp64 pass (screened closure), None: all m_std
+    m_exact = scr["exact_rows"] if scr else m_std
     n_ind = args.n_inducing
     # algorithmic flops per launch (unpadded N): V = K*·L⁻ᵀ is triangular, N(N+1)/2 MACs per
-    # query; W = V·L⁻¹ (= (E11⁻¹k)ᵀ) at the variance cost's argmax fingertip only, also triangular
-    flops = m_std * float(n_ind) * (n_ind + 1)
-    flops_g = m_grad * float(n_ind) * (n_ind + 1)
-    std_ms, grad_ms = stage_ms["gpis_std_var"], stage_ms["gpis_std_grad"]
+    # query; W = V·L⁻¹ (= (E11⁻¹k)ᵀ) at the variance cost's argmax fingertip only, also triangular;
+    # the screen runs the triangular product for every all-tip row as 6 bf16 slice products
+    tri = float(n_ind) * (n_ind + 1)
+    flops, flops_g, flops_s = m_exact * tri, m_grad * tri, 6 * m_std * tri
+    std_ms, grad_ms, scr_ms = stage_ms["gpis_std_var"], stage_ms["gpis_std_grad"], stage_ms["gpis_screen"]
     achieved = flops / (std_ms * 1e-3) / 1e12 if std_ms else None
     achieved_g = flops_g / (grad_ms * 1e-3) / 1e12 if grad_ms else None
+    achieved_s = flops_s / (scr_ms * 1e-3) / 1e12 if scr_ms else None
 
     if rank == 0:
         out = {
@@ -242,15 +247,20 @@ def main():
                          "note": "pack (nonzero + gather of surviving rows) + all_gather + unpack, inside the timed "
                                  "region after the last step"},
             "stage_ms": stage_ms,
-            "stage_ms_note": "gpis_std_var / gpis_std_grad: HIP events over the timed steps; the other "
-                              "stages from a 10-step all-stage pass after the timed region",
-            "roofline": {"bound": "mfma", "kernel": "gpis_std_kernel<VAR> (v_mfma_f64_16x16x4_f64, K*·L⁻ᵀ)",
-                         "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
-                         "traffic": hbm_traffic(E, n_ind),
-                         "flops_per_launch": flops,
-                         "note": f"{m_std} std queries x N(N+1) (triangular whitened form; all-tip queries "
-                                 f"deduplicated over the 3 identical pregrasp levels, the reference does 3x)"},
+            "stage_ms_note": "gpis_screen / gpis_std_var (the refine kernel) / gpis_std_grad: HIP events over "
+                              "the timed steps; the other stages from a 10-step all-stage pass after the timed "
+                              "region; the selection / merge / finalize kernels between them are in no stage",
+            "roofline_refine": {"bound": "mfma",
+                                "kernel": ("gpis_std_kernel<VARL> (v_mfma_f64_16x16x4_f64, K*·L⁻ᵀ, screened rows)" if scr
+                                           else "gpis_std_kernel<VAR> (v_mfma_f64_16x16x4_f64, K*·L⁻ᵀ)"),
+                                "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
+                                "traffic": hbm_traffic(E, n_ind, "gpis_refine_bytes_per_launch" if scr
+                                                       else "gpis_var_bytes_per_launch"),
+                                "flops_per_launch": flops, "ms": std_ms,
+                                "note": f"{m_exact} of {m_std} all-tip rows x N(N+1) in the exact fp64 whitened "
+                                        f"form (triangular; all-tip queries deduplicated over the 3 identical "
+                                        f"pregrasp levels, the reference does 3x)"},
             "roofline_grad": {"bound": "mfma", "kernel": "gpis_std_kernel<GRADV> (V·L⁻¹ = (E11⁻¹k)ᵀ, ∇std)",
                               "achieved": achieved_g, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": (achieved_g / FP64_MFMA_PEAK_TFLOPS) if achieved_g else None,
@@ -260,6 +270,23 @@ def main():
                                       f"from the whitened vectors the std pass keeps"},
             "nan_candidates": nan_candidates,  # reference semantics: unclamped log in :708-709
         }
+        if scr:
+            out["roofline_screen"] = {
+                "bound": "mfma", "kernel": "gpis_screen_kernel (v_mfma_f32_32x32x16_bf16, 3-slice bf16 split of "
+                                           "(K*−k0)·L⁻ᵀ, 6 slice products)",
+                "achieved": achieved_s, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": (achieved_s / BF16_MFMA_PEAK_TFLOPS) if achieved_s else None,
+                "traffic": hbm_traffic(E, n_ind, "gpis_screen_bytes_per_launch"),
+                "flops_per_launch": flops_s, "ms": scr_ms,
+                "note": f"{m_std} all-tip rows x 6 x N(N+1) bf16 MFMA flops (the split-precision estimate that "
+                        f"selects the rows of the exact pass)"}
+            out["screen"] = {"exact_rows": scr["exact_rows"], "screened_rows": scr["screened_rows"],
+                             "bound_misses": scr["bound_misses"],
+                             "delta_over_k0": gpis.native_state().desc.screen_delta / float(gpis.R) ** 3}
+        # the dominant kernel (longest per launch) is the headline roofline
+        cands = [k for k in ("roofline_refine", "roofline_screen", "roofline_grad") if k in out and out[k]["achieved"]]
+        dom = max(cands, key=lambda k: out[k]["flops_per_launch"] / out[k]["achieved"]) if cands else "roofline_refine"
+        out["roofline"] = dict(out[dom], which=dom)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, ref_q, cfg)
         print(json.dumps(out), flush=True)

@@ -424,6 +424,14 @@ struct ClosureWs {
 
 // The closure screens the all-tip rows with the bf16 estimate when the GPIS state carries a
 // calibrated screen (cdx_gpis_screen_prepare + screen_delta) and CDX_NO_SCREEN is unset.
+// Opt-in (CDX_FORK_MEAN=1): measured a net loss on MI355X, so off by default — the mean beside the
+// screen stretches the screen 0.334 → 0.425 ms and itself to 0.37 ms (1.334 vs 1.347 ms per closure
+// at config 2, profiles/r02g_fork_mean_ab.txt; also with the screen's waves at s_setprio 2).
+bool fork_mean() {
+  static const bool on = getenv("CDX_FORK_MEAN") != nullptr;
+  return on;
+}
+
 bool screen_on(const cdx_problem* p) {
   static const bool off = getenv("CDX_NO_SCREEN") != nullptr;
   return !off && p->gpis.screen && p->gpis.screen_delta > 0 && p->chain.n_tips <= CDX_MAX_TIPS;
@@ -468,6 +476,40 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
 #endif
   w.bytes = off;
   return w;
+}
+
+// Side stream of the screened closure (one per device, created on first use): the GPIS mean
+// (fp64 VALU-bound, 4-wave workgroups, 96 VGPRs, 8 KB LDS) can run concurrently with the bf16 screen
+// (one 512-thread workgroup per CU, 2 waves × 208 VGPRs per SIMD, 135 KB LDS), whose CUs keep room
+// for exactly one mean wave per SIMD and one mean workgroup of LDS, the idea being that the mean's
+// f64 VALU work hides behind the screen's MFMA work (see fork_mean).  Fork and join are event waits
+// (hipGraph-capturable).  Not for
+// concurrent cdx_closure calls from several host threads on one device.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+bool side_stream(SideStream& out) {
+  static SideStream per_dev[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  SideStream& ss = per_dev[dev];
+  if (!ss.s) {
+    hipStream_t st;
+    hipEvent_t a, b;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+    if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    ss.s = st;
+    ss.fork = a;
+    ss.join = b;
+  }
+  out = ss;
+  return true;
 }
 
 bool problem_ok(const cdx_problem* p) {
@@ -585,20 +627,32 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                      pregrasp_tip);
   cdx::prof_mark(cdx::PROF_QUERIES, false, s);
   if (hipGetLastError() != hipSuccess) return CDX_ELAUNCH;
-  int rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
-  if (rc) return rc;
+  const bool scr = screen_on(p);
+  SideStream ss;
+  const bool fork = scr && fork_mean() && side_stream(ss);
+  int rc;
+  if (!fork) {
+    rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
+    if (rc) return rc;
+  }
   // whitened std at every all-tip query, keeping V = (L⁻¹K*ᵀ)ᵀ for the ∇std pass
   // … and the ∇std fingertip of each (distinct level, candidate): the all-tip rows q_alltip(u, e, f)
   // = (u·E + e)·T + f form groups of T, selected in the std finalize
   const int64_t Mg = (int64_t)p->n_query_levels * E;
-  if (screen_on(p)) {
+  if (scr) {
     // bf16 screen of every all-tip row → exact whitened fp64 pass for the fingertips that can still
-    // be their group's maximum (≈ 1 per group) → ∇std at the group's maximum from its kept V row
+    // be their group's maximum (≈ 1 per group) → ∇std at the group's maximum from its kept V row;
+    // the mean on the side stream beside the screen (SideStream)
     const int T = p->chain.n_tips;
-    cdx::prof_mark(cdx::PROF_SCREEN, true, s);
+    if (fork && (hipEventRecord(ss.fork, s) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess))
+      return CDX_ELAUNCH;
     rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.stats, s);
-    cdx::prof_mark(cdx::PROF_SCREEN, false, s);
     if (rc) return rc;
+    if (fork) {
+      rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, reinterpret_cast<cdx_stream_t>(ss.s));
+      if (rc) return rc;
+      if (hipEventRecord(ss.join, ss.s) != hipSuccess) return CDX_ELAUNCH;
+    }
     double* rpart = nullptr;
     int64_t rpad = 0;
     rc = cdx::gpis_refine_launch(p->gpis, w.X, w.rows, w.stats, (int)Mg, Ms, w.refine_ws, w.V, s, &rpart, &rpad);
@@ -607,6 +661,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                                    w.vrow, w.stats, s);
     if (rc) return rc;
     rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V, w.vrow);
+    if (!rc && fork && hipStreamWaitEvent(s, ss.join, 0) != hipSuccess) return CDX_ELAUNCH;
   } else {
     const cdx::VarSelect vs{p->chain.n_tips, w.sel, w.Xg};
     rc = cdx::gpis_var_launch(p->gpis, w.X, Ms, w.std_, w.var, w.var_ws, s, w.V, &vs);

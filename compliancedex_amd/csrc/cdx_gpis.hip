@@ -189,6 +189,28 @@ __device__ __host__ inline int gradv_ksteps(int nt, int N) {
   return N > lo ? (N - lo + ST_BK - 1) / ST_BK : 0;
 }
 
+// Refine pass (MODE_VARL) work sequence: the (stripe, query tile) units of var_ksteps(nt) K-steps,
+// stripe-major (all tiles of stripe 0, then stripe 1, …), so that the contiguous 1/8 of it each XCD
+// runs touches few stripes of L⁻ᵀ (L2 reuse).  Unit containing position q: stripe nt, tile mt,
+// sequence range [S0, S1).
+__device__ inline void refine_locate(int64_t q, int MtL, int N, int Np, int& nt, int& mt, int64_t& S0, int64_t& S1) {
+  int64_t off = 0;
+  nt = 0;
+  for (;; ++nt) {
+    const int64_t len = (int64_t)MtL * var_ksteps(nt, N, Np);
+    if (q < off + len || nt == Np / ST_BN - 1) break;
+    off += len;
+  }
+  const int ks = var_ksteps(nt, N, Np);
+  mt = (int)((q - off) / ks);
+  S0 = off + (int64_t)mt * ks;
+  S1 = S0 + ks;
+}
+
+// Piece of the refine pass run by block b: the 256 pieces in sequence order, 32 consecutive ones per
+// XCD (blocks b, b+8, … share an XCD).
+__device__ inline int refine_piece(int b, int G) { return (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b; }
+
 #if defined(CDX_DIAG_WGTIME)
 // timing-only diagnostic: per-workgroup [start, end] (s_memrealtime, 100 MHz), HW_ID, XCC_ID, stripe,
 // K-steps of the whitened pass (read back by cdx_diag_wgtime)
@@ -555,26 +577,25 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   };  // tile
 
   if constexpr (LIST) {
-    // pieces of the concatenated K-sequence of all (query tile, stripe) pairs, tile-major
+    // pieces of the concatenated K-sequence of all (stripe, query tile) units (refine_locate)
     const int MtL = (int)((Mrows + ST_BM - 1) / ST_BM);
     int W = 0;
     for (int t = 0; t < Nt; ++t) W += var_ksteps(t, g.N, Np);
     const int64_t total = (int64_t)MtL * W;
-    const int64_t q0 = total * b / gridDim.x, q1 = total * (b + 1) / gridDim.x;
+    const int pc = refine_piece(b, gridDim.x);
+    const int64_t q0 = total * pc / gridDim.x, q1 = total * (pc + 1) / gridDim.x;
     bool first = true;
     for (int64_t q = q0; q < q1;) {
-      const int mt = (int)(q / W);
-      const int r = (int)(q - (int64_t)mt * W);
-      int nt = 0, s0 = 0;
-      while (s0 + var_ksteps(nt, g.N, Np) <= r) s0 += var_ksteps(nt++, g.N, Np);
-      const int s1 = s0 + var_ksteps(nt, g.N, Np);
-      const int64_t e = min(q1, (int64_t)mt * W + s1);
+      int nt, mt;
+      int64_t S0, S1;
+      refine_locate(q, MtL, g.N, Np, nt, mt, S0, S1);
+      const int64_t e = min(q1, S1);
       const int hi = min(g.N, nt * ST_BN + ST_BN - vsh);
-      const int kbeg = (r - s0) * ST_BK, kend = min(hi, (int)(e - (int64_t)mt * W - s0) * ST_BK);
-      const bool full = r == s0 && e == (int64_t)mt * W + s1;
+      const int kbeg = (int)(q - S0) * ST_BK, kend = min(hi, (int)(e - S0) * ST_BK);
+      const bool full = q == S0 && e == S1;
       if (!first) __syncthreads();  // the previous segment's epilogue used the stage buffers
       first = false;
-      tile(mt, nt, kbeg, kend, full ? nt : 2 * b + (q == q0 ? 0 : 1), full);
+      tile(mt, nt, kbeg, kend, full ? nt : 2 * pc + (q == q0 ? 0 : 1), full);
       q = e;
     }
     return;
@@ -787,11 +808,9 @@ __global__ __launch_bounds__(256) void gpis_var_merge(cdx_gpis g, RefineList rl,
   auto qof = [&](int pp) { return total * pp / pieces; };
   const int64_t q0 = qof(p), q1 = qof(p + 1);
   if (q0 >= q1 || q0 >= total) return;
-  const int mt = (int)(q0 / W);
-  const int r = (int)(q0 - (int64_t)mt * W);
-  int nt = 0, s0 = 0;
-  while (s0 + var_ksteps(nt, g.N, Np) <= r) s0 += var_ksteps(nt++, g.N, Np);
-  const int64_t S0 = (int64_t)mt * W + s0, S1 = S0 + var_ksteps(nt, g.N, Np);
+  int nt, mt;
+  int64_t S0, S1;
+  refine_locate(q0, MtL, g.N, Np, nt, mt, S0, S1);
   if (!(S0 < q0 && S1 <= q1)) return;
   int pf = p;
   while (pf > 0 && qof(pf) > S0) --pf;  // the stripe's first piece (possibly an empty one before it)
@@ -1048,8 +1067,10 @@ size_t gpis_refine_ws_bytes(const cdx_gpis& g, int64_t Mcap) {
 template <int KT>
 static void refine_launch_kt(const cdx_gpis& g, const double* X, int64_t Mcap, const RefineList& rl, double* partial,
                              int64_t M_pad, double* vout, hipStream_t s) {
+  prof_mark(PROF_GPIS_STD, true, s);
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VARL>), dim3(REFINE_PIECES), dim3(ST_THREADS), 0, s, g, X, Mcap, partial,
                      M_pad, 0, g.N_pad / ST_BN, vout, nullptr, nullptr, 0, rl);
+  prof_mark(PROF_GPIS_STD, false, s);
   hipLaunchKernelGGL(gpis_var_merge, dim3(REFINE_PIECES), dim3(256), 0, s, g, rl, M_pad, partial, vout);
 }
 
@@ -1060,13 +1081,11 @@ int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, cons
   double* partial = static_cast<double*>(ws);
   const size_t part = (size_t)(g.N_pad / ST_BN) * (size_t)M_pad * sizeof(double);
   RefineList rl{rows, extra, G, reinterpret_cast<double*>(static_cast<char*>(ws) + (part + 255) / 256 * 256)};
-  prof_mark(PROF_GPIS_STD, true, s);
   switch (g.kernel) {
     case CDX_KERNEL_TPS: refine_launch_kt<CDX_KERNEL_TPS>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
     case CDX_KERNEL_RBF: refine_launch_kt<CDX_KERNEL_RBF>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
     default: refine_launch_kt<CDX_KERNEL_JOINT>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
   }
-  prof_mark(PROF_GPIS_STD, false, s);
   if (partial_out) *partial_out = partial;
   if (M_pad_out) *M_pad_out = M_pad;
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;

@@ -26,6 +26,7 @@
 
 #include "cdx_gpis.h"
 #include "cdx_gpis_launch.h"
+#include "cdx_prof.h"
 #include "cdx_screen.h"
 
 namespace {
@@ -40,8 +41,10 @@ constexpr int SC_BM = 256;                 // query rows per workgroup
 constexpr int SC_THREADS = 512;            // 8 waves: 2 (rows) × 4 (columns), 128 × 64 outputs each
 constexpr int SC_REG = 6 * 256;            // 16-byte LDS units of one operand stage: [slice][khalf][256]
 constexpr int SC_LDT = 264;               // fp32 row pitch of the epilogue's accumulator image (4 rows ≡ 32 banks)
-constexpr int SC_SMEM = std::max(2 * 2 * SC_REG * 16 + 3 * 16 * 16,  // 2 buffers × (A + B) + X1 stages
-                                 128 * SC_LDT * 4);                 // epilogue: one row half of the tile
+// LDS: A stages (generated, 2 buffers) | B stages (LDS-DMA ring of 3)
+constexpr int SC_A_OFF = 0, SC_B_OFF = 2 * SC_REG * 16;
+constexpr int SC_SMEM = std::max(SC_B_OFF + 3 * SC_REG * 16,  // stage buffers
+                                 128 * SC_LDT * 4);            // epilogue: one row half of the tile
 static_assert(SC_SMEM <= 160 * 1024, "screen stage buffers exceed the CU's LDS");
 
 // K-steps (16 rows of L⁻ᵀ) of stripe nt: rows [0, min(N, (nt+1)·256 − shift)) as in the fp64 pass.
@@ -77,8 +80,8 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
                                                                     double* __restrict__ partial, int64_t M_pad, int Mt,
                                                                     int Nt) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[SC_SMEM];
-  u32x4* const s4 = reinterpret_cast<u32x4*>(smem);  // buffer b: A at s4 + 2b·SC_REG, B after it
-  float4* xs = reinterpret_cast<float4*>(smem + 4 * SC_REG * 16);  // [3][16] centred X1 rows
+  u32x4* const sA4 = reinterpret_cast<u32x4*>(smem + SC_A_OFF);  // A buffer b at sA4 + b·SC_REG
+  u32x4* const sB4 = reinterpret_cast<u32x4*>(smem + SC_B_OFF);  // B ring slot r at sB4 + r·SC_REG
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Np = g.N_pad, N = g.N;
   const cdx::ScreenView sv = cdx::screen_view(g);
@@ -130,24 +133,36 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  u32x4 bst[3];      // B stage in flight: 3 × 16 B per thread
-  u32x4 ast[3];      // generated A stage: 8 entries × 3 bf16 slices, packed in pairs
-  auto load_b = [&](int s) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(sv.L);
+  // Staging by LDS-DMA (global_load_lds: no VGPRs, no ds_write).  issue(st): every wave DMAs 3 × 1 KB
+  // of B stage st (instruction u = wave + 8i: slice/k-half region u>>2, columns 64·(u&3) + lane).
+  // issue(s+2) runs during step s; the counted `s_waitcnt vmcnt(3)` at the end of each step keeps
+  // exactly that step's DMAs in flight across the raw s_barrier (__syncthreads would wait vmcnt(0)),
+  // with B stage s+1 landed for step s+1.  Clamped stages past the stripe's end load into free
+  // slots, so every step issues the same count.
+  const char* Lb = static_cast<const char*>(sv.L);
+  auto issue = [&](int st) {
+    const int sc = std::min(st, nK - 1);
+    const int slot = st % 3;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const int idx = tid + SC_THREADS * i, reg = idx >> 8, col = idx & 255;
-#if defined(CDX_SC_DIAG_NOBLOAD)  // timing-only diagnostic build: outputs are wrong
-      bst[i] = u32x4{(unsigned)s, (unsigned)reg, (unsigned)col, 0u};
-#else
-      bst[i] = src[((int64_t)(s * 6 + reg)) * Np + n0 + col];
-#endif
+      const int u = wave + 8 * i, reg = u >> 2, col = 64 * (u & 3) + lane;
+      const char* src = Lb + (((int64_t)(sc * 6 + reg)) * Np + n0 + col) * 16;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sB4 + slot * SC_REG + u * 64), 16, 0, 0);
     }
   };
-  auto gen_a = [&](const float4* x1) {  // 8 consecutive k of this thread's half, packed in pairs
+  u32x4 ast[3];      // generated A stage: 8 entries × 3 bf16 slices, packed in pairs
+  // X1 rows of the generated stage: wave-uniform addresses → scalar loads (SMEM; the vector memory
+  // counter stays free for the DMAs' counted waits)
+  auto gen_a = [&](int st) {  // 8 consecutive k of this thread's half, packed in pairs
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) float4 cfloat4;  // constant space: SMEM loads
+#else
+    typedef const float4 cfloat4;
+#endif
+    cfloat4* x1 = (cfloat4*)(sv.X1f) + __builtin_amdgcn_readfirstlane(st * SC_BK + 8 * gkh);
 #pragma unroll
     for (int e = 0; e < 8; e += 2) {
-      const float4 p = x1[8 * gkh + e], p1 = x1[8 * gkh + e + 1];
+      const float4 p = x1[e], p1 = x1[e + 1];
       unsigned a0, a1, a2, b0, b1, b2;
 #if defined(CDX_SC_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
       a0 = __float_as_uint(qx - p.x); a1 = __float_as_uint(qy - p.y); a2 = __float_as_uint(qz - p.z);
@@ -161,31 +176,26 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
       ast[2][e / 2] = __builtin_amdgcn_perm(b2, a2, 0x07060302u);
     }
   };
-  auto write_stage = [&](int buf) {
+  auto write_a = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      s4[2 * buf * SC_REG + (i * 2 + gkh) * 256 + grow] = ast[i];
-      s4[(2 * buf + 1) * SC_REG + tid + SC_THREADS * i] = bst[i];
-    }
+    for (int i = 0; i < 3; ++i) sA4[buf * SC_REG + (i * 2 + gkh) * 256 + grow] = ast[i];
   };
-  auto x1_row = [&](int s) { return std::min(s, nK - 1) * SC_BK; };  // clamped: extra stages unused
   // one stage's 48 MFMAs: lane → (row/col l&31, k-half l>>5); B slices of both column blocks, A
   // slice by slice (products of slice-index sum ≤ 2, smallest first)
-  auto mfma_stage = [&](int cur, auto more_c) {
+  auto mfma_stage = [&](int abuf, int bslot, auto more_c) {
     constexpr bool MORE = decltype(more_c)::value;
     bf16x8 fb[3][2];
 #pragma unroll
     for (int sb = 0; sb < 3; ++sb)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        fb[sb][j] = __builtin_bit_cast(bf16x8, s4[(2 * cur + 1) * SC_REG + (sb * 2 + (lane >> 5)) * 256 + wc + 32 * j +
-                                                  (lane & 31)]);
+        fb[sb][j] = __builtin_bit_cast(bf16x8, sB4[bslot * SC_REG + (sb * 2 + (lane >> 5)) * 256 + wc + 32 * j + (lane & 31)]);
 #pragma unroll
     for (int sa = 2; sa >= 0; --sa) {
       bf16x8 fa[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        fa[i] = __builtin_bit_cast(bf16x8, s4[2 * cur * SC_REG + (sa * 2 + (lane >> 5)) * 256 + wr + 32 * i + (lane & 31)]);
+        fa[i] = __builtin_bit_cast(bf16x8, sA4[abuf * SC_REG + (sa * 2 + (lane >> 5)) * 256 + wr + 32 * i + (lane & 31)]);
 #pragma unroll
       for (int sb = 2 - sa; sb >= 0; --sb)
 #pragma unroll
@@ -201,28 +211,27 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
     }
   };
 
-  // prologue: X1 rows of stages 0 and 1, then stage 0 into buffer 0
-  if (tid < 32) xs[tid] = sv.X1f[x1_row(tid >> 4) + (tid & 15)];
-  __syncthreads();
-  load_b(0);
-  gen_a(xs);
-  write_stage(0);
-  __syncthreads();
+  // prologue: B stages 0–1 landed, A of stage 0 generated
+  issue(0);
+  issue(1);
+  gen_a(0);
+  write_a(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
-  // Step s multiplies stage s (buffer s&1) while stage s+1 is loaded / generated into registers
-  // and written to the other buffer; the X1 rows of stage s+2 go to xs[(s+2)%3].  LIVE: this wave's
-  // B columns are non-zero in stage s; MORE: a stage s+1 exists.  The (LIVE, MORE) body is one
-  // straight-line block, so the generation's VALU work can interleave with the MFMAs.
+  // Step s multiplies stage s (A buffer s&1, B slot s%3) while stage s+2 is DMA'd into slot (s+2)%3
+  // and stage s+1's A is generated (X1 slot (s+1)%3) and written to the other A buffer.  LIVE: this
+  // wave's B columns are non-zero in stage s; MORE: a stage s+1 exists.  The (LIVE, MORE) body is
+  // one straight-line block, so the generation's VALU work interleaves with the MFMAs.
   auto step = [&](int s, auto live_c, auto more_c) {
     constexpr bool LIVE = decltype(live_c)::value, MORE = decltype(more_c)::value;
-    const int cur = s & 1;
-    if (MORE) load_b(s + 1);
-    const float4 xl = sv.X1f[x1_row(s + 2) + (tid & 15)];
-    if (MORE) gen_a(xs + ((s + 1) % 3) * 16);
-    if (LIVE) mfma_stage(cur, more_c);
-    if (MORE) write_stage(cur ^ 1);
-    if (tid < 16) xs[((s + 2) % 3) * 16 + tid] = xl;
-    __syncthreads();
+    issue(s + 2);
+    if (MORE) gen_a(s + 1);
+    if (LIVE) mfma_stage(s & 1, s % 3, more_c);
+    if (MORE) write_a((s + 1) & 1);
+    asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");  // B stage s+1 landed, A written
+    __builtin_amdgcn_s_barrier();
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
@@ -230,8 +239,9 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
   int s = 0;
   for (; s < std::min(s_live, nK - 1); ++s) step(s, T_{}, T_{});
   for (; s < nK - 1; ++s) step(s, F_{}, T_{});
-  // last stage: its MFMAs only (no stage s+1), then the barrier before the epilogue reuses the LDS
-  if (s < s_live) mfma_stage(s & 1, F_{});
+  // last stage: its MFMAs only; then every DMA drained before the epilogue reuses the LDS
+  if (s < s_live) mfma_stage(s & 1, s % 3, F_{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   // Epilogue: per row Σ over the stripe's 256 columns of (Ṽ + c)² in f64.  The accumulators go
@@ -462,17 +472,24 @@ __global__ __launch_bounds__(256) void screen_split_kernel(cdx_gpis g, bf16x8* _
   for (int s = 0; s < 3; ++s) L[(((int64_t)kb * 3 + s) * 2 + h) * Np + col] = o[s];
 }
 
-// csum[j] = k0 · Σ_{n<N} L⁻ᵀ[n][j − shift] (zero for j < shift): Ṽ = Ã·L⁻ᵀ + csum.
+// csum[j] = k0 · Σ_{n<N} L⁻ᵀ[n][j − shift] (zero for j < shift): Ṽ = Ã·L⁻ᵀ + csum.  One 1024-thread
+// block per 64 columns: 16 row groups each sum every 16th row, then a fixed-order combine.
 template <int KT>
-__global__ __launch_bounds__(256) void screen_csum_kernel(cdx_gpis g, double* __restrict__ csum) {
+__global__ __launch_bounds__(1024) void screen_csum_kernel(cdx_gpis g, double* __restrict__ csum) {
+  __shared__ double part[16][64];
   const int Np = g.N_pad, shift = cdx::screen_shift(g.N, Np);
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= Np) return;
-  const int j = col - shift;
+  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c, j = col - shift;
   double s = 0;
   if (j >= 0)
-    for (int n = 0; n < g.N; ++n) s += g.Linv_t[(int64_t)n * Np + j];
-  csum[col] = cdx::gpis_k0<KT>(g.R) * s;
+    for (int n = rg; n < g.N; n += 16) s += g.Linv_t[(int64_t)n * Np + j];
+  part[rg][c] = s;
+  __syncthreads();
+  if (rg == 0) {
+    double t = 0;
+    for (int r = 0; r < 16; ++r) t += part[r][c];
+    csum[col] = cdx::gpis_k0<KT>(g.R) * t;
+  }
 }
 
 int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
@@ -524,15 +541,21 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
   const dim3 grid((unsigned)(Mt * Nt)), sgrid((unsigned)((G + 255) / 256));
   switch (g.kernel) {
     case CDX_KERNEL_TPS:
+      prof_mark(PROF_SCREEN, true, s);
       hipLaunchKernelGGL(gpis_screen_kernel<CDX_KERNEL_TPS>, grid, dim3(SC_THREADS), 0, s, g, X, Ms, partial, M_pad, Mt, Nt);
+      prof_mark(PROF_SCREEN, false, s);
       hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(256), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
       break;
     case CDX_KERNEL_RBF:
+      prof_mark(PROF_SCREEN, true, s);
       hipLaunchKernelGGL(gpis_screen_kernel<CDX_KERNEL_RBF>, grid, dim3(SC_THREADS), 0, s, g, X, Ms, partial, M_pad, Mt, Nt);
+      prof_mark(PROF_SCREEN, false, s);
       hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(256), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
       break;
     default:
+      prof_mark(PROF_SCREEN, true, s);
       hipLaunchKernelGGL(gpis_screen_kernel<CDX_KERNEL_JOINT>, grid, dim3(SC_THREADS), 0, s, g, X, Ms, partial, M_pad, Mt, Nt);
+      prof_mark(PROF_SCREEN, false, s);
       hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(256), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
       break;
   }
@@ -581,11 +604,11 @@ int cdx_gpis_screen_prepare(const cdx_gpis* g, void* screen, cdx_stream_t stream
   const int64_t nsplit = (int64_t)(Np / 16) * 2 * Np;
   hipLaunchKernelGGL(screen_split_kernel, dim3((unsigned)((nsplit + 255) / 256)), dim3(256), 0, s, gv,
                      reinterpret_cast<bf16x8*>(const_cast<void*>(v.L)));
-  const dim3 cgrid((unsigned)((Np + 255) / 256));
+  const dim3 cgrid((unsigned)(Np / 64)), cblk(1024);
   switch (g->kernel) {
-    case CDX_KERNEL_TPS: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_TPS>, cgrid, dim3(256), 0, s, gv, const_cast<double*>(v.csum)); break;
-    case CDX_KERNEL_RBF: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_RBF>, cgrid, dim3(256), 0, s, gv, const_cast<double*>(v.csum)); break;
-    default: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_JOINT>, cgrid, dim3(256), 0, s, gv, const_cast<double*>(v.csum)); break;
+    case CDX_KERNEL_TPS: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_TPS>, cgrid, cblk, 0, s, gv, const_cast<double*>(v.csum)); break;
+    case CDX_KERNEL_RBF: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_RBF>, cgrid, cblk, 0, s, gv, const_cast<double*>(v.csum)); break;
+    default: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_JOINT>, cgrid, cblk, 0, s, gv, const_cast<double*>(v.csum)); break;
   }
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }

@@ -1,6 +1,6 @@
-"""Per-launch means of the std kernels' SQ counters from tools/pmc_std.sh output.
+"""Per-launch means of the std / screen kernels' SQ counters from tools/pmc_std.sh / pmc_screen.sh output.
 
-  python tools/pmc_std_summary.py gpurun_out/pmc_std_<tag>
+  python tools/pmc_std_summary.py gpurun_out/pmc_std_<tag>   (or gpurun_out/pmc_screen_<tag>)
 """
 import collections
 import csv
@@ -14,10 +14,13 @@ def main(d):
     for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
+            if "gpis_screen_kernel<" in k:
+                agg["SCREEN"][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                continue
             if "gpis_std_kernel<" not in k:
                 continue
-            mode = k.split("gpis_std_kernel<")[1].split(",")[1].strip()
-            agg[{"1": "VAR", "2": "GRADV", "0": "GRAD"}[mode]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            mode = k.split("gpis_std_kernel<")[1].split(",")[1].split(">")[0].strip()
+            agg[{"1": "VAR", "2": "GRADV", "0": "GRAD", "3": "VARL"}[mode]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for key, c in agg.items():
         m = {n: sum(v) / len(v) for n, v in c.items()}
         print(key)

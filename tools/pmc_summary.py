@@ -71,10 +71,13 @@ def main():
         summary["kernels"][short(k)] = {"FETCH_SIZE_kB": f, "WRITE_SIZE_kB": w, "hbm_bytes": (2 * f + w) * 1024,
                                         "dispatches": len(fetch.get(k, []))}
         m = re.search(r"gpis_std_kernel<\d+, (\d)", k)
-        if m:  # template <KT, MODE, T4>: MODE 1 = whitened std pass (VAR), 2 = ∇std pass (GRADV)
-            key = {"1": "gpis_var_bytes_per_launch", "2": "gpis_grad_bytes_per_launch"}.get(m.group(1))
+        if m:  # template <KT, MODE>: 1 = whitened std pass (VAR), 2 = ∇std pass (GRADV), 3 = refine (VARL)
+            key = {"1": "gpis_var_bytes_per_launch", "2": "gpis_grad_bytes_per_launch",
+                   "3": "gpis_refine_bytes_per_launch"}.get(m.group(1))
             if key:
                 summary[key] = (2 * f + w) * 1024
+        if "gpis_screen_kernel" in k:
+            summary["gpis_screen_bytes_per_launch"] = (2 * f + w) * 1024
     json.dump(summary, open(os.path.join(REPO, "profiles", f"{tag}_pmc.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
 
