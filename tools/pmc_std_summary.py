@@ -19,6 +19,8 @@ def main(d):
                 continue
             if "gpis_std_kernel<" not in k:
                 continue
+            if "gpis_std_kernel<" in k and r.get("Counter_Name") is None:
+                continue
             mode = k.split("gpis_std_kernel<")[1].split(",")[1].split(">")[0].strip()
             agg[{"1": "VAR", "2": "GRADV", "0": "GRAD", "3": "VARL"}[mode]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for key, c in agg.items():
