@@ -422,8 +422,6 @@ struct ClosureWs {
   size_t bytes;
 };
 
-// The closure screens the all-tip rows with the bf16 estimate when the GPIS state carries a
-// calibrated screen (cdx_gpis_screen_prepare + screen_delta) and CDX_NO_SCREEN is unset.
 // Opt-in (CDX_FORK_MEAN=1): measured a net loss on MI355X, so off by default — the mean beside the
 // screen stretches the screen 0.334 → 0.425 ms and itself to 0.37 ms (1.334 vs 1.347 ms per closure
 // at config 2, profiles/r02g_fork_mean_ab.txt; also with the screen's waves at s_setprio 2).
@@ -432,9 +430,18 @@ bool fork_mean() {
   return on;
 }
 
-bool screen_on(const cdx_problem* p) {
+// The closure screens the all-tip rows with the bf16 estimate when the GPIS state carries a
+// calibrated screen (cdx_gpis_screen_prepare + screen_delta), CDX_NO_SCREEN is unset and there are
+// enough rows to fill the chip: below SCREEN_MIN_ROWS the screen runs a handful of workgroups and
+// its fixed cost (five launches) exceeds the fp64 pass it saves (config 1: E = 64, N = 361 runs
+// 0.16 ms unscreened on split-K, 1.6 ms screened).
+constexpr int64_t SCREEN_MIN_ROWS = 4096;
+
+bool screen_on(const cdx_problem* p, int64_t E) {
   static const bool off = getenv("CDX_NO_SCREEN") != nullptr;
-  return !off && p->gpis.screen && p->gpis.screen_delta > 0 && p->chain.n_tips <= CDX_MAX_TIPS;
+  const int64_t Ms = (int64_t)p->n_query_levels * E * p->chain.n_tips;
+  return !off && p->gpis.screen && p->gpis.screen_delta > 0 && p->chain.n_tips <= CDX_MAX_TIPS &&
+         Ms >= SCREEN_MIN_ROWS;
 }
 
 // The variance cost takes max_f log(100·std_f) (:730), so ∇std is only ever needed at one
@@ -457,7 +464,7 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   w.gstd = (double*)take(Ms * 3 * sizeof(double));
   w.sel = (int64_t*)take(Mg * sizeof(int64_t));
   w.Xg = (double*)take(Mg * 3 * sizeof(double));
-  const bool scr = screen_on(p);
+  const bool scr = screen_on(p, E);
   w.var_ws = scr ? nullptr : take(cdx::gpis_var_ws_bytes(p->gpis, Ms));
   w.grad_ws = take(cdx::gpis_grad_ws_bytes(p->gpis, Mg));
   w.sv2 = scr ? (double*)take(Ms * sizeof(double)) : nullptr;
@@ -627,7 +634,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                      pregrasp_tip);
   cdx::prof_mark(cdx::PROF_QUERIES, false, s);
   if (hipGetLastError() != hipSuccess) return CDX_ELAUNCH;
-  const bool scr = screen_on(p);
+  const bool scr = screen_on(p, E);
   SideStream ss;
   const bool fork = scr && fork_mean() && side_stream(ss);
   int rc;
@@ -712,7 +719,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
 
 int cdx_closure_screen_stats(const cdx_problem* p, int64_t E, const void* workspace, int32_t* out) {
   if (!problem_ok(p) || E <= 0 || !workspace || !out) return CDX_EINVAL;
-  if (!screen_on(p)) {
+  if (!screen_on(p, E)) {
     out[0] = out[1] = out[2] = -1;
     return CDX_OK;
   }

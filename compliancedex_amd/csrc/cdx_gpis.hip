@@ -207,9 +207,18 @@ __device__ inline void refine_locate(int64_t q, int MtL, int N, int Np, int& nt,
   S1 = S0 + ks;
 }
 
-// Piece of the refine pass run by block b: the 256 pieces in sequence order, 32 consecutive ones per
-// XCD (blocks b, b+8, … share an XCD).
-__device__ inline int refine_piece(int b, int G) { return (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b; }
+// Pieces of the refine pass: one per block (gridDim.x = 256, one per CU), fewer when the sequence is
+// short — at least REFINE_MIN_KSTEPS each, so that a cut unit is never spread over dozens of
+// nearly empty pieces whose partial tiles the merge would then sum (config-1-sized problems).
+constexpr int REFINE_MIN_KSTEPS = 16;
+__device__ inline int refine_pieces(int64_t total, int G) {
+  return (int)max((int64_t)1, min((int64_t)G, total / REFINE_MIN_KSTEPS));
+}
+// Piece run by block b: with all G pieces, 32 consecutive ones per XCD (blocks b, b+8, … share an
+// XCD); with fewer, piece b (blocks spread round-robin over the XCDs).
+__device__ inline int refine_piece(int b, int G, int pieces) {
+  return pieces == G && (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b;
+}
 
 #if defined(CDX_DIAG_WGTIME)
 // timing-only diagnostic: per-workgroup [start, end] (s_memrealtime, 100 MHz), HW_ID, XCC_ID, stripe,
@@ -582,8 +591,10 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     int W = 0;
     for (int t = 0; t < Nt; ++t) W += var_ksteps(t, g.N, Np);
     const int64_t total = (int64_t)MtL * W;
-    const int pc = refine_piece(b, gridDim.x);
-    const int64_t q0 = total * pc / gridDim.x, q1 = total * (pc + 1) / gridDim.x;
+    const int pieces = refine_pieces(total, gridDim.x);
+    const int pc = refine_piece(b, gridDim.x, pieces);
+    if (pc >= pieces) return;
+    const int64_t q0 = total * pc / pieces, q1 = total * (pc + 1) / pieces;
     bool first = true;
     for (int64_t q = q0; q < q1;) {
       int nt, mt;
@@ -804,7 +815,8 @@ __global__ __launch_bounds__(256) void gpis_var_merge(cdx_gpis g, RefineList rl,
   int W = 0;
   for (int t = 0; t < Nt; ++t) W += var_ksteps(t, g.N, Np);
   const int64_t total = (int64_t)MtL * W;
-  const int pieces = gridDim.x, p = blockIdx.x;
+  const int pieces = refine_pieces(total, gridDim.x), p = blockIdx.x;
+  if (p >= pieces) return;
   auto qof = [&](int pp) { return total * pp / pieces; };
   const int64_t q0 = qof(p), q1 = qof(p + 1);
   if (q0 >= q1 || q0 >= total) return;

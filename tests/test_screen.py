@@ -104,7 +104,7 @@ def test_screen_var_c_abi_edges(banana2000):
     assert lib.cdx_gpis_screen_var(bare, N.ptr(X), 4, N.ptr(out), N.ptr(out), None) == -1
 
 
-@pytest.mark.parametrize("case", ["config2_E4096", "stored_banana_E64", "config3_mug_E4096"])
+@pytest.mark.parametrize("case", ["config2_E4096", "stored_banana_E1024", "config3_mug_E4096"])
 def test_screened_closure_equals_fp64_closure(case, banana2000):
     """Screened vs unscreened closure on the same inputs: equal to TOL_EQ, NaNs and Kabsch masks
     identical; the exact pass ran for ≤ 1.25 fingertips per group and no kept estimate left its bound."""
@@ -112,8 +112,8 @@ def test_screened_closure_equals_fp64_closure(case, banana2000):
     cfg, opt = _opt()
     if case == "config2_E4096":
         gpis, E, center = banana2000, 4096, None
-    elif case == "stored_banana_E64":
-        gpis, E, center = stored_gpis("banana", DEV), 64, None
+    elif case == "stored_banana_E1024":  # the smallest screened size (4096 all-tip rows), N = 361
+        gpis, E, center = stored_gpis("banana", DEV), 1024, None
     else:
         _, gpis = config3_gpis(1, DEV)
         E, center = 4096, surface_center(gpis)
@@ -127,6 +127,16 @@ def test_screened_closure_equals_fp64_closure(case, banana2000):
     assert np.array_equal(a["flip"], b["flip"])
     for k in OUTS:
         assert rel_err(a[k], b[k]) <= TOL_EQ, (k, rel_err(a[k], b[k]))
+
+
+def test_small_closure_not_screened():
+    """Below 4096 all-tip rows (config 1: E = 64) the closure runs the fp64 pass for every row: the
+    screen's fixed cost would exceed what it saves (cdx_closure.hip SCREEN_MIN_ROWS)."""
+    from compliancedex_amd.workloads import prob_inputs, stored_gpis
+    cfg, opt = _opt()
+    gpis = stored_gpis("banana", DEV)
+    _, st = _closure(opt, gpis, prob_inputs(cfg["ref_q"], 64, seed=1, spread=True))
+    assert st is None
 
 
 def test_screened_closure_deterministic(banana2000):
