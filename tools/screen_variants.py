@@ -16,9 +16,10 @@ sys.path.insert(0, REPO)
 BASE = ("CDX_FAST_SQRT", "CDX_STD_SCHED")
 VARIANTS = {"base": BASE,
             "diag_nogen": BASE + ("CDX_SC_DIAG_NOGEN",),
-            "diag_nobload": BASE + ("CDX_SC_DIAG_NOBLOAD",),
             "diag_nomfma": BASE + ("CDX_SC_DIAG_NOMFMA",),
-            "diag_nogen_nobload": BASE + ("CDX_SC_DIAG_NOGEN", "CDX_SC_DIAG_NOBLOAD")}
+            "diag_nogen_nomfma": BASE + ("CDX_SC_DIAG_NOGEN", "CDX_SC_DIAG_NOMFMA")}
+# measured and dropped (profiles/r02j_screen_variants.jsonl): sched_group_barrier 1 MFMA : 6 VALU
+# interleave (+10 %), s_setprio 1 around the MFMA block (+6 %)
 if os.environ.get("CDX_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CDX_VARIANTS"].split(",")}
 
