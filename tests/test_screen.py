@@ -129,6 +129,27 @@ def test_screened_closure_equals_fp64_closure(case, banana2000):
         assert rel_err(a[k], b[k]) <= TOL_EQ, (k, rel_err(a[k], b[k]))
 
 
+@pytest.mark.parametrize("kernel", ["rbf", "joint"])
+def test_screened_closure_other_gpis_kernels(kernel):
+    """The screen's RBF (expm1 offset) and joint-kernel generation: the screened closure equals the
+    unscreened one on an N = 2000 state fitted with that kernel (E = 1024, Leap hand for variety)."""
+    from compliancedex_amd.gpis import GPIS
+    from compliancedex_amd.workloads import prob_inputs, synthetic_banana_arrays
+    X1, y, noise = synthetic_banana_arrays(2000)
+    g = GPIS(0.08, 1.0, kernel=kernel)
+    g.fit(torch.from_numpy(X1).to(DEV), torch.from_numpy(y).to(DEV), noise=torch.from_numpy(noise).to(DEV))
+    g.bias = torch.tensor(1.0, dtype=torch.float64, device=DEV)
+    cfg, opt = _opt("leap")
+    inputs = prob_inputs(cfg["ref_q"], 1024, seed=11, spread=True)
+    a, st = _closure(opt, g, inputs, screen=True)
+    b, st0 = _closure(opt, g, inputs, screen=False)
+    assert st0 is None and st is not None and st["bound_misses"] == 0
+    assert 1024 <= st["exact_rows"] <= 4 * 1024
+    assert np.array_equal(a["flip"], b["flip"])
+    for k in OUTS:
+        assert rel_err(a[k], b[k]) <= TOL_EQ, (k, rel_err(a[k], b[k]))
+
+
 def test_small_closure_not_screened():
     """Below 4096 all-tip rows (config 1: E = 64) the closure runs the fp64 pass for every row: the
     screen's fixed cost would exceed what it saves (cdx_closure.hip SCREEN_MIN_ROWS)."""
