@@ -30,7 +30,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6  # gfx950 vendor spec; MI355X_MICROARCH.md has no f64 row
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md § Matrix cores)
+F16_MFMA_PEAK_TFLOPS = 2500.0  # dense fp16/bf16 MFMA (MI355X_MICROARCH.md § Matrix cores)
 
 
 def parse():
@@ -220,9 +220,9 @@ def main():
     n_ind = args.n_inducing
     # algorithmic flops per launch (unpadded N): V = K*·L⁻ᵀ is triangular, N(N+1)/2 MACs per
     # query; W = V·L⁻¹ (= (E11⁻¹k)ᵀ) at the variance cost's argmax fingertip only, also triangular;
-    # the screen runs the triangular product for every all-tip row as 6 bf16 slice products
+    # the screen runs the triangular product for every all-tip row as 3 fp16 slice products
     tri = float(n_ind) * (n_ind + 1)
-    flops, flops_g, flops_s = m_exact * tri, m_grad * tri, 6 * m_std * tri
+    flops, flops_g, flops_s = m_exact * tri, m_grad * tri, 3 * m_std * tri
     std_ms, grad_ms, scr_ms = stage_ms["gpis_std_var"], stage_ms["gpis_std_grad"], stage_ms["gpis_screen"]
     achieved = flops / (std_ms * 1e-3) / 1e12 if std_ms else None
     achieved_g = flops_g / (grad_ms * 1e-3) / 1e12 if grad_ms else None
@@ -272,13 +272,13 @@ def main():
         }
         if scr:
             out["roofline_screen"] = {
-                "bound": "mfma", "kernel": "gpis_screen_kernel (v_mfma_f32_32x32x16_bf16, 3-slice bf16 split of "
-                                           "(K*−k0)·L⁻ᵀ, 6 slice products)",
-                "achieved": achieved_s, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": (achieved_s / BF16_MFMA_PEAK_TFLOPS) if achieved_s else None,
+                "bound": "mfma", "kernel": "gpis_screen_kernel (v_mfma_f32_32x32x16_f16, 2-slice fp16 split of "
+                                           "(K*−k0)·L⁻ᵀ, 3 slice products)",
+                "achieved": achieved_s, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": (achieved_s / F16_MFMA_PEAK_TFLOPS) if achieved_s else None,
                 "traffic": hbm_traffic(E, n_ind, "gpis_screen_bytes_per_launch"),
                 "flops_per_launch": flops_s, "ms": scr_ms,
-                "note": f"{m_std} all-tip rows x 6 x N(N+1) bf16 MFMA flops (the split-precision estimate that "
+                "note": f"{m_std} all-tip rows x 3 x N(N+1) fp16 MFMA flops (the split-precision estimate that "
                         f"selects the rows of the exact pass)"}
             out["screen"] = {"exact_rows": scr["exact_rows"], "screened_rows": scr["screened_rows"],
                              "bound_misses": scr["bound_misses"],

@@ -9,7 +9,7 @@
 
 namespace cdx {
 
-constexpr int SC_BK = 16;   // K rows per stage (one v_mfma_f32_32x32x16_bf16 deep)
+constexpr int SC_BK = 16;   // K rows per stage (one v_mfma_f32_32x32x16_f16 deep)
 constexpr int SC_BN = 256;  // columns per stripe (= CDX_NPAD_ALIGN)
 
 // Column shift of the whitened products (the fp64 pass's var_shift): the N_pad − N padding
@@ -18,14 +18,16 @@ __device__ __host__ inline int screen_shift(int N, int Np) { return std::min((Np
 
 __device__ __host__ inline size_t screen_align(size_t b) { return (b + 255) / 256 * 256; }
 
-// [L: N_pad/16 × 3 slices × 2 k-halves × N_pad columns × 8 bf16][csum: N_pad f64][X1f: N_pad float4][centre: 4 f64]
+// [L: N_pad/16 × 2 slices × 2 k-halves × N_pad columns × 8 f16][csum: N_pad f64][cscale: N_pad f64]
+// [X1f: N_pad float4][centre: cx, cy, cz, SA (A-operand scale), rq² (largest safe |x − centre|²)]
 inline size_t screen_bytes(int Np) {
-  return screen_align((size_t)Np * Np * 6) + screen_align((size_t)Np * 8) + screen_align((size_t)Np * 16) + 256;
+  return screen_align((size_t)Np * Np * 4) + 2 * screen_align((size_t)Np * 8) + screen_align((size_t)Np * 16) + 256;
 }
 
 struct ScreenView {
   const void* L;
   const double* csum;
+  const double* cscale;  // 1 / (SA · SB_j): the column's product scale, a power of two
   const float4* X1f;
   const double* center;
 };
@@ -33,10 +35,10 @@ struct ScreenView {
 __device__ __host__ inline ScreenView screen_view(const cdx_gpis& g) {
   const char* p = static_cast<const char*>(g.screen);
   const size_t Np = (size_t)g.N_pad;
-  const size_t oL = 0, oc = oL + screen_align(Np * Np * 6), ox = oc + screen_align(Np * 8),
+  const size_t oL = 0, oc = oL + screen_align(Np * Np * 4), os = oc + screen_align(Np * 8), ox = os + screen_align(Np * 8),
                oz = ox + screen_align(Np * 16);
-  return ScreenView{p + oL, reinterpret_cast<const double*>(p + oc), reinterpret_cast<const float4*>(p + ox),
-                    reinterpret_cast<const double*>(p + oz)};
+  return ScreenView{p + oL, reinterpret_cast<const double*>(p + oc), reinterpret_cast<const double*>(p + os),
+                    reinterpret_cast<const float4*>(p + ox), reinterpret_cast<const double*>(p + oz)};
 }
 
 // partials [N_pad/256][round_up(M, 256)] f64

@@ -1,4 +1,4 @@
-// Split-precision screen of the GPIS posterior variance on the bf16 matrix cores (gfx950).
+// Split-precision screen of the GPIS posterior variance on the fp16 matrix cores (gfx950).
 //
 // The closure's variance cost reads only max_f log(100·std_f) over a candidate's fingertips
 // (optimize_pregrasp.py:733): one fingertip per (level, candidate) reaches the loss and its
@@ -8,20 +8,25 @@
 //
 //   Ṽ = Ã·L⁻ᵀ + k0·colsum(L⁻ᵀ),  Ã = K* − k0   (the offset keeps |Ã| small near the query, where
 //                                              the cancellation in k0 − ‖V‖² is worst)
-//   Ã and L⁻ᵀ are each split into three bf16 slices (x = x0 + x1 + x2, ≈ 24 bits: Ã exactly, it
-//   is generated in fp32), and the six slice products of index sum ≤ 2 are accumulated into one
-//   fp32 accumulator per output by v_mfma_f32_32x32x16_bf16 — fp32-level accuracy at 6 bf16
-//   MFMAs (2.5 PF/s dense) instead of one fp64 MFMA (78.6 TF/s): 2.1× the flop rate and no f64
-//   VALU work on the DP pipe.  Σ Ṽ² is summed in f64.
+//   Ã (scaled by a power of two SA, k0·SA ≤ 2¹⁰) and L⁻ᵀ (column j scaled by a power of two SB_j,
+//   max |column|·SB_j < 2¹⁴) are each split into two fp16 slices (x = x0 + x1, ≈ 22 bits), and the
+//   three slice products of index sum ≤ 1 are accumulated into one fp32 accumulator per output by
+//   v_mfma_f32_32x32x16_f16; the epilogue multiplies by 1/(SA·SB_j) (exact).  The error is set by
+//   the fp32 generation and accumulation, not the 22-bit operands: the CPU emulation gives the same
+//   1.5e-6·k0 as three bf16 slices with six products (round 2's first version), at half the MFMAs
+//   and two thirds of the operand bytes.  Σ Ṽ² is summed in f64.  A query farther than rq from the
+//   inducing points' centre (where SA·Ã could leave fp16's range) is made NaN, so the closure runs
+//   the exact pass for its whole group.
 //
 // The estimate carries no parity claim by itself: the closure only uses it to discard fingertips
 // whose estimated std² is below the leader's by more than twice the per-object error bound
 // (cdx_gpis.screen_delta, calibrated against the fp64 pass when the state is built), and writes
 // exact fp64 values for every fingertip it keeps.  tools/screen_emul.py emulates this arithmetic
-// bit-for-bit on the CPU (max |Δstd²|/k0 = 1.8e-6 on the config-2 workload).
+// on the CPU (max |Δstd²|/k0 = 1.5e-6 on the config-2 workload).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 #include "cdx_gpis.h"
@@ -31,7 +36,7 @@
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -39,7 +44,7 @@ using cdx::SC_BK;
 using cdx::SC_BN;
 constexpr int SC_BM = 256;                 // query rows per workgroup
 constexpr int SC_THREADS = 512;            // 8 waves: 2 (rows) × 4 (columns), 128 × 64 outputs each
-constexpr int SC_REG = 6 * 256;            // 16-byte LDS units of one operand stage: [slice][khalf][256]
+constexpr int SC_REG = 4 * 256;            // 16-byte LDS units of one operand stage: [slice][khalf][256]
 constexpr int SC_LDT = 264;               // fp32 row pitch of the epilogue's accumulator image (4 rows ≡ 32 banks)
 // LDS: A stages (generated, 2 buffers) | B stages (LDS-DMA ring of 3)
 constexpr int SC_A_OFF = 0, SC_B_OFF = 2 * SC_REG * 16;
@@ -53,24 +58,25 @@ __device__ __host__ inline int sc_ksteps(int nt, int N, int Np) {
   return (hi + SC_BK - 1) / SC_BK;
 }
 
-// Ã = k(r) − k(0) in fp32 from a centred fp32 offset (d = x − x_n).
+// SA·Ã = SA·(k(r) − k(0)) in fp32 from a centred fp32 offset (d = x − x_n); kc = {SA·w_rbf,
+// 2·SA·w_tps, 3R·SA·w_tps, −0.5/σ²} with the joint kernel's weights w (0.3, 0.7) or 1.
 template <int KT>
-__device__ __forceinline__ float k_offset(float dx, float dy, float dz, float R, float inv_s2) {
+__device__ __forceinline__ float k_offset(float dx, float dy, float dz, const float4& kc) {
   const float r2 = dx * dx + dy * dy + dz * dz;
-  if (KT == CDX_KERNEL_RBF) return expm1f(-0.5f * r2 * inv_s2);
+  if (KT == CDX_KERNEL_RBF) return kc.x * expm1f(r2 * kc.w);
   const float r = __builtin_amdgcn_sqrtf(r2);  // v_sqrt_f32 (≤ 1 ulp): ample for a screen
-  const float tps = r2 * (2.0f * r - 3.0f * R);  // 2r³ − 3Rr²  (= TPS − R³)
+  const float tps = r2 * (kc.y * r - kc.z);    // SA·(2r³ − 3Rr²)  (= SA·(TPS − R³))
   if (KT == CDX_KERNEL_TPS) return tps;
-  return 0.3f * expm1f(-0.5f * r2 * inv_s2) + 0.7f * tps;
+  return kc.x * expm1f(r2 * kc.w) + tps;
 }
 
-// x = s0 + s1 + s2 exactly, each a bf16 given as the high half of an fp32 bit pattern: truncated
-// 8-bit pieces of x's 24-bit significand (the remainders are exact in fp32).
-__device__ __forceinline__ void split3(float x, unsigned& s0, unsigned& s1, unsigned& s2) {
-  s0 = __float_as_uint(x) & 0xffff0000u;
-  const float r1 = x - __uint_as_float(s0);
-  s1 = __float_as_uint(r1) & 0xffff0000u;
-  s2 = __float_as_uint(r1 - __uint_as_float(s1));  // ≤ 8 significant bits: low half already zero
+// (xa, xb) = (a0 + a1, b0 + b1): fp16 pairs truncated from fp32 (v_cvt_pkrtz_f16_f32); the
+// remainders x − x0 are exact in fp32, so the split loses only the second truncation (≤ 2⁻²⁰·|x|).
+__device__ __forceinline__ void split2(float xa, float xb, unsigned& h0, unsigned& h1) {
+  const auto p = __builtin_amdgcn_cvt_pkrtz(xa, xb);
+  const auto q = __builtin_amdgcn_cvt_pkrtz(xa - (float)p[0], xb - (float)p[1]);
+  h0 = __builtin_bit_cast(unsigned, p);
+  h1 = __builtin_bit_cast(unsigned, q);
 }
 
 // One workgroup per (query tile of 256 rows, stripe of 256 columns); stripes paired heavy+light per
@@ -115,8 +121,14 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
     qx = (float)(X[3 * m] - sv.center[0]);
     qy = (float)(X[3 * m + 1] - sv.center[1]);
     qz = (float)(X[3 * m + 2] - sv.center[2]);
+    if (!(qx * qx + qy * qy + qz * qz <= (float)sv.center[4])) qx = __builtin_nanf("");  // SA·Ã may overflow fp16
   }
-  const float R = (float)g.R, inv_s2 = (float)(1.0 / (g.sigma * g.sigma));
+  float4 kc;
+  {
+    const double SA = sv.center[3], w = KT == CDX_KERNEL_JOINT ? 0.7 : 1.0;
+    kc = make_float4((float)(SA * (KT == CDX_KERNEL_JOINT ? 0.3 : 1.0)), (float)(2.0 * SA * w), (float)(3.0 * g.R * SA * w),
+                     (float)(-0.5 / (g.sigma * g.sigma)));
+  }
 
   // wave → 128 × 64 output sub-tile; waves w and w+4 share a SIMD and take complementary columns
   const int cwave = wave < 4 ? wave : 7 - wave;
@@ -133,9 +145,9 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // Staging by LDS-DMA (global_load_lds: no VGPRs, no ds_write).  issue(st): every wave DMAs 3 × 1 KB
+  // Staging by LDS-DMA (global_load_lds: no VGPRs, no ds_write).  issue(st): every wave DMAs 2 × 1 KB
   // of B stage st (instruction u = wave + 8i: slice/k-half region u>>2, columns 64·(u&3) + lane).
-  // issue(s+2) runs during step s; the counted `s_waitcnt vmcnt(3)` at the end of each step keeps
+  // issue(s+2) runs during step s; the counted `s_waitcnt vmcnt(2)` at the end of each step keeps
   // exactly that step's DMAs in flight across the raw s_barrier (__syncthreads would wait vmcnt(0)),
   // with B stage s+1 landed for step s+1.  Clamped stages past the stripe's end load into free
   // slots, so every step issues the same count.
@@ -144,13 +156,13 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
     const int sc = std::min(st, nK - 1);
     const int slot = st % 3;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 2; ++i) {
       const int u = wave + 8 * i, reg = u >> 2, col = 64 * (u & 3) + lane;
-      const char* src = Lb + (((int64_t)(sc * 6 + reg)) * Np + n0 + col) * 16;
+      const char* src = Lb + (((int64_t)(sc * 4 + reg)) * Np + n0 + col) * 16;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sB4 + slot * SC_REG + u * 64), 16, 0, 0);
     }
   };
-  u32x4 ast[3];      // generated A stage: 8 entries × 3 bf16 slices, packed in pairs
+  u32x4 ast[2];      // generated A stage: 8 entries × 2 fp16 slices, packed in pairs
   // X1 rows of the generated stage: wave-uniform addresses → scalar loads (SMEM; the vector memory
   // counter stays free for the DMAs' counted waits)
   auto gen_a = [&](int st) {  // 8 consecutive k of this thread's half, packed in pairs
@@ -163,41 +175,38 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
 #pragma unroll
     for (int e = 0; e < 8; e += 2) {
       const float4 p = x1[e], p1 = x1[e + 1];
-      unsigned a0, a1, a2, b0, b1, b2;
+      unsigned h0, h1;
 #if defined(CDX_SC_DIAG_NOGEN)  // timing-only diagnostic build: outputs are wrong
-      a0 = __float_as_uint(qx - p.x); a1 = __float_as_uint(qy - p.y); a2 = __float_as_uint(qz - p.z);
-      b0 = __float_as_uint(qx - p1.x); b1 = __float_as_uint(qy - p1.y); b2 = __float_as_uint(qz - p1.z);
+      split2(qx - p.x, qy - p1.y, h0, h1);
 #else
-      split3(k_offset<KT>(qx - p.x, qy - p.y, qz - p.z, R, inv_s2), a0, a1, a2);
-      split3(k_offset<KT>(qx - p1.x, qy - p1.y, qz - p1.z, R, inv_s2), b0, b1, b2);
+      split2(k_offset<KT>(qx - p.x, qy - p.y, qz - p.z, kc), k_offset<KT>(qx - p1.x, qy - p1.y, qz - p1.z, kc), h0, h1);
 #endif
-      ast[0][e / 2] = __builtin_amdgcn_perm(b0, a0, 0x07060302u);
-      ast[1][e / 2] = __builtin_amdgcn_perm(b1, a1, 0x07060302u);
-      ast[2][e / 2] = __builtin_amdgcn_perm(b2, a2, 0x07060302u);
+      ast[0][e / 2] = h0;
+      ast[1][e / 2] = h1;
     }
   };
   auto write_a = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) sA4[buf * SC_REG + (i * 2 + gkh) * 256 + grow] = ast[i];
+    for (int i = 0; i < 2; ++i) sA4[buf * SC_REG + (i * 2 + gkh) * 256 + grow] = ast[i];
   };
-  // one stage's 48 MFMAs: lane → (row/col l&31, k-half l>>5); B slices of both column blocks, A
-  // slice by slice (products of slice-index sum ≤ 2, smallest first)
+  // one stage's 24 MFMAs: lane → (row/col l&31, k-half l>>5); B slices of both column blocks, A
+  // slice by slice (products of slice-index sum ≤ 1, smallest first)
   auto mfma_stage = [&](int abuf, int bslot, auto more_c) {
     constexpr bool MORE = decltype(more_c)::value;
-    bf16x8 fb[3][2];
+    f16x8 fb[2][2];
 #pragma unroll
-    for (int sb = 0; sb < 3; ++sb)
+    for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        fb[sb][j] = __builtin_bit_cast(bf16x8, sB4[bslot * SC_REG + (sb * 2 + (lane >> 5)) * 256 + wc + 32 * j + (lane & 31)]);
+        fb[sb][j] = __builtin_bit_cast(f16x8, sB4[bslot * SC_REG + (sb * 2 + (lane >> 5)) * 256 + wc + 32 * j + (lane & 31)]);
 #pragma unroll
-    for (int sa = 2; sa >= 0; --sa) {
-      bf16x8 fa[4];
+    for (int sa = 1; sa >= 0; --sa) {
+      f16x8 fa[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        fa[i] = __builtin_bit_cast(bf16x8, sA4[abuf * SC_REG + (sa * 2 + (lane >> 5)) * 256 + wr + 32 * i + (lane & 31)]);
+        fa[i] = __builtin_bit_cast(f16x8, sA4[abuf * SC_REG + (sa * 2 + (lane >> 5)) * 256 + wr + 32 * i + (lane & 31)]);
 #pragma unroll
-      for (int sb = 2 - sa; sb >= 0; --sb)
+      for (int sb = 1 - sa; sb >= 0; --sb)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -205,7 +214,7 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
 #if defined(CDX_SC_DIAG_NOMFMA)  // timing-only diagnostic build: outputs are wrong
             acc[i][j][0] += (float)fa[i][0] * (float)fb[sb][j][0];
 #else
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[sb][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[sb][j], acc[i][j], 0, 0, 0);
 #endif
       if (!MORE) __builtin_amdgcn_sched_barrier(0);  // tail step: no fragment hoisting past a slice group
     }
@@ -230,7 +239,7 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
     if (MORE) gen_a(s + 1);
     if (LIVE) mfma_stage(s & 1, s % 3, more_c);
     if (MORE) write_a((s + 1) & 1);
-    asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");  // B stage s+1 landed, A written
+    asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");  // B stage s+1 landed, A written
     __builtin_amdgcn_s_barrier();
   };
   using T_ = std::true_type;
@@ -267,12 +276,13 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
     __syncthreads();
     const float4* Tr = reinterpret_cast<const float4*>(T + erow * SC_LDT + 64 * epart);
     const double* cs = sv.csum + n0 + 64 * epart;
+    const double* cf = sv.cscale + n0 + 64 * epart;
     double sum = 0.0;
 #pragma unroll 4
     for (int c = 0; c < 16; ++c) {
       const float4 v = Tr[c];
-      const double x0 = (double)v.x + cs[4 * c], x1 = (double)v.y + cs[4 * c + 1], x2 = (double)v.z + cs[4 * c + 2],
-                   x3 = (double)v.w + cs[4 * c + 3];
+      const double x0 = fma((double)v.x, cf[4 * c], cs[4 * c]), x1 = fma((double)v.y, cf[4 * c + 1], cs[4 * c + 1]),
+                   x2 = fma((double)v.z, cf[4 * c + 2], cs[4 * c + 2]), x3 = fma((double)v.w, cf[4 * c + 3], cs[4 * c + 3]);
       sum = fma(x0, x0, sum);
       sum = fma(x1, x1, sum);
       sum = fma(x2, x2, sum);
@@ -297,11 +307,17 @@ __global__ __launch_bounds__(256) void gpis_screen_finalize(cdx_gpis g, const do
 
 // ------------------------------------------------------------------ closure screening
 // Groups of T consecutive all-tip rows (one (distinct level, candidate) each); the variance cost
-// takes max_f log(100·std_f) over a group (optimize_pregrasp.py:733).  Per group: s̃²_f = k0 − Σ
-// stripe partials; leader = first maximum; the fingertips kept for the exact pass are the leader
-// and every f with s̃²_f + Δ ≥ s̃²_lead − Δ (Δ = g.screen_delta ≥ max |s̃² − std²|), or all T when a
-// value is not finite or s̃²_lead ≤ 2Δ.  A discarded fingertip gets std = sqrt(max(s̃², 0)), which
-// is below the leader's exact std, so the level kernel's own argmax is unchanged.
+// takes max_f log(100·std_f) over a group (optimize_pregrasp.py:733) with std = sqrt(|var|)
+// (gpis.py:59).  Per group: s̃²_f = k0 − Σ stripe partials, a_f = |s̃²_f| with the row's margin
+// Δ_f = Δ·max(1, (k0 − s̃²_f)/k0) (Δ = g.screen_delta, calibrated so |s̃² − var| ≤ Δ_f; the factor is
+// ‖Ṽ‖²/k0, the scale of the estimate's rounding, 1 near the object), so |var_f| ∈ [a_f − Δ_f, a_f +
+// Δ_f].  Leader = first maximum of a_f; kept for the exact pass: every f with a_f + Δ_f ≥ max_g (a_g
+// − Δ_g) (the leader always), all T when a value is not finite.  A discarded fingertip gets std =
+// sqrt(a_f), below the exact std of the group's maximum, so the level kernel's argmax is unchanged.
+__device__ __forceinline__ double screen_margin(double delta, double k0, double s2) {
+  return delta * fmax(1.0, (k0 - s2) / k0);
+}
+
 template <int KT>
 __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const double* __restrict__ partial,
                                                             int64_t M_pad, int Nt, int64_t G, int T,
@@ -311,31 +327,33 @@ __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const do
   const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= G) return;
   const double k0 = cdx::gpis_k0<KT>(g.R), delta = g.screen_delta;
-  double s2[CDX_MAX_TIPS];
+  double a[CDX_MAX_TIPS], d[CDX_MAX_TIPS];
   bool finite = true;
   int lead = 0;
+  double lo = -INFINITY;
   for (int f = 0; f < T; ++f) {
     const int64_t q = gi * T + f;
     double acc = 0;
     for (int t = 0; t < Nt; ++t) acc += partial[(int64_t)t * M_pad + q];
-    s2[f] = k0 - acc;
-    sv2[q] = s2[f];
-    finite = finite && isfinite(s2[f]);
-    if (s2[f] > s2[lead]) lead = f;
+    const double s2 = k0 - acc;
+    sv2[q] = s2;
+    a[f] = fabs(s2);
+    d[f] = screen_margin(delta, k0, s2);
+    finite = finite && isfinite(s2) && isfinite(d[f]);
+    if (a[f] > a[lead]) lead = f;
+    lo = fmax(lo, a[f] - d[f]);
   }
-  const bool all = !finite || !(s2[lead] > 2 * delta);
-  const double lo = s2[lead] - delta;
   unsigned mask = 0;
   for (int f = 0; f < T; ++f) {
     const int64_t q = gi * T + f;
     if (f == lead) {
       vpos[q] = (int)gi;
       rows[gi] = (int)q;
-    } else if (all || s2[f] + delta >= lo) {
+    } else if (!finite || a[f] + d[f] >= lo) {
       mask |= 1u << f;  // position assigned by screen_compact_kernel
     } else {
       vpos[q] = -1;
-      std_[q] = sqrt(fmax(s2[f], 0.0));
+      std_[q] = sqrt(a[f]);
     }
   }
   keep[gi] = (unsigned char)mask;
@@ -382,8 +400,9 @@ __global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, 
 
 // Exact values of the kept fingertips from the refine pass's stripe partials, then the group's
 // first maximum of log(100·std) — the level kernel's choice — as the ∇std row: sel = its query,
-// Xg = its point, vrow = its V row (list position).  stats[1] counts kept rows whose screen value
-// missed the exact one by more than Δ (the calibration bound; 0 expected).
+// Xg = its point, vrow = its V row (list position).  stats[1] counts kept rows whose finite screen
+// value missed the exact one by more than Δ_f (the calibration bound; 0 expected; a NaN estimate kept
+// its whole group).
 template <int KT>
 __global__ __launch_bounds__(256) void refine_select_kernel(cdx_gpis g, const double* __restrict__ rpartial,
                                                             int64_t M_pad, int Nt, int64_t G, int T,
@@ -408,7 +427,8 @@ __global__ __launch_bounds__(256) void refine_select_kernel(cdx_gpis g, const do
       sd = sqrt(fabs(v));
       std_[q] = sd;
       var[q] = v;
-      if (!(fabs(sv2[q] - v) <= delta) && isfinite(v)) atomicAdd(&stats[1], 1);
+      if (!(fabs(sv2[q] - v) <= screen_margin(delta, k0, sv2[q])) && isfinite(v) && isfinite(sv2[q]))
+        atomicAdd(&stats[1], 1);
     } else {
       sd = std_[q];
     }
@@ -422,9 +442,10 @@ __global__ __launch_bounds__(256) void refine_select_kernel(cdx_gpis g, const do
 }
 
 // ------------------------------------------------------------------ preparation (once per state)
-// Centre of the inducing points (mean of rows < N, one block, fixed-order tree reduction) and the
-// centred fp32 copy X1f [N_pad] (padding rows = row 0).
-__global__ __launch_bounds__(256) void screen_center_kernel(cdx_gpis g, double* __restrict__ center,
+// Centre of the inducing points (mean of rows < N, one block, fixed-order tree reduction), the
+// centred fp32 copy X1f [N_pad] (padding rows = row 0), the A scale SA and rq² = (max(0, r_safe −
+// max_n |x_n − centre|))²: within rq of the centre every |x − x_n| ≤ r_safe, where |SA·Ã| < 2¹⁶.
+__global__ __launch_bounds__(256) void screen_center_kernel(cdx_gpis g, double SA, double r_safe, double* __restrict__ center,
                                                             float4* __restrict__ X1f) {
   __shared__ double red[3][256];
   const int t = threadIdx.x;
@@ -439,7 +460,23 @@ __global__ __launch_bounds__(256) void screen_center_kernel(cdx_gpis g, double* 
     __syncthreads();
   }
   const double cx = red[0][0] / g.N, cy = red[1][0] / g.N, cz = red[2][0] / g.N;
-  if (t == 0) { center[0] = cx; center[1] = cy; center[2] = cz; center[3] = 0.0; }
+  __syncthreads();
+  double rm = 0;
+  for (int j = t; j < g.N; j += 256) {
+    const double dx = g.X1[3 * j] - cx, dy = g.X1[3 * j + 1] - cy, dz = g.X1[3 * j + 2] - cz;
+    rm = fmax(rm, dx * dx + dy * dy + dz * dz);
+  }
+  red[0][t] = rm;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) red[0][t] = fmax(red[0][t], red[0][t + w]);
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double rq = fmax(0.0, r_safe - sqrt(red[0][0]));
+    center[0] = cx; center[1] = cy; center[2] = cz; center[3] = SA;
+    center[4] = isinf(r_safe) ? r_safe : rq * rq;
+  }
   for (int j = t; j < g.N_pad; j += 256) {
     const int src = j < g.N ? j : 0;
     X1f[j] = make_float4((float)(g.X1[3 * src] - cx), (float)(g.X1[3 * src + 1] - cy), (float)(g.X1[3 * src + 2] - cz),
@@ -447,48 +484,61 @@ __global__ __launch_bounds__(256) void screen_center_kernel(cdx_gpis g, double* 
   }
 }
 
-// L [N_pad/16][3][2][N_pad][8] bf16: slice s of L⁻ᵀ[16kb + 8h + e][j − shift] (zero for j < shift),
-// the B-operand image the screen stages with one 16-byte load per (slice, k-half, column).
-__global__ __launch_bounds__(256) void screen_split_kernel(cdx_gpis g, bf16x8* __restrict__ L) {
+// L [N_pad/16][2][2][N_pad][8] f16: slice s of SB_j·L⁻ᵀ[16kb + 8h + e][j − shift] (zero for
+// j < shift), the B-operand image the screen stages with one 16-byte load per (slice, k-half,
+// column).  SB_j = 1/(SA·cscale[j]) (exact powers of two).
+__global__ __launch_bounds__(256) void screen_split_kernel(cdx_gpis g, f16x8* __restrict__ L, const double* __restrict__ cscale,
+                                                           const double* __restrict__ center) {
   const int Np = g.N_pad, shift = cdx::screen_shift(g.N, Np);
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)(Np / 16) * 2 * Np) return;
   const int col = (int)(t % Np);
   const int h = (int)((t / Np) % 2);
   const int kb = (int)(t / (2 * (int64_t)Np));
-  bf16x8 o[3];
+  const double SB = 1.0 / (cscale[col] * center[3]);
+  f16x8 o[2];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int n = 16 * kb + 8 * h + e, j = col - shift;
-    const double x = j >= 0 ? g.Linv_t[(int64_t)n * Np + j] : 0.0;
-    const __bf16 a = (__bf16)(float)x;  // f64 → f32 → bf16: the f32 step keeps the split exact
-    const double r1 = x - (double)(float)a;
-    const __bf16 b = (__bf16)(float)r1;
-    const double r2 = r1 - (double)(float)b;
+    const float x = (float)(j >= 0 ? g.Linv_t[(int64_t)n * Np + j] * SB : 0.0);
+    const _Float16 a = (_Float16)x;  // round to nearest; x − a is exact in fp32
     o[0][e] = a;
-    o[1][e] = b;
-    o[2][e] = (__bf16)(float)r2;
+    o[1][e] = (_Float16)(x - (float)a);
   }
-  for (int s = 0; s < 3; ++s) L[(((int64_t)kb * 3 + s) * 2 + h) * Np + col] = o[s];
+  for (int s = 0; s < 2; ++s) L[(((int64_t)kb * 2 + s) * 2 + h) * Np + col] = o[s];
 }
 
-// csum[j] = k0 · Σ_{n<N} L⁻ᵀ[n][j − shift] (zero for j < shift): Ṽ = Ã·L⁻ᵀ + csum.  One 1024-thread
-// block per 64 columns: 16 row groups each sum every 16th row, then a fixed-order combine.
+// csum[j] = k0 · Σ_{n<N} L⁻ᵀ[n][j − shift] (zero for j < shift): Ṽ = Ã·L⁻ᵀ + csum, and the column's
+// product scale cscale[j] = 1/(SA·SB_j) with SB_j = 2^(14 − e), max_n |L⁻ᵀ[n][j − shift]| < 2^e.
+// One 1024-thread block per 64 columns: 16 row groups each take every 16th row, then a
+// fixed-order combine.
 template <int KT>
-__global__ __launch_bounds__(1024) void screen_csum_kernel(cdx_gpis g, double* __restrict__ csum) {
-  __shared__ double part[16][64];
+__global__ __launch_bounds__(1024) void screen_csum_kernel(cdx_gpis g, double SA, double* __restrict__ csum,
+                                                           double* __restrict__ cscale) {
+  __shared__ double part[16][64], pmax[16][64];
   const int Np = g.N_pad, shift = cdx::screen_shift(g.N, Np);
   const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + c, j = col - shift;
-  double s = 0;
+  double s = 0, mx = 0;
   if (j >= 0)
-    for (int n = rg; n < g.N; n += 16) s += g.Linv_t[(int64_t)n * Np + j];
+    for (int n = rg; n < g.N; n += 16) {
+      const double v = g.Linv_t[(int64_t)n * Np + j];
+      s += v;
+      mx = fmax(mx, fabs(v));
+    }
   part[rg][c] = s;
+  pmax[rg][c] = mx;
   __syncthreads();
   if (rg == 0) {
     double t = 0;
-    for (int r = 0; r < 16; ++r) t += part[r][c];
+    for (int r = 0; r < 16; ++r) {
+      t += part[r][c];
+      mx = fmax(mx, pmax[r][c]);
+    }
     csum[col] = cdx::gpis_k0<KT>(g.R) * t;
+    int e = 14;
+    if (mx > 0) frexp(mx, &e);  // mx < 2^e
+    cscale[col] = ldexp(1.0 / SA, e - 14);
   }
 }
 
@@ -599,17 +649,29 @@ int cdx_gpis_screen_prepare(const cdx_gpis* g, void* screen, cdx_stream_t stream
   gv.screen = screen;
   const cdx::ScreenView v = cdx::screen_view(gv);
   const int Np = g->N_pad;
-  hipLaunchKernelGGL(screen_center_kernel, dim3(1), dim3(256), 0, s, gv, const_cast<double*>(v.center),
+  // SA: k0·SA ∈ (2⁹, 2¹⁰].  r_safe: |Ã(r)| ≤ 49·k0 for r ≤ 3.5R (TPS and the joint kernel's TPS part;
+  // R bounds every inducing-point distance), so |SA·Ã| < 2¹⁶ there; the RBF offset is bounded by k0.
+  const double k0 = g->kernel == CDX_KERNEL_TPS ? cdx::gpis_k0<CDX_KERNEL_TPS>(g->R)
+                    : g->kernel == CDX_KERNEL_RBF ? cdx::gpis_k0<CDX_KERNEL_RBF>(g->R)
+                                                  : cdx::gpis_k0<CDX_KERNEL_JOINT>(g->R);
+  if (!std::isfinite(k0)) return CDX_EINVAL;
+  int ek = 0;
+  if (k0 > 0) frexp(k0, &ek);  // k0 < 2^ek (a single inducing point, R = 0: SA = 2¹⁰, rq = 0)
+  const double SA = ldexp(1.0, 10 - ek);
+  const double r_safe = g->kernel == CDX_KERNEL_RBF ? INFINITY : 3.5 * g->R;
+  hipLaunchKernelGGL(screen_center_kernel, dim3(1), dim3(256), 0, s, gv, SA, r_safe, const_cast<double*>(v.center),
                      const_cast<float4*>(v.X1f));
+  const dim3 cgrid((unsigned)(Np / 64)), cblk(1024);
+  double* csum = const_cast<double*>(v.csum);
+  double* cscale = const_cast<double*>(v.cscale);
+  switch (g->kernel) {
+    case CDX_KERNEL_TPS: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_TPS>, cgrid, cblk, 0, s, gv, SA, csum, cscale); break;
+    case CDX_KERNEL_RBF: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_RBF>, cgrid, cblk, 0, s, gv, SA, csum, cscale); break;
+    default: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_JOINT>, cgrid, cblk, 0, s, gv, SA, csum, cscale); break;
+  }
   const int64_t nsplit = (int64_t)(Np / 16) * 2 * Np;
   hipLaunchKernelGGL(screen_split_kernel, dim3((unsigned)((nsplit + 255) / 256)), dim3(256), 0, s, gv,
-                     reinterpret_cast<bf16x8*>(const_cast<void*>(v.L)));
-  const dim3 cgrid((unsigned)(Np / 64)), cblk(1024);
-  switch (g->kernel) {
-    case CDX_KERNEL_TPS: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_TPS>, cgrid, cblk, 0, s, gv, const_cast<double*>(v.csum)); break;
-    case CDX_KERNEL_RBF: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_RBF>, cgrid, cblk, 0, s, gv, const_cast<double*>(v.csum)); break;
-    default: hipLaunchKernelGGL(screen_csum_kernel<CDX_KERNEL_JOINT>, cgrid, cblk, 0, s, gv, const_cast<double*>(v.csum)); break;
-  }
+                     reinterpret_cast<f16x8*>(const_cast<void*>(v.L)), (const double*)cscale, v.center);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 

@@ -21,7 +21,7 @@ import torch
 from . import _native as N
 
 _PKG_STATES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "gpis_states")
-# Closure screening margin Δ = SCREEN_MARGIN × the calibrated max error of the bf16 estimate of std²
+# Closure screening margin Δ = SCREEN_MARGIN × the calibrated max error of the split-precision estimate of std²
 # (cdx_gpis.screen_delta); CDX_SCREEN_MARGIN overrides it, 0 disables screening.
 SCREEN_MARGIN = float(os.environ.get("CDX_SCREEN_MARGIN", "32"))
 CALIB_QUERIES = 8192
@@ -69,7 +69,8 @@ class _State:
         self.screen_err = self._calibrate_screen(X1[:n].to(torch.float64), R, kernel)
         # the closure keeps every fingertip whose estimate is within 2Δ of its group's leader
         k0 = {"tps": float(R) ** 3, "rbf": 1.0, "joint": 0.3 + 0.7 * float(R) ** 3}[kernel]
-        self.desc.screen_delta = max(SCREEN_MARGIN * self.screen_err, 2.0 ** -40 * k0) if SCREEN_MARGIN > 0 else 0.0
+        ok = SCREEN_MARGIN > 0 and np.isfinite(self.screen_err)
+        self.desc.screen_delta = max(SCREEN_MARGIN * self.screen_err, 2.0 ** -40 * k0) if ok else 0.0
 
     def _calibrate_screen(self, X1, R, kernel):
         """max |estimate − exact| of k0 − ‖L⁻¹k‖² over calibration queries around this state:
@@ -88,7 +89,16 @@ class _State:
         Xc = Xc.contiguous()
         est = self.screen_var(Xc)
         exact = exact_var(self, Xc)
-        return float((est - exact).abs().max())
+        # a query beyond the screen's safe radius estimates NaN (the closure then runs its whole
+        # group exactly), so the bound is over finite estimates; mostly NaN: no screening
+        ok = torch.isfinite(est)
+        if int(ok.sum()) < Xc.shape[0] // 2:
+            return float("nan")
+        # in units of the row's rounding scale max(1, ‖Ṽ‖²/k0) = max(1, (k0 − est)/k0), the factor
+        # the closure's selection multiplies Δ by (cdx_screen.hip screen_margin)
+        k0 = {"tps": float(R) ** 3, "rbf": 1.0, "joint": 0.3 + 0.7 * float(R) ** 3}[kernel]
+        scale = ((k0 - est[ok]) / k0).clamp(min=1.0) if k0 > 0 else torch.ones_like(est[ok])
+        return float(((est[ok] - exact[ok]).abs() / scale).max())
 
     def screen_var(self, X):
         """Split-precision estimate of k0 − ‖L⁻¹k‖² at X [M, 3] (cdx_gpis_screen_var)."""

@@ -75,7 +75,7 @@ def _all_tip_queries(cfg, E, seed, center=None):
 
 
 def test_screen_estimate_within_bound(banana2000):
-    """The bf16 estimate of k0 − ‖L⁻¹k‖² against the fp64 pass on the bench's 16 384 all-tip rows:
+    """The split-precision estimate of k0 − ‖L⁻¹k‖² against the fp64 pass on the bench's 16 384 all-tip rows:
     inside an eighth of the closure's margin Δ (= 32× the state's calibrated error; measured ≈ 3e-6·k0
     against a calibrated 2-4e-6·k0)."""
     from compliancedex_amd.gpis import exact_var
@@ -102,6 +102,33 @@ def test_screen_var_c_abi_edges(banana2000):
     assert lib.cdx_gpis_screen_var(st.desc, N.ptr(X), 4, N.ptr(out), None, None) == -1
     bare = N.CdxGpis(X1=st.desc.X1, alpha=st.desc.alpha, Linv_t=st.desc.Linv_t, N=st.desc.N, N_pad=st.desc.N_pad)
     assert lib.cdx_gpis_screen_var(bare, N.ptr(X), 4, N.ptr(out), N.ptr(out), None) == -1
+
+
+def test_screen_far_queries_are_nan(banana2000):
+    """Beyond the safe radius (3.5R from the inducing points, where SA·Ã could leave fp16's range) the
+    estimate is NaN, never a silently clamped number; near queries stay finite."""
+    st = banana2000.native_state()
+    X = torch.zeros(8, 3, dtype=torch.float64, device=DEV)
+    X[:4] = banana2000.X1[:4].to(torch.float64)
+    X[4:, 0] = torch.tensor([2.0, -3.0, 10.0, 1e6], dtype=torch.float64)
+    est = st.screen_var(X).cpu().numpy()
+    assert np.isfinite(est[:4]).all() and np.isnan(est[4:]).all(), est
+
+
+def test_screened_closure_far_candidates(banana2000):
+    """Candidates whose palm is 2 m away screen to NaN: their groups run the exact pass for every
+    fingertip, and the closure still equals the unscreened one."""
+    from compliancedex_amd.workloads import prob_inputs
+    cfg, opt = _opt()
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], 2048, seed=99, spread=True)
+    palm = palm.copy()
+    palm[:128, 0] += 2.0
+    a, st = _closure(opt, banana2000, (q, comp, target, palm), screen=True)
+    b, _ = _closure(opt, banana2000, (q, comp, target, palm), screen=False)
+    assert st["bound_misses"] == 0 and st["exact_rows"] >= 2048 + 3 * 128, st
+    assert np.array_equal(a["flip"], b["flip"])
+    for k in OUTS:
+        assert rel_err(a[k], b[k]) <= TOL_EQ, (k, rel_err(a[k], b[k]))
 
 
 @pytest.mark.parametrize("case", ["config2_E4096", "stored_banana_E1024", "config3_mug_E4096"])
