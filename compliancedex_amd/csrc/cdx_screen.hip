@@ -43,13 +43,34 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 using cdx::SC_BK;
 using cdx::SC_BN;
 constexpr int SC_BM = 256;                 // query rows per workgroup
-constexpr int SC_THREADS = 512;            // 8 waves: 2 (rows) × 4 (columns), 128 × 64 outputs each
-constexpr int SC_REG = 4 * 256;            // 16-byte LDS units of one operand stage: [slice][khalf][256]
+#ifndef CDX_SC_WAVES
+#define CDX_SC_WAVES 8
+#endif
+// 8 waves (two per SIMD): 2 (rows) × 4 (columns), 128 × 64 outputs each; 4 waves (one per SIMD,
+// accumulators in AGPRs): 2 × 2, 128 × 128 outputs each (half the fragment reads per MFMA)
+constexpr int SC_W = CDX_SC_WAVES;
+static_assert(SC_W == 8 || SC_W == 4, "8 or 4 waves per workgroup");
+constexpr int SC_THREADS = 64 * SC_W;
+constexpr int SC_WC = SC_W == 8 ? 64 : 128;  // columns per wave
+constexpr int SC_NJ = SC_WC / 32;            // 32-column accumulator blocks per wave
+constexpr int SC_GKH = SC_W == 8 ? 1 : 2;    // k-halves generated per thread per sub-step
+constexpr int SC_REG = 4 * 256;            // 16-byte LDS units of one 16-K sub-step: [slice][khalf][256]
+#ifndef CDX_SC_SUB
+#define CDX_SC_SUB 2
+#endif
+constexpr int SC_SUB = CDX_SC_SUB;         // 16-K sub-steps per stage (one barrier per stage)
+#ifndef CDX_SC_RING
+#define CDX_SC_RING (CDX_SC_SUB == 1 ? 3 : 2)
+#endif
+constexpr int SC_RING = CDX_SC_RING;       // B stages in LDS: DMA'd SC_RING − 1 stages ahead
+static_assert(SC_RING == 2 || SC_RING == 3, "B ring of 2 or 3 stages");
+constexpr int SC_NDMA = 16 * SC_SUB / SC_W;  // 1-KB DMAs per wave per stage
+static_assert(SC_SUB == 1 || SC_SUB == 2, "stage = 16 or 32 K rows");
 constexpr int SC_LDT = 264;               // fp32 row pitch of the epilogue's accumulator image (4 rows ≡ 32 banks)
-// LDS: A stages (generated, 2 buffers) | B stages (LDS-DMA ring of 3)
-constexpr int SC_A_OFF = 0, SC_B_OFF = 2 * SC_REG * 16;
-constexpr int SC_SMEM = std::max(SC_B_OFF + 3 * SC_REG * 16,  // stage buffers
-                                 128 * SC_LDT * 4);            // epilogue: one row half of the tile
+// LDS: A stages (generated, 2 buffers) | B stages (LDS-DMA ring)
+constexpr int SC_A_OFF = 0, SC_B_OFF = 2 * SC_SUB * SC_REG * 16;
+constexpr int SC_SMEM = std::max(SC_B_OFF + SC_RING * SC_SUB * SC_REG * 16,  // stage buffers
+                                 128 * SC_LDT * 4);                          // epilogue: one row half of the tile
 static_assert(SC_SMEM <= 160 * 1024, "screen stage buffers exceed the CU's LDS");
 
 // K-steps (16 rows of L⁻ᵀ) of stripe nt: rows [0, min(N, (nt+1)·256 − shift)) as in the fp64 pass.
@@ -82,7 +103,7 @@ __device__ __forceinline__ void split2(float xa, float xb, unsigned& h0, unsigne
 // One workgroup per (query tile of 256 rows, stripe of 256 columns); stripes paired heavy+light per
 // XCD as in gpis_std_kernel<VAR>.  partial[nt][m] = Σ over the stripe's columns of (Ã·L⁻ᵀ + c)².
 template <int KT>
-__global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
+__global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
                                                                     double* __restrict__ partial, int64_t M_pad, int Mt,
                                                                     int Nt) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[SC_SMEM];
@@ -110,11 +131,12 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
   }
   const int64_t m0 = (int64_t)mt * SC_BM;
   const int n0 = nt * SC_BN;
-  const int nK = sc_ksteps(nt, N, Np);
+  const int nK = sc_ksteps(nt, N, Np);        // 16-K sub-steps
+  const int nS = (nK + SC_SUB - 1) / SC_SUB;  // stages
 
-  // generation: thread → query row grow, k-half gkh (wave-uniform), 8 entries per stage
+  // generation: thread → query row grow, k-halves gkh .. gkh + SC_GKH − 1 (wave-uniform), 8 entries each
   const int grow = tid & (SC_BM - 1);
-  const int gkh = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gkh = SC_W == 8 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;
   float qx, qy, qz;
   {
     const int64_t m = std::min(m0 + grow, M - 1);  // pad rows replicate a valid query
@@ -130,48 +152,54 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
                      (float)(-0.5 / (g.sigma * g.sigma)));
   }
 
-  // wave → 128 × 64 output sub-tile; waves w and w+4 share a SIMD and take complementary columns
-  const int cwave = wave < 4 ? wave : 7 - wave;
-  const int wr = (wave >> 2) * 128;
-  const int wc = cwave * 64;
+  // wave → 128 × SC_WC output sub-tile; with 8 waves, waves w and w+4 share a SIMD and take
+  // complementary columns
+  const int cwave = SC_W == 8 ? (wave < 4 ? wave : 7 - wave) : (wave & 1);
+  const int wr = (SC_W == 8 ? (wave >> 2) : (wave >> 1)) * 128;
+  const int wc = cwave * SC_WC;
   // B rows past this wave's last column are zero (upper-triangular L⁻ᵀ, shifted columns)
-  const int kend_w = __builtin_amdgcn_readfirstlane(n0 + wc + 64 - shift);
+  const int kend_w = __builtin_amdgcn_readfirstlane(n0 + wc + SC_WC - shift);
 
-  f32x16 acc[4][2];
+  f32x16 acc[4][SC_NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < SC_NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // Staging by LDS-DMA (global_load_lds: no VGPRs, no ds_write).  issue(st): every wave DMAs 2 × 1 KB
-  // of B stage st (instruction u = wave + 8i: slice/k-half region u>>2, columns 64·(u&3) + lane).
-  // issue(s+2) runs during step s; the counted `s_waitcnt vmcnt(2)` at the end of each step keeps
-  // exactly that step's DMAs in flight across the raw s_barrier (__syncthreads would wait vmcnt(0)),
-  // with B stage s+1 landed for step s+1.  Clamped stages past the stripe's end load into free
-  // slots, so every step issues the same count.
+  // Staging by LDS-DMA (global_load_lds: no VGPRs, no ds_write).  issue(st): every wave DMAs
+  // SC_NDMA × 1 KB of B stage st (instruction u = wave + 8i: sub-step u>>4, slice/k-half region
+  // (u>>2)&3, columns 64·(u&3) + lane) into ring slot st % SC_RING, SC_RING − 1 stages ahead.
+  // 32-K stages (default): issue(s+1) during step s, `s_waitcnt vmcnt(0)` before the step's raw
+  // s_barrier.  16-K stages: issue(s+2) during step s and a counted `vmcnt(2)` keeps that step's DMAs
+  // in flight across the barrier (__syncthreads would wait vmcnt(0)); clamped stages past the
+  // stripe's end load into free slots, so every step issues the same count.
   const char* Lb = static_cast<const char*>(sv.L);
   auto issue = [&](int st) {
-    const int sc = std::min(st, nK - 1);
-    const int slot = st % 3;
+    const int sc = std::min(st, nS - 1);
+    const int slot = st % SC_RING;
+#if defined(CDX_SC_DIAG_NODMA)  // timing-only diagnostic build: outputs are wrong
+    if (st > 0) return;
+#endif
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int u = wave + 8 * i, reg = u >> 2, col = 64 * (u & 3) + lane;
-      const char* src = Lb + (((int64_t)(sc * 4 + reg)) * Np + n0 + col) * 16;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sB4 + slot * SC_REG + u * 64), 16, 0, 0);
+    for (int i = 0; i < SC_NDMA; ++i) {
+      const int u = wave + SC_W * i, sub = u >> 4, r = u & 15, col = 64 * (r & 3) + lane;
+      const char* src = Lb + (((int64_t)((sc * SC_SUB + sub) * 4 + (r >> 2))) * Np + n0 + col) * 16;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sB4 + (slot * SC_SUB + sub) * SC_REG + r * 64),
+                                       16, 0, 0);
     }
   };
-  u32x4 ast[2];      // generated A stage: 8 entries × 2 fp16 slices, packed in pairs
+  u32x4 ast[2];      // generated A sub-step: 8 entries × 2 fp16 slices, packed in pairs
   // X1 rows of the generated stage: wave-uniform addresses → scalar loads (SMEM; the vector memory
   // counter stays free for the DMAs' counted waits)
-  auto gen_a = [&](int st) {  // 8 consecutive k of this thread's half, packed in pairs
+  auto gen_a = [&](int st, int sub, int kh) {  // 8 consecutive k of k-half kh, packed in pairs
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef const __attribute__((address_space(4))) float4 cfloat4;  // constant space: SMEM loads
 #else
     typedef const float4 cfloat4;
 #endif
-    cfloat4* x1 = (cfloat4*)(sv.X1f) + __builtin_amdgcn_readfirstlane(st * SC_BK + 8 * gkh);
+    cfloat4* x1 = (cfloat4*)(sv.X1f) + __builtin_amdgcn_readfirstlane((st * SC_SUB + sub) * SC_BK + 8 * kh);
 #pragma unroll
     for (int e = 0; e < 8; e += 2) {
       const float4 p = x1[e], p1 = x1[e + 1];
@@ -185,32 +213,49 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
       ast[1][e / 2] = h1;
     }
   };
-  auto write_a = [&](int buf) {
+  auto write_a = [&](int buf, int sub, int kh) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) sA4[buf * SC_REG + (i * 2 + gkh) * 256 + grow] = ast[i];
+    for (int i = 0; i < 2; ++i) sA4[(buf * SC_SUB + sub) * SC_REG + (i * 2 + kh) * 256 + grow] = ast[i];
   };
-  // one stage's 24 MFMAs: lane → (row/col l&31, k-half l>>5); B slices of both column blocks, A
-  // slice by slice (products of slice-index sum ≤ 1, smallest first)
-  auto mfma_stage = [&](int abuf, int bslot, auto more_c) {
+  auto gen_write = [&](int st, int buf, int sub) {
+#pragma unroll
+    for (int h = 0; h < SC_GKH; ++h) {
+      gen_a(st, sub, gkh + h);
+      write_a(buf, sub, gkh + h);
+    }
+  };
+  // one sub-step's 12·SC_NJ MFMAs: lane → (row/col l&31, k-half l>>5); B slices of the wave's column
+  // blocks, A slice by slice (products of slice-index sum ≤ 1, smallest first)
+  auto mfma_sub = [&](int abuf, int bslot, int sub, auto more_c) {
     constexpr bool MORE = decltype(more_c)::value;
-    f16x8 fb[2][2];
+    const u32x4* a4 = sA4 + (abuf * SC_SUB + sub) * SC_REG;
+    const u32x4* b4 = sB4 + (bslot * SC_SUB + sub) * SC_REG;
+    f16x8 fb[2][SC_NJ];
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fb[sb][j] = __builtin_bit_cast(f16x8, sB4[bslot * SC_REG + (sb * 2 + (lane >> 5)) * 256 + wc + 32 * j + (lane & 31)]);
+      for (int j = 0; j < SC_NJ; ++j)
+#if defined(CDX_SC_DIAG_NOREAD)  // timing-only diagnostic build: outputs are wrong
+        fb[sb][j] = __builtin_bit_cast(f16x8, u32x4{(unsigned)lane, (unsigned)j, (unsigned)sb, (unsigned)sub});
+#else
+        fb[sb][j] = __builtin_bit_cast(f16x8, b4[(sb * 2 + (lane >> 5)) * 256 + wc + 32 * j + (lane & 31)]);
+#endif
 #pragma unroll
     for (int sa = 1; sa >= 0; --sa) {
       f16x8 fa[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        fa[i] = __builtin_bit_cast(f16x8, sA4[abuf * SC_REG + (sa * 2 + (lane >> 5)) * 256 + wr + 32 * i + (lane & 31)]);
+#if defined(CDX_SC_DIAG_NOREAD)
+        fa[i] = __builtin_bit_cast(f16x8, u32x4{(unsigned)lane, (unsigned)i, (unsigned)sa, (unsigned)abuf});
+#else
+        fa[i] = __builtin_bit_cast(f16x8, a4[(sa * 2 + (lane >> 5)) * 256 + wr + 32 * i + (lane & 31)]);
+#endif
 #pragma unroll
       for (int sb = 1 - sa; sb >= 0; --sb)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < SC_NJ; ++j)
 #if defined(CDX_SC_DIAG_NOMFMA)  // timing-only diagnostic build: outputs are wrong
             acc[i][j][0] += (float)fa[i][0] * (float)fb[sb][j][0];
 #else
@@ -220,66 +265,93 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
     }
   };
 
-  // prologue: B stages 0–1 landed, A of stage 0 generated
-  issue(0);
-  issue(1);
-  gen_a(0);
-  write_a(0);
+  // prologue: B stages 0 .. SC_RING−2 landed, A of stage 0 generated
+#pragma unroll
+  for (int st = 0; st < SC_RING - 1; ++st) issue(st);
+#pragma unroll
+  for (int u = 0; u < SC_SUB; ++u) gen_write(0, 0, u);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  // Step s multiplies stage s (A buffer s&1, B slot s%3) while stage s+2 is DMA'd into slot (s+2)%3
-  // and stage s+1's A is generated (X1 slot (s+1)%3) and written to the other A buffer.  LIVE: this
-  // wave's B columns are non-zero in stage s; MORE: a stage s+1 exists.  The (LIVE, MORE) body is
-  // one straight-line block, so the generation's VALU work interleaves with the MFMAs.
-  auto step = [&](int s, auto live_c, auto more_c) {
-    constexpr bool LIVE = decltype(live_c)::value, MORE = decltype(more_c)::value;
-    issue(s + 2);
-    if (MORE) gen_a(s + 1);
-    if (LIVE) mfma_stage(s & 1, s % 3, more_c);
-    if (MORE) write_a((s + 1) & 1);
-    asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");  // B stage s+1 landed, A written
+  // Step s multiplies stage s (A buffer s&1, B slot s % SC_RING) while stage s + SC_RING − 1 is DMA'd
+  // and stage s+1's A is generated and written to the other A buffer, sub-step by sub-step.  NLIVE:
+  // this wave's B columns are non-zero in the first NLIVE sub-steps of stage s; MORE: a stage s+1
+  // exists.  Each (NLIVE, MORE) body is one straight-line block, so the generation's VALU work
+  // interleaves with the MFMAs.
+  auto step = [&](int s, auto nlive_c, auto more_c) {
+    constexpr int NLIVE = decltype(nlive_c)::value;
+    constexpr bool MORE = decltype(more_c)::value;
+    if (SC_RING > 2 || s + 1 < nS) issue(s + SC_RING - 1);
+#pragma unroll
+    for (int u = 0; u < SC_SUB; ++u) {
+      if (SC_GKH == 1) {
+        if (MORE) gen_a(s + 1, u, gkh);
+        if (u < NLIVE) mfma_sub(s & 1, s % SC_RING, u, more_c);
+        if (MORE) write_a((s + 1) & 1, u, gkh);
+      } else {
+        if (u < NLIVE) mfma_sub(s & 1, s % SC_RING, u, more_c);
+        if (MORE) gen_write(s + 1, (s + 1) & 1, u);
+      }
+    }
+    // B stage s+1 landed (the newest stage's DMAs may stay in flight), A written
+    if constexpr (SC_RING == 2)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else if constexpr (SC_NDMA == 2)
+      asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+#if !defined(CDX_SC_DIAG_NOBAR)  // timing-only diagnostic build (races): outputs are wrong
     __builtin_amdgcn_s_barrier();
+#endif
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  const int s_live = std::min(nK, std::max(0, (kend_w + SC_BK - 1) / SC_BK));  // wave-uniform
+  const int k_live = std::min(nK, std::max(0, (kend_w + SC_BK - 1) / SC_BK));  // live sub-steps (wave-uniform)
+  const int full = k_live / SC_SUB;
   int s = 0;
-  for (; s < std::min(s_live, nK - 1); ++s) step(s, T_{}, T_{});
-  for (; s < nK - 1; ++s) step(s, F_{}, T_{});
+  for (; s < std::min(full, nS - 1); ++s) step(s, std::integral_constant<int, SC_SUB>{}, T_{});
+  if (SC_SUB == 2 && s < nS - 1 && s * SC_SUB < k_live) {
+    step(s, std::integral_constant<int, 1>{}, T_{});
+    ++s;
+  }
+  for (; s < nS - 1; ++s) step(s, std::integral_constant<int, 0>{}, T_{});
   // last stage: its MFMAs only; then every DMA drained before the epilogue reuses the LDS
-  if (s < s_live) mfma_stage(s & 1, s % 3, F_{});
+#pragma unroll
+  for (int u = 0; u < SC_SUB; ++u)
+    if (s * SC_SUB + u < k_live) mfma_sub(s & 1, s % SC_RING, u, F_{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   // Epilogue: per row Σ over the stripe's 256 columns of (Ṽ + c)² in f64.  The accumulators go
   // through LDS one row half at a time ([128][SC_LDT] fp32, the stage buffers are free after the
-  // loop), then 4 threads per row sum 64 columns each and combine with two xor-shuffles.  (Summing
+  // loop), then SC_THREADS/128 threads per row sum a share of its columns each and combine by
+  // xor-shuffles.  (Summing
   // in registers needs the f64 squares of a whole row block live next to the accumulators and
   // made the allocator spill.)  C map (32x32x16): reg r of lane l is row (r&3) + 8(r>>2) + 4(l>>5),
   // column l&31.
   float* T = reinterpret_cast<float*>(smem);
-  const int erow = tid >> 2, epart = tid & 3;
+  constexpr int EP = SC_THREADS / 128, ECOL = SC_BN / EP;  // threads per row, columns per thread
+  const int erow = tid / EP, epart = tid % EP;
 #pragma unroll
   for (int ph = 0; ph < 2; ++ph) {
     if (ph) __syncthreads();  // phase 0's readers are done with T
-    if ((wave >> 2) == ph) {
+    if (wr == 128 * ph) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < SC_NJ; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r)
             T[(32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * SC_LDT + wc + 32 * j + (lane & 31)] = acc[i][j][r];
     }
     __syncthreads();
-    const float4* Tr = reinterpret_cast<const float4*>(T + erow * SC_LDT + 64 * epart);
-    const double* cs = sv.csum + n0 + 64 * epart;
-    const double* cf = sv.cscale + n0 + 64 * epart;
+    const float4* Tr = reinterpret_cast<const float4*>(T + erow * SC_LDT + ECOL * epart);
+    const double* cs = sv.csum + n0 + ECOL * epart;
+    const double* cf = sv.cscale + n0 + ECOL * epart;
     double sum = 0.0;
 #pragma unroll 4
-    for (int c = 0; c < 16; ++c) {
+    for (int c = 0; c < ECOL / 4; ++c) {
       const float4 v = Tr[c];
       const double x0 = fma((double)v.x, cf[4 * c], cs[4 * c]), x1 = fma((double)v.y, cf[4 * c + 1], cs[4 * c + 1]),
                    x2 = fma((double)v.z, cf[4 * c + 2], cs[4 * c + 2]), x3 = fma((double)v.w, cf[4 * c + 3], cs[4 * c + 3]);
@@ -288,8 +360,8 @@ __global__ __launch_bounds__(SC_THREADS, 2) void gpis_screen_kernel(cdx_gpis g, 
       sum = fma(x2, x2, sum);
       sum = fma(x3, x3, sum);
     }
-    sum += __shfl_xor(sum, 1);
-    sum += __shfl_xor(sum, 2);
+#pragma unroll
+    for (int w = 1; w < EP; w <<= 1) sum += __shfl_xor(sum, w);
     if (epart == 0) partial[(int64_t)nt * M_pad + m0 + 128 * ph + erow] = sum;
   }
 }
