@@ -59,7 +59,7 @@ class _State:
         self.desc = N.CdxGpis(X1=self.X1.data_ptr(), alpha=self.alpha.data_ptr(), Ainv=self.Ainv.data_ptr(),
                               Linv_t=self.Linv_t.data_ptr(), Linv=self.Linv.data_ptr(), N=n,
                               N_pad=Np, kernel=N.KERNELS[kernel], R=float(R), sigma=float(sigma), bias=float(bias))
-        # split-precision variance screen (bf16 slices of L⁻ᵀ): built once per state
+        # split-precision variance screen (fp16 slices of scaled L⁻ᵀ): built once per state
         self.screen = torch.empty(lib.cdx_gpis_screen_bytes(Np), dtype=torch.uint8, device=dev)
         N.check(lib.cdx_gpis_screen_prepare(self.desc, N.ptr(self.screen), N.stream_ptr(dev)), "cdx_gpis_screen_prepare")
         self.desc.screen = self.screen.data_ptr()

@@ -153,7 +153,7 @@ class ProbabilisticGraspOptimizer:
 
     def screen_stats(self, gpis, E, friction_mu=1):
         """Screening of the last closure over E candidates (cdx_closure_screen_stats): dict of the
-        all-tip rows that ran the exact fp64 pass, the rows whose bf16 estimate missed its bound,
+        all-tip rows that ran the exact fp64 pass, the rows whose screen estimate missed its bound,
         and the rows screened — or None when the closure ran the full fp64 pass."""
         import ctypes
         out = (ctypes.c_int32 * 3)()

@@ -104,14 +104,16 @@ int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pa
                     double* Ainv, double* Linv_t, double* Linv, double* alpha, int32_t* info,
                     cdx_stream_t stream);
 
-/* Split-precision variance screen (bf16 matrix cores).  Estimates std² = k0 − ‖L⁻¹k‖² (gpis.py:56-59)
- * as k0 − ‖Ã·L⁻ᵀ + k0·colsum(L⁻ᵀ)‖² with Ã = K* − k0 generated in fp32 and both operands split into
- * three bf16 slices (six slice products, fp32 accumulation): fp32-level accuracy at 2.1× the fp64
- * MFMA flop rate.  The closure uses it to skip the fp64 pass for fingertips that cannot be the
- * variance cost's maximum; alone it is a throughput estimate with no parity claim.
- * cdx_gpis_screen_bytes: size of the per-state screen buffer (≈ 6·N_pad² bytes);
- * cdx_gpis_screen_prepare: fills it from g->Linv_t and g->X1 (the descriptor's own screen field is
- *   ignored; point it at the buffer afterwards);
+/* Split-precision variance screen (fp16 matrix cores).  Estimates std² = k0 − ‖L⁻¹k‖² (gpis.py:56-59)
+ * as k0 − ‖Ã·L⁻ᵀ + k0·colsum(L⁻ᵀ)‖² with Ã = K* − k0 generated in fp32, both operands scaled by
+ * powers of two and split into two fp16 slices (three slice products, fp32 accumulation):
+ * fp32-level accuracy at 32× the fp64 MFMA rate per product.  The closure uses it to skip the fp64
+ * pass for fingertips that cannot be the variance cost's maximum; alone it is a throughput estimate
+ * with no parity claim.  A query farther than 3.5R − max_n |x_n − centre| from the inducing points'
+ * centre (TPS / joint kernels) estimates NaN.
+ * cdx_gpis_screen_bytes: size of the per-state screen buffer (≈ 4·N_pad² bytes);
+ * cdx_gpis_screen_prepare: fills it from g->Linv_t, g->X1, g->kernel and g->R (the descriptor's own
+ *   screen field is ignored; point it at the buffer afterwards);
  * cdx_gpis_screen_var: var [M] = the estimate of k0 − ‖L⁻¹k‖² (signed), workspace
  *   cdx_gpis_screen_workspace bytes. */
 size_t cdx_gpis_screen_bytes(int32_t N_pad);
@@ -323,7 +325,7 @@ const char* cdx_version(void);
 /* Per-stage kernel timing with HIP events recorded on the launch stream (off by default).
  * Stages: 0 closure query generation, 1 GPIS mean, 2 GPIS std (whitened K*·L⁻ᵀ fp64 GEMM only; in a
  * screened closure the refine pass and its merge), 3 closure cost+backward, 4 GPIS ∇std GEMM only,
- * 5 the closure's split-precision screen (bf16 GEMM + selection).  cdx_profile_read syncs on the
+ * 5 the closure's split-precision screen (fp16 GEMM + selection).  cdx_profile_read syncs on the
  * recorded events, returns the summed milliseconds and launch counts per stage (arrays of 6),
  * and clears the pool (4096 launches per stage).  `stages` is a bit mask (bit s = stage s; 0x3f
  * all, 0 off): each event record costs ≈ 5 µs of stream time, so a throughput run times only
