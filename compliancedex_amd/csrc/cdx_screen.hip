@@ -66,6 +66,13 @@ constexpr int SC_RING = CDX_SC_RING;       // B stages in LDS: DMA'd SC_RING −
 static_assert(SC_RING == 2 || SC_RING == 3, "B ring of 2 or 3 stages");
 constexpr int SC_NDMA = 16 * SC_SUB / SC_W;  // 1-KB DMAs per wave per stage
 static_assert(SC_SUB == 1 || SC_SUB == 2, "stage = 16 or 32 K rows");
+#ifndef CDX_SC_PP
+#define CDX_SC_PP 0
+#endif
+// Ping-pong: the two waves of a SIMD (waves w, w+4) multiply in alternate half-stages; in the
+// other half each generates one 16-K sub-step of the next stage's A and DMAs its B.
+constexpr bool SC_PP = CDX_SC_PP;
+static_assert(!SC_PP || (SC_W == 8 && SC_SUB == 2 && SC_RING == 2), "ping-pong: 8 waves, 32-K stages, B ring of 2");
 constexpr int SC_LDT = 264;               // fp32 row pitch of the epilogue's accumulator image (4 rows ≡ 32 banks)
 // LDS: A stages (generated, 2 buffers) | B stages (LDS-DMA ring)
 constexpr int SC_A_OFF = 0, SC_B_OFF = 2 * SC_SUB * SC_REG * 16;
@@ -308,18 +315,55 @@ __global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_ker
   using T_ = std::true_type;
   using F_ = std::false_type;
   const int k_live = std::min(nK, std::max(0, (kend_w + SC_BK - 1) / SC_BK));  // live sub-steps (wave-uniform)
-  const int full = k_live / SC_SUB;
-  int s = 0;
-  for (; s < std::min(full, nS - 1); ++s) step(s, std::integral_constant<int, SC_SUB>{}, T_{});
-  if (SC_SUB == 2 && s < nS - 1 && s * SC_SUB < k_live) {
-    step(s, std::integral_constant<int, 1>{}, T_{});
-    ++s;
-  }
-  for (; s < nS - 1; ++s) step(s, std::integral_constant<int, 0>{}, T_{});
-  // last stage: its MFMAs only; then every DMA drained before the epilogue reuses the LDS
+  if constexpr (SC_PP) {
+    // Phase ph of stage s: waves 0–3 (ph 0) or 4–7 (ph 1) multiply stage s; the other half DMAs
+    // sub-step ph of B(s+1) (4 KB per wave) and generates sub-step ph of A(s+1) (both k-halves of
+    // its 256 rows).  Buffers: A(s+1) and B(s+1) go to the slots stage s−1 used, free since the
+    // barrier that ended stage s−1; B(s+1) has landed at the barrier that ends stage s.
+    const bool P = wave < 4;
+    for (int s = 0; s < nS; ++s) {
+      const bool more = s + 1 < nS;
 #pragma unroll
-  for (int u = 0; u < SC_SUB; ++u)
-    if (s * SC_SUB + u < k_live) mfma_sub(s & 1, s % SC_RING, u, F_{});
+      for (int ph = 0; ph < 2; ++ph) {
+        if (P == (ph == 0)) {
+          if (2 * s < k_live) mfma_sub(s & 1, s % SC_RING, 0, T_{});
+          if (2 * s + 1 < k_live) mfma_sub(s & 1, s % SC_RING, 1, T_{});
+        } else if (more) {
+          const int sc = s + 1, slot = sc % SC_RING;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = (wave & 3) + 4 * i, col = 64 * (r & 3) + lane;
+            const char* src = Lb + (((int64_t)((sc * SC_SUB + ph) * 4 + (r >> 2))) * Np + n0 + col) * 16;
+            __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sB4 + (slot * SC_SUB + ph) * SC_REG + r * 64),
+                                             16, 0, 0);
+          }
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh) {
+            gen_a(sc, ph, kh);
+            write_a(sc & 1, ph, kh);
+          }
+        }
+        if (ph == 0)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+  } else {
+    const int full = k_live / SC_SUB;
+    int s = 0;
+    for (; s < std::min(full, nS - 1); ++s) step(s, std::integral_constant<int, SC_SUB>{}, T_{});
+    if (SC_SUB == 2 && s < nS - 1 && s * SC_SUB < k_live) {
+      step(s, std::integral_constant<int, 1>{}, T_{});
+      ++s;
+    }
+    for (; s < nS - 1; ++s) step(s, std::integral_constant<int, 0>{}, T_{});
+    // last stage: its MFMAs only; then every DMA drained before the epilogue reuses the LDS
+#pragma unroll
+    for (int u = 0; u < SC_SUB; ++u)
+      if (s * SC_SUB + u < k_live) mfma_sub(s & 1, s % SC_RING, u, F_{});
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
