@@ -806,8 +806,10 @@ __global__ __launch_bounds__(256) void gpis_var_splitk_finalize(cdx_gpis g, cons
 
 // Refine pass (MODE_VARL), cut stripes: workgroup p finishes the stripe whose K-range ends inside
 // piece p after starting in an earlier one — V = its partial tiles summed in piece order, stored at
-// the list positions, and Σ V² per row into partial[nt][position] (4 waves, 4 columns per lane).
-__global__ __launch_bounds__(256) void gpis_var_merge(cdx_gpis g, RefineList rl, int64_t M_pad,
+// the list positions, and Σ V² per row into partial[nt][position] (8 waves, 4 columns per lane,
+// MERGE_RB rows per batch so a batch's loads are in flight together).
+constexpr int MERGE_THREADS = 512, MERGE_RB = 8;
+__global__ __launch_bounds__(MERGE_THREADS) void gpis_var_merge(cdx_gpis g, RefineList rl, int64_t M_pad,
                                                       double* __restrict__ partial, double* __restrict__ vout) {
   const int Np = g.N_pad, Nt = Np / ST_BN;
   const int64_t Mrows = (int64_t)rl.G + *rl.extra;
@@ -827,29 +829,39 @@ __global__ __launch_bounds__(256) void gpis_var_merge(cdx_gpis g, RefineList rl,
   int pf = p;
   while (pf > 0 && qof(pf) > S0) --pf;  // the stripe's first piece (possibly an empty one before it)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int row = wave; row < ST_BM; row += 4) {
-    double v[4] = {0, 0, 0, 0};
+  constexpr int NW = MERGE_THREADS / 64;
+  for (int r0 = wave * MERGE_RB; r0 < ST_BM; r0 += NW * MERGE_RB) {
+    double v[MERGE_RB][4] = {};
     for (int pp = pf; pp <= p; ++pp) {
       // this stripe's segment in piece pp (empty pieces — fewer K-steps than pieces — hold none);
       // slot 0 if it is the piece's first segment, else 1 (gpis_std_kernel<VARL>'s rule)
       const int64_t a = max(qof(pp), S0), e = min(qof(pp + 1), S1);
       if (a >= e) continue;
       const int slot = 2 * pp + (a == qof(pp) ? 0 : 1);
-      const double* src = rl.slots + ((int64_t)slot * ST_BM + row) * ST_BN + 4 * lane;
+      const double* src = rl.slots + ((int64_t)slot * ST_BM + r0) * ST_BN + 4 * lane;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) v[c] += src[c];
+      for (int rr = 0; rr < MERGE_RB; ++rr)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[rr][c] += src[rr * ST_BN + c];
     }
-    const int64_t pos = (int64_t)mt * ST_BM + row;
-    double* dst = vout + pos * Np + nt * ST_BN + 4 * lane;
-    double sq = 0.0;
+    double sq[MERGE_RB];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      dst[c] = v[c];
-      sq = fma(v[c], v[c], sq);
+    for (int rr = 0; rr < MERGE_RB; ++rr) {
+      double* dst = vout + ((int64_t)mt * ST_BM + r0 + rr) * Np + nt * ST_BN + 4 * lane;
+      sq[rr] = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        dst[c] = v[rr][c];
+        sq[rr] = fma(v[rr][c], v[rr][c], sq[rr]);
+      }
     }
 #pragma unroll
-    for (int w = 1; w < 64; w <<= 1) sq += __shfl_xor(sq, w);
-    if (lane == 0) partial[(int64_t)nt * M_pad + pos] = sq;
+    for (int w = 1; w < 64; w <<= 1)
+#pragma unroll
+      for (int rr = 0; rr < MERGE_RB; ++rr) sq[rr] += __shfl_xor(sq[rr], w);
+    if (lane == 0)
+#pragma unroll
+      for (int rr = 0; rr < MERGE_RB; ++rr) partial[(int64_t)nt * M_pad + (int64_t)mt * ST_BM + r0 + rr] = sq[rr];
   }
 }
 
@@ -1083,7 +1095,7 @@ static void refine_launch_kt(const cdx_gpis& g, const double* X, int64_t Mcap, c
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VARL>), dim3(REFINE_PIECES), dim3(ST_THREADS), 0, s, g, X, Mcap, partial,
                      M_pad, 0, g.N_pad / ST_BN, vout, nullptr, nullptr, 0, rl);
   prof_mark(PROF_GPIS_STD, false, s);
-  hipLaunchKernelGGL(gpis_var_merge, dim3(REFINE_PIECES), dim3(256), 0, s, g, rl, M_pad, partial, vout);
+  hipLaunchKernelGGL(gpis_var_merge, dim3(REFINE_PIECES), dim3(MERGE_THREADS), 0, s, g, rl, M_pad, partial, vout);
 }
 
 int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
