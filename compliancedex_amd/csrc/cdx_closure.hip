@@ -422,11 +422,22 @@ struct ClosureWs {
   size_t bytes;
 };
 
-// Opt-in (CDX_FORK_MEAN=1): measured a net loss on MI355X, so off by default — the mean beside the
-// screen stretches the screen 0.334 → 0.425 ms and itself to 0.37 ms (1.334 vs 1.347 ms per closure
-// at config 2, profiles/r02g_fork_mean_ab.txt; also with the screen's waves at s_setprio 2).
+// Where the screened closure forks the GPIS mean onto its side stream (CDX_FORK_MEAN overrides):
+//   2 (default): after the screen — the mean fills the CUs the selection / compaction kernels leave
+//     idle and shares the machine with the exact pass: 1.156–1.163 vs 1.188–1.200 ms per closure at
+//     config 2 unforked (profiles/r02o_fork_point_ab.txt);
+//   1: beside the screen — the screen stretched 0.334 → 0.425 ms (bf16 version), net loss
+//     (profiles/r02g_fork_mean_ab.txt);  3: after the exact pass, beside the ∇std pass: 1.175 ms;
+//   0: no fork.
+int fork_point() {
+  static const int at = [] {
+    const char* e = getenv("CDX_FORK_MEAN");
+    return e ? std::max(0, atoi(e)) : 2;
+  }();
+  return at;
+}
 bool fork_mean() {
-  static const bool on = getenv("CDX_FORK_MEAN") != nullptr;
+  static const bool on = fork_point() > 0;
   return on;
 }
 
@@ -486,12 +497,10 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
 }
 
 // Side stream of the screened closure (one per device, created on first use): the GPIS mean
-// (fp64 VALU-bound, 4-wave workgroups, 96 VGPRs, 8 KB LDS) can run concurrently with the bf16 screen
-// (one 512-thread workgroup per CU, 2 waves × 208 VGPRs per SIMD, 135 KB LDS), whose CUs keep room
-// for exactly one mean wave per SIMD and one mean workgroup of LDS, the idea being that the mean's
-// f64 VALU work hides behind the screen's MFMA work (see fork_mean).  Fork and join are event waits
-// (hipGraph-capturable).  Not for
-// concurrent cdx_closure calls from several host threads on one device.
+// (fp64 VALU-bound, 4-wave workgroups, 96 VGPRs, 8 KB LDS) runs concurrently with the selection and
+// exact-pass kernels (fork_point); the level kernel waits for it.  Fork and join are event waits
+// (hipGraph-capturable).  Not for concurrent cdx_closure calls from several host threads on one
+// device.
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
@@ -506,8 +515,14 @@ bool side_stream(SideStream& out) {
     hipStream_t st;
     hipEvent_t a, b;
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
-    if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess) {
+      (void)hipStreamDestroy(st);
+      (void)hipGetLastError();
+      return false;
+    }
+    if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      (void)hipStreamDestroy(st);
       (void)hipGetLastError();
       return false;
     }
@@ -651,19 +666,21 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     // be their group's maximum (≈ 1 per group) → ∇std at the group's maximum from its kept V row;
     // the mean on the side stream beside the screen (SideStream)
     const int T = p->chain.n_tips;
-    if (fork && (hipEventRecord(ss.fork, s) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess))
-      return CDX_ELAUNCH;
+    auto launch_fork = [&]() -> int {
+      if (hipEventRecord(ss.fork, s) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess) return CDX_ELAUNCH;
+      const int r = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, reinterpret_cast<cdx_stream_t>(ss.s));
+      if (r) return r;
+      return hipEventRecord(ss.join, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
+    };
+    if (fork && fork_point() == 1 && (rc = launch_fork())) return rc;
     rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.stats, s);
     if (rc) return rc;
-    if (fork) {
-      rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, reinterpret_cast<cdx_stream_t>(ss.s));
-      if (rc) return rc;
-      if (hipEventRecord(ss.join, ss.s) != hipSuccess) return CDX_ELAUNCH;
-    }
+    if (fork && fork_point() == 2 && (rc = launch_fork())) return rc;
     double* rpart = nullptr;
     int64_t rpad = 0;
     rc = cdx::gpis_refine_launch(p->gpis, w.X, w.rows, w.stats, (int)Mg, Ms, w.refine_ws, w.V, s, &rpart, &rpad);
     if (rc) return rc;
+    if (fork && fork_point() >= 3 && (rc = launch_fork())) return rc;
     rc = cdx::refine_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.sv2, w.vpos, w.std_, w.var, w.sel, w.Xg,
                                    w.vrow, w.stats, s);
     if (rc) return rc;
