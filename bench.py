@@ -249,7 +249,9 @@ def main():
             "stage_ms": stage_ms,
             "stage_ms_note": "gpis_screen / gpis_std_var (the refine kernel) / gpis_std_grad: HIP events over "
                               "the timed steps; the other stages from a 10-step all-stage pass after the timed "
-                              "region; the selection / merge / finalize kernels between them are in no stage",
+                              "region; the selection / merge / finalize kernels between them are in no stage; "
+                              "gpis_mean runs on a side stream concurrently with the selection, exact-pass and "
+                              "merge kernels (screened closure), so its stage time is wall time shared with them",
             "roofline_refine": {"bound": "mfma",
                                 "kernel": ("gpis_std_kernel<VARL> (v_mfma_f64_16x16x4_f64, K*·L⁻ᵀ, screened rows)" if scr
                                            else "gpis_std_kernel<VAR> (v_mfma_f64_16x16x4_f64, K*·L⁻ᵀ)"),
