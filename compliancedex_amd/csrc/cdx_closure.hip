@@ -260,12 +260,14 @@ __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_
   in.comp = comp + e * T;
   in.target = target + e * T * 3;
   in.palm_pos = in.palm_ori = nullptr;
+  // the draw is copied into registers either way: a pointer that may address either global memory
+  // or this array would keep nz in scratch
   if (noise) {
-    in.noise = noise + t * 9;
+    for (int i = 0; i < 9; ++i) nz[i] = noise[t * 9 + i];
   } else {
     device_noise(P.loop ? seed ^ splitmix64(P.loop->seed) : seed, t, nz);
-    in.noise = nz;
   }
+  in.noise = nz;
   in.noise_stride = 0;
   double dq[CDX_MAX_DOFS];
   const double qnorm = cdx::ref_dist(P, in.q, dq);

@@ -18,6 +18,23 @@
 namespace cdx {
 
 // ---------------------------------------------------------------- 3×3 SVD (f64)
+// Compare-exchange of singular value j and j+1 (descending) with their columns of A and V, by
+// selects: static register indices, where a permutation array would put A and V in scratch.
+CDX_HD void svd3_cswap(double* s, double* A, double* V, int j) {
+  const bool sw = s[j] < s[j + 1];
+  const double a = s[j], b = s[j + 1];
+  s[j] = sw ? b : a;
+  s[j + 1] = sw ? a : b;
+  for (int i = 0; i < 3; ++i) {
+    const double x = A[3 * i + j], y = A[3 * i + j + 1];
+    A[3 * i + j] = sw ? y : x;
+    A[3 * i + j + 1] = sw ? x : y;
+    const double v = V[3 * i + j], w = V[3 * i + j + 1];
+    V[3 * i + j] = sw ? w : v;
+    V[3 * i + j + 1] = sw ? v : w;
+  }
+}
+
 // One-sided Jacobi on the columns of A: A·V = U·diag(S), S descending.  Backward-stable
 // with high relative accuracy for the small singular values the rank-1-plus-noise
 // Kabsch matrices of the reference's initial configuration have.
@@ -54,20 +71,15 @@ CDX_HD void svd3(const double* H, double* U, double* S, double* V) {
   }
   double s[3];
   for (int j = 0; j < 3; ++j) s[j] = sqrt(A[j] * A[j] + A[3 + j] * A[3 + j] + A[6 + j] * A[6 + j]);
-  int o[3] = {0, 1, 2};
-  for (int i = 0; i < 2; ++i)
-    for (int j = 0; j < 2 - i; ++j)
-      if (s[o[j]] < s[o[j + 1]]) { const int t = o[j]; o[j] = o[j + 1]; o[j + 1] = t; }
-  double Vs[9];
+  // descending bubble network (0,1), (1,2), (0,1) with strict comparisons: the permutation of a
+  // bubble sort of the column indices by s
+  svd3_cswap(s, A, V, 0);
+  svd3_cswap(s, A, V, 1);
+  svd3_cswap(s, A, V, 0);
   for (int j = 0; j < 3; ++j) {
-    const int c = o[j];
-    S[j] = s[c];
-    for (int i = 0; i < 3; ++i) {
-      U[3 * i + j] = s[c] > 0 ? A[3 * i + c] / s[c] : 0.0;
-      Vs[3 * i + j] = V[3 * i + c];
-    }
+    S[j] = s[j];
+    for (int i = 0; i < 3; ++i) U[3 * i + j] = s[j] > 0 ? A[3 * i + j] / s[j] : 0.0;
   }
-  for (int i = 0; i < 9; ++i) V[i] = Vs[i];
   if (!(S[2] > 0)) {  // exactly singular: complete U with the cross product
     U[2] = U[3] * U[7] - U[6] * U[4];
     U[5] = U[6] * U[1] - U[0] * U[7];
@@ -251,12 +263,14 @@ template <int NT, int G = -1>
 struct ForceEq {
   static constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
   int T_rt, NP_rt;
+  // The tape keeps what backward cannot cheaply recompute; the weighted centred points, R·S1,
+  // the residuals, directions, rotated normals and forces are recomputed there by the same
+  // expressions (bit-identical values) — keeping them made the level kernel spill to scratch.
   double S1[NTA + 1][3], S2[NTA + 1][3], w[NTA + 1], n[NTA][3];
-  double c1[3], c2[3], Pm[NTA + 1][3], Qm[NTA + 1][3];
+  double c1[3], c2[3];
   KabschTape tp;
-  double R[9], W, t[3], RS1[NTA + 1][3];
-  double diff[NTA][3], dn[NTA], dir[NTA][3], ne[NTA][3], ang[NTA], mpre[NTA], margin[NTA], fn[NTA];
-  double force[NTA][3];
+  double R[9], W, t[3];
+  double dn[NTA], ang[NTA], mpre[NTA], margin[NTA], fn[NTA];
   double reward;
   int flip;
 
@@ -283,17 +297,20 @@ struct ForceEq {
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { c1[j] += S1[i][j]; c2[j] += S2[i][j]; }
     for (int j = 0; j < 3; ++j) { c1[j] /= NP; c2[j] /= NP; }
-#pragma unroll
-    for (int i = 0; i < NP; ++i)
-      for (int j = 0; j < 3; ++j) { Pm[i][j] = w[i] * (S1[i][j] - c1[j]); Qm[i][j] = w[i] * (S2[i][j] - c2[j]); }
     double H[9];
-    for (int r = 0; r < 3; ++r)
-      for (int c = 0; c < 3; ++c) {
-        double acc = 0.0;
+    {
+      double Pm[NTA + 1][3], Qm[NTA + 1][3];
 #pragma unroll
-        for (int i = 0; i < NP; ++i) acc += Pm[i][r] * Qm[i][c];
-        H[3 * r + c] = acc;
-      }
+      for (int i = 0; i < NP; ++i)
+        for (int j = 0; j < 3; ++j) { Pm[i][j] = w[i] * (S1[i][j] - c1[j]); Qm[i][j] = w[i] * (S2[i][j] - c2[j]); }
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+          double acc = 0.0;
+#pragma unroll
+          for (int i = 0; i < NP; ++i) acc += Pm[i][r] * Qm[i][c];
+          H[3 * r + c] = acc;
+        }
+    }
     {
       // svd3 sorts with data-dependent indices: run it on a separate tape so that only this small
       // object, not the whole ForceEq, has to live in scratch
@@ -307,23 +324,32 @@ struct ForceEq {
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       W += w[i];
-      mat3_vec(R, S1[i], RS1[i]);
-      for (int j = 0; j < 3; ++j) num[j] += w[i] * (S2[i][j] - RS1[i][j]);
+      double rs[3];
+      mat3_vec(R, S1[i], rs);
+      for (int j = 0; j < 3; ++j) num[j] += w[i] * (S2[i][j] - rs[j]);
     }
     for (int j = 0; j < 3; ++j) t[j] = num[j] / W;
     reward = 0.0;
 #pragma unroll
     for (int f = 0; f < T; ++f) {
-      for (int i = 0; i < 3; ++i) diff[f][i] = RS1[f][i] + t[i] - target[3 * f + i];
-      dn[f] = sqrt(dot3(diff[f], diff[f]));
-      for (int i = 0; i < 3; ++i) { dir[f][i] = diff[f][i] / dn[f]; force[f][i] = comp[f] * (-diff[f][i]); }
-      mat3_vec(R, n[f], ne[f]);
-      ang[f] = dot3(dir[f], ne[f]);
+      double diff[3], dir[3], ne[3], force[3];
+      residual(f, diff);
+      dn[f] = sqrt(dot3(diff, diff));
+      for (int i = 0; i < 3; ++i) { dir[i] = diff[i] / dn[f]; force[i] = comp[f] * (-diff[i]); }
+      mat3_vec(R, n[f], ne);
+      ang[f] = dot3(dir, ne);
       mpre[f] = ang[f] - fp.cos_mu;
       margin[f] = mpre[f] < -0.9999 ? -0.9999 : mpre[f];
-      fn[f] = sqrt(dot3(force[f], force[f]));
+      fn[f] = sqrt(dot3(force, force));
       reward += 0.2 * log(ang[f] + 1) + 0.8 * log(margin[f] + 1);
     }
+  }
+
+  // diff_f = R·S1_f + t − target_f (S2_f holds target_f)
+  CDX_HDM void residual(int f, double* diff) const {
+    double rs[3];
+    mat3_vec(R, S1[f], rs);
+    for (int i = 0; i < 3; ++i) diff[i] = rs[i] + t[i] - S2[f][i];
   }
 
   CDX_HDM void backward(double g_rw, const double* g_fn, const double* comp, double (*g_tip)[3], double (*g_target)[3],
@@ -336,23 +362,27 @@ struct ForceEq {
     for (int i = 0; i < NP; ++i) { g_S1[i][0] = g_S1[i][1] = g_S1[i][2] = 0; g_S2[i][0] = g_S2[i][1] = g_S2[i][2] = 0; g_w[i] = 0; }
 #pragma unroll
     for (int f = 0; f < T; ++f) {
+      double diff[3], dir[3], ne[3];
+      residual(f, diff);
+      for (int i = 0; i < 3; ++i) dir[i] = diff[i] / dn[f];
+      mat3_vec(R, n[f], ne);
       double gang = g_rw * 0.2 / (ang[f] + 1);
       if (mpre[f] >= -0.9999) gang += g_rw * 0.8 / (margin[f] + 1);
       double gdiff[3] = {0, 0, 0};
       // force norm → force = −comp·diff
       if (fn[f] > 0) {
         double gforce[3];
-        for (int i = 0; i < 3; ++i) gforce[i] = g_fn[f] * force[f][i] / fn[f];
-        g_w[f] += -dot3(gforce, diff[f]);
+        for (int i = 0; i < 3; ++i) gforce[i] = g_fn[f] * (comp[f] * (-diff[i])) / fn[f];
+        g_w[f] += -dot3(gforce, diff);
         for (int i = 0; i < 3; ++i) gdiff[i] += -comp[f] * gforce[i];
       }
       // ang = dir·ne ; ne = R·n (n detached)
       double gdir[3], gne[3];
-      for (int i = 0; i < 3; ++i) { gdir[i] = gang * ne[f][i]; gne[i] = gang * dir[f][i]; }
+      for (int i = 0; i < 3; ++i) { gdir[i] = gang * ne[i]; gne[i] = gang * dir[i]; }
       for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) gR[3 * r + c] += gne[r] * n[f][c];
-      const double pd = dot3(dir[f], gdir);
-      for (int i = 0; i < 3; ++i) gdiff[i] += (gdir[i] - dir[f][i] * pd) / dn[f];
+      const double pd = dot3(dir, gdir);
+      for (int i = 0; i < 3; ++i) gdiff[i] += (gdir[i] - dir[i] * pd) / dn[f];
       // diff = R·S1_f + t − target_f
       for (int i = 0; i < 3; ++i) { g_t[i] += gdiff[i]; g_target[f][i] -= gdiff[i]; }
       for (int r = 0; r < 3; ++r)
@@ -367,7 +397,9 @@ struct ForceEq {
       const double gW = -dot3(g_t, t) / W;
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
-        double r_i[3] = {S2[i][0] - RS1[i][0], S2[i][1] - RS1[i][1], S2[i][2] - RS1[i][2]};
+        double rs[3];
+        mat3_vec(R, S1[i], rs);
+        double r_i[3] = {S2[i][0] - rs[0], S2[i][1] - rs[1], S2[i][2] - rs[2]};
         g_w[i] += gW + dot3(gnum, r_i);
         for (int j = 0; j < 3; ++j) g_S2[i][j] += w[i] * gnum[j];
         for (int r = 0; r < 3; ++r)
@@ -384,10 +416,11 @@ struct ForceEq {
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       double gP[3], gQ[3];
-      mat3_vec(gH, Qm[i], gP);
-      mat3t_vec(gH, Pm[i], gQ);
       double d1[3] = {S1[i][0] - c1[0], S1[i][1] - c1[1], S1[i][2] - c1[2]};
       double d2[3] = {S2[i][0] - c2[0], S2[i][1] - c2[1], S2[i][2] - c2[2]};
+      const double Pm[3] = {w[i] * d1[0], w[i] * d1[1], w[i] * d1[2]}, Qm[3] = {w[i] * d2[0], w[i] * d2[1], w[i] * d2[2]};
+      mat3_vec(gH, Qm, gP);
+      mat3t_vec(gH, Pm, gQ);
       g_w[i] += dot3(gP, d1) + dot3(gQ, d2);
       for (int j = 0; j < 3; ++j) {
         g_S1[i][j] += w[i] * gP[j];
@@ -495,9 +528,12 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
     for (int i = 0; i < 3; ++i) o.g_target[f][i] += wk * 20.0 * gt.gmean[i];
   }
   {
+    // (fmax is data-dependent: the update is selected per fingertip so g_a keeps static indices)
     const GpisPoint& ga = gp(0, u, fmax);
-    const double gs = wk * P.uncertainty / s[fmax];
-    for (int i = 0; i < 3; ++i) g_a[fmax][i] += gs * ga.gstd[i];
+    const double gs = wk * P.uncertainty / ga.std;
+    for (int f = 0; f < T; ++f)
+      if (f == fmax)
+        for (int i = 0; i < 3; ++i) g_a[f][i] += gs * ga.gstd[i];
   }
   // force cost
   double g_fn[NTA], g_sm[NTA];
