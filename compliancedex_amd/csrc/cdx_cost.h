@@ -478,15 +478,20 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
   ForceEq<NT, G> fe;
   fe.forward(force_eq_params(P), T, a, in.target, in.comp, n, in.noise + k * in.noise_stride);
   o.flip = fe.flip;
-  // contact margin (unclamped)
-  double cd[NTA][3], cdn[NTA], cdir[NTA][3], cang[NTA];
+  // contact margin (unclamped), from the copies ForceEq keeps (fe.S1 = a, fe.S2 = target, fe.n = n):
+  // the backward recomputes it the same way, so a and n need not stay live through the SVD
+  auto contact = [&](int f, double* cdir, double& cdn, double& cang) {
+    double cd[3];
+    for (int i = 0; i < 3; ++i) cd[i] = fe.S1[f][i] - fe.S2[f][i];
+    cdn = sqrt(dot3(cd, cd));
+    for (int i = 0; i < 3; ++i) cdir[i] = cd[i] / cdn;
+    cang = dot3(cdir, fe.n[f]);
+  };
   double creward = 0.0;
   for (int f = 0; f < T; ++f) {
-    for (int i = 0; i < 3; ++i) cd[f][i] = a[f][i] - in.target[3 * f + i];
-    cdn[f] = sqrt(dot3(cd[f], cd[f]));
-    for (int i = 0; i < 3; ++i) cdir[f][i] = cd[f][i] / cdn[f];
-    cang[f] = dot3(cdir[f], n[f]);
-    creward += 0.1 * log(cang[f] + 1) + 0.9 * log(cang[f] - cos_mu + 1);
+    double cdir[3], cdn, cang;
+    contact(f, cdir, cdn, cang);
+    creward += 0.1 * log(cang + 1) + 0.9 * log(cang - cos_mu + 1);
   }
   // force cost: −Σ clamp(fn·softmin(fn), max=10)
   const double* fn = fe.fn;
@@ -548,11 +553,13 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
   // contact margin reward (gain −200·wk)
   const double g_cr = -200.0 * wk;
   for (int f = 0; f < T; ++f) {
-    const double gcang = g_cr * (0.1 / (cang[f] + 1) + 0.9 / (cang[f] - cos_mu + 1));
-    double gdir[3] = {gcang * n[f][0], gcang * n[f][1], gcang * n[f][2]};
-    const double pd = dot3(cdir[f], gdir);
+    double cdir[3], cdn, cang;
+    contact(f, cdir, cdn, cang);
+    const double gcang = g_cr * (0.1 / (cang + 1) + 0.9 / (cang - cos_mu + 1));
+    double gdir[3] = {gcang * fe.n[f][0], gcang * fe.n[f][1], gcang * fe.n[f][2]};
+    const double pd = dot3(cdir, gdir);
     for (int i = 0; i < 3; ++i) {
-      const double gcd = (gdir[i] - cdir[f][i] * pd) / cdn[f];
+      const double gcd = (gdir[i] - cdir[i] * pd) / cdn;
       g_a[f][i] += gcd;
       o.g_target[f][i] -= gcd;
     }
