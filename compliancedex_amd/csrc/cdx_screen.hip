@@ -272,6 +272,9 @@ __global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_ker
     }
   };
 
+#if defined(CDX_SC_PRIO_YOUNG)  // A/B: static priority for the second-dispatched half (waves 4–7)
+  if (wave >= SC_W / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   // prologue: B stages 0 .. SC_RING−2 landed, A of stage 0 generated
 #pragma unroll
   for (int st = 0; st < SC_RING - 1; ++st) issue(st);
