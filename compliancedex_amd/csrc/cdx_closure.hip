@@ -430,11 +430,13 @@ struct ClosureWs {
 //     config 2 unforked (profiles/r02o_fork_point_ab.txt);
 //   1: beside the screen — the screen stretched 0.334 → 0.425 ms (bf16 version), net loss
 //     (profiles/r02g_fork_mean_ab.txt);  3: after the exact pass, beside the ∇std pass: 1.175 ms;
-//   0: no fork.
+//   4: after the screen kernel, before its selection / compaction (≈ 30 µs of a nearly idle chip);
+//   0: no fork.  Values above 4 are taken as 0.
 int fork_point() {
   static const int at = [] {
     const char* e = getenv("CDX_FORK_MEAN");
-    return e ? std::max(0, atoi(e)) : 2;
+    const int v = e ? std::max(0, atoi(e)) : 2;
+    return v > 4 ? 0 : v;
   }();
   return at;
 }
@@ -516,7 +518,20 @@ bool side_stream(SideStream& out) {
   if (!ss.s) {
     hipStream_t st;
     hipEvent_t a, b;
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+    // CDX_SIDE_PRIO: < 0 creates the side stream at the device's lowest priority, > 0 at its
+    // highest (the CP prefers a higher-priority queue's dispatches), 0 (default) normal.
+    const char* pe = getenv("CDX_SIDE_PRIO");
+    const int want = pe ? atoi(pe) : 0;
+    int least = 0, greatest = 0;
+    hipError_t ce;
+    if (want != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      ce = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, want < 0 ? least : greatest);
+    else
+      ce = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (ce != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
     if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess) {
       (void)hipStreamDestroy(st);
       (void)hipGetLastError();
@@ -675,14 +690,17 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
       return hipEventRecord(ss.join, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
     };
     if (fork && fork_point() == 1 && (rc = launch_fork())) return rc;
-    rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.stats, s);
+    auto fork_cb = [](void* c) { return (*static_cast<decltype(launch_fork)*>(c))(); };
+    const bool fork_after_screen = fork && fork_point() == 4;
+    rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.stats, s,
+                                   fork_after_screen ? +fork_cb : nullptr, &launch_fork);
     if (rc) return rc;
     if (fork && fork_point() == 2 && (rc = launch_fork())) return rc;
     double* rpart = nullptr;
     int64_t rpad = 0;
     rc = cdx::gpis_refine_launch(p->gpis, w.X, w.rows, w.stats, (int)Mg, Ms, w.refine_ws, w.V, s, &rpart, &rpad);
     if (rc) return rc;
-    if (fork && fork_point() >= 3 && (rc = launch_fork())) return rc;
+    if (fork && fork_point() == 3 && (rc = launch_fork())) return rc;
     rc = cdx::refine_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.sv2, w.vpos, w.std_, w.var, w.sel, w.Xg,
                                    w.vrow, w.stats, s);
     if (rc) return rc;

@@ -49,9 +49,12 @@ int screen_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* var
 // Closure screening of the all-tip rows (G groups of T, M = G·T): screen partials in ws
 // (screen_ws_bytes(g, M)), per-row estimate sv2, rows kept for the exact pass listed in rows[0 .. G +
 // stats[0]) (the G group leaders first, at position = group), vpos[q] = list position or −1 (then
-// std_[q] = the estimate), keep [G] scratch.
+// std_[q] = the estimate), keep [G] scratch.  after_screen(ctx), when given, runs on the host between
+// the screen kernel's launch and the selection's (the closure forks its side stream there); its
+// nonzero return is returned.
 int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, void* ws, double* sv2, double* std_,
-                         int* vpos, int* rows, unsigned char* keep, int* stats, hipStream_t s);
+                         int* vpos, int* rows, unsigned char* keep, int* stats, hipStream_t s,
+                         int (*after_screen)(void*) = nullptr, void* ctx = nullptr);
 // After the refine pass (gpis_refine_launch): exact std/var of the kept rows, then per group the ∇std
 // row (sel = query, Xg = point, vrow = V row); stats[1] = kept rows whose estimate missed by > Δ.
 int refine_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, const double* rpartial, int64_t M_pad,

@@ -699,7 +699,8 @@ int screen_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* var
 size_t screen_select_ws_bytes(const cdx_gpis& g, int64_t Ms) { return screen_ws_bytes(g, Ms); }
 
 int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, void* ws, double* sv2, double* std_,
-                         int* vpos, int* rows, unsigned char* keep, int* stats, hipStream_t s) {
+                         int* vpos, int* rows, unsigned char* keep, int* stats, hipStream_t s,
+                         int (*after_screen)(void*), void* ctx) {
   const int64_t Ms = G * T;
   if (G <= 0 || T <= 0 || T > CDX_MAX_TIPS) return CDX_EINVAL;
   const int64_t M_pad = round_up(Ms, SC_BM);
@@ -713,18 +714,27 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       prof_mark(PROF_SCREEN, true, s);
       hipLaunchKernelGGL(gpis_screen_kernel<CDX_KERNEL_TPS>, grid, dim3(SC_THREADS), 0, s, g, X, Ms, partial, M_pad, Mt, Nt);
       prof_mark(PROF_SCREEN, false, s);
+      if (after_screen) {
+        if (const int r = after_screen(ctx)) return r;
+      }
       hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(256), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
       break;
     case CDX_KERNEL_RBF:
       prof_mark(PROF_SCREEN, true, s);
       hipLaunchKernelGGL(gpis_screen_kernel<CDX_KERNEL_RBF>, grid, dim3(SC_THREADS), 0, s, g, X, Ms, partial, M_pad, Mt, Nt);
       prof_mark(PROF_SCREEN, false, s);
+      if (after_screen) {
+        if (const int r = after_screen(ctx)) return r;
+      }
       hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(256), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
       break;
     default:
       prof_mark(PROF_SCREEN, true, s);
       hipLaunchKernelGGL(gpis_screen_kernel<CDX_KERNEL_JOINT>, grid, dim3(SC_THREADS), 0, s, g, X, Ms, partial, M_pad, Mt, Nt);
       prof_mark(PROF_SCREEN, false, s);
+      if (after_screen) {
+        if (const int r = after_screen(ctx)) return r;
+      }
       hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(256), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
       break;
   }
