@@ -39,6 +39,94 @@ namespace {
 // LDS-broadcast reads) at 0.122–0.133 ms (64-query workgroups quantise to 3.25 rounds).
 constexpr int MEAN_Q = 16, MEAN_SPLIT = 16, MEAN_BLOCK = MEAN_Q * MEAN_SPLIT;
 
+// TPS mean in moment form.  With k = 2r³ − 3Rr² + R³ and ∇k = 6(r − R)(x − x_n):
+//   Σ α k   = 2·Σ (αr)·r² − 3R·Σ α r² + R³·Σ α
+//   Σ α ∇k  = 6·Σ (αr)(x − x_n) − 6R·Σ α (x − x_n)
+// and the r² / (x − x_n) sums are closed forms in the moments S0 = Σ α, S1 = Σ α p̃, S2 = Σ α |p̃|²
+// (p̃ = x_n − c, x̃ = x − c, c = the first inducing point, so both stay at the object's scale):
+//   Σ α r² = |x̃|² S0 − 2 x̃·S1 + S2,   Σ α (x − x_n) = x̃ S0 − S1.
+// Per pair only r, αr, Σ (αr) r² and Σ (αr) d remain: 19 f64 ops + v_rsq against 23 + v_rsq.
+// The moments are summed by the staging threads (one point each per block), then over the workgroup.
+__device__ __forceinline__ void mean_tps_moments(const cdx_gpis& g, int64_t M, int64_t m, double x0, double x1,
+                                                 double x2, double* __restrict__ mean, double* __restrict__ gmean,
+                                                 double* __restrict__ normal, dbl4* sp) {
+  const int tid = threadIdx.x;
+  const int split = tid & (MEAN_SPLIT - 1);
+  const double c0 = g.X1[0], c1 = g.X1[1], c2 = g.X1[2];
+  double a3 = 0, h0 = 0, h1 = 0, h2 = 0;        // Σ (αr) r², Σ (αr) d
+  double s0 = 0, s1x = 0, s1y = 0, s1z = 0, s2 = 0;  // this thread's staged points' moments
+  for (int j0 = 0; j0 < g.N; j0 += MEAN_BLOCK) {
+    const int j = j0 + tid;
+    __syncthreads();
+    dbl4 v;
+    if (j < g.N) {
+      v.x = g.X1[3 * j]; v.y = g.X1[3 * j + 1]; v.z = g.X1[3 * j + 2]; v.w = g.alpha[j];
+      const double px = v.x - c0, py = v.y - c1, pz = v.z - c2;
+      s0 += v.w;
+      s1x += v.w * px; s1y += v.w * py; s1z += v.w * pz;
+      s2 += v.w * (px * px + py * py + pz * pz);
+    } else {
+      v.x = x0 + 1.0; v.y = v.z = 0.0; v.w = 0.0;  // any finite point; α = 0
+    }
+    sp[tid] = v;
+    __syncthreads();
+#pragma unroll 4
+    for (int jj = split; jj < MEAN_BLOCK; jj += MEAN_SPLIT) {
+      const dbl4 p = sp[jj];
+      const double dx = x0 - p.x, dy = x1 - p.y, dz = x2 - p.z;
+      const double r2 = dx * dx + dy * dy + dz * dz;
+      const double ar = p.w * cdx::sqrt_r2(r2);
+      a3 += ar * r2;
+      h0 += ar * dx;
+      h1 += ar * dy;
+      h2 += ar * dz;
+    }
+  }
+#pragma unroll
+  for (int w = 1; w < MEAN_SPLIT; w <<= 1) {
+    a3 += __shfl_xor(a3, w);
+    h0 += __shfl_xor(h0, w);
+    h1 += __shfl_xor(h1, w);
+    h2 += __shfl_xor(h2, w);
+  }
+  // workgroup sums of the five moments: wave reduction, then the four waves' partials through LDS
+#pragma unroll
+  for (int w = 1; w < 64; w <<= 1) {
+    s0 += __shfl_xor(s0, w);
+    s1x += __shfl_xor(s1x, w);
+    s1y += __shfl_xor(s1y, w);
+    s1z += __shfl_xor(s1z, w);
+    s2 += __shfl_xor(s2, w);
+  }
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(sp);
+  const int wave = tid >> 6;
+  if ((tid & 63) == 0) {
+    red[wave * 5 + 0] = s0; red[wave * 5 + 1] = s1x; red[wave * 5 + 2] = s1y; red[wave * 5 + 3] = s1z;
+    red[wave * 5 + 4] = s2;
+  }
+  __syncthreads();
+  s0 = s1x = s1y = s1z = s2 = 0;
+#pragma unroll
+  for (int w = 0; w < MEAN_BLOCK / 64; ++w) {
+    s0 += red[w * 5 + 0]; s1x += red[w * 5 + 1]; s1y += red[w * 5 + 2]; s1z += red[w * 5 + 3];
+    s2 += red[w * 5 + 4];
+  }
+  if (m >= M || split != 0) return;
+  const double R = g.R;
+  const double qx = x0 - c0, qy = x1 - c1, qz = x2 - c2;
+  const double sr2 = (qx * qx + qy * qy + qz * qz) * s0 - 2.0 * (qx * s1x + qy * s1y + qz * s1z) + s2;
+  mean[m] = 2.0 * a3 - 3.0 * R * sr2 + R * R * R * s0 + g.bias;
+  const double gx = 6.0 * h0 - 6.0 * R * (qx * s0 - s1x);
+  const double gy = 6.0 * h1 - 6.0 * R * (qy * s0 - s1y);
+  const double gz = 6.0 * h2 - 6.0 * R * (qz * s0 - s1z);
+  if (gmean) { gmean[3 * m] = gx; gmean[3 * m + 1] = gy; gmean[3 * m + 2] = gz; }
+  if (normal) {
+    const double nn = sqrt(gx * gx + gy * gy + gz * gz) + 1e-8;
+    normal[3 * m] = gx / nn; normal[3 * m + 1] = gy / nn; normal[3 * m + 2] = gz / nn;
+  }
+}
+
 template <int KT>
 __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
                                                                double* __restrict__ mean, double* __restrict__ gmean,
@@ -51,6 +139,12 @@ __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const
   if (m < M) { x0 = X[3 * m]; x1 = X[3 * m + 1]; x2 = X[3 * m + 2]; }
   const double R = g.R, inv_s2 = 1.0 / (g.sigma * g.sigma);
   double acc = 0, g0 = 0, g1 = 0, g2 = 0;
+#ifndef CDX_MEAN_DIRECT  // A/B switch: the per-pair k / ∇k form for TPS too
+  if constexpr (KT == CDX_KERNEL_TPS) {
+    mean_tps_moments(g, M, m, x0, x1, x2, mean, gmean, normal, sp);
+    return;
+  }
+#endif
   for (int j0 = 0; j0 < g.N; j0 += MEAN_BLOCK) {
     const int j = j0 + tid;
     __syncthreads();
