@@ -45,7 +45,8 @@ constexpr int MEAN_Q = 16, MEAN_SPLIT = 16, MEAN_BLOCK = MEAN_Q * MEAN_SPLIT;
 // and the r² / (x − x_n) sums are closed forms in the moments S0 = Σ α, S1 = Σ α p̃, S2 = Σ α |p̃|²
 // (p̃ = x_n − c, x̃ = x − c, c = the first inducing point, so both stay at the object's scale):
 //   Σ α r² = |x̃|² S0 − 2 x̃·S1 + S2,   Σ α (x − x_n) = x̃ S0 − S1.
-// Per pair only r, αr, Σ (αr) r² and Σ (αr) d remain: 19 f64 ops + v_rsq against 23 + v_rsq.
+// Per pair only r, αr, Σ (αr) r² and Σ (αr) d remain: 17 f64 ops + v_rsq against 23 + v_rsq (r
+// without the root's final Newton correction, ≤ 1 ulp, as the whitened pass's K* generation).
 // The moments are summed by the staging threads (one point each per block), then over the workgroup.
 __device__ __forceinline__ void mean_tps_moments(const cdx_gpis& g, int64_t M, int64_t m, double x0, double x1,
                                                  double x2, double* __restrict__ mean, double* __restrict__ gmean,
@@ -70,12 +71,19 @@ __device__ __forceinline__ void mean_tps_moments(const cdx_gpis& g, int64_t M, i
     }
     sp[tid] = v;
     __syncthreads();
-#pragma unroll 4
+#ifndef CDX_MEAN_UNROLL
+#define CDX_MEAN_UNROLL 4
+#endif
+#pragma unroll CDX_MEAN_UNROLL
     for (int jj = split; jj < MEAN_BLOCK; jj += MEAN_SPLIT) {
       const dbl4 p = sp[jj];
       const double dx = x0 - p.x, dy = x1 - p.y, dz = x2 - p.z;
       const double r2 = dx * dx + dy * dy + dz * dz;
+#ifndef CDX_MEAN_FULLSQRT  // the root without its final Newton correction (≤ 1 ulp), as the K* generation
+      const double ar = p.w * cdx::sqrt_r2_gen(r2);
+#else
       const double ar = p.w * cdx::sqrt_r2(r2);
+#endif
       a3 += ar * r2;
       h0 += ar * dx;
       h1 += ar * dy;

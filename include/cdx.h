@@ -209,8 +209,10 @@ size_t cdx_closure_workspace(const cdx_problem* p, int64_t E);
  *   gradients of Σ total_loss: g_q [E*n_dofs], g_comp [E*n_tips], g_target [E*n_tips*3],
  *   g_palm_pos [E*3], g_palm_ori [E*3]; flip [n_levels*E] int32 Kabsch det<0 mask (nullable).
  * All work is ordered on `stream`; a screened call also runs the GPIS mean on a per-device side
- * stream forked from and joined back into `stream` by events (CDX_FORK_MEAN=0 disables it), so
- * concurrent calls from several host threads on one device are not supported. */
+ * stream forked from and joined back into `stream` by events (CDX_FORK_MEAN=0 disables it; 1–4
+ * choose the fork point, CDX_SIDE_PRIO=-1/1 creates the side stream at the lowest / highest
+ * priority — A/B switches, read once per process), so concurrent calls from several host threads
+ * on one device are not supported. */
 int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* comp,
                 const double* target, const double* palm_pos, const double* palm_ori,
                 const double* kabsch_noise, uint64_t seed, void* workspace,
