@@ -479,40 +479,47 @@ __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const do
 }
 
 // Deterministic compaction of the kept non-leader fingertips behind the G leaders (group order,
-// fingertip order): one workgroup scans the per-group counts in chunks of 1024.  stats[0] = their
-// number, stats[1] (exact-pass bound violations, refine_select) reset here.
+// fingertip order): one workgroup; thread t owns the contiguous groups [t·C, t·C + C), C =
+// ceil(G/1024); one scan of the per-thread counts (wave shuffles, then the 16 wave totals through
+// LDS: two barriers in all).  stats[0] = their number, stats[1] (exact-pass bound violations,
+// refine_select) reset here.
 __global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, const unsigned char* __restrict__ keep,
                                                               int* __restrict__ vpos, int* __restrict__ rows,
                                                               int* __restrict__ stats) {
-  __shared__ int sc[1024];
-  const int t = threadIdx.x;
-  int carry = 0;
-  for (int64_t c0 = 0; c0 < G; c0 += 1024) {
-    const int64_t gi = c0 + t;
-    const unsigned m = gi < G ? keep[gi] : 0u;
-    const int n = __popc(m);
-    sc[t] = n;
-    __syncthreads();
-    for (int w = 1; w < 1024; w <<= 1) {  // inclusive Hillis-Steele scan
-      const int v = t >= w ? sc[t - w] : 0;
-      __syncthreads();
-      sc[t] += v;
-      __syncthreads();
-    }
-    int pos = (int)G + carry + sc[t] - n;
-    if (gi < G)
-      for (int f = 0; f < T; ++f)
-        if ((m >> f) & 1u) {
-          const int64_t q = gi * T + f;
-          vpos[q] = pos;
-          rows[pos] = (int)q;
-          ++pos;
-        }
-    carry += sc[1023];
-    __syncthreads();
+  __shared__ int wsum[16];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t C = (G + 1023) / 1024;
+  const int64_t g0 = (int64_t)t * C, g1 = g0 + C < G ? g0 + C : G;
+  int n = 0;
+  for (int64_t gi = g0; gi < g1; ++gi) n += __popc((unsigned)keep[gi]);
+  int inc = n;  // inclusive scan over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(inc, d);
+    if (lane >= d) inc += v;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  int before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    const int s = wsum[w];
+    before += w < wave ? s : 0;
+    total += s;
+  }
+  int pos = (int)G + before + inc - n;
+  for (int64_t gi = g0; gi < g1; ++gi) {
+    const unsigned m = keep[gi];
+    for (int f = 0; f < T; ++f)
+      if ((m >> f) & 1u) {
+        const int64_t q = gi * T + f;
+        vpos[q] = pos;
+        rows[pos] = (int)q;
+        ++pos;
+      }
   }
   if (t == 0) {
-    stats[0] = carry;
+    stats[0] = total;
     stats[1] = 0;
   }
 }
