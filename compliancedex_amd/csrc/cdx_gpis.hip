@@ -1138,7 +1138,7 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
                        X, M, partial, M_pad, Mt, n_tiles, nullptr, nullptr, nullptr, 0, RefineList{});
   }
   prof_mark(PROF_GPIS_GRAD, false, s);
-  hipLaunchKernelGGL(gpis_grad_finalize, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, partial, M, M_pad,
+  hipLaunchKernelGGL(gpis_grad_finalize, dim3((unsigned)((M + 63) / 64)), dim3(64), 0, s, partial, M, M_pad,
                      slots, sel, var, gstd);
 }
 

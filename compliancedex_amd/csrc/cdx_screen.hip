@@ -433,6 +433,10 @@ __global__ __launch_bounds__(256) void gpis_screen_finalize(cdx_gpis g, const do
 // Δ_f].  Leader = first maximum of a_f; kept for the exact pass: every f with a_f + Δ_f ≥ max_g (a_g
 // − Δ_g) (the leader always), all T when a value is not finite.  A discarded fingertip gets std =
 // sqrt(a_f), below the exact std of the group's maximum, so the level kernel's argmax is unchanged.
+// The per-group selection kernels (one thread per group, latency-bound loads of the stripe partials)
+// run in 64-thread workgroups: G = 4096 groups spread over 64 CUs instead of 16.
+constexpr int SEL_BLOCK = 64;
+
 __device__ __forceinline__ double screen_margin(double delta, double k0, double s2) {
   return delta * fmax(1.0, (k0 - s2) / k0);
 }
@@ -715,7 +719,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
   if (M_pad / SC_BM * Nt > 0x7fffffff || Ms > 0x7fffffff) return CDX_EINVAL;
   const int Mt = (int)(M_pad / SC_BM);
   double* partial = static_cast<double*>(ws);
-  const dim3 grid((unsigned)(Mt * Nt)), sgrid((unsigned)((G + 255) / 256));
+  const dim3 grid((unsigned)(Mt * Nt)), sgrid((unsigned)((G + SEL_BLOCK - 1) / SEL_BLOCK));
   switch (g.kernel) {
     case CDX_KERNEL_TPS:
       prof_mark(PROF_SCREEN, true, s);
@@ -724,7 +728,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(256), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
       break;
     case CDX_KERNEL_RBF:
       prof_mark(PROF_SCREEN, true, s);
@@ -733,7 +737,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(256), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
       break;
     default:
       prof_mark(PROF_SCREEN, true, s);
@@ -742,7 +746,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(256), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
       break;
   }
   hipLaunchKernelGGL(screen_compact_kernel, dim3(1), dim3(1024), 0, s, G, T, (const unsigned char*)keep, vpos, rows, stats);
@@ -753,16 +757,16 @@ int refine_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, c
                          const double* sv2, const int* vpos, double* std_, double* var, int64_t* sel, double* Xg,
                          int64_t* vrow, int* stats, hipStream_t s) {
   const int Nt = g.N_pad / SC_BN;
-  const dim3 sgrid((unsigned)((G + 255) / 256));
+  const dim3 sgrid((unsigned)((G + SEL_BLOCK - 1) / SEL_BLOCK));
   switch (g.kernel) {
     case CDX_KERNEL_TPS:
-      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(256), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, X, std_, var, sel, Xg, vrow, stats);
+      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, X, std_, var, sel, Xg, vrow, stats);
       break;
     case CDX_KERNEL_RBF:
-      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(256), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, X, std_, var, sel, Xg, vrow, stats);
+      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, X, std_, var, sel, Xg, vrow, stats);
       break;
     default:
-      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(256), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, X, std_, var, sel, Xg, vrow, stats);
+      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, X, std_, var, sel, Xg, vrow, stats);
       break;
   }
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
