@@ -37,7 +37,15 @@ namespace {
 // ≈ 90 % of the 30 T f64-op/s the VALU sustains, profiles/r01z_valu_f64.jsonl).  64 × 4 layouts
 // (1 wave per SIMD) ran at 0.137 ms; one query per lane with per-wave point ranges (scalar or
 // LDS-broadcast reads) at 0.122–0.133 ms (64-query workgroups quantise to 3.25 rounds).
-constexpr int MEAN_Q = 16, MEAN_SPLIT = 16, MEAN_BLOCK = MEAN_Q * MEAN_SPLIT;
+// 32 queries × 8 lanes per workgroup since the moment form (fewer VALU ops per pair, so the
+// staging and barriers per pair matter more): 0.095 ms against 0.101 for 16 × 16 and 64 × 4 at
+// 53 248 queries (profiles/r02zd_mean_layout_ab.txt).
+#ifndef CDX_MEAN_Q  // A/B switches (tools/mean_variants.sh); MEAN_Q · MEAN_SPLIT = 256
+#define CDX_MEAN_Q 32
+#define CDX_MEAN_SPLIT 8
+#endif
+constexpr int MEAN_Q = CDX_MEAN_Q, MEAN_SPLIT = CDX_MEAN_SPLIT, MEAN_BLOCK = MEAN_Q * MEAN_SPLIT;
+static_assert(MEAN_BLOCK == 256, "the mean kernel's moment reduction assumes 4 waves");
 
 // TPS mean in moment form.  With k = 2r³ − 3Rr² + R³ and ∇k = 6(r − R)(x − x_n):
 //   Σ α k   = 2·Σ (αr)·r² − 3R·Σ α r² + R³·Σ α

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Builds lib/libcdx_mean_<name>.so per VARIANTS entry (name:-Dflags; direct = the per-pair TPS mean)
+# Builds lib/libcdx_mean_<name>.so per VARIANTS entry (name:-Dflag,-Dflag; direct = the per-pair TPS mean)
 # beside libcdx.so (moment form); on the GPU ("run") times cdx_gpis_mean alone (tools/time_mean.py, M = 53 248 =
 # config 2's 13 queries per candidate) and bench.py unforked (CDX_FORK_MEAN=0) for each library.
 set -eu
@@ -11,7 +11,7 @@ if [ "${1:-}" = build ]; then
   for s in cdx_screen cdx_fit cdx_optim; do /opt/rocm/bin/hipcc $F -c $ROOT/compliancedex_amd/csrc/$s.hip -o $T/$s.o; done
   for s in cdx_closure cdx_sdf; do /opt/rocm/bin/hipcc $F -ffp-contract=off -c $ROOT/compliancedex_amd/csrc/$s.hip -o $T/$s.o; done
   for v in $VARIANTS; do
-    /opt/rocm/bin/hipcc $F ${v#*:} -c $ROOT/compliancedex_amd/csrc/cdx_gpis.hip -o $T/gpis.o
+    /opt/rocm/bin/hipcc $F $(echo ${v#*:} | tr ',' ' ') -c $ROOT/compliancedex_amd/csrc/cdx_gpis.hip -o $T/gpis.o
     /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $T/cdx_*.o $T/gpis.o -o $ROOT/compliancedex_amd/lib/libcdx_mean_${v%%:*}.so
   done
   rm -rf $T
