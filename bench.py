@@ -92,18 +92,28 @@ def cpu_baseline(args, ref_q, cfg):
 
 
 def hbm_traffic(E, n, key="gpis_var_bytes_per_launch"):
-    """Per-launch HBM bytes of a std kernel from the committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py), when one matches this config."""
+    """Per-launch HBM bytes of a GEMM kernel, measured by rocprofv3 PMC counters on the same
+    workload: profiles/pmc_traffic.json (tools/pmc_summary.py writes it from the newest
+    profiles/TAG_pmc.json; it is the one file of profiles/ shipped to the GPU box), else the newest
+    matching profiles/*_pmc.json.  (gfx950-corrected: (2·FETCH_SIZE + WRITE_SIZE)·1 KiB.)"""
     import glob
-    best = None
-    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
+    cands = [os.path.join(REPO, "profiles", "pmc_traffic.json")] + \
+        sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True)
+    for p in cands:
         try:
             d = json.load(open(p))
         except Exception:
             continue
         if d.get("E") == E and d.get("n_inducing") == n and key in d:
-            best = d[key]
-    return best
+            return d[key], d.get("source", os.path.relpath(p, REPO))
+    return None, None
+
+
+def traffic_block(E, n, key, algorithmic):
+    """roofline.traffic (PMC bytes per launch), the algorithmic bytes beside it and their ratio."""
+    t, src = hbm_traffic(E, n, key)
+    return {"traffic": t, "traffic_source": src, "algorithmic_bytes": algorithmic,
+            "traffic_over_algorithmic": (t / algorithmic) if (t and algorithmic) else None}
 
 
 CONFIG3 = ["banana", "mug", "mug2", "hammer", "lego", "coffeebottle", "box", "realsense"]
@@ -223,6 +233,14 @@ def main():
     # the screen runs the triangular product for every all-tip row as 3 fp16 slice products
     tri = float(n_ind) * (n_ind + 1)
     flops, flops_g, flops_s = m_exact * tri, m_grad * tri, 3 * m_std * tri
+    # algorithmic HBM bytes per launch: the triangle of L⁻ᵀ / L⁻¹ read once (f64), the V rows the
+    # refine pass writes / the ∇std pass reads (N_pad f64 each), the screen's fp16 slice pair of the
+    # scaled L⁻ᵀ triangle plus its stripe partials (8 f64 per row); queries and outputs are < 1 %
+    n_pad = (n_ind + 255) // 256 * 256
+    tri_bytes = 8.0 * n_ind * (n_ind + 1) / 2
+    alg_refine = tri_bytes + 8.0 * m_exact * n_pad
+    alg_grad = tri_bytes + 8.0 * m_grad * n_pad
+    alg_screen = 4.0 * n_ind * (n_ind + 1) / 2 + 8.0 * m_std * (n_pad // 256)
     std_ms, grad_ms, scr_ms = stage_ms["gpis_std_var"], stage_ms["gpis_std_grad"], stage_ms["gpis_screen"]
     achieved = flops / (std_ms * 1e-3) / 1e12 if std_ms else None
     achieved_g = flops_g / (grad_ms * 1e-3) / 1e12 if grad_ms else None
@@ -257,8 +275,8 @@ def main():
                                            else "gpis_std_kernel<VAR> (v_mfma_f64_16x16x4_f64, K*·L⁻ᵀ)"),
                                 "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                 "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
-                                "traffic": hbm_traffic(E, n_ind, "gpis_refine_bytes_per_launch" if scr
-                                                       else "gpis_var_bytes_per_launch"),
+                                **traffic_block(E, n_ind, "gpis_refine_bytes_per_launch" if scr
+                                                else "gpis_var_bytes_per_launch", alg_refine),
                                 "flops_per_launch": flops, "ms": std_ms,
                                 "note": f"{m_exact} of {m_std} all-tip rows x N(N+1) in the exact fp64 whitened "
                                         f"form (triangular; all-tip queries deduplicated over the 3 identical "
@@ -266,7 +284,7 @@ def main():
             "roofline_grad": {"bound": "mfma", "kernel": "gpis_std_kernel<GRADV> (V·L⁻¹ = (E11⁻¹k)ᵀ, ∇std)",
                               "achieved": achieved_g, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": (achieved_g / FP64_MFMA_PEAK_TFLOPS) if achieved_g else None,
-                              "traffic": hbm_traffic(E, n_ind, "gpis_grad_bytes_per_launch"),
+                              **traffic_block(E, n_ind, "gpis_grad_bytes_per_launch", alg_grad),
                               "flops_per_launch": flops_g,
                               "note": f"{m_grad} queries (the variance cost's argmax fingertip) x N(N+1), "
                                       f"from the whitened vectors the std pass keeps"},
@@ -278,13 +296,20 @@ def main():
                                            "(K*−k0)·L⁻ᵀ, 3 slice products)",
                 "achieved": achieved_s, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": (achieved_s / F16_MFMA_PEAK_TFLOPS) if achieved_s else None,
-                "traffic": hbm_traffic(E, n_ind, "gpis_screen_bytes_per_launch"),
+                **traffic_block(E, n_ind, "gpis_screen_bytes_per_launch", alg_screen),
                 "flops_per_launch": flops_s, "ms": scr_ms,
                 "note": f"{m_std} all-tip rows x 3 x N(N+1) fp16 MFMA flops (the split-precision estimate that "
                         f"selects the rows of the exact pass)"}
-            out["screen"] = {"exact_rows": scr["exact_rows"], "screened_rows": scr["screened_rows"],
-                             "bound_misses": scr["bound_misses"],
-                             "delta_over_k0": gpis.native_state().desc.screen_delta / float(gpis.R) ** 3}
+            rep = opt.screen_report(gpis, E)
+            out["screen"] = {k: rep[k] for k in ("exact_rows", "screened_rows", "audited_rows", "bound_misses",
+                                                  "audit_misses", "audit_flips", "faults", "max_ratio",
+                                                  "max_ratio_audit", "cum_closures", "cum_audited_rows",
+                                                  "cum_bound_misses", "cum_audit_misses", "cum_audit_flips",
+                                                  "cum_faults", "cum_max_ratio", "cum_max_ratio_audit")}
+            out["screen"]["delta_over_k0"] = gpis.native_state().desc.screen_delta / float(gpis.R) ** 3
+            out["screen"]["note"] = ("every closure re-checks its kept rows and an audit sample of discarded rows "
+                                     "with the exact fp64 pass; max_ratio = max |estimate − exact| / margin; cum_* "
+                                     "over all closures of this run")
         # the dominant kernel (longest per launch) is the headline roofline
         cands = [k for k in ("roofline_refine", "roofline_screen", "roofline_grad") if k in out and out[k]["achieved"]]
         dom = max(cands, key=lambda k: out[k]["flops_per_launch"] / out[k]["achieved"]) if cands else "roofline_refine"

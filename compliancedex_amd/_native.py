@@ -76,6 +76,18 @@ class CdxOptBuffers(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in OPT_BUFFER_FIELDS] + [("loop", C.c_void_p)]
 
 
+class CdxScreenReport(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("screened", "screened_rows", "exact_rows", "audited_rows", "bound_misses",
+                                         "audit_misses", "audit_flips", "faults")] + \
+               [("max_ratio", C.c_double), ("max_ratio_audit", C.c_double)] + \
+               [(n, C.c_int64) for n in ("cum_closures", "cum_audited_rows", "cum_bound_misses", "cum_audit_misses",
+                                         "cum_audit_flips", "cum_faults")] + \
+               [("cum_max_ratio", C.c_double), ("cum_max_ratio_audit", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 _P = C.c_void_p
 _I64 = C.c_int64
 _SIGS = {
@@ -98,8 +110,12 @@ _SIGS = {
     "cdx_collision_loss": (C.c_int, [C.POINTER(CdxCollision), _I64, _P, _P, _P, _P, _P, _P, _P, C.c_int32, _P]),
     "cdx_closure_workspace": (C.c_size_t, [C.POINTER(CdxProblem), _I64]),
     "cdx_closure_screen_stats": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, C.POINTER(C.c_int32)]),
+    "cdx_closure_screen_report": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, C.POINTER(CdxScreenReport), _P]),
+    "cdx_closure_screen_reset": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, _P]),
     "cdx_closure": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, _P, _P, _P, _P, _P, C.c_uint64, _P,
                               _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cdx_pack_survivors": (C.c_int, [_I64, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_double,
+                                     _I64, _I64, _P, _P]),
     "cdx_sdf_forward": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "cdx_sdf_backward": (C.c_int, [_P, _P, _P, _I64, _P, _P]),
     "cdx_version": (C.c_char_p, []),
@@ -134,10 +150,11 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        sizes = (C.c_size_t * 8)()
+        sizes = (C.c_size_t * 9)()
         lib.cdx_abi_sizes(sizes)
         mine = [C.sizeof(CdxGpis), C.sizeof(CdxBody), C.sizeof(CdxChain), C.sizeof(CdxProblem),
-                C.sizeof(CdxCollision), C.sizeof(CdxAdam), C.sizeof(CdxOptBuffers), C.sizeof(CdxForceEq)]
+                C.sizeof(CdxCollision), C.sizeof(CdxAdam), C.sizeof(CdxOptBuffers), C.sizeof(CdxForceEq),
+                C.sizeof(CdxScreenReport)]
         if list(sizes) != mine:
             raise ImportError(f"ABI struct size mismatch: library {list(sizes)} vs binding {mine}")
         _lib = lib

@@ -19,7 +19,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "lib")
 ARCH = os.environ.get("CDX_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["cdx_gpis.hip", "cdx_screen.hip", "cdx_fit.hip", "cdx_closure.hip", "cdx_sdf.hip", "cdx_optim.hip"]
+HIP_SOURCES = ["cdx_gpis.hip", "cdx_screen.hip", "cdx_fit.hip", "cdx_closure.hip", "cdx_sdf.hip", "cdx_optim.hip", "cdx_exchange.hip"]
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
 

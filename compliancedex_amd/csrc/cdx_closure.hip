@@ -415,10 +415,10 @@ struct ClosureWs {
   int64_t* sel;
   void *var_ws, *grad_ws;
   // split-precision screening (screen_on): estimates, list positions, the kept-row list, per-group
-  // keep masks, stats [refined extra rows, bound misses], ∇std V rows, screen / refine scratch
+  // keep / audit masks, statistics (cdx::ScreenStat), ∇std V rows, screen / refine scratch
   double* sv2;
   int *vpos, *rows, *stats;
-  unsigned char* keep;
+  unsigned short* keep;
   int64_t* vrow;
   void *screen_ws, *refine_ws;
   size_t bytes;
@@ -453,6 +453,9 @@ bool fork_mean() {
 constexpr int64_t SCREEN_MIN_ROWS = 4096;
 
 bool screen_on(const cdx_problem* p, int64_t E) {
+#if defined(CDX_GRAD_EXPLICIT)
+  return false;  // the screened path keeps V for the ∇std pass, which this build does not allocate
+#endif
   static const bool off = getenv("CDX_NO_SCREEN") != nullptr;
   const int64_t Ms = (int64_t)p->n_query_levels * E * p->chain.n_tips;
   return !off && p->gpis.screen && p->gpis.screen_delta > 0 && p->chain.n_tips <= CDX_MAX_TIPS &&
@@ -485,8 +488,8 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   w.sv2 = scr ? (double*)take(Ms * sizeof(double)) : nullptr;
   w.vpos = scr ? (int*)take(Ms * sizeof(int)) : nullptr;
   w.rows = scr ? (int*)take(Ms * sizeof(int)) : nullptr;
-  w.stats = scr ? (int*)take(4 * sizeof(int)) : nullptr;
-  w.keep = scr ? (unsigned char*)take(Mg) : nullptr;
+  w.stats = scr ? (int*)take(cdx::SS_WORDS * sizeof(int)) : nullptr;
+  w.keep = scr ? (unsigned short*)take(Mg * sizeof(unsigned short)) : nullptr;
   w.vrow = scr ? (int64_t*)take(Mg * sizeof(int64_t)) : nullptr;
   w.screen_ws = scr ? take(cdx::screen_ws_bytes(p->gpis, Ms)) : nullptr;
   w.refine_ws = scr ? take(cdx::gpis_refine_ws_bytes(p->gpis, Ms)) : nullptr;
@@ -683,29 +686,40 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     // be their group's maximum (≈ 1 per group) → ∇std at the group's maximum from its kept V row;
     // the mean on the side stream beside the screen (SideStream)
     const int T = p->chain.n_tips;
+    // Once the fork point has passed, every return joins the side stream back into `s` first:
+    // under capture an unjoined fork invalidates the graph, and eagerly the mean would keep writing
+    // the workspace after the error return.  (A join recorded before a failed launch_fork only waits
+    // on the event's previous record.)
+    bool forked = false;
     auto launch_fork = [&]() -> int {
+      forked = true;
       if (hipEventRecord(ss.fork, s) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess) return CDX_ELAUNCH;
       const int r = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, reinterpret_cast<cdx_stream_t>(ss.s));
       if (r) return r;
       return hipEventRecord(ss.join, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
     };
-    if (fork && fork_point() == 1 && (rc = launch_fork())) return rc;
+    auto joined = [&](int r) -> int {
+      if (forked && hipStreamWaitEvent(s, ss.join, 0) != hipSuccess && !r) r = CDX_ELAUNCH;
+      return r;
+    };
+    if (fork && fork_point() == 1 && (rc = launch_fork())) return joined(rc);
     auto fork_cb = [](void* c) { return (*static_cast<decltype(launch_fork)*>(c))(); };
     const bool fork_after_screen = fork && fork_point() == 4;
-    rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.stats, s,
-                                   fork_after_screen ? +fork_cb : nullptr, &launch_fork);
-    if (rc) return rc;
-    if (fork && fork_point() == 2 && (rc = launch_fork())) return rc;
+    rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.stats,
+                                   s, fork_after_screen ? +fork_cb : nullptr, &launch_fork);
+    if (rc) return joined(rc);
+    if (fork && fork_point() == 2 && (rc = launch_fork())) return joined(rc);
     double* rpart = nullptr;
     int64_t rpad = 0;
-    rc = cdx::gpis_refine_launch(p->gpis, w.X, w.rows, w.stats, (int)Mg, Ms, w.refine_ws, w.V, s, &rpart, &rpad);
-    if (rc) return rc;
-    if (fork && fork_point() == 3 && (rc = launch_fork())) return rc;
-    rc = cdx::refine_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.sv2, w.vpos, w.std_, w.var, w.sel, w.Xg,
-                                   w.vrow, w.stats, s);
-    if (rc) return rc;
+    rc = cdx::gpis_refine_launch(p->gpis, w.X, w.rows, w.stats + cdx::SS_EXTRA, (int)Mg, Ms, w.refine_ws, w.V, s, &rpart,
+                                 &rpad);
+    if (rc) return joined(rc);
+    if (fork && fork_point() == 3 && (rc = launch_fork())) return joined(rc);
+    rc = cdx::refine_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.sv2, w.vpos, w.keep, w.std_, w.var, w.sel,
+                                   w.Xg, w.vrow, w.stats, s);
+    if (rc) return joined(rc);
     rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V, w.vrow);
-    if (!rc && fork && hipStreamWaitEvent(s, ss.join, 0) != hipSuccess) return CDX_ELAUNCH;
+    rc = joined(rc);
   } else {
     const cdx::VarSelect vs{p->chain.n_tips, w.sel, w.Xg};
     rc = cdx::gpis_var_launch(p->gpis, w.X, Ms, w.std_, w.var, w.var_ws, s, w.V, &vs);
@@ -763,10 +777,52 @@ int cdx_closure_screen_stats(const cdx_problem* p, int64_t E, const void* worksp
   ClosureWs w = closure_ws_layout(p, E, static_cast<char*>(const_cast<void*>(workspace)));
   int st[2] = {0, 0};
   if (hipMemcpy(st, w.stats, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess) return CDX_ELAUNCH;
-  out[0] = (int32_t)((int64_t)p->n_query_levels * E + st[0]);  // rows of the exact pass
-  out[1] = st[1];                                                // estimates off by more than Δ
-  out[2] = (int32_t)((int64_t)p->n_query_levels * E * p->chain.n_tips);  // all-tip rows screened
+  out[0] = (int32_t)((int64_t)p->n_query_levels * E + st[cdx::SS_EXTRA]);  // rows of the exact pass
+  out[1] = st[cdx::SS_MISS];                                                // estimates off by more than Δ
+  out[2] = (int32_t)((int64_t)p->n_query_levels * E * p->chain.n_tips);     // all-tip rows screened
   return CDX_OK;
+}
+
+int cdx_closure_screen_report(const cdx_problem* p, int64_t E, const void* workspace, cdx_screen_report* out,
+                              cdx_stream_t stream) {
+  if (!problem_ok(p) || E <= 0 || !workspace || !out) return CDX_EINVAL;
+  *out = cdx_screen_report{};
+  if (!screen_on(p, E)) return CDX_OK;
+  ClosureWs w = closure_ws_layout(p, E, static_cast<char*>(const_cast<void*>(workspace)));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int st[cdx::SS_WORDS];
+  if (hipMemcpyAsync(st, w.stats, sizeof(st), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return CDX_ELAUNCH;
+  auto ratio = [&](int k) { return (double)__builtin_bit_cast(float, st[k]); };
+  const int64_t Mg = (int64_t)p->n_query_levels * E;
+  out->screened = 1;
+  out->screened_rows = (int32_t)(Mg * p->chain.n_tips);
+  out->exact_rows = (int32_t)(Mg + st[cdx::SS_EXTRA]);
+  out->audited_rows = st[cdx::SS_AUDIT];
+  out->bound_misses = st[cdx::SS_MISS];
+  out->audit_misses = st[cdx::SS_AUDIT_MISS];
+  out->audit_flips = st[cdx::SS_AUDIT_FLIP];
+  out->faults = st[cdx::SS_FAULT];
+  out->max_ratio = ratio(cdx::SS_RATIO);
+  out->max_ratio_audit = ratio(cdx::SS_RATIO_AUDIT);
+  const int c = cdx::SS_CUM;
+  out->cum_closures = (uint32_t)st[c];
+  out->cum_audited_rows = (uint32_t)st[c + cdx::SS_AUDIT];
+  out->cum_bound_misses = (uint32_t)st[c + cdx::SS_MISS];
+  out->cum_audit_misses = (uint32_t)st[c + cdx::SS_AUDIT_MISS];
+  out->cum_audit_flips = (uint32_t)st[c + cdx::SS_AUDIT_FLIP];
+  out->cum_faults = (uint32_t)st[c + cdx::SS_FAULT];
+  out->cum_max_ratio = ratio(c + cdx::SS_RATIO);
+  out->cum_max_ratio_audit = ratio(c + cdx::SS_RATIO_AUDIT);
+  return CDX_OK;
+}
+
+int cdx_closure_screen_reset(const cdx_problem* p, int64_t E, void* workspace, cdx_stream_t stream) {
+  if (!problem_ok(p) || E <= 0 || !workspace) return CDX_EINVAL;
+  if (!screen_on(p, E)) return CDX_OK;
+  ClosureWs w = closure_ws_layout(p, E, static_cast<char*>(workspace));
+  return hipMemsetAsync(w.stats, 0, cdx::SS_WORDS * sizeof(int), reinterpret_cast<hipStream_t>(stream)) == hipSuccess
+             ? CDX_OK : CDX_ELAUNCH;
 }
 
 const char* cdx_version(void) { return "compliancedex_amd 0.1 gfx950"; }
@@ -843,4 +899,5 @@ extern "C" void cdx_abi_sizes(size_t* out) {
   out[5] = sizeof(cdx_adam);
   out[6] = sizeof(cdx_opt_buffers);
   out[7] = sizeof(cdx_force_eq);
+  out[8] = sizeof(cdx_screen_report);
 }

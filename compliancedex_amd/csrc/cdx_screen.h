@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 
 #include "cdx.h"
 
@@ -46,19 +47,42 @@ size_t screen_ws_bytes(const cdx_gpis& g, int64_t M);
 // var[m] = estimate of k0 − ‖L⁻¹k(x_m)‖² (g.screen prepared)
 int screen_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* var, void* ws, hipStream_t s);
 
+// Screening statistics in the closure workspace (int32 words; "ratio" words hold the float bits of
+// max |estimate − exact| / Δ_f over the rows checked, finite rows only).  Per closure (reset by the
+// compaction kernel): the rows checked are every kept row and the audit sample (a deterministic
+// pseudo-random draw of discarded rows, run through the exact pass as well).  Cumulative (reset only
+// by cdx_closure_screen_reset): the same events summed over closures.
+enum ScreenStat {
+  SS_EXTRA = 0,        // rows in the exact-pass list past the G group leaders (kept + audited)
+  SS_MISS = 1,         // kept rows whose finite estimate missed the exact value by more than Δ_f
+  SS_AUDIT = 2,        // audited (discarded) rows
+  SS_AUDIT_MISS = 3,   // audited rows whose estimate missed by more than Δ_f
+  SS_AUDIT_FLIP = 4,   // groups whose exact maximum was an audited row (discarded by the screen)
+  SS_FAULT = 5,        // groups whose maximum fell on a row the exact pass did not run (safe fallback)
+  SS_RATIO = 6,        // max error ratio over kept rows (float bits)
+  SS_RATIO_AUDIT = 7,  // max error ratio over audited rows (float bits)
+  SS_CUM = 8,          // cumulative block: closures, then SS_MISS .. SS_RATIO_AUDIT summed / maxed
+  SS_WORDS = 16
+};
+
+// Audited discarded rows per closure (expected count; 0 disables the audit): CDX_SCREEN_AUDIT.
+int screen_audit_rows();
+
 // Closure screening of the all-tip rows (G groups of T, M = G·T): screen partials in ws
 // (screen_ws_bytes(g, M)), per-row estimate sv2, rows kept for the exact pass listed in rows[0 .. G +
-// stats[0]) (the G group leaders first, at position = group), vpos[q] = list position or −1 (then
-// std_[q] = the estimate), keep [G] scratch.  after_screen(ctx), when given, runs on the host between
-// the screen kernel's launch and the selection's (the closure forks its side stream there); its
-// nonzero return is returned.
+// stats[SS_EXTRA]) (the G group leaders first, at position = group, then the other kept rows and the
+// audited rows in group order), vpos[q] = list position or −1 (then std_[q] = the estimate), keep [G]
+// masks (low byte kept, high byte audited).  The audit draw is a hash of the rows' query points.
+// after_screen(ctx), when given, runs on the host between the screen kernel's launch and the
+// selection's (the closure forks its side stream there); its nonzero return is returned.
 int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, void* ws, double* sv2, double* std_,
-                         int* vpos, int* rows, unsigned char* keep, int* stats, hipStream_t s,
+                         int* vpos, int* rows, unsigned short* keep, int* stats, hipStream_t s,
                          int (*after_screen)(void*) = nullptr, void* ctx = nullptr);
-// After the refine pass (gpis_refine_launch): exact std/var of the kept rows, then per group the ∇std
-// row (sel = query, Xg = point, vrow = V row); stats[1] = kept rows whose estimate missed by > Δ.
+// After the refine pass (gpis_refine_launch): exact std/var of the kept and audited rows, then per
+// group the ∇std row (sel = query, Xg = point, vrow = V row, always a row the exact pass ran) and the
+// per-closure / cumulative statistics above.
 int refine_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, const double* rpartial, int64_t M_pad,
-                         const double* sv2, const int* vpos, double* std_, double* var, int64_t* sel, double* Xg,
-                         int64_t* vrow, int* stats, hipStream_t s);
+                         const double* sv2, const int* vpos, const unsigned short* keep, double* std_, double* var,
+                         int64_t* sel, double* Xg, int64_t* vrow, int* stats, hipStream_t s);
 
 }  // namespace cdx

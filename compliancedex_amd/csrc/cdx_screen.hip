@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 
 #include "cdx_gpis.h"
@@ -441,12 +442,25 @@ __device__ __forceinline__ double screen_margin(double delta, double k0, double 
   return delta * fmax(1.0, (k0 - s2) / k0);
 }
 
+__device__ __forceinline__ uint64_t audit_mix(uint64_t x) {  // splitmix64 finaliser
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// Per group: estimates, leader, kept rows, and the audit draw — a discarded row q joins the exact
+// pass as an audited row when the high word of a hash of (q, its query point's bits) is below
+// audit_thresh (expected count CDX_SCREEN_AUDIT per closure).  Keyed by the inputs, not by a
+// counter: the same inputs give the same exact-pass list, hence bit-identical results (the refine
+// pass's K-split depends on the list length), and every optimiser step draws a new sample.
 template <int KT>
 __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const double* __restrict__ partial,
                                                             int64_t M_pad, int Nt, int64_t G, int T,
                                                             double* __restrict__ sv2, double* __restrict__ std_,
                                                             int* __restrict__ vpos, int* __restrict__ rows,
-                                                            unsigned char* __restrict__ keep) {
+                                                            unsigned short* __restrict__ keep,
+                                                            const double* __restrict__ X, unsigned audit_thresh) {
   const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= G) return;
   const double k0 = cdx::gpis_k0<KT>(g.R), delta = g.screen_delta;
@@ -473,49 +487,63 @@ __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const do
       vpos[q] = (int)gi;
       rows[gi] = (int)q;
     } else if (!finite || a[f] + d[f] >= lo) {
-      mask |= 1u << f;  // position assigned by screen_compact_kernel
+      mask |= 1u << f;  // kept: position assigned by screen_compact_kernel
+    } else if (audit_thresh &&
+               (unsigned)(audit_mix(audit_mix((uint64_t)q) ^ audit_mix(__double_as_longlong(X[3 * q])) ^
+                                    audit_mix(__double_as_longlong(X[3 * q + 1]) + 1) ^
+                                    audit_mix(__double_as_longlong(X[3 * q + 2]) + 2)) >> 32) < audit_thresh) {
+      mask |= 0x100u << f;  // discarded by the screen, audited by the exact pass
     } else {
       vpos[q] = -1;
       std_[q] = sqrt(a[f]);
     }
   }
-  keep[gi] = (unsigned char)mask;
+  keep[gi] = (unsigned short)mask;
 }
 
-// Deterministic compaction of the kept non-leader fingertips behind the G leaders (group order,
-// fingertip order): one workgroup; thread t owns the contiguous groups [t·C, t·C + C), C =
-// ceil(G/1024); one scan of the per-thread counts (wave shuffles, then the 16 wave totals through
-// LDS: two barriers in all).  stats[0] = their number, stats[1] (exact-pass bound violations,
-// refine_select) reset here.
-__global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, const unsigned char* __restrict__ keep,
+// Deterministic compaction of the kept non-leader fingertips and the audited rows behind the G
+// leaders (group order, fingertip order): one workgroup; thread t owns the contiguous groups [t·C,
+// t·C + C), C = ceil(G/1024); one scan of the per-thread counts (wave shuffles, then the 16 wave
+// totals through LDS: two barriers in all).  Resets the per-closure statistics and counts the closure
+// and its audited rows in the cumulative block.
+__global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, const unsigned short* __restrict__ keep,
                                                               int* __restrict__ vpos, int* __restrict__ rows,
                                                               int* __restrict__ stats) {
-  __shared__ int wsum[16];
+  __shared__ int wsum[16], wsa[16];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t C = (G + 1023) / 1024;
   const int64_t g0 = (int64_t)t * C, g1 = g0 + C < G ? g0 + C : G;
-  int n = 0;
-  for (int64_t gi = g0; gi < g1; ++gi) n += __popc((unsigned)keep[gi]);
+  int n = 0, na = 0;
+  for (int64_t gi = g0; gi < g1; ++gi) {
+    const unsigned m = keep[gi];
+    n += __popc(m);
+    na += __popc(m >> 8);
+  }
   int inc = n;  // inclusive scan over the wave
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const int v = __shfl_up(inc, d);
     if (lane >= d) inc += v;
   }
+  int wa = na;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) wa += __shfl_xor(wa, d);
   if (lane == 63) wsum[wave] = inc;
+  if (lane == 0) wsa[wave] = wa;
   __syncthreads();
-  int before = 0, total = 0;
+  int before = 0, total = 0, total_a = 0;
 #pragma unroll
   for (int w = 0; w < 16; ++w) {
     const int s = wsum[w];
     before += w < wave ? s : 0;
     total += s;
+    total_a += wsa[w];
   }
   int pos = (int)G + before + inc - n;
   for (int64_t gi = g0; gi < g1; ++gi) {
     const unsigned m = keep[gi];
     for (int f = 0; f < T; ++f)
-      if ((m >> f) & 1u) {
+      if (((m >> f) | (m >> (8 + f))) & 1u) {
         const int64_t q = gi * T + f;
         vpos[q] = pos;
         rows[pos] = (int)q;
@@ -523,52 +551,110 @@ __global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, 
       }
   }
   if (t == 0) {
-    stats[0] = total;
-    stats[1] = 0;
+    stats[cdx::SS_EXTRA] = total;
+    stats[cdx::SS_AUDIT] = total_a;
+    for (int k = cdx::SS_MISS; k < cdx::SS_CUM; ++k)
+      if (k != cdx::SS_AUDIT) stats[k] = 0;
+    stats[cdx::SS_CUM] += 1;
+    stats[cdx::SS_CUM + cdx::SS_AUDIT] += total_a;
   }
 }
 
-// Exact values of the kept fingertips from the refine pass's stripe partials, then the group's
-// first maximum of log(100·std) — the level kernel's choice — as the ∇std row: sel = its query,
-// Xg = its point, vrow = its V row (list position).  stats[1] counts kept rows whose finite screen
-// value missed the exact one by more than Δ_f (the calibration bound; 0 expected; a NaN estimate kept
-// its whole group).
+// Exact values of the kept and audited fingertips from the refine pass's stripe partials, then the
+// group's first maximum of log(100·std) — the level kernel's choice — as the ∇std row: sel = its
+// query, Xg = its point, vrow = its V row (list position).  Checks every refined row's estimate
+// against its margin Δ_f.  A maximum on a row the exact pass did not run (only possible when a
+// margin failed) is a fault: the group falls back to its best refined row and its unrefined rows get
+// std 0, so the level kernel's argmax agrees and no V row outside the list is read.  One wave per
+// workgroup: counts and maxima are wave-reduced, then one atomic per statistic per wave.
 template <int KT>
 __global__ __launch_bounds__(256) void refine_select_kernel(cdx_gpis g, const double* __restrict__ rpartial,
                                                             int64_t M_pad, int Nt, int64_t G, int T,
                                                             const double* __restrict__ sv2, const int* __restrict__ vpos,
+                                                            const unsigned short* __restrict__ keep,
                                                             const double* __restrict__ X, double* __restrict__ std_,
                                                             double* __restrict__ var, int64_t* __restrict__ sel,
                                                             double* __restrict__ Xg, int64_t* __restrict__ vrow,
                                                             int* __restrict__ stats) {
   const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi >= G) return;
-  const double k0 = cdx::gpis_k0<KT>(g.R), delta = g.screen_delta;
-  int fmax = 0;
-  double lmax = 0;
-  for (int f = 0; f < T; ++f) {
-    const int64_t q = gi * T + f;
-    const int pos = vpos[q];
-    double sd;
-    if (pos >= 0) {
-      double acc = 0;
-      for (int t = 0; t < Nt; ++t) acc += rpartial[(int64_t)t * M_pad + pos];
-      const double v = k0 - acc;
-      sd = sqrt(fabs(v));
-      std_[q] = sd;
-      var[q] = v;
-      if (!(fabs(sv2[q] - v) <= screen_margin(delta, k0, sv2[q])) && isfinite(v) && isfinite(sv2[q]))
-        atomicAdd(&stats[1], 1);
-    } else {
-      sd = std_[q];
+  int miss = 0, amiss = 0, aflip = 0, fault = 0;
+  float rk = 0.f, ra = 0.f;
+  if (gi < G) {
+    const double k0 = cdx::gpis_k0<KT>(g.R), delta = g.screen_delta;
+    const unsigned m = keep[gi];
+    int fmax = 0, fref = -1;
+    double lmax = 0, lref = 0;
+    for (int f = 0; f < T; ++f) {
+      const int64_t q = gi * T + f;
+      const int pos = vpos[q];
+      double sd;
+      if (pos >= 0) {
+        double acc = 0;
+        for (int t = 0; t < Nt; ++t) acc += rpartial[(int64_t)t * M_pad + pos];
+        const double v = k0 - acc;
+        sd = sqrt(fabs(v));
+        std_[q] = sd;
+        var[q] = v;
+        const double e = fabs(sv2[q] - v), dd = screen_margin(delta, k0, sv2[q]);
+        if (isfinite(v) && isfinite(sv2[q])) {
+          const float r = (float)(e / dd);
+          const bool bad = !(e <= dd);
+          if ((m >> (8 + f)) & 1u) {
+            ra = fmaxf(ra, r);
+            amiss += bad;
+          } else {
+            rk = fmaxf(rk, r);
+            miss += bad;
+          }
+        }
+      } else {
+        sd = std_[q];
+      }
+      const double lv = log(100 * sd);
+      if (f == 0 || lv > lmax) { lmax = lv; fmax = f; }
+      if (pos >= 0 && (fref < 0 || lv > lref)) { lref = lv; fref = f; }
     }
-    const double lv = log(100 * sd);
-    if (f == 0 || lv > lmax) { lmax = lv; fmax = f; }
+    if (vpos[gi * T + fmax] < 0) {
+      fault = 1;
+      fmax = fref;  // the leader is always refined: fref ≥ 0
+      for (int f = 0; f < T; ++f)
+        if (vpos[gi * T + f] < 0) std_[gi * T + f] = 0.0;
+    } else if ((m >> (8 + fmax)) & 1u) {
+      aflip = 1;  // the exact maximum is an audited row: the screen had discarded it
+    }
+    const int64_t qi = gi * T + fmax;
+    sel[gi] = qi;
+    vrow[gi] = vpos[qi];
+    for (int i = 0; i < 3; ++i) Xg[3 * gi + i] = X[3 * qi + i];
   }
-  const int64_t qi = gi * T + fmax;
-  sel[gi] = qi;
-  vrow[gi] = vpos[qi];
-  for (int i = 0; i < 3; ++i) Xg[3 * gi + i] = X[3 * qi + i];
+#pragma unroll
+  for (int w = 1; w < 64; w <<= 1) {
+    miss += __shfl_xor(miss, w);
+    amiss += __shfl_xor(amiss, w);
+    aflip += __shfl_xor(aflip, w);
+    fault += __shfl_xor(fault, w);
+    rk = fmaxf(rk, __shfl_xor(rk, w));
+    ra = fmaxf(ra, __shfl_xor(ra, w));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    const int cnt[4] = {miss, amiss, aflip, fault};
+    const int idx[4] = {cdx::SS_MISS, cdx::SS_AUDIT_MISS, cdx::SS_AUDIT_FLIP, cdx::SS_FAULT};
+    for (int k = 0; k < 4; ++k)
+      if (cnt[k]) {
+        atomicAdd(&stats[idx[k]], cnt[k]);
+        atomicAdd(&stats[cdx::SS_CUM + idx[k]], cnt[k]);
+      }
+    // non-negative floats order like their bit patterns
+    unsigned* us = reinterpret_cast<unsigned*>(stats);
+    if (rk > 0.f) {
+      atomicMax(&us[cdx::SS_RATIO], __float_as_uint(rk));
+      atomicMax(&us[cdx::SS_CUM + cdx::SS_RATIO], __float_as_uint(rk));
+    }
+    if (ra > 0.f) {
+      atomicMax(&us[cdx::SS_RATIO_AUDIT], __float_as_uint(ra));
+      atomicMax(&us[cdx::SS_CUM + cdx::SS_RATIO_AUDIT], __float_as_uint(ra));
+    }
+  }
 }
 
 // ------------------------------------------------------------------ preparation (once per state)
@@ -709,8 +795,16 @@ int screen_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* var
 
 size_t screen_select_ws_bytes(const cdx_gpis& g, int64_t Ms) { return screen_ws_bytes(g, Ms); }
 
+int screen_audit_rows() {
+  static const int n = [] {
+    const char* e = getenv("CDX_SCREEN_AUDIT");
+    return e ? std::max(0, atoi(e)) : 64;
+  }();
+  return n;
+}
+
 int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, void* ws, double* sv2, double* std_,
-                         int* vpos, int* rows, unsigned char* keep, int* stats, hipStream_t s,
+                         int* vpos, int* rows, unsigned short* keep, int* stats, hipStream_t s,
                          int (*after_screen)(void*), void* ctx) {
   const int64_t Ms = G * T;
   if (G <= 0 || T <= 0 || T > CDX_MAX_TIPS) return CDX_EINVAL;
@@ -720,6 +814,11 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
   const int Mt = (int)(M_pad / SC_BM);
   double* partial = static_cast<double*>(ws);
   const dim3 grid((unsigned)(Mt * Nt)), sgrid((unsigned)((G + SEL_BLOCK - 1) / SEL_BLOCK));
+  // audit draw: P(row audited) = A / ((T − 1)·G), about A of the (T − 1)·G non-leader rows
+  const int64_t cand = (int64_t)(T - 1) * G;
+  const int A = screen_audit_rows();
+  const unsigned thresh = (A <= 0 || cand <= 0) ? 0u
+                          : (unsigned)std::min<double>(4294967295.0, std::ceil(4294967296.0 * A / (double)cand));
   switch (g.kernel) {
     case CDX_KERNEL_TPS:
       prof_mark(PROF_SCREEN, true, s);
@@ -728,7 +827,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, X, thresh);
       break;
     case CDX_KERNEL_RBF:
       prof_mark(PROF_SCREEN, true, s);
@@ -737,7 +836,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, X, thresh);
       break;
     default:
       prof_mark(PROF_SCREEN, true, s);
@@ -746,27 +845,27 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, X, thresh);
       break;
   }
-  hipLaunchKernelGGL(screen_compact_kernel, dim3(1), dim3(1024), 0, s, G, T, (const unsigned char*)keep, vpos, rows, stats);
+  hipLaunchKernelGGL(screen_compact_kernel, dim3(1), dim3(1024), 0, s, G, T, (const unsigned short*)keep, vpos, rows, stats);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
 int refine_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, const double* rpartial, int64_t M_pad,
-                         const double* sv2, const int* vpos, double* std_, double* var, int64_t* sel, double* Xg,
-                         int64_t* vrow, int* stats, hipStream_t s) {
+                         const double* sv2, const int* vpos, const unsigned short* keep, double* std_, double* var,
+                         int64_t* sel, double* Xg, int64_t* vrow, int* stats, hipStream_t s) {
   const int Nt = g.N_pad / SC_BN;
   const dim3 sgrid((unsigned)((G + SEL_BLOCK - 1) / SEL_BLOCK));
   switch (g.kernel) {
     case CDX_KERNEL_TPS:
-      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, X, std_, var, sel, Xg, vrow, stats);
+      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
       break;
     case CDX_KERNEL_RBF:
-      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, X, std_, var, sel, Xg, vrow, stats);
+      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
       break;
     default:
-      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, X, std_, var, sel, Xg, vrow, stats);
+      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
       break;
   }
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;

@@ -16,7 +16,13 @@ Row 0 of a rank's buffer is the header: [stored count, true survivor count, capa
 two counts differ when more candidates survived than the buffer holds (``overflow``).
 
 Every rank must pass an equal-shaped buffer to ``all_gather`` (RCCL sizes its receive buffers from
-the local one), so the default capacity is the same on every rank: ⌈total / world⌉.
+the local one), so the default capacity is the same on every rank: ⌈total / world⌉ for a sharded
+batch, the largest per-rank candidate count (one all_reduce) for one object per rank.
+
+On the GPU the pack is one kernel (cdx_pack_survivors: block-scan compaction in candidate order,
+header counts written on the device, no host synchronisation); CPU tensors (the gloo tests) take
+the same layout through torch ops.  Reading the gathered headers (``unpack_records``) is the one
+host synchronisation of the exchange.
 """
 from __future__ import annotations
 
@@ -42,30 +48,42 @@ def default_capacity(total, world):
     return -(-int(total) // int(world))
 
 
+def _f64(t, shape):
+    return t.detach().to(torch.float64).reshape(shape).contiguous()
+
+
 def pack_survivors(capacity, object_id, rank, cand_offset, best_loss, margin, q, comp, target, palm):
     """[capacity + 1, W] float64 buffer; row 0 = header [stored, survived, capacity], rows 1.. =
-    surviving candidates in candidate order (the first ``capacity`` of them)."""
+    surviving candidates in candidate order (the first ``capacity`` of them), the rest zero."""
     E, T = margin.shape
     D = q.shape[1]
     W = record_width(D, T)
     dev = margin.device
+    capacity = int(capacity)
+    buf = torch.empty(capacity + 1, W, dtype=torch.float64, device=dev)
+    ins = [_f64(margin, (E, T)), _f64(best_loss, (E,)), _f64(q, (E, D)), _f64(comp, (E, T)), _f64(target, (E, 3 * T)),
+           _f64(palm, (E, 6))]
+    if dev.type == "cuda":
+        from . import _native as N
+        N.check(N.load().cdx_pack_survivors(E, T, D, *(N.ptr(t) for t in ins), float(object_id), float(rank),
+                                            int(cand_offset), capacity, N.ptr(buf), N.stream_ptr(dev)),
+                "cdx_pack_survivors")
+        return buf
+    margin, best_loss, q, comp, target, palm = ins
     survive = (margin > 0).all(dim=1)
-    all_idx = torch.nonzero(survive).flatten()
-    idx = all_idx[:capacity]
-    buf = torch.zeros(capacity + 1, W, dtype=torch.float64, device=dev)
-    n = idx.numel()
-    buf[0, 0] = n
-    buf[0, 1] = all_idx.numel()
+    pos = torch.cumsum(survive.to(torch.int64), 0) - 1
+    keep = survive & (pos < capacity)
+    rows = torch.cat([torch.full((E, 1), float(object_id), dtype=torch.float64),
+                      torch.full((E, 1), float(rank), dtype=torch.float64),
+                      (torch.arange(E, dtype=torch.float64) + cand_offset).unsqueeze(1), best_loss.unsqueeze(1),
+                      torch.ones(E, 1, dtype=torch.float64), margin, q, comp, target, palm], dim=1)
+    ext = torch.zeros(capacity + 2, W, dtype=torch.float64)  # row capacity + 1 takes the dropped rows
+    ext.index_copy_(0, torch.where(keep, pos + 1, torch.full_like(pos, capacity + 1)), rows)
+    buf.copy_(ext[:capacity + 1])
+    n = survive.sum()
+    buf[0, 0] = torch.clamp(n, max=capacity)
+    buf[0, 1] = n
     buf[0, 2] = capacity
-    if n:
-        cols = [torch.full((n, 1), float(object_id), dtype=torch.float64, device=dev),
-                torch.full((n, 1), float(rank), dtype=torch.float64, device=dev),
-                (idx + cand_offset).to(torch.float64).unsqueeze(1),
-                best_loss[idx].to(torch.float64).unsqueeze(1),
-                torch.ones(n, 1, dtype=torch.float64, device=dev),
-                margin[idx].to(torch.float64), q[idx].to(torch.float64), comp[idx].to(torch.float64),
-                target[idx].reshape(n, -1).to(torch.float64), palm[idx].to(torch.float64)]
-        buf[1:n + 1] = torch.cat(cols, dim=1)
     return buf
 
 
@@ -89,12 +107,25 @@ def all_gather_survivors(buf, group=None, return_buffers=False):
     return (unpack_records(out), out) if return_buffers else unpack_records(out)
 
 
+def agreed_capacity(n_local, device, group=None):
+    """The largest per-rank candidate count (one all_reduce of a scalar): the common buffer
+    capacity when every rank optimises its own object's candidates (``shard=False``)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return int(n_local)
+    dev = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.tensor([int(n_local)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
 def optimize_sharded(optimizer, gpis, q, target, comp, friction_mu, object_id=0, capacity=None, group=None,
-                     shard=True):
+                     shard=True, return_buffers=False):
     """Each rank optimises its shard of the global candidate arrays (already resident on
-    its GPU), then all ranks exchange surviving grasps.  Returns (local results, records).
-    ``shard=False`` (config 3, one object per rank): the arrays are this rank's own object's
-    candidates, optimised whole; every rank must then hold the same candidate count."""
+    its GPU), then all ranks exchange surviving grasps.  Returns (local results, records), plus
+    the gathered per-rank buffers when ``return_buffers`` (``overflow(buffers)`` then reports
+    survivors that did not fit).  ``shard=False`` (config 3, one object per rank): the arrays are
+    this rank's own object's candidates, optimised whole; ranks may hold different counts — the
+    capacity is the largest of them (``agreed_capacity``)."""
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if shard:
@@ -110,8 +141,10 @@ def optimize_sharded(optimizer, gpis, q, target, comp, friction_mu, object_id=0,
     opt_q, opt_comp, opt_target, opt_palm, opt_margin = res
     best = optimizer.best_loss if hasattr(optimizer, "best_loss") else torch.zeros(hi - lo, dtype=torch.float64,
                                                                                   device=q.device)
-    cap = capacity or (default_capacity(q.shape[0], world) if shard else q.shape[0])
+    cap = capacity or (default_capacity(q.shape[0], world) if shard else agreed_capacity(q.shape[0], q.device, group))
     buf = pack_survivors(cap, object_id, rank, lo, best, opt_margin, opt_q, opt_comp, opt_target, opt_palm)
     if world == 1:
-        return res, unpack_records([buf])
-    return res, all_gather_survivors(buf, group)
+        records, bufs = unpack_records([buf]), [buf]
+    else:
+        records, bufs = all_gather_survivors(buf, group, return_buffers=True)
+    return (res, records, bufs) if return_buffers else (res, records)

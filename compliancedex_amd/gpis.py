@@ -24,7 +24,8 @@ _PKG_STATES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "
 # Closure screening margin Δ = SCREEN_MARGIN × the calibrated max error of the split-precision estimate of std²
 # (cdx_gpis.screen_delta); CDX_SCREEN_MARGIN overrides it, 0 disables screening.
 SCREEN_MARGIN = float(os.environ.get("CDX_SCREEN_MARGIN", "32"))
-CALIB_QUERIES = 8192
+CALIB_QUERIES = 8192      # near the object (displaced inducing points, bounding box ± 5 cm)
+CALIB_FAR_QUERIES = 4096  # 5 cm … 3.5R from the inducing points (the screen's whole finite range)
 
 
 def _require_cuda(t, what):
@@ -73,9 +74,13 @@ class _State:
         self.desc.screen_delta = max(SCREEN_MARGIN * self.screen_err, 2.0 ** -40 * k0) if ok else 0.0
 
     def _calibrate_screen(self, X1, R, kernel):
-        """max |estimate − exact| of k0 − ‖L⁻¹k‖² over calibration queries around this state:
-        the inducing points displaced by 0–3 cm and uniform points in their bounding box ± 5 cm
-        (one host sync).  The closure's screening margin is SCREEN_MARGIN × this."""
+        """max |estimate − exact| of k0 − ‖L⁻¹k‖² over calibration queries around this state, in
+        units of the row scale max(1, ‖Ṽ‖²/k0) the closure's margin uses: the inducing points
+        displaced by 0–3 cm and uniform points in their bounding box ± 5 cm (the near set: mostly
+        finite estimates, else the state is not screened), plus the far set — inducing points pushed
+        5 cm … 3.5R along random directions, log-uniform, i.e. the screen's whole finite range,
+        where the margin grows with ‖Ṽ‖² (one host sync).  The closure's margin is SCREEN_MARGIN ×
+        this."""
         dev = X1.device
         gen = torch.Generator(device="cpu").manual_seed(0)
         n = X1.shape[0]
@@ -83,22 +88,29 @@ class _State:
                for sc in (0.0, 0.002, 0.005, 0.01, 0.03)]
         lo, hi = X1.min(0).values - 0.05, X1.max(0).values + 0.05
         pts.append(lo + (hi - lo) * torch.rand(2 * n, 3, generator=gen, dtype=torch.float64).to(dev))
-        Xc = torch.cat(pts)
-        if Xc.shape[0] > CALIB_QUERIES:
-            Xc = Xc[torch.randperm(Xc.shape[0], generator=gen)[:CALIB_QUERIES].to(dev)]
-        Xc = Xc.contiguous()
+        Xn = torch.cat(pts)
+        if Xn.shape[0] > CALIB_QUERIES:
+            Xn = Xn[torch.randperm(Xn.shape[0], generator=gen)[:CALIB_QUERIES].to(dev)]
+        r_far = max(3.5 * float(R), 0.05) if kernel != "rbf" else 1.0
+        d = torch.exp(torch.empty(CALIB_FAR_QUERIES, dtype=torch.float64).uniform_(
+            float(np.log(0.05)), float(np.log(max(r_far, 0.0501))), generator=gen))
+        u = torch.randn(CALIB_FAR_QUERIES, 3, generator=gen, dtype=torch.float64)
+        u = u / u.norm(dim=1, keepdim=True)
+        base = torch.randint(0, n, (CALIB_FAR_QUERIES,), generator=gen)
+        Xf = X1[base.to(dev)] + (d.unsqueeze(1) * u).to(dev)
+        Xc = torch.cat([Xn, Xf]).contiguous()
         est = self.screen_var(Xc)
         exact = exact_var(self, Xc)
         # a query beyond the screen's safe radius estimates NaN (the closure then runs its whole
-        # group exactly), so the bound is over finite estimates; mostly NaN: no screening
+        # group exactly), so the bound is over finite estimates; mostly NaN near the object: no screening
         ok = torch.isfinite(est)
-        if int(ok.sum()) < Xc.shape[0] // 2:
+        if int(ok[:Xn.shape[0]].sum()) < Xn.shape[0] // 2:
             return float("nan")
-        # in units of the row's rounding scale max(1, ‖Ṽ‖²/k0) = max(1, (k0 − est)/k0), the factor
-        # the closure's selection multiplies Δ by (cdx_screen.hip screen_margin)
         k0 = {"tps": float(R) ** 3, "rbf": 1.0, "joint": 0.3 + 0.7 * float(R) ** 3}[kernel]
         scale = ((k0 - est[ok]) / k0).clamp(min=1.0) if k0 > 0 else torch.ones_like(est[ok])
-        return float(((est[ok] - exact[ok]).abs() / scale).max())
+        err = (est[ok] - exact[ok]).abs() / scale
+        self.calib_far_finite = int(ok[Xn.shape[0]:].sum())
+        return float(err.max())
 
     def screen_var(self, X):
         """Split-precision estimate of k0 − ‖L⁻¹k‖² at X [M, 3] (cdx_gpis_screen_var)."""
@@ -187,6 +199,7 @@ class GPIS:
         self.kernel = kernel
         self._state = None
         self._state_key = None
+        self._gen = 0  # bumped by fit / load_state_data
 
     # ----------------------------------------------------------------- fit / io
     def fit(self, X1, y1, noise=0.0):
@@ -213,6 +226,7 @@ class GPIS:
         self.noise = noise
         self.E11 = E11
         self._state = None
+        self._gen += 1
 
     def save_state_data(self, name="gpis_state"):
         """npz {R, X1, y1, E11, bias} under gpis_states/ (gpis.py:155-160)."""
@@ -233,17 +247,38 @@ class GPIS:
         self.E11 = torch.from_numpy(data["E11"]).to(device)
         self.bias = torch.from_numpy(data["bias"]).double().to(device)
         self._state = None
+        self._gen += 1
 
     # ------------------------------------------------------------ native state
+    def _state_inputs(self):
+        return (self.X1, self.y1, self.E11, getattr(self, "R", None), self.bias)
+
+    def _state_current(self):
+        """The cached state is current while every input is the same object (the cache holds them,
+        so an id cannot be recycled) at the same torch version counter (an in-place edit bumps it),
+        with the same kernel / sigma and no fit / load since."""
+        if self._state is None or self._state_key is None:
+            return False
+        refs, vers, kernel, sigma, gen = self._state_key
+        cur = self._state_inputs()
+        for a, b, v in zip(refs, cur, vers):
+            if torch.is_tensor(a) or torch.is_tensor(b):
+                if a is not b or a._version != v:
+                    return False
+            elif a != b:
+                return False
+        return kernel == self.kernel and sigma == self.sigma and gen == self._gen
+
     def native_state(self):
-        # identity key: no device->host sync per query; fit/load reset the state
-        key = (id(self.X1), id(self.y1), id(self.E11), id(getattr(self, "R", None)), id(self.bias), self.kernel,
-               self.sigma)
-        if self._state is None or self._state_key != key:
+        # no device->host sync per query (the key is host-side object identity + version counters);
+        # the reference re-solves E11 on every call (gpis.py:53), this rebuilds only when it changed
+        if not self._state_current():
             _require_cuda(self.X1, "GPIS state")
             R = float(self.R) if hasattr(self, "R") else 0.0
             self._state = _State(self.X1, self.y1, self.E11, R, float(self.bias), self.kernel, self.sigma)
-            self._state_key = key
+            ins = self._state_inputs()
+            self._state_key = (ins, tuple(t._version if torch.is_tensor(t) else None for t in ins), self.kernel,
+                               self.sigma, self._gen)
         return self._state
 
     # ---------------------------------------------------------------- queries

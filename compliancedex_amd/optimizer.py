@@ -7,6 +7,8 @@ target clamps).  Module constants mirror optimize_pregrasp.py:13-30.
 """
 from __future__ import annotations
 
+import warnings
+
 import numpy as np
 import torch
 
@@ -104,7 +106,9 @@ class ProbabilisticGraspOptimizer:
         self._chain_desc = self.robot_model._descriptor(self.ee_link_names, self.ee_link_offsets)
         self._problem = self._problem_state = self._problem_key = None
         self._ws = None
+        self._last_ws = None  # workspace of the most recent closure (the optimiser's or a graph's own)
         self._seed = int(seed)
+        self.screen_fallbacks = 0  # optimise loops re-run unscreened after a failed screen check
         self._graphs = {}
         self.optim = None
 
@@ -151,22 +155,34 @@ class ProbabilisticGraspOptimizer:
             self._problem_key = key
         return self._problem
 
-    def screen_stats(self, gpis, E, friction_mu=1):
-        """Screening of the last closure over E candidates (cdx_closure_screen_stats): dict of the
-        all-tip rows that ran the exact fp64 pass, the rows whose screen estimate missed its bound,
-        and the rows screened — or None when the closure ran the full fp64 pass."""
-        import ctypes
-        out = (ctypes.c_int32 * 3)()
-        N.check(N.load().cdx_closure_screen_stats(self.problem(gpis, friction_mu), E, N.ptr(self._ws), out),
-                "cdx_closure_screen_stats")
-        if out[0] < 0:
+    def screen_report(self, gpis, E, friction_mu=1):
+        """Verification record of the last closure over E candidates (cdx_closure_screen_report, one
+        stream-ordered device→host copy): exact / audited rows, margin misses, audit flips, faults,
+        the largest estimate error in units of its margin, and the same summed since the workspace's
+        last reset — or None when the closure ran the full fp64 pass."""
+        if self._last_ws is None:
             return None
-        return {"exact_rows": out[0], "bound_misses": out[1], "screened_rows": out[2]}
+        rep = N.CdxScreenReport()
+        N.check(N.load().cdx_closure_screen_report(self.problem(gpis, friction_mu), E, N.ptr(self._last_ws), rep,
+                                                   N.stream_ptr(self._last_ws.device)), "cdx_closure_screen_report")
+        return rep.as_dict() if rep.screened else None
+
+    def screen_stats(self, gpis, E, friction_mu=1):
+        """The main counts of ``screen_report``: exact_rows, bound_misses, screened_rows (+ audit)."""
+        r = self.screen_report(gpis, E, friction_mu)
+        if r is None:
+            return None
+        return {k: r[k] for k in ("exact_rows", "bound_misses", "screened_rows", "audited_rows", "audit_misses",
+                                  "audit_flips", "faults", "max_ratio", "max_ratio_audit")}
+
+    def _reset_screen(self, p, E, ws):
+        N.check(N.load().cdx_closure_screen_reset(p, E, N.ptr(ws), N.stream_ptr(ws.device)), "cdx_closure_screen_reset")
 
     def _ensure_ws(self, p, E, dev):
         need = N.load().cdx_closure_workspace(p, E)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
+            self._reset_screen(p, E, self._ws)
 
     def _closure_into(self, p, q, comp, target, pp, po, noise, out, seed=None, ws=None):
         """cdx_closure on contiguous f64 device tensors, writing into the preallocated ``out``.
@@ -180,6 +196,7 @@ class ProbabilisticGraspOptimizer:
         if seed is None:
             self._seed += 1
             seed = self._seed
+        self._last_ws = ws
         stream = N.stream_ptr(q.device)
         N.check(lib.cdx_closure(p, E, N.ptr(q), N.ptr(comp), N.ptr(target), N.ptr(pp), N.ptr(po), N.ptr(noise),
                                 seed, N.ptr(ws), N.ptr(out["total_loss"]), N.ptr(out["total_margin"]),
@@ -239,24 +256,26 @@ class ProbabilisticGraspOptimizer:
 
     # -------------------------------------------------------------- optimize
     def optimize(self, init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose=True,
-                 noise_tape=None, fused=True, init_palm=None, graph=False):
+                 noise_tape=None, fused=True, init_palm=None, graph=False, step_hook=None):
         """The reference's optimisation loop (:771-839).  ``fused=True`` (default): per iteration
         one cdx_closure + one cdx_optimizer_step (Adam, best iterate, clamps on device, no host
         sync); ``fused=False``: the same loop with torch.optim.Adam.  ``noise_tape``: optional
         per-iteration Kabsch noise tensors (parity replay).  ``init_palm`` [E, 6]: start from these
         palm poses instead of ``palm_offset`` (the annealing outer loop's proposals).  ``graph=True``
-        (fused only): capture the whole loop once per (E, problem) as a hipGraph and replay it."""
+        (fused only): capture the whole loop once per (E, problem) as a hipGraph and replay it.
+        ``step_hook(s, out)`` (fused, eager only): called after closure s with its output buffers
+        (tests: per-step traces)."""
         if init_palm is not None:
             saved = self.palm_offset
             self.palm_offset = init_palm.detach().to(torch.float64)
             try:
                 return self.optimize(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
-                                     noise_tape, fused, graph=graph)
+                                     noise_tape, fused, graph=graph, step_hook=step_hook)
             finally:
                 self.palm_offset = saved
         if fused:
             return self._optimize_fused(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
-                                        noise_tape, graph)
+                                        noise_tape, graph, step_hook)
         joint_angles = init_joint_angles.clone().requires_grad_(True)
         compliance = compliance.clone().requires_grad_(True)
         params_list = [{"params": joint_angles, "lr": 1e-3}, {"params": compliance, "lr": 0.2}]
@@ -317,11 +336,40 @@ class ProbabilisticGraspOptimizer:
         return cfg
 
     def _optimize_fused(self, init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose, noise_tape,
-                        graph=False):
+                        graph=False, step_hook=None):
         """Device-resident loop: per iteration one cdx_closure + one cdx_optimizer_step, with the
         Kabsch-noise key and Adam's step count in device loop counters (cdx_loop), so the loop is
         the same whether launched eagerly or replayed from a captured hipGraph (``graph=True``;
-        captured once per (E, problem), replayed on later calls)."""
+        captured once per (E, problem), replayed on later calls).
+
+        Screened closures verify themselves (cdx_screen_report): the loop's cumulative record is
+        read once at the end (one host sync), and if any closure missed a margin or took the fault
+        fallback, the whole loop is run again without the screen (``screen_fallbacks`` counts it), so
+        the returned results are those of the full fp64 path either way."""
+        seed0 = self._seed
+        res = self._optimize_fused_once(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
+                                        noise_tape, graph, step_hook)
+        rep = self.screen_report(gpis, init_joint_angles.shape[0], friction_mu)
+        self.last_screen_report = rep
+        if rep is not None and (rep["cum_bound_misses"] or rep["cum_audit_misses"] or rep["cum_faults"]
+                                or rep["cum_audit_flips"]):
+            warnings.warn(f"screened optimise loop failed its checks ({rep}); re-running it unscreened")
+            self.screen_fallbacks += 1
+            p = self.problem(gpis, friction_mu)
+            delta = p.gpis.screen_delta
+            p.gpis.screen_delta = 0.0
+            seed_after = self._seed
+            self._seed = seed0  # the same noise keys: the re-run is the screened loop's exact counterpart
+            try:
+                res = self._optimize_fused_once(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
+                                                noise_tape, False, step_hook)
+            finally:
+                p.gpis.screen_delta = delta
+                self._seed = seed_after
+        return res
+
+    def _optimize_fused_once(self, init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
+                             noise_tape, graph=False, step_hook=None):
         lib = N.load()
         p = self.problem(gpis, friction_mu)
         E = init_joint_angles.shape[0]
@@ -330,6 +378,8 @@ class ProbabilisticGraspOptimizer:
         f64 = dict(dtype=torch.float64, device=dev)
         if graph and noise_tape is not None:
             raise ValueError("graph=True draws the Kabsch noise on device; noise_tape needs graph=False")
+        if graph and step_hook is not None:
+            raise ValueError("step_hook needs graph=False (a replayed graph has no host steps)")
         # A captured graph replays raw device pointers: each cache entry owns its workspace and
         # holds the GPIS state it captured (so neither is freed or reused while the entry lives;
         # the id() in the key cannot be recycled while the entry references the object).
@@ -371,6 +421,12 @@ class ProbabilisticGraspOptimizer:
         c["loop"][0] = self._seed  # fresh noise keys per call, identical eager / replayed
         c["loop"].view(torch.int32)[2] = -1
         self._seed += self.num_iters
+        # the loop's cumulative screen record starts at zero (outside any captured graph)
+        if graph:
+            self._reset_screen(p, E, c["ws"])
+        else:
+            self._ensure_ws(p, E, dev)
+            self._reset_screen(p, E, self._ws)
         st = {k: c[k] for k in ("m_q", "v_q", "m_comp", "v_comp", "m_target", "v_target", "m_palm_pos", "v_palm_pos",
                                 "m_palm_ori", "v_palm_ori", "opt_value", "opt_margin", "opt_q", "opt_comp",
                                 "opt_target", "opt_palm")}
@@ -392,6 +448,8 @@ class ProbabilisticGraspOptimizer:
                         noise = noise_tape[s].to(**f64).contiguous()
                     self._closure_into(p, c["q"], c["comp"], c["target"], c["pp"], c["po"], noise, out, seed=0,
                                        ws=c.get("ws"))
+                    if step_hook is not None:
+                        step_hook(s, out)
                     N.check(lib.cdx_optimizer_step(cfg, bufs, E, D, T, s, stream), "cdx_optimizer_step")
             finally:
                 p.loop = None
@@ -399,6 +457,7 @@ class ProbabilisticGraspOptimizer:
         if not graph:
             run_loop()
         elif "graph" in cache:
+            self._last_ws = c["ws"]
             cache["graph"].replay()
         else:
             # workspace and library state exist before capture; the first call captures AND runs

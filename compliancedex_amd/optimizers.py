@@ -126,8 +126,10 @@ class KinGraspOptimizer:
         return (tips.view(-1, 3) + self.palm_offset).view(-1, 3)
 
     def optimize(self, joint_angles, target_pose, compliance, friction_mu, object_mesh, verbose=True,
-                 kabsch_noise=None):
+                 kabsch_noise=None, trace_rows=False):
+        """``trace_rows``: also keep every iteration's per-candidate loss in ``loss_rows`` (device)."""
         self.loss_history = []
+        self.loss_rows = []
         joint_angles = joint_angles.clone().requires_grad_(True)
         compliance = compliance.clone().requires_grad_(True)
         faces = _face_vertices(object_mesh, self.device)
@@ -159,6 +161,8 @@ class KinGraspOptimizer:
             l = c + dist_cost + tar_dist_cost + center_cost + _force_cost(force_norm, 1.0) + ref_cost
             l.sum().backward()
             self.loss_history.append(l.detach().sum())  # device scalar, no sync
+            if trace_rows:
+                self.loss_rows.append(l.detach().clone())
             if verbose:
                 print("Loss:", float(l.sum()), compliance)
             best.update(l, margin, normal, q=joint_angles, comp=compliance, target=target_pose)
@@ -181,9 +185,12 @@ class SDFGraspOptimizer:
         self.optimize_target = optimize_target
         self.mass, self.com, self.gravity = mass, list(com), gravity
 
-    def optimize(self, tip_pose, target_pose, compliance, friction_mu, object_mesh, verbose=True, kabsch_noise=None):
+    def optimize(self, tip_pose, target_pose, compliance, friction_mu, object_mesh, verbose=True, kabsch_noise=None,
+                 trace_rows=False):
+        """``trace_rows``: also keep every iteration's per-candidate loss in ``loss_rows`` (device)."""
         tip_pose = tip_pose.clone().requires_grad_(True)
         self.loss_history = []
+        self.loss_rows = []
         compliance = compliance.clone().requires_grad_(True)
         faces = _face_vertices(object_mesh, self.device)
         object_mesh.scale(0.9, center=[0, 0, 0])
@@ -211,6 +218,8 @@ class SDFGraspOptimizer:
             l = c + dist_cost + tar_dist_cost + center_cost + _force_cost(force_norm, 1.0)
             l.sum().backward()
             self.loss_history.append(l.detach().sum())  # device scalar, no sync
+            if trace_rows:
+                self.loss_rows.append(l.detach().clone())
             if verbose:
                 print("Loss:", float(l.sum()), float(dist_cost.sum()), float(tar_dist_cost.sum()))
             best.update(l, margin, normal, tip=tip_pose, comp=compliance, target=target_pose)

@@ -220,11 +220,59 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                 double* g_q, double* g_comp, double* g_target, double* g_palm_pos,
                 double* g_palm_ori, int32_t* flip, cdx_stream_t stream);
 
-/* Screening statistics of the last cdx_closure on this workspace (one device→host copy): out[0] =
- * all-tip rows that ran the exact fp64 whitened pass, out[1] = rows whose split-precision estimate
- * missed the exact value by more than screen_delta (0 expected: the calibration bound), out[2] =
- * all-tip rows screened; all −1 when the closure did not screen (no screen / CDX_NO_SCREEN set). */
+/* Screening statistics of the last cdx_closure on this workspace (one device→host copy on the null
+ * stream; prefer cdx_closure_screen_report): out[0] = all-tip rows that ran the exact fp64 whitened
+ * pass, out[1] = kept rows whose split-precision estimate missed the exact value by more than its
+ * margin, out[2] = all-tip rows screened; all −1 when the closure did not screen. */
 int cdx_closure_screen_stats(const cdx_problem* p, int64_t E, const void* workspace, int32_t* out3);
+
+/* The screened closure's verification record.  Every screened closure runs the exact fp64 pass for
+ * each group's leader, every fingertip the selection keeps, and an AUDIT sample of the fingertips it
+ * discards (a hash of the rows' query points — the same inputs draw the same sample, each optimiser
+ * step a new one; CDX_SCREEN_AUDIT rows expected, default 64), and checks each of those estimates
+ * against its margin Δ_f.  The maximum of each group is taken over
+ * exact values; an audited row that turns out to be its group's maximum is used (audit_flips), and a
+ * maximum on a row the exact pass did not run (possible only after a margin failure) takes the best
+ * exact row instead and is counted as a fault.  Fields cum_* accumulate over closures since the last
+ * cdx_closure_screen_reset (call it once after allocating the workspace). */
+typedef struct {
+  int32_t screened;        /* 1 if the last closure on this workspace screened (else all fields 0) */
+  int32_t screened_rows;   /* all-tip rows estimated by the screen */
+  int32_t exact_rows;      /* rows of the exact fp64 pass: leaders + kept + audited */
+  int32_t audited_rows;    /* screen-discarded rows re-checked by the exact pass */
+  int32_t bound_misses;    /* kept rows whose estimate missed the exact value by more than Δ_f */
+  int32_t audit_misses;    /* audited rows whose estimate missed by more than Δ_f */
+  int32_t audit_flips;     /* groups whose exact maximum was an audited (screen-discarded) row */
+  int32_t faults;          /* groups whose maximum fell on a row the exact pass did not run */
+  double max_ratio;        /* max |estimate − exact| / Δ_f over kept rows (finite estimates) */
+  double max_ratio_audit;  /* the same over audited rows */
+  int64_t cum_closures;
+  int64_t cum_audited_rows;
+  int64_t cum_bound_misses;
+  int64_t cum_audit_misses;
+  int64_t cum_audit_flips;
+  int64_t cum_faults;
+  double cum_max_ratio;
+  double cum_max_ratio_audit;
+} cdx_screen_report;
+
+/* Reads the record (an async copy on `stream`, then a wait on that stream). */
+int cdx_closure_screen_report(const cdx_problem* p, int64_t E, const void* workspace, cdx_screen_report* out,
+                              cdx_stream_t stream);
+/* Zeroes the cumulative fields (stream-ordered); a no-op when the closure does not screen. */
+int cdx_closure_screen_reset(const cdx_problem* p, int64_t E, void* workspace, cdx_stream_t stream);
+
+/* ------------------------------------------------------------ survivor exchange ------
+ * Multi-GPU record pack (no reference counterpart — the reference is single-GPU):
+ * candidates whose margins are all > 0 (the success test `opt_margin > 0`, optimize_pregrasp.py:226)
+ * go to buf [(capacity + 1) * W] f64, W = 5 + n_tips + n_dofs + n_tips + 3·n_tips + 6: row 0 the header
+ * [stored, survived, capacity, 0, …], rows 1.. the first `capacity` survivors in candidate order as
+ * [object_id, rank, cand_offset + e, best_loss, 1, margin[T], q[D], comp[T], target[3T], palm[6]],
+ * the remaining rows zero.  One launch, no host synchronisation; the buffer feeds one all_gather. */
+int cdx_pack_survivors(int64_t E, int32_t n_tips, int32_t n_dofs, const double* margin, const double* best_loss,
+                       const double* q, const double* comp, const double* target, const double* palm,
+                       double object_id, double rank, int64_t cand_offset, int64_t capacity, double* buf,
+                       cdx_stream_t stream);
 
 /* ------------------------------------------------------------ force_eq_reward ------
  * Replaces force_eq_reward (optimize_pregrasp.py:73-118) with optimal_transformation_batch
@@ -339,9 +387,10 @@ int cdx_profile_enable(int stages);
 int cdx_profile_read(double* ms6, int64_t* count6);
 
 /* sizeof(cdx_gpis), sizeof(cdx_body), sizeof(cdx_chain), sizeof(cdx_problem),
- * sizeof(cdx_collision), sizeof(cdx_adam), sizeof(cdx_opt_buffers), sizeof(cdx_force_eq) — lets
+ * sizeof(cdx_collision), sizeof(cdx_adam), sizeof(cdx_opt_buffers), sizeof(cdx_force_eq),
+ * sizeof(cdx_screen_report) — lets
  * a binding verify its struct layouts before the first call. */
-void cdx_abi_sizes(size_t* out8);
+void cdx_abi_sizes(size_t* out9);
 
 /* Test hook: D[16×16] = A[16×4]·B[4×16] through one v_mfma_f64_16x16x4_f64 (checks the
  * fragment layout the GPIS std kernel relies on). */

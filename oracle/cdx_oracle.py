@@ -425,3 +425,58 @@ def closure_with_grads(problem, q, comp, target, palm, noise):
     return dict(loss=float(loss), total_loss=tl.numpy(), total_margin=tm.numpy(), pregrasp_tip=pre.numpy(),
                 flip=flip.numpy(), grad_q=q.grad.numpy(), grad_comp=comp.grad.numpy(),
                 grad_target=target.grad.numpy(), grad_palm_pos=pp.grad.numpy(), grad_palm_ori=po.grad.numpy())
+
+
+# ----------------------------------------------------------------------------- Kin mode (config 4)
+def kin_sdf_loop(chain, ee_links, ee_offsets, palm_offset, ref_q, q0, target0, comp0, mu, faces, faces_deflate, sdf,
+                 noise_tape, iters, mass=0.1, com=(0.0, 0.0, 0.0), gravity=True):
+    """KinGraspOptimizer.optimize with optimize_target=True (optimize_pregrasp.py:152-227), in the
+    reference's float32: FK (:143-150, fresh-state — the loop only calls it recursively), the three
+    TorchSDF calls per iteration (:186-188) through ``sdf(points, faces) -> (sqdist, sign, normals,
+    clst)`` (autograd w.r.t. points; the caller passes the C oracle of the TorchSDF kernel), blended
+    signed normals (:190-191), force_eq_reward with the replayed Kabsch noise (:192-198), the six cost
+    terms (:199-208), backward, best-iterate tracking (:214-222) and Adam (:171-173, :223).
+    ``tar_sign`` is read as [E, T] (the reference's [E·T] broadcast at :207 runs only for E = 1, where
+    the two agree).  Returns (loss [iters, E], opt_q, opt_comp, opt_target, success flag)."""
+    q = torch.as_tensor(q0, dtype=F32).clone().requires_grad_(True)
+    comp = torch.as_tensor(comp0, dtype=F32).clone().requires_grad_(True)
+    target = torch.as_tensor(target0, dtype=F32).clone().requires_grad_(True)
+    palm = torch.as_tensor(palm_offset, dtype=F32).view(1, 3)
+    ref = torch.tensor(list(map(float, ref_q)))
+    optim = torch.optim.Adam([{"params": q, "lr": 2e-3}, {"params": target, "lr": 1e-5},
+                              {"params": comp, "lr": 0.2}])
+    E, T = target.shape[0], target.shape[1]
+    opt_q, opt_comp, opt_target = q.detach().clone(), comp.detach().clone(), target.detach().clone()
+    opt_value = torch.full((E,), float("inf"))
+    opt_margin = None
+    trace = []
+    for s in range(iters):
+        optim.zero_grad()
+        tips = (chain.forward_kinematics(q, ee_links, ee_offsets)[0].view(-1, 3) + palm).view(-1, 3)
+        _, sign1, n1, _ = sdf(tips, faces_deflate)
+        dist, sign2, n2, _ = sdf(tips, faces)
+        tar_dist, tar_sign, _, _ = sdf(target.reshape(-1, 3), faces)
+        normal = 0.5 * sign1.unsqueeze(1) * n1 + 0.5 * sign2.unsqueeze(1) * n2
+        normal = normal / normal.norm(dim=1).unsqueeze(1)
+        noise = torch.as_tensor(noise_tape[s]).to(F32)
+        reward, margin, fnorm, _ = force_eq_reward(tips.view(E, T, 3), target, comp, mu, normal.view(E, T, 3).detach(),
+                                                   noise, mass=mass, gravity=10.0 if gravity else None, COM=com)
+        c = -reward * 5.0
+        center_cost = (tips.view(E, T, 3).mean(dim=1) - target.mean(dim=1)).norm(dim=1) * 10.0
+        force_cost = -(fnorm * torch.nn.functional.softmin(fnorm, dim=1)).clamp(max=1.0).sum(dim=1)
+        ref_cost = (q - ref).norm(dim=1) * 10.0
+        dist_cost = 1000 * torch.sqrt(dist).view(E, T).sum(dim=1)
+        tar_dist_cost = 10 * (tar_sign.view(E, T) * torch.sqrt(tar_dist).view(E, T)).sum(dim=1)
+        l = c + dist_cost + tar_dist_cost + center_cost + force_cost + ref_cost
+        l.sum().backward()
+        trace.append(l.detach().clone())
+        with torch.no_grad():
+            flag = l < opt_value
+            if flag.any():
+                opt_margin = margin.detach().clone()
+                opt_value[flag] = l[flag]
+                opt_q[flag] = q[flag]
+                opt_target[flag] = target[flag]
+                opt_comp[flag] = comp[flag]
+        optim.step()
+    return torch.stack(trace), opt_q, opt_comp, opt_target, bool((opt_margin > 0.0).all())

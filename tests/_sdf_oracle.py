@@ -41,3 +41,27 @@ def backward(grad, points, clst):
     gp = np.zeros_like(points)
     lib().sdf_oracle_backward(_p(grad), _p(points), _p(clst), C.c_int64(len(points)), _p(gp))
     return gp
+
+
+
+def oracle_sdf(points, faces):
+    """``sdf(points, faces)`` for the oracle loops: the C oracle's forward with the TorchSDF
+    backward 2·g·(p − c) (sdf.py:56-64, .cu:256-270) as a torch autograd function on CPU tensors."""
+    import torch
+
+    class _Fn(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, p, f):
+            d, s, n, c, _ = forward(p.detach().numpy(), f.detach().numpy())
+            ct = torch.from_numpy(c)
+            ctx.save_for_backward(p.detach().clone(), ct)
+            out = torch.from_numpy(d), torch.from_numpy(s), torch.from_numpy(n), ct
+            ctx.mark_non_differentiable(*out[1:])
+            return out
+
+        @staticmethod
+        def backward(ctx, gd, *_):
+            p, c = ctx.saved_tensors
+            return torch.from_numpy(backward(gd.contiguous().numpy(), p.numpy(), c.numpy())), None
+
+    return _Fn.apply(points, faces)

@@ -183,3 +183,59 @@ def test_sharded_gloo_world2_equals_world1(kind):
         assert np.array_equal(np.delete(res[r], 1, axis=1), np.delete(ref, 1, axis=1))
         lo, _ = shard_range(TOTAL, 1, 2)
         assert np.array_equal(res[r][:, 1], (res[r][:, 2] >= lo).astype(float))
+
+
+def _object_inputs(rank):
+    """Rank r's own object (config 3): 11 − r candidates (unequal counts across ranks)."""
+    g = torch.Generator().manual_seed(100 + rank)
+    E = 11 - rank
+    f64 = dict(dtype=torch.float64)
+    return dict(q=torch.rand(E, 16, generator=g, **f64), target=torch.rand(E, 4, 3, generator=g, **f64),
+                comp=torch.rand(E, 4, generator=g, **f64), palm=torch.rand(E, 6, generator=g, **f64))
+
+
+def _per_object_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        x = _object_inputs(rank)
+        opt = _ScriptedOpt(x["palm"])
+        res, rec, bufs = optimize_sharded(opt, None, x["q"], x["target"], x["comp"], 1, object_id=rank, shard=False,
+                                          return_buffers=True)
+        q.put((rank, rec.numpy(), [tuple(b.shape) for b in bufs], overflow(bufs)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_optimize_sharded_one_object_per_rank_gloo_world2():
+    """shard=False (config 3, distributed.py): each rank optimises its own object's candidates — 11
+    and 10 here — and the capacity is agreed over ranks (the larger count), so the all_gather buffers
+    have one shape; every rank receives exactly the concatenation of the two ranks' own world-1
+    records, with nothing lost to overflow."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_per_object_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, rec, shapes, ovf = q.get(timeout=120)
+        res[r] = (rec, shapes, ovf)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = []
+    for r in range(2):
+        x = _object_inputs(r)
+        opt = _ScriptedOpt(x["palm"])
+        out = opt.optimize(x["q"], x["target"], x["comp"], 1, None)
+        buf = pack_survivors(11, r, r, 0, opt.best_loss, out[4], out[0], out[1], out[2], out[3])
+        expect.append(unpack_records([buf]).numpy())
+    full = np.concatenate(expect)
+    assert full.shape[0] >= 2 and set(full[:, 0]) == {0.0, 1.0}
+    for r in range(2):
+        rec, shapes, ovf = res[r]
+        assert shapes == [(12, record_width(16, 4))] * 2
+        assert ovf == [0, 0]
+        assert np.array_equal(rec, full)

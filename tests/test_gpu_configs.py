@@ -156,6 +156,83 @@ def test_config4_full_batch_vs_oracle_slices():
     assert np.array_equal(out["flip"].reshape(3, E)[:, sl].reshape(-1).astype(bool), ref["flip"])
 
 
+def test_config4_sdf_loop_at_size_vs_oracle():
+    """Config 4's TorchSDF leg at its own size: the Kin-mode optimiser (optimize_pregrasp.py:152-227)
+    on iiwa7_allegro with E = 16 384 candidates against the 16 384-face banana — three compute_sdf
+    calls per iteration (:186-188), 3 × 65 536 = 196 608 points — for 3 iterations.
+    (a) every TorchSDF call of the loop, on row slices of its ~65 k points: distance, sign, normal
+        and closest point bit-identical to the C oracle of the kernel (oracle/sdf_oracle.c), and the
+        argmin face identical (compute_sdf_with_faces on the same points);
+    (b) the loop on candidate slices against the oracle's Kin loop (oracle.kin_sdf_loop, pinned to the
+        reference's own run by test_oracle_golden) with the same Kabsch noise: per-iteration
+        per-candidate loss and the best-iterate outputs within 1e-4 (the reference computes this mode
+        in float32; ours takes the force-equilibrium reward in f64)."""
+    import os
+    import compliancedex_amd.optimizers as opts
+    from compliancedex_amd import DifferentiableRobotModel, KinGraspOptimizer, TriangleMesh, compute_sdf_with_faces
+    from compliancedex_amd.urdf import load_robot
+    from oracle.cdx_oracle import kin_sdf_loop
+    from tests import _sdf_oracle
+    from tests.conftest import REPO
+    E, D, iters = 16384, 23, 3
+    links = load_robot("iiwa7_allegro")["config"]["ee_link_name"]
+    offs = [[0.0, -0.04, 0.015]] * 3 + [[0.0, -0.05, -0.015]]
+    center = np.load(os.path.join(REPO, "compliancedex_amd", "data", "banana_center.npy"))
+    tips0 = DifferentiableRobotModel("iiwa7_allegro", device=DEV).compute_forward_kinematics(
+        torch.zeros(1, D, device=DEV), links, offsets=offs)[0].view(4, 3).double().mean(0).cpu().numpy()
+    palm_off = (center - tips0).astype(np.float32)  # the arm base that puts the fingertips around the banana
+    rng = np.random.default_rng(44)
+    q = (0.05 * rng.standard_normal((E, D))).astype(np.float32)
+    target = (np.tile(center, (E, 4, 1)) + 0.01 * rng.standard_normal((E, 4, 3))).astype(np.float32)
+    comp = np.tile(np.array([10.0, 10.0, 10.0, 20.0], np.float32), (E, 1))
+    noise = rng.random((iters, E, 3, 3)).astype(np.float32)
+    mesh_path = os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_mesh.npz")
+    calls = []
+    real = opts.compute_sdf
+
+    def spy(points, faces):
+        out = real(points, faces)
+        calls.append((points.detach().clone(), faces, [t.detach().clone() for t in out]))
+        return out
+
+    kin = KinGraspOptimizer("iiwa7_allegro", links, offs, palm_offset=palm_off.tolist(), num_iters=iters,
+                            optimize_target=True, ref_q=[0.0] * D)
+    opts.compute_sdf = spy
+    try:
+        res = kin.optimize(torch.from_numpy(q).to(DEV), torch.from_numpy(target).to(DEV),
+                           torch.from_numpy(comp).to(DEV), 1, TriangleMesh.from_npz(mesh_path), verbose=False,
+                           kabsch_noise=[torch.from_numpy(n).to(DEV) for n in noise], trace_rows=True)
+    finally:
+        opts.compute_sdf = real
+    torch.cuda.synchronize()
+    assert len(calls) == 3 * iters and all(c[0].shape == (4 * E, 3) for c in calls)
+    assert calls[0][1].shape[0] == 16384
+    # (a) each call: 1500 random rows + the first / last 8, bitwise against the C oracle
+    for pts, faces, (d, sg, nr, cl) in calls:
+        P = pts.shape[0]
+        rows = np.unique(np.concatenate([rng.choice(P, 1500, replace=False), np.arange(8), np.arange(P - 8, P)]))
+        p_np = pts[rows].cpu().numpy()
+        f_np = faces.cpu().numpy()
+        o = _sdf_oracle.forward(p_np, f_np)
+        face = compute_sdf_with_faces(pts[rows].contiguous(), faces)[4].cpu().numpy()
+        assert np.array_equal(sg[rows].cpu().numpy(), o[1]) and np.array_equal(face, o[4])
+        for a, b in zip((d[rows], nr[rows], cl[rows]), (o[0], o[2], o[3])):
+            assert np.array_equal(a.cpu().numpy().view(np.uint32), b.view(np.uint32))
+    # (b) candidate slices through the oracle loop
+    sl = np.unique(np.concatenate([np.arange(8), rng.choice(E, 16, replace=False), np.arange(E - 8, E)]))
+    chain, _ = oracle_chain("iiwa7_allegro")
+    mesh = TriangleMesh.from_npz(mesh_path)
+    faces = opts._face_vertices(mesh, "cpu")
+    faces_def = opts._face_vertices(mesh.scale(0.9, center=[0, 0, 0]), "cpu")
+    loss, oq, oc, ot, _ = kin_sdf_loop(chain, links, offs, palm_off, [0.0] * D, q[sl], target[sl], comp[sl], 1, faces,
+                                       faces_def, _sdf_oracle.oracle_sdf, noise[:, sl], iters)
+    got = torch.stack(kin.loss_rows).cpu().numpy()[:, sl]
+    assert np.isfinite(got).all()
+    assert rel_err(got, loss.double().numpy()) < 1e-4, (got, loss)
+    for x, y in zip(res[:3], (oq, oc, ot)):
+        assert rel_err(x.detach().cpu().double().numpy()[sl], y.double().numpy()) < 1e-4
+
+
 # ------------------------------------------------------------------------------ config 3
 CONFIG3 = ["banana", "mug", "mug2", "hammer", "lego", "coffeebottle", "box", "dummy"]
 

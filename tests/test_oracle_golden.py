@@ -114,3 +114,31 @@ def test_reference_results_are_allegro_fk(exp):
     prob = oracle_problem("allegro", "banana")
     out = prob.forward_kinematics(torch.from_numpy(d["joint_angle"]), torch.from_numpy(d["wrist"]))
     assert rel_err(out.detach(), d["contact"]) < 1e-6
+
+
+def test_kin_sdf_loop_oracle_vs_reference_run():
+    """The oracle's Kin-mode loop (oracle.kin_sdf_loop: FK → 3 TorchSDF calls through the C oracle →
+    force_eq_reward → costs → Adam, float32) against the reference's own KinGraspOptimizer run
+    (golden mode_kin: 12 iterations, E = 1, replayed Kabsch noise; its TorchSDF was the same C
+    oracle, the reference's _C being absent).  This pins the oracle the config-4 GPU test compares
+    the full-size SDF loop with."""
+    import os
+    from compliancedex_amd.optimizers import TriangleMesh, _face_vertices
+    from oracle.cdx_oracle import kin_sdf_loop
+    from tests._sdf_oracle import oracle_sdf
+    from tests.conftest import REPO
+    d = golden("mode_kin.npz")
+    chain, robot = oracle_chain("allegro")
+    cfg = robot["config"]
+    mesh = TriangleMesh.from_npz(os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_mesh.npz"))
+    faces = _face_vertices(mesh, "cpu")
+    faces_def = _face_vertices(mesh.scale(0.9, center=[0, 0, 0]), "cpu")
+    loss, oq, oc, ot, flag = kin_sdf_loop(chain, cfg["ee_link_name"], cfg["ee_link_offset"], d["palm3"], cfg["ref_q"],
+                                          d["q"], d["target"], d["comp"], 1, faces, faces_def, oracle_sdf,
+                                          d["noise"], int(d["iters"]))
+    trace = loss.sum(dim=1).double().numpy()
+    assert np.abs(trace - d["loss_trace"]).max() <= 1e-5 * np.abs(d["loss_trace"]).max(), (trace, d["loss_trace"])
+    # float32 end to end (as the reference): 12 Adam steps of f32 FK / Kabsch rounding → measured 1.9e-5
+    for i, x in enumerate((oq, oc, ot)):
+        assert rel_err(x.double(), d[f"out{i}"]) < 1e-4, i
+    assert flag == bool(d["flag"])

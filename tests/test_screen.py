@@ -197,3 +197,169 @@ def test_screened_closure_deterministic(banana2000):
     b, _ = _closure(opt, banana2000, inputs)
     for k in OUTS:
         assert np.array_equal(a[k], b[k], equal_nan=True), k
+
+
+def _report(opt, gpis, E):
+    r = opt.screen_report(gpis, E)
+    assert r is not None
+    return r
+
+
+def test_screen_report_audits_discarded_rows(banana2000):
+    """Every screened closure verifies itself (cdx_closure_screen_report): the exact pass also runs an
+    audit sample of the rows the screen discards (≈ CDX_SCREEN_AUDIT = 64 expected), and every kept and
+    audited estimate is checked against its margin Δ_f.  On the bench workload: no miss, no audited
+    row that turned out to be its group's maximum, no fault, and the worst estimate error a small
+    fraction of its margin; the cumulative block counts the closures."""
+    from compliancedex_amd.workloads import prob_inputs
+    cfg, opt = _opt()
+    inputs = prob_inputs(cfg["ref_q"], 4096, seed=1000, spread=True)
+    _closure(opt, banana2000, inputs)
+    r = _report(opt, banana2000, 4096)
+    assert r["screened"] == 1 and r["screened_rows"] == 4 * 4096
+    assert 16 <= r["audited_rows"] <= 200, r
+    assert r["exact_rows"] >= 4096 + r["audited_rows"]
+    assert r["bound_misses"] == r["audit_misses"] == r["audit_flips"] == r["faults"] == 0, r
+    assert 0 < r["max_ratio"] < 0.5 and 0 < r["max_ratio_audit"] < 0.5, r
+    n0 = r["cum_closures"]
+    _closure(opt, banana2000, inputs)
+    r2 = _report(opt, banana2000, 4096)
+    assert r2["cum_closures"] == n0 + 1
+    assert r2["cum_audited_rows"] >= r["audited_rows"] + r2["audited_rows"] or n0 == 0
+    # reset zeroes the cumulative block only
+    from compliancedex_amd import _native as N
+    p = opt.problem(banana2000, 1)
+    N.check(N.load().cdx_closure_screen_reset(p, 4096, N.ptr(opt._last_ws), N.stream_ptr(opt._last_ws.device)), "reset")
+    r3 = _report(opt, banana2000, 4096)
+    assert r3["cum_closures"] == 0 and r3["cum_audited_rows"] == 0 and r3["audited_rows"] == r2["audited_rows"]
+
+
+def test_screened_closure_adversarial_far_queries(banana2000):
+    """The regime the margin's row scale max(1, ‖Ṽ‖²/k0) has to cover: palms pushed 5 cm … 3.5R away
+    along random directions (log-uniform), so the fingertip queries spread from the surface to beyond
+    the screen's safe radius (NaN estimates → whole group exact).  Screened = unscreened to TOL_EQ;
+    no margin miss, audit miss or fault; some far groups really were screened."""
+    from compliancedex_amd.workloads import prob_inputs
+    cfg, opt = _opt()
+    E = 4096
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=4242, spread=True)
+    rng = np.random.default_rng(4242)
+    R = float(banana2000.R)
+    d = np.exp(rng.uniform(np.log(0.05), np.log(3.5 * R), E))
+    u = rng.standard_normal((E, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    palm = palm.copy()
+    palm[:, :3] += d[:, None] * u
+    a, st = _closure(opt, banana2000, (q, comp, target, palm), screen=True)
+    r = _report(opt, banana2000, E)
+    b, _ = _closure(opt, banana2000, (q, comp, target, palm), screen=False)
+    assert r["bound_misses"] == r["audit_misses"] == r["audit_flips"] == r["faults"] == 0, r
+    # far groups are screened too: fewer exact rows than "every group beyond 5 cm runs all four"
+    assert E <= r["exact_rows"] < 3 * E, r
+    assert np.array_equal(a["flip"], b["flip"])
+    for k in OUTS:
+        assert rel_err(a[k], b[k]) <= TOL_EQ, (k, rel_err(a[k], b[k]))
+
+
+def test_optimize_trajectory_screened_equals_unscreened_every_step(banana2000):
+    """A 200-iteration config-2 optimise loop (fused Adam, best iterate, clamps) screened and
+    unscreened from the same start with the same device noise keys: the per-step total loss and the
+    joint / target / palm gradients agree to TOL_EQ at EVERY step, and the loop's cumulative screen
+    record has no miss or fault (so no fallback re-run happened)."""
+    from compliancedex_amd.workloads import prob_inputs
+    cfg, opt = _opt()
+    opt.num_iters = 200
+    E = 4096
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=77, spread=True)
+    opt.palm_offset = torch.from_numpy(palm).to(DEV)
+    args = [torch.from_numpy(np.ascontiguousarray(x)).to(DEV) for x in (q, target, comp)]
+
+    def run(screen):
+        trace = []
+        p = opt.problem(banana2000, 1)
+        delta = p.gpis.screen_delta
+        if not screen:
+            p.gpis.screen_delta = 0.0
+        opt._seed = 123  # same noise keys for both runs
+        try:
+            res = opt.optimize(*args, 1, banana2000, verbose=False,
+                               step_hook=lambda s, out: trace.append(torch.cat([
+                                   out["total_loss"].unsqueeze(1), out["g_q"], out["g_target"].reshape(E, -1),
+                                   out["g_palm_pos"], out["g_palm_ori"]], 1).clone()))
+        finally:
+            p.gpis.screen_delta = delta
+        return torch.stack(trace).cpu().numpy(), [r.cpu().numpy() for r in res]
+
+    fallbacks = opt.screen_fallbacks
+    ta, ra = run(True)
+    rep = opt.last_screen_report
+    tb, rb = run(False)
+    assert opt.screen_fallbacks == fallbacks
+    assert rep["cum_closures"] == 200 and rep["cum_bound_misses"] == rep["cum_faults"] == 0, rep
+    assert rep["cum_audit_misses"] == rep["cum_audit_flips"] == 0 and rep["cum_audited_rows"] > 200 * 16, rep
+    assert ta.shape == (200, E, 1 + 16 + 12 + 6)
+    for s in range(200):
+        for c0, c1 in ((0, 1), (1, 17), (17, 29), (29, 35)):
+            assert rel_err(ta[s][:, c0:c1], tb[s][:, c0:c1]) <= TOL_EQ, (s, c0, rel_err(ta[s][:, c0:c1], tb[s][:, c0:c1]))
+    for x, y in zip(ra, rb):
+        assert rel_err(x, y) <= TOL_EQ
+
+
+def test_screened_graph_replay_matches_eager(banana2000):
+    """hipGraph capture of the screened closure (E = 1024: 4096 all-tip rows, the screen's threshold):
+    the captured fork/join of the side-stream GPIS mean, the device-side refine row count and the
+    audit replay bit-identically to the eager loop; screen_report reads the graph's own workspace."""
+    from compliancedex_amd.workloads import prob_inputs
+    cfg, opt = _opt()
+    opt.num_iters = 12
+    E = 1024
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=31, spread=True)
+    opt.palm_offset = torch.from_numpy(palm).to(DEV)
+    args = [torch.from_numpy(np.ascontiguousarray(x)).to(DEV) for x in (q, target, comp)]
+    opt._seed = 9
+    eager = [r.cpu().numpy() for r in opt.optimize(*args, 1, banana2000, verbose=False)]
+    rep_e = opt.last_screen_report
+    opt._seed = 9
+    graph = [r.cpu().numpy() for r in opt.optimize(*args, 1, banana2000, verbose=False, graph=True)]
+    rep_g = opt.last_screen_report
+    opt._seed = 9
+    replay = [r.cpu().numpy() for r in opt.optimize(*args, 1, banana2000, verbose=False, graph=True)]
+    assert rep_e is not None and rep_g is not None
+    assert rep_g["cum_closures"] == 12 and rep_g["exact_rows"] == rep_e["exact_rows"], (rep_e, rep_g)
+    for x, y, z in zip(eager, graph, replay):
+        assert np.array_equal(x, y, equal_nan=True) and np.array_equal(x, z, equal_nan=True)
+
+
+_FIRST_CAPTURE = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {repo!r})
+from compliancedex_amd import ProbabilisticGraspOptimizer
+from compliancedex_amd.urdf import load_robot
+from compliancedex_amd.workloads import prob_inputs, stored_gpis
+cfg = load_robot("allegro")["config"]
+g = stored_gpis("banana", "cuda")
+q, comp, target, palm = prob_inputs(cfg["ref_q"], 1024, seed=3, spread=True)
+res = []
+for graph in (True, False):  # the capture is this process's FIRST screened closure
+    opt = ProbabilisticGraspOptimizer("allegro", cfg["ee_link_name"], cfg["ee_link_offset"], palm_offset=palm,
+                                      ref_q=cfg["ref_q"], optimize_target=True, optimize_palm=True, device="cuda",
+                                      num_iters=6, seed=5)
+    a = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (q, target, comp)]
+    res.append([r.cpu().numpy() for r in opt.optimize(*a, 1, g, verbose=False, graph=graph)])
+    assert opt.last_screen_report is not None and opt.last_screen_report["cum_faults"] == 0
+for x, y in zip(*res):
+    assert np.array_equal(x, y, equal_nan=True)
+print("first-capture ok")
+"""
+
+
+def test_screened_graph_first_capture_creates_side_stream():
+    """The per-device side stream is created lazily by the first screened closure — here inside a
+    hipGraph capture, in a fresh process (one child, bounded by a timeout): the capture and replay
+    still equal the eager loop bit for bit."""
+    import subprocess
+    import sys
+    from tests.conftest import REPO
+    r = subprocess.run([sys.executable, "-c", _FIRST_CAPTURE.format(repo=REPO)], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "first-capture ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])

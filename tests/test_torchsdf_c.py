@@ -71,3 +71,52 @@ def test_shim_rejects_double_and_noncontiguous():
     with pytest.raises(RuntimeError, match="contiguous"):
         _C.unbatched_triangle_distance_forward_cuda(torch.zeros(3, 4, device="cuda").t(), faces.float(),
                                                     *(o.float() if o.dtype == torch.float64 else o for o in outs))
+
+
+@pytest.mark.gpu
+def test_shim_checks_sizes_before_any_launch():
+    """CHECK_SIZES (unbatched_triangle_distance.cpp:60-67, :90-94): an undersized or mis-shaped
+    output, points that are not [P, 3] or faces that are not [F, 3, 3] raise a RuntimeError and no
+    kernel runs — the caller's buffers keep their sentinel (the unchecked version wrote past them)."""
+    import compliancedex_amd.torchsdf_c as _C
+    dev = "cuda"
+    P, F = 64, 8
+    pts = torch.rand(P, 3, device=dev)
+    faces = torch.rand(F, 3, 3, device=dev)
+
+    def outs():
+        return [torch.full((P,), 7.0, device=dev), torch.full((P,), 7, device=dev, dtype=torch.int32),
+                torch.full((P, 3), 7.0, device=dev), torch.full((P, 3), 7.0, device=dev)]
+
+    bad_fwd = [
+        ("dist", lambda o: o.__setitem__(0, torch.full((P - 1,), 7.0, device=dev))),
+        ("dist_sign", lambda o: o.__setitem__(1, torch.full((P // 2,), 7, device=dev, dtype=torch.int32))),
+        ("normals", lambda o: o.__setitem__(2, torch.full((P, 2), 7.0, device=dev))),
+        ("clst_points", lambda o: o.__setitem__(3, torch.full((P * 3,), 7.0, device=dev))),
+    ]
+    for arg, mutate in bad_fwd:
+        o = outs()
+        mutate(o)
+        with pytest.raises(RuntimeError, match=f"{arg} must of size"):
+            _C.unbatched_triangle_distance_forward_cuda(pts, faces, *o)
+        torch.cuda.synchronize()
+        assert all(bool((t == 7).all()) for t in o), arg
+    with pytest.raises(RuntimeError, match="points must of size"):
+        _C.unbatched_triangle_distance_forward_cuda(torch.rand(P, 4, device=dev), faces, *outs())
+    with pytest.raises(RuntimeError, match="face_vertices must of size"):
+        _C.unbatched_triangle_distance_forward_cuda(pts, torch.rand(F, 9, device=dev), *outs())
+    g = torch.ones(P, device=dev)
+    for args, arg in (((torch.ones(P - 3, device=dev), pts, outs()[3], outs()[2]), "grad_dist"),
+                      ((g, pts, torch.full((P - 1, 3), 7.0, device=dev), outs()[2]), "clst_points"),
+                      ((g, pts, outs()[3], torch.full((P, 1), 7.0, device=dev)), "grad_points")):
+        with pytest.raises(RuntimeError, match=f"{arg} must of size"):
+            _C.unbatched_triangle_distance_backward_cuda(*args)
+        torch.cuda.synchronize()
+        assert bool((args[3] == 7).all())
+    # well-formed calls still run
+    o = outs()
+    _C.unbatched_triangle_distance_forward_cuda(pts, faces, *o)
+    gp = torch.zeros(P, 3, device=dev)
+    _C.unbatched_triangle_distance_backward_cuda(g, pts, o[3], gp)
+    torch.cuda.synchronize()
+    assert bool((o[1].abs() == 1).all()) and torch.isfinite(gp).all()

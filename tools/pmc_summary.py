@@ -80,6 +80,26 @@ def main():
             summary["gpis_screen_bytes_per_launch"] = (2 * f + w) * 1024
     json.dump(summary, open(os.path.join(REPO, "profiles", f"{tag}_pmc.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
+    write_traffic(summary)
+
+
+TRAFFIC_KEYS = ("gpis_screen_bytes_per_launch", "gpis_refine_bytes_per_launch", "gpis_grad_bytes_per_launch",
+                "gpis_var_bytes_per_launch")
+
+
+def write_traffic(summary):
+    """profiles/pmc_traffic.json: the roofline kernels' HBM bytes per launch of the newest PMC run —
+    the one file of profiles/ that travels to the GPU box (.gpurunignore), where bench.py puts it in
+    the roofline's ``traffic`` (PMC counters cannot be read inside the timed run itself)."""
+    t = {"source": f"profiles/{summary['tag']}_pmc.json", "E": summary["E"], "n_inducing": summary["n_inducing"],
+         "unit": summary["unit"], "correction": summary["correction"]}
+    t.update({k: summary[k] for k in TRAFFIC_KEYS if k in summary})
+    json.dump(t, open(os.path.join(REPO, "profiles", "pmc_traffic.json"), "w"), indent=1)
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[1] == "--traffic-from":
+    write_traffic(json.load(open(sys.argv[2])))
+    sys.exit(0)
 
 
 if __name__ == "__main__":
