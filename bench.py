@@ -262,8 +262,9 @@ def main():
                          "backend": (args.backend if world > 1 else None), "ms": gather_s * 1e3,
                          "bytes_per_rank": int(buf.numel() * 8), "records_gathered": n_records,
                          "overflow": D.overflow(bufs),
-                         "note": "pack (nonzero + gather of surviving rows) + all_gather + unpack, inside the timed "
-                                 "region after the last step"},
+                         "note": "pack (one cdx_pack_survivors launch: device compaction, header counts on "
+                                 "device) + all_gather + unpack (the one host read of the headers), inside the "
+                                 "timed region after the last step"},
             "stage_ms": stage_ms,
             "stage_ms_note": "gpis_screen / gpis_std_var (the refine kernel) / gpis_std_grad: HIP events over "
                               "the timed steps; the other stages from a 10-step all-stage pass after the timed "

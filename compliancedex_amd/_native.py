@@ -15,6 +15,7 @@ LIB_DIR = os.path.join(_HERE, "lib")
 MAX_BODIES, MAX_TIPS, MAX_DOFS, MAX_LEVELS = 32, 8, 32, 4
 KERNELS = {"tps": 0, "rbf": 1, "joint": 2}
 NPAD_ALIGN = 256  # CDX_NPAD_ALIGN
+SCREEN_BANDS = 24  # CDX_SCREEN_BANDS
 PROF_STAGES = 6   # cdx_profile_read array length
 ERRORS = {-1: "invalid argument", -2: "unsupported GPIS kernel", -3: "chain exceeds descriptor capacity",
           -10: "HIP launch failed"}
@@ -96,6 +97,7 @@ _SIGS = {
     "cdx_gpis_std": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P, _P]),
     "cdx_gpis_screen_bytes": (C.c_size_t, [C.c_int32]),
     "cdx_gpis_screen_prepare": (C.c_int, [C.POINTER(CdxGpis), _P, _P]),
+    "cdx_gpis_screen_set_bands": (C.c_int, [C.POINTER(CdxGpis), C.POINTER(C.c_double), _P]),
     "cdx_gpis_screen_workspace": (C.c_size_t, [C.POINTER(CdxGpis), _I64]),
     "cdx_gpis_screen_var": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P]),
     "cdx_gpis_fit": (C.c_int, [_P, C.c_int32, _P, C.c_int32, C.c_double, _P, _P, _P]),

@@ -818,10 +818,12 @@ int cdx_closure_screen_report(const cdx_problem* p, int64_t E, const void* works
 }
 
 int cdx_closure_screen_reset(const cdx_problem* p, int64_t E, void* workspace, cdx_stream_t stream) {
-  if (!problem_ok(p) || E <= 0 || !workspace) return CDX_EINVAL;
-  if (!screen_on(p, E)) return CDX_OK;
+  if (!problem_ok(p) || E < 0) return CDX_EINVAL;
+  if (E == 0 || !screen_on(p, E)) return CDX_OK;
+  if (!workspace) return CDX_EINVAL;
   ClosureWs w = closure_ws_layout(p, E, static_cast<char*>(workspace));
-  return hipMemsetAsync(w.stats, 0, cdx::SS_WORDS * sizeof(int), reinterpret_cast<hipStream_t>(stream)) == hipSuccess
+  return hipMemsetAsync(w.stats + cdx::SS_CUM, 0, (cdx::SS_WORDS - cdx::SS_CUM) * sizeof(int),
+                        reinterpret_cast<hipStream_t>(stream)) == hipSuccess
              ? CDX_OK : CDX_ELAUNCH;
 }
 

@@ -13,6 +13,7 @@ form k0 − ‖L⁻¹k‖² (the reference builds the M×M matrix, gpis.py:57-58
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import numpy as np
@@ -67,15 +68,19 @@ class _State:
         self.desc.screen_delta = 0.0
         self.ws = None
         self.screen_ws = None
-        self.screen_err = self._calibrate_screen(X1[:n].to(torch.float64), R, kernel)
-        # the closure keeps every fingertip whose estimate is within 2Δ of its group's leader
+        self.screen_err, bands = self._calibrate_screen(X1[:n].to(torch.float64), R, kernel)
+        # the closure keeps every fingertip whose estimate is within 2Δ_f of its group's leader
         k0 = {"tps": float(R) ** 3, "rbf": 1.0, "joint": 0.3 + 0.7 * float(R) ** 3}[kernel]
         ok = SCREEN_MARGIN > 0 and np.isfinite(self.screen_err)
         self.desc.screen_delta = max(SCREEN_MARGIN * self.screen_err, 2.0 ** -40 * k0) if ok else 0.0
+        if ok:
+            self.screen_bands = bands
+            w = (ctypes.c_double * N.SCREEN_BANDS)(*bands)
+            N.check(lib.cdx_gpis_screen_set_bands(self.desc, w, N.stream_ptr(dev)), "cdx_gpis_screen_set_bands")
 
     def _calibrate_screen(self, X1, R, kernel):
-        """max |estimate − exact| of k0 − ‖L⁻¹k‖² over calibration queries around this state, in
-        units of the row scale max(1, ‖Ṽ‖²/k0) the closure's margin uses: the inducing points
+        """(max |estimate − exact| of k0 − ‖L⁻¹k‖², per-band weights) over calibration queries around
+        this state, in units of the row scale max(1, ‖Ṽ‖²/k0) the closure's margin uses: the inducing points
         displaced by 0–3 cm and uniform points in their bounding box ± 5 cm (the near set: mostly
         finite estimates, else the state is not screened), plus the far set — inducing points pushed
         5 cm … 3.5R along random directions, log-uniform, i.e. the screen's whole finite range,
@@ -105,12 +110,25 @@ class _State:
         # group exactly), so the bound is over finite estimates; mostly NaN near the object: no screening
         ok = torch.isfinite(est)
         if int(ok[:Xn.shape[0]].sum()) < Xn.shape[0] // 2:
-            return float("nan")
+            return float("nan"), None
         k0 = {"tps": float(R) ** 3, "rbf": 1.0, "joint": 0.3 + 0.7 * float(R) ** 3}[kernel]
         scale = ((k0 - est[ok]) / k0).clamp(min=1.0) if k0 > 0 else torch.ones_like(est[ok])
         err = (est[ok] - exact[ok]).abs() / scale
         self.calib_far_finite = int(ok[Xn.shape[0]:].sum())
-        return float(err.max())
+        gmax = float(err.max())
+        # per-band envelope (cdx_screen.h screen_margin): band b = ⌊log₂ scale⌋; a band's weight is the
+        # largest error of its own and every lower band, relative to the global maximum — bands above
+        # the highest calibrated one keep the global maximum (weight 1)
+        band = torch.clamp(torch.floor(torch.log2(scale)), 0, N.SCREEN_BANDS - 1).to(torch.int64)
+        per = torch.zeros(N.SCREEN_BANDS, dtype=torch.float64, device=dev).scatter_reduce(0, band, err, "amax")
+        per = per.cpu().numpy()
+        top = int(band.max())
+        env = np.maximum.accumulate(per)
+        w = np.ones(N.SCREEN_BANDS)
+        if gmax > 0:
+            w[:top + 1] = np.maximum(env[:top + 1] / gmax, 2.0 ** -20)
+        self.calib_band_err = per
+        return gmax, [float(x) for x in w]
 
     def screen_var(self, X):
         """Split-precision estimate of k0 − ‖L⁻¹k‖² at X [M, 3] (cdx_gpis_screen_var)."""

@@ -263,8 +263,8 @@ class ProbabilisticGraspOptimizer:
         per-iteration Kabsch noise tensors (parity replay).  ``init_palm`` [E, 6]: start from these
         palm poses instead of ``palm_offset`` (the annealing outer loop's proposals).  ``graph=True``
         (fused only): capture the whole loop once per (E, problem) as a hipGraph and replay it.
-        ``step_hook(s, out)`` (fused, eager only): called after closure s with its output buffers
-        (tests: per-step traces)."""
+        ``step_hook(s, out, state)`` (fused, eager only): called after closure s with its output
+        buffers and the parameter buffers / Kabsch noise it ran on (tests: per-step checks)."""
         if init_palm is not None:
             saved = self.palm_offset
             self.palm_offset = init_palm.detach().to(torch.float64)
@@ -449,7 +449,8 @@ class ProbabilisticGraspOptimizer:
                     self._closure_into(p, c["q"], c["comp"], c["target"], c["pp"], c["po"], noise, out, seed=0,
                                        ws=c.get("ws"))
                     if step_hook is not None:
-                        step_hook(s, out)
+                        step_hook(s, out, dict(q=c["q"], comp=c["comp"], target=c["target"], pp=c["pp"],
+                                               po=c["po"], noise=noise))
                     N.check(lib.cdx_optimizer_step(cfg, bufs, E, D, T, s, stream), "cdx_optimizer_step")
             finally:
                 p.loop = None

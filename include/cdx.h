@@ -118,6 +118,11 @@ int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pa
  *   cdx_gpis_screen_workspace bytes. */
 size_t cdx_gpis_screen_bytes(int32_t N_pad);
 int cdx_gpis_screen_prepare(const cdx_gpis* g, void* screen, cdx_stream_t stream);
+/* Closure margin of a screened row: screen_delta · w[b] · max(1, ‖Ṽ‖²/k0), b = ⌊log₂ max(1, ‖Ṽ‖²/k0)⌋
+ * (last band for larger); w[CDX_SCREEN_BANDS] (host array, each in (0, 1]) are the calibrated error
+ * envelope per band relative to the largest; cdx_gpis_screen_prepare sets them all to 1. */
+#define CDX_SCREEN_BANDS 24
+int cdx_gpis_screen_set_bands(const cdx_gpis* g, const double* w, cdx_stream_t stream);
 size_t cdx_gpis_screen_workspace(const cdx_gpis* g, int64_t M);
 int cdx_gpis_screen_var(const cdx_gpis* g, const double* X, int64_t M, double* var, void* workspace,
                         cdx_stream_t stream);

@@ -262,10 +262,13 @@ def test_screened_closure_adversarial_far_queries(banana2000):
 
 
 def test_optimize_trajectory_screened_equals_unscreened_every_step(banana2000):
-    """A 200-iteration config-2 optimise loop (fused Adam, best iterate, clamps) screened and
-    unscreened from the same start with the same device noise keys: the per-step total loss and the
-    joint / target / palm gradients agree to TOL_EQ at EVERY step, and the loop's cumulative screen
-    record has no miss or fault (so no fallback re-run happened)."""
+    """A 200-iteration config-2 optimise loop (fused Adam, best iterate, clamps), screened: at EVERY
+    step the closure's loss, margins and five gradients equal the unscreened fp64 closure's on the
+    same parameters and Kabsch noise to TOL_EQ, and the loop's cumulative screen record shows no
+    miss, fault or audit flip (so no fallback re-run).
+    (Two separately run trajectories are not compared: the screened and unscreened exact passes sum
+    V in different K-splits — 1e-16 relative — and 200 Adam steps amplify that to 1e-9 by step 26.)"""
+    from compliancedex_amd import ProbabilisticGraspOptimizer
     from compliancedex_amd.workloads import prob_inputs
     cfg, opt = _opt()
     opt.num_iters = 200
@@ -273,36 +276,40 @@ def test_optimize_trajectory_screened_equals_unscreened_every_step(banana2000):
     q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=77, spread=True)
     opt.palm_offset = torch.from_numpy(palm).to(DEV)
     args = [torch.from_numpy(np.ascontiguousarray(x)).to(DEV) for x in (q, target, comp)]
+    ref = ProbabilisticGraspOptimizer("allegro", cfg["ee_link_name"], cfg["ee_link_offset"], ref_q=cfg["ref_q"],
+                                      optimize_target=True, optimize_palm=True, device=DEV)
+    p_ref = ref.problem(banana2000, 1)
+    assert p_ref.gpis.screen_delta > 0
+    p_ref.gpis.screen_delta = 0.0  # this optimiser's own descriptor copy: the full fp64 pass
 
-    def run(screen):
-        trace = []
-        p = opt.problem(banana2000, 1)
-        delta = p.gpis.screen_delta
-        if not screen:
-            p.gpis.screen_delta = 0.0
-        opt._seed = 123  # same noise keys for both runs
-        try:
-            res = opt.optimize(*args, 1, banana2000, verbose=False,
-                               step_hook=lambda s, out: trace.append(torch.cat([
-                                   out["total_loss"].unsqueeze(1), out["g_q"], out["g_target"].reshape(E, -1),
-                                   out["g_palm_pos"], out["g_palm_ori"]], 1).clone()))
-        finally:
-            p.gpis.screen_delta = delta
-        return torch.stack(trace).cpu().numpy(), [r.cpu().numpy() for r in res]
+    class Tape:  # per-step Kabsch noise, drawn on the device from a seeded generator
+        def __init__(self):
+            self.g = torch.Generator(device=DEV).manual_seed(2024)
 
-    fallbacks = opt.screen_fallbacks
-    ta, ra = run(True)
+        def __getitem__(self, s):
+            return torch.rand(3 * E, 3, 3, generator=self.g, device=DEV, dtype=torch.float64)
+
+    keys = ("total_loss", "total_margin", "g_q", "g_comp", "g_target", "g_palm_pos", "g_palm_ori")
+    worst = torch.zeros(len(keys), dtype=torch.float64, device=DEV)
+    steps = []
+
+    def hook(s, out, st):
+        o2 = ref._outputs(E, 4, 16, 3, torch.device(DEV))
+        ref._closure_into(p_ref, st["q"], st["comp"], st["target"], st["pp"], st["po"], st["noise"], o2, seed=0)
+        for i, k in enumerate(keys):
+            a, b = out[k], o2[k]
+            e = (a - b).abs().max() / b.abs().max().clamp(min=1e-300)
+            worst[i] = torch.maximum(worst[i], torch.nan_to_num(e, nan=1.0))
+            assert torch.equal(torch.isnan(a), torch.isnan(b))
+        steps.append(s)
+
+    opt.optimize(*args, 1, banana2000, verbose=False, noise_tape=Tape(), step_hook=hook)
     rep = opt.last_screen_report
-    tb, rb = run(False)
-    assert opt.screen_fallbacks == fallbacks
+    assert steps == list(range(200)) and opt.screen_fallbacks == 0
     assert rep["cum_closures"] == 200 and rep["cum_bound_misses"] == rep["cum_faults"] == 0, rep
     assert rep["cum_audit_misses"] == rep["cum_audit_flips"] == 0 and rep["cum_audited_rows"] > 200 * 16, rep
-    assert ta.shape == (200, E, 1 + 16 + 12 + 6)
-    for s in range(200):
-        for c0, c1 in ((0, 1), (1, 17), (17, 29), (29, 35)):
-            assert rel_err(ta[s][:, c0:c1], tb[s][:, c0:c1]) <= TOL_EQ, (s, c0, rel_err(ta[s][:, c0:c1], tb[s][:, c0:c1]))
-    for x, y in zip(ra, rb):
-        assert rel_err(x, y) <= TOL_EQ
+    w = worst.cpu().numpy()
+    assert (w <= TOL_EQ).all(), dict(zip(keys, w))
 
 
 def test_screened_graph_replay_matches_eager(banana2000):
