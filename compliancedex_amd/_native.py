@@ -98,6 +98,7 @@ _SIGS = {
     "cdx_gpis_screen_bytes": (C.c_size_t, [C.c_int32]),
     "cdx_gpis_screen_prepare": (C.c_int, [C.POINTER(CdxGpis), _P, _P]),
     "cdx_gpis_screen_set_bands": (C.c_int, [C.POINTER(CdxGpis), C.POINTER(C.c_double), _P]),
+    "cdx_gpis_screen_info": (C.c_int, [C.POINTER(CdxGpis), C.POINTER(C.c_double), _P]),
     "cdx_gpis_screen_workspace": (C.c_size_t, [C.POINTER(CdxGpis), _I64]),
     "cdx_gpis_screen_var": (C.c_int, [C.POINTER(CdxGpis), _P, _I64, _P, _P, _P]),
     "cdx_gpis_fit": (C.c_int, [_P, C.c_int32, _P, C.c_int32, C.c_double, _P, _P, _P]),
@@ -120,6 +121,8 @@ _SIGS = {
                                      _I64, _I64, _P, _P]),
     "cdx_sdf_forward": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "cdx_sdf_backward": (C.c_int, [_P, _P, _P, _I64, _P, _P]),
+    "cdx_sdf_forward_f64": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
+    "cdx_sdf_backward_f64": (C.c_int, [_P, _P, _P, _I64, _P, _P]),
     "cdx_version": (C.c_char_p, []),
     "cdx_abi_sizes": (None, [C.POINTER(C.c_size_t)]),
     "cdx_selftest_mfma_f64": (C.c_int, [_P, _P, _P, _P]),

@@ -21,23 +21,25 @@ __device__ __host__ inline int screen_shift(int N, int Np) { return std::min((Np
 __device__ __host__ inline size_t screen_align(size_t b) { return (b + 255) / 256 * 256; }
 
 // [L: N_pad/16 × 2 slices × 2 k-halves × N_pad columns × 8 f16][csum: N_pad f64][cscale: N_pad f64]
-// [X1f: N_pad float4][centre: cx, cy, cz, SA (A-operand scale), rq² (largest safe |x − centre|²), 0, 0, 0,
-//  band weights w[CDX_SCREEN_BANDS] (below)]
+// [X1f: N_pad float4][centre: cx, cy, cz, SA (A-operand scale), rq² (largest safe |x − centre|²),
+//  4/ρ (ρ = max_n |x_n − centre|; 0 when ρ = 0), 0, 0, band weights w[CDX_SCREEN_BANDS] (below)]
 inline size_t screen_bytes(int Np) {
   return screen_align((size_t)Np * Np * 4) + 2 * screen_align((size_t)Np * 8) + screen_align((size_t)Np * 16) + 256;
 }
 
-// Margin of a screened row: Δ_f = screen_delta · w[b] · scale, scale = max(1, (k0 − s̃²)/k0) (the
-// estimate's rounding scale ‖Ṽ‖²/k0), b = ⌊log₂ scale⌋ clamped to the last band.  w[b] ∈ (0, 1] is
-// the calibrated error envelope of band b relative to the largest (1 everywhere until calibrated):
-// near-object rows keep their own, smaller margin when far rows calibrate a larger one.
+// Margin of a screened row at query x: Δ_f = screen_delta · w[b] · scale, scale = max(1, (k0 − s̃²)/k0)
+// (the estimate's rounding scale ‖Ṽ‖²/k0), b = ⌊4·|x − centre|/ρ⌋ clamped to the last band (distance
+// bands of a quarter object radius).  w[b] ∈ (0, 1] is the calibrated error envelope of bands ≤ b
+// relative to the largest (1 everywhere until calibrated): the error grows with the distance from the
+// object before ‖Ṽ‖² does, and near-object rows keep their own, smaller margin.
 constexpr int SCREEN_BAND_OFF = 8;  // doubles into the centre block
-__device__ __host__ inline double screen_margin(double delta, const double* bands, double k0, double s2) {
-  const double scale = fmax(1.0, (k0 - s2) / k0);
-  int e = 0;
-  (void)frexp(scale, &e);  // scale ∈ [2^(e−1), 2^e): band e − 1
-  const int b = e - 1 < 0 ? 0 : (e - 1 >= CDX_SCREEN_BANDS ? CDX_SCREEN_BANDS - 1 : e - 1);
-  return delta * bands[b] * scale;
+__device__ __host__ inline int screen_band(const double* center, double x, double y, double z) {
+  const double dx = x - center[0], dy = y - center[1], dz = z - center[2];
+  const double t = sqrt(dx * dx + dy * dy + dz * dz) * center[5];
+  return t < (double)(CDX_SCREEN_BANDS - 1) ? (int)t : CDX_SCREEN_BANDS - 1;  // NaN → last band
+}
+__device__ __host__ inline double screen_margin(double delta, const double* center, int band, double k0, double s2) {
+  return delta * center[SCREEN_BAND_OFF + band] * fmax(1.0, (k0 - s2) / k0);
 }
 
 struct ScreenView {

@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const do
   const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= G) return;
   const double k0 = cdx::gpis_k0<KT>(g.R), delta = g.screen_delta;
-  const double* bands = cdx::screen_view(g).center + cdx::SCREEN_BAND_OFF;
+  const double* ctr = cdx::screen_view(g).center;
   double a[CDX_MAX_TIPS], d[CDX_MAX_TIPS];
   bool finite = true;
   int lead = 0;
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const do
     const double s2 = k0 - acc;
     sv2[q] = s2;
     a[f] = fabs(s2);
-    d[f] = screen_margin(delta, bands, k0, s2);
+    d[f] = screen_margin(delta, ctr, cdx::screen_band(ctr, X[3 * q], X[3 * q + 1], X[3 * q + 2]), k0, s2);
     finite = finite && isfinite(s2) && isfinite(d[f]);
     if (a[f] > a[lead]) lead = f;
     lo = fmax(lo, a[f] - d[f]);
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(256) void refine_select_kernel(cdx_gpis g, const do
   float rk = 0.f, ra = 0.f;
   if (gi < G) {
     const double k0 = cdx::gpis_k0<KT>(g.R), delta = g.screen_delta;
-    const double* bands = cdx::screen_view(g).center + cdx::SCREEN_BAND_OFF;
+    const double* ctr = cdx::screen_view(g).center;
     const unsigned m = keep[gi];
     int fmax = 0, fref = -1;
     double lmax = 0, lref = 0;
@@ -595,7 +595,9 @@ __global__ __launch_bounds__(256) void refine_select_kernel(cdx_gpis g, const do
         sd = sqrt(fabs(v));
         std_[q] = sd;
         var[q] = v;
-        const double e = fabs(sv2[q] - v), dd = screen_margin(delta, bands, k0, sv2[q]);
+        const double e = fabs(sv2[q] - v),
+                     dd = screen_margin(delta, ctr, cdx::screen_band(ctr, X[3 * q], X[3 * q + 1], X[3 * q + 2]), k0,
+                                        sv2[q]);
         if (isfinite(v) && isfinite(sv2[q])) {
           const float r = (float)(e / dd);
           const bool bad = !(e <= dd);
@@ -692,7 +694,8 @@ __global__ __launch_bounds__(256) void screen_center_kernel(cdx_gpis g, double S
     const double rq = fmax(0.0, r_safe - sqrt(red[0][0]));
     center[0] = cx; center[1] = cy; center[2] = cz; center[3] = SA;
     center[4] = isinf(r_safe) ? r_safe : rq * rq;
-    center[5] = center[6] = center[7] = 0.0;
+    center[5] = red[0][0] > 0 ? 4.0 / sqrt(red[0][0]) : 0.0;
+    center[6] = center[7] = 0.0;
     for (int b = 0; b < CDX_SCREEN_BANDS; ++b) center[cdx::SCREEN_BAND_OFF + b] = 1.0;
   }
   for (int j = t; j < g.N_pad; j += 256) {
@@ -914,6 +917,15 @@ int cdx_gpis_screen_prepare(const cdx_gpis* g, void* screen, cdx_stream_t stream
   hipLaunchKernelGGL(screen_split_kernel, dim3((unsigned)((nsplit + 255) / 256)), dim3(256), 0, s, gv,
                      reinterpret_cast<f16x8*>(const_cast<void*>(v.L)), (const double*)cscale, v.center);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+int cdx_gpis_screen_info(const cdx_gpis* g, double* out8, cdx_stream_t stream) {
+  if (!g || !g->screen || !out8 || g->N_pad <= 0 || g->N_pad % CDX_NPAD_ALIGN) return CDX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemcpyAsync(out8, cdx::screen_view(*g).center, 8 * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return CDX_ELAUNCH;
+  return CDX_OK;
 }
 
 int cdx_gpis_screen_set_bands(const cdx_gpis* g, const double* w, cdx_stream_t stream) {

@@ -57,6 +57,57 @@ CDX_HD float point_face(F3 p, F3 v1, F3 v2, F3 v3, F3& clst, F3& nrm, int& sgn) 
   return dd;
 }
 
+// ---------------------------------------------------------------- double dispatch
+// The reference dispatches float AND double (AT_DISPATCH_FLOATING_TYPES, .cu:282); with double inputs
+// its per-face body (.cu:201-237) computes in double EXCEPT where it names float: the edge parameter
+// passed to point_at is a `float t` (.cu:171-173: c = v + e·(double)(float)u), and the squared
+// distance is stored through `float dist` (.cu:237) — so the result's distance is a float value, and
+// the tile comparisons (.cu:238, :245) compare float values widened to double.  The 1e-16f of the
+// normal's rsqrt is a float literal widened to double.  rsqrt is correctly rounded 1/sqrt here too.
+struct D3 { double x, y, z; };
+CDX_HD D3 d3(double x, double y, double z) { D3 r; r.x = x; r.y = y; r.z = z; return r; }
+CDX_HD D3 subd(D3 a, D3 b) { return d3(a.x - b.x, a.y - b.y, a.z - b.z); }
+CDX_HD D3 addd(D3 a, D3 b) { return d3(a.x + b.x, a.y + b.y, a.z + b.z); }
+CDX_HD D3 scld(D3 a, double s) { return d3(a.x * s, a.y * s, a.z * s); }
+CDX_HD double dotd(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+CDX_HD D3 crossd(D3 a, D3 b) { return d3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+CDX_HD double rsqrt_crd(double x) { return 1.0 / sqrt(x); }
+
+CDX_HD float point_face_d(D3 p, D3 v1, D3 v2, D3 v3, D3& clst, D3& nrm, int& sgn) {
+  const D3 e12 = subd(v2, v1), e23 = subd(v3, v2), e31 = subd(v1, v3);
+  const D3 normal = crossd(subd(v1, v2), e31);
+  const double uab = dotd(subd(p, v1), e12) / dotd(e12, e12);
+  const double uca = dotd(subd(p, v3), e31) / dotd(e31, e31);
+  D3 c;
+  if (uca > 1 && uab < 0) {
+    c = v1;
+  } else {
+    const double ubc = dotd(subd(p, v2), e23) / dotd(e23, e23);
+    if (uab > 1 && ubc < 0) {
+      c = v2;
+    } else if (ubc > 1 && uca < 0) {
+      c = v3;
+    } else if (uab <= 1 && uab >= 0 && dotd(crossd(normal, e12), subd(p, v1)) <= 0) {
+      c = addd(v1, scld(e12, (double)(float)uab));
+    } else if (ubc <= 1 && ubc >= 0 && dotd(crossd(normal, e23), subd(p, v2)) <= 0) {
+      c = addd(v2, scld(e23, (double)(float)ubc));
+    } else if (uca <= 1 && uca >= 0 && dotd(crossd(normal, e31), subd(p, v3)) <= 0) {
+      c = addd(v3, scld(e31, (double)(float)uca));
+    } else {
+      const double inv_len = rsqrt_crd(dotd(normal, normal));
+      const D3 un = scld(normal, inv_len);
+      const double d = (p.x - v1.x) * un.x + (p.y - v1.y) * un.y + (p.z - v1.z) * un.z;
+      c = subd(p, scld(un, d));
+    }
+  }
+  const D3 dv = subd(p, c);
+  const double dd = dotd(dv, dv);
+  nrm = scld(dv, rsqrt_crd((double)1e-16f + dd));
+  sgn = dotd(dv, normal) >= 0 ? 1 : -1;
+  clst = c;
+  return (float)dd;
+}
+
 // The reference scans faces in 512-face tiles (.cu:186-246): inside a tile the first
 // face is always taken and later faces replace it only when strictly closer (:238);
 // a tile's winner replaces the running result only when strictly closer (:245), except

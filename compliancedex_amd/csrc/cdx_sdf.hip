@@ -326,6 +326,59 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_exact_kernel(const float* __res
   if (out_face) out_face[pi] = bface;
 }
 
+// Double inputs (.cu:282 dispatch): brute force with the tile rule, 512-face tiles of doubles in LDS
+// (36 KB), one point per lane.  Not a hot path (the reference's live path is float32).
+__global__ __launch_bounds__(SDF_BLOCK) void sdf_exact_f64_kernel(const double* __restrict__ points, int64_t P,
+                                                                  const double* __restrict__ faces, int64_t F,
+                                                                  double* __restrict__ out_dist,
+                                                                  int32_t* __restrict__ out_sign,
+                                                                  double* __restrict__ out_nrm,
+                                                                  double* __restrict__ out_clst,
+                                                                  int32_t* __restrict__ out_face) {
+  __shared__ double sf[SDF_TILE * 9];
+  const int64_t pi = (int64_t)blockIdx.x * SDF_BLOCK + threadIdx.x;
+  const bool live = pi < P;
+  cdx::D3 p = cdx::d3(0.0, 0.0, 0.0);
+  if (live) p = cdx::d3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
+  double best = 0.0;
+  int bsign = 0, bface = -1;
+  cdx::D3 bn = cdx::d3(0.0, 0.0, 0.0), bc = bn;
+  for (int64_t f0 = 0; f0 < F; f0 += SDF_TILE) {
+    const int nt = (int)min((int64_t)SDF_TILE, F - f0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < nt * 9; j += SDF_BLOCK) sf[j] = faces[f0 * 9 + j];
+    __syncthreads();
+    double tbest = 0.0;
+    int tsign = 0, tface = -1;
+    cdx::D3 tn = cdx::d3(0.0, 0.0, 0.0), tc = tn;
+    for (int s = 0; s < nt; ++s) {
+      const double* v = &sf[9 * s];
+      cdx::D3 c, n;
+      int sg;
+      const double d = (double)cdx::point_face_d(p, cdx::d3(v[0], v[1], v[2]), cdx::d3(v[3], v[4], v[5]),
+                                                 cdx::d3(v[6], v[7], v[8]), c, n, sg);
+      if (s == 0 || tbest > d) { tbest = d; tsign = sg; tn = n; tc = c; tface = (int)(f0 + s); }
+    }
+    if (f0 == 0 || best > tbest) { best = tbest; bsign = tsign; bn = tn; bc = tc; bface = tface; }
+  }
+  if (!live) return;
+  out_dist[pi] = best;
+  out_sign[pi] = bsign;
+  out_nrm[3 * pi] = bn.x; out_nrm[3 * pi + 1] = bn.y; out_nrm[3 * pi + 2] = bn.z;
+  out_clst[3 * pi] = bc.x; out_clst[3 * pi + 1] = bc.y; out_clst[3 * pi + 2] = bc.z;
+  if (out_face) out_face[pi] = bface;
+}
+
+__global__ __launch_bounds__(256) void sdf_backward_f64_kernel(const double* __restrict__ gd,
+                                                               const double* __restrict__ points,
+                                                               const double* __restrict__ clst, int64_t P,
+                                                               double* __restrict__ gp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  const double g = 2. * gd[i];
+  for (int c = 0; c < 3; ++c) gp[3 * i + c] = (points[3 * i + c] - clst[3 * i + c]) * g;
+}
+
 __global__ __launch_bounds__(256) void sdf_backward_kernel(const float* __restrict__ gd, const float* __restrict__ points,
                                                            const float* __restrict__ clst, int64_t P,
                                                            float* __restrict__ gp) {
@@ -418,6 +471,27 @@ int cdx_sdf_backward(const float* grad_dist, const float* points, const float* c
   if (P == 0) return CDX_OK;
   if (!grad_dist || !points || !clst || !grad_points) return CDX_EINVAL;
   hipLaunchKernelGGL(sdf_backward_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), grad_dist, points, clst, P, grad_points);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+int cdx_sdf_forward_f64(const double* points, int64_t P, const double* faces, int64_t F, double* sqdist,
+                        int32_t* sign, double* normals, double* clst, int32_t* face_idx, cdx_stream_t stream) {
+  if (P < 0 || F < 0) return CDX_EINVAL;
+  if (P == 0) return CDX_OK;
+  if (F == 0 || !points || !faces || !sqdist || !sign || !normals || !clst) return CDX_EINVAL;
+  if (P > INT32_MAX || F > INT32_MAX / 9) return CDX_EINVAL;
+  hipLaunchKernelGGL(sdf_exact_f64_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0,
+                     reinterpret_cast<hipStream_t>(stream), points, P, faces, F, sqdist, sign, normals, clst, face_idx);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+int cdx_sdf_backward_f64(const double* grad_dist, const double* points, const double* clst, int64_t P,
+                         double* grad_points, cdx_stream_t stream) {
+  if (P < 0) return CDX_EINVAL;
+  if (P == 0) return CDX_OK;
+  if (!grad_dist || !points || !clst || !grad_points) return CDX_EINVAL;
+  hipLaunchKernelGGL(sdf_backward_f64_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), grad_dist, points, clst, P, grad_points);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }

@@ -116,10 +116,14 @@ class _State:
         err = (est[ok] - exact[ok]).abs() / scale
         self.calib_far_finite = int(ok[Xn.shape[0]:].sum())
         gmax = float(err.max())
-        # per-band envelope (cdx_screen.h screen_margin): band b = ⌊log₂ scale⌋; a band's weight is the
-        # largest error of its own and every lower band, relative to the global maximum — bands above
-        # the highest calibrated one keep the global maximum (weight 1)
-        band = torch.clamp(torch.floor(torch.log2(scale)), 0, N.SCREEN_BANDS - 1).to(torch.int64)
+        # per-band envelope (cdx_screen.h screen_margin): band b = ⌊4·|x − c|/ρ⌋ with the device's own
+        # centre c and 4/ρ; a band's weight is the largest error of its own and every lower band,
+        # relative to the global maximum — bands above the highest calibrated one keep weight 1
+        info = (ctypes.c_double * 8)()
+        N.check(N.load().cdx_gpis_screen_info(self.desc, info, N.stream_ptr(dev)), "cdx_gpis_screen_info")
+        ctr = torch.tensor([info[0], info[1], info[2]], dtype=torch.float64, device=dev)
+        t = (Xc[ok] - ctr).norm(dim=1) * info[5]
+        band = torch.clamp(torch.floor(t), 0, N.SCREEN_BANDS - 1).to(torch.int64)
         per = torch.zeros(N.SCREEN_BANDS, dtype=torch.float64, device=dev).scatter_reduce(0, band, err, "amax")
         per = per.cpu().numpy()
         top = int(band.max())

@@ -2,8 +2,10 @@
 
 ``compute_sdf(points, face_vertices) -> (sqdist, sign, normals, clst_points)``: squared
 distance (autograd w.r.t. points), int32 sign, unit (p − c) normal and closest point
-(sdf.py:34-64), computed by cdx_sdf_forward / cdx_sdf_backward.  ``compute_sdf_with_faces``
-additionally returns the argmin face index.
+(sdf.py:34-64), computed by cdx_sdf_forward / cdx_sdf_backward (float32, the culled path) or
+cdx_sdf_forward_f64 / cdx_sdf_backward_f64 (float64, the reference's double instantiation,
+unbatched_triangle_distance_cuda.cu:282).  ``compute_sdf_with_faces`` additionally returns the
+argmin face index.
 """
 from __future__ import annotations
 
@@ -22,9 +24,9 @@ def index_vertices_by_faces(vertices_features, faces):
 def _check(points, faces):
     if not (points.is_cuda and faces.is_cuda):
         raise RuntimeError("points must be a CUDA tensor")  # unbatched_triangle_distance.cpp:48-53
-    if points.dtype != torch.float32 or faces.dtype != torch.float32:
-        raise RuntimeError("compute_sdf supports float32 points and face_vertices (the dtype of the "
-                           "reference's live path, optimize_pregrasp.py:165-168)")
+    if points.dtype not in (torch.float32, torch.float64) or faces.dtype != points.dtype:
+        raise RuntimeError("compute_sdf takes float32 or float64 points with face_vertices of the same dtype "
+                           "(the reference's dispatch, unbatched_triangle_distance_cuda.cu:32-41, :282)")
     if points.ndim != 2 or points.shape[1] != 3:
         raise RuntimeError(f"points must have shape [P, 3], got {tuple(points.shape)}")
     if faces.ndim != 3 or faces.shape[1:] != (3, 3):
@@ -42,9 +44,9 @@ def _forward(points, faces, want_face):
     normals = torch.zeros(P, 3, dtype=points.dtype, device=points.device)
     clst = torch.zeros(P, 3, dtype=points.dtype, device=points.device)
     face = torch.zeros(P, dtype=torch.int32, device=points.device) if want_face else None
-    N.check(lib.cdx_sdf_forward(N.ptr(points), P, N.ptr(faces), faces.shape[0], N.ptr(dist), N.ptr(sign),
-                                N.ptr(normals), N.ptr(clst), N.ptr(face), N.stream_ptr(points.device)),
-            "cdx_sdf_forward")
+    fwd = lib.cdx_sdf_forward if points.dtype == torch.float32 else lib.cdx_sdf_forward_f64
+    N.check(fwd(N.ptr(points), P, N.ptr(faces), faces.shape[0], N.ptr(dist), N.ptr(sign), N.ptr(normals), N.ptr(clst),
+                N.ptr(face), N.stream_ptr(points.device)), "cdx_sdf_forward")
     return dist, sign, normals, clst, face
 
 
@@ -60,10 +62,11 @@ class _UnbatchedTriangleDistance(torch.autograd.Function):
     def backward(ctx, grad_dist, grad_sign, grad_normals, grad_clst):
         points, clst = ctx.saved_tensors
         lib = N.load()
-        grad_dist = grad_dist.contiguous()
+        grad_dist = grad_dist.to(points.dtype).contiguous()
         grad_points = torch.zeros_like(points)
-        N.check(lib.cdx_sdf_backward(N.ptr(grad_dist), N.ptr(points), N.ptr(clst), points.shape[0],
-                                     N.ptr(grad_points), N.stream_ptr(points.device)), "cdx_sdf_backward")
+        bwd = lib.cdx_sdf_backward if points.dtype == torch.float32 else lib.cdx_sdf_backward_f64
+        N.check(bwd(N.ptr(grad_dist), N.ptr(points), N.ptr(clst), points.shape[0], N.ptr(grad_points),
+                    N.stream_ptr(points.device)), "cdx_sdf_backward")
         return grad_points, None
 
 

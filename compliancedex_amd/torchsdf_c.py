@@ -11,9 +11,10 @@ unbatched_triangle_distance_cuda.cu:32-41), so that
     import compliancedex_amd.torchsdf_c as _C      # in torchsdf/sdf.py, instead of `from torchsdf import _C`
 
 runs the reference's ``sdf.py`` unchanged on gfx950 (cdx_sdf_forward / cdx_sdf_backward).
-The reference dispatches float and double; this build computes float32 only — the dtype of the
-reference's live path (optimize_pregrasp.py:165-168) — and rejects double with the same
-``RuntimeError`` an unsupported dtype gets there.
+Both of the reference's dtypes are dispatched: float32 (the live path, optimize_pregrasp.py:165-168)
+on the culled kernel, float64 on the double instantiation (cdx_sdf_forward_f64: double arithmetic
+except the reference's two ``float``s, .cu:171-173 and :237); anything else gets the dispatch's
+``RuntimeError``.
 """
 from __future__ import annotations
 
@@ -39,9 +40,8 @@ def _sizes(name, **shapes):
 
 
 def _dtype(name, points):
-    if points.dtype != torch.float32:  # AT_ERROR of DISPATCH_INPUT_TYPES (float, double in the reference)
-        raise RuntimeError(f"{name} not implemented for '{str(points.dtype).replace('torch.', '').capitalize()}' "
-                           "(this build: float32)")
+    if points.dtype not in (torch.float32, torch.float64):  # AT_ERROR of DISPATCH_INPUT_TYPES (.cu:32-41)
+        raise RuntimeError(f"{name} not implemented for '{str(points.dtype).replace('torch.', '').capitalize()}'")
 
 
 def unbatched_triangle_distance_forward_cuda(points, face_vertices, dist, dist_sign, normals, clst_points):
@@ -58,9 +58,10 @@ def unbatched_triangle_distance_forward_cuda(points, face_vertices, dist, dist_s
     if face_vertices.dtype != points.dtype or dist.dtype != points.dtype or normals.dtype != points.dtype \
             or clst_points.dtype != points.dtype or dist_sign.dtype != torch.int32:
         raise RuntimeError(f"{name}: output dtypes must match the points (dist_sign int32)")
-    N.check(N.load().cdx_sdf_forward(N.ptr(points), P, N.ptr(face_vertices), face_vertices.shape[0], N.ptr(dist),
-                                     N.ptr(dist_sign), N.ptr(normals), N.ptr(clst_points), None,
-                                     N.stream_ptr(points.device)), name)
+    lib = N.load()
+    fwd = lib.cdx_sdf_forward if points.dtype == torch.float32 else lib.cdx_sdf_forward_f64
+    N.check(fwd(N.ptr(points), P, N.ptr(face_vertices), face_vertices.shape[0], N.ptr(dist), N.ptr(dist_sign),
+                N.ptr(normals), N.ptr(clst_points), None, N.stream_ptr(points.device)), name)
 
 
 def unbatched_triangle_distance_backward_cuda(grad_dist, points, clst_points, grad_points):
@@ -76,5 +77,7 @@ def unbatched_triangle_distance_backward_cuda(grad_dist, points, clst_points, gr
     _dtype(name, points)
     if grad_dist.dtype != points.dtype or clst_points.dtype != points.dtype or grad_points.dtype != points.dtype:
         raise RuntimeError(f"{name}: grad_dist, clst_points and grad_points must match the points' dtype")
-    N.check(N.load().cdx_sdf_backward(N.ptr(grad_dist), N.ptr(points), N.ptr(clst_points), points.shape[0],
-                                      N.ptr(grad_points), N.stream_ptr(points.device)), name)
+    lib = N.load()
+    bwd = lib.cdx_sdf_backward if points.dtype == torch.float32 else lib.cdx_sdf_backward_f64
+    N.check(bwd(N.ptr(grad_dist), N.ptr(points), N.ptr(clst_points), points.shape[0], N.ptr(grad_points),
+                N.stream_ptr(points.device)), name)

@@ -118,11 +118,14 @@ int cdx_gpis_factor(const double* E11, const double* y1, int32_t N, int32_t N_pa
  *   cdx_gpis_screen_workspace bytes. */
 size_t cdx_gpis_screen_bytes(int32_t N_pad);
 int cdx_gpis_screen_prepare(const cdx_gpis* g, void* screen, cdx_stream_t stream);
-/* Closure margin of a screened row: screen_delta · w[b] · max(1, ‖Ṽ‖²/k0), b = ⌊log₂ max(1, ‖Ṽ‖²/k0)⌋
- * (last band for larger); w[CDX_SCREEN_BANDS] (host array, each in (0, 1]) are the calibrated error
- * envelope per band relative to the largest; cdx_gpis_screen_prepare sets them all to 1. */
+/* Closure margin of a screened row at query x: screen_delta · w[b] · max(1, ‖Ṽ‖²/k0) with the distance
+ * band b = ⌊4·|x − c|/ρ⌋ (last band beyond), c the inducing points' centre and ρ their largest distance
+ * from it; w[CDX_SCREEN_BANDS] (host array, each in (0, 1]) is the calibrated error envelope of bands
+ * ≤ b relative to the largest; cdx_gpis_screen_prepare sets them all to 1.
+ * cdx_gpis_screen_info: out8 = [cx, cy, cz, SA, rq², 4/ρ, 0, 0] (host). */
 #define CDX_SCREEN_BANDS 24
 int cdx_gpis_screen_set_bands(const cdx_gpis* g, const double* w, cdx_stream_t stream);
+int cdx_gpis_screen_info(const cdx_gpis* g, double* out8, cdx_stream_t stream);
 size_t cdx_gpis_screen_workspace(const cdx_gpis* g, int64_t M);
 int cdx_gpis_screen_var(const cdx_gpis* g, const double* X, int64_t M, double* var, void* workspace,
                         cdx_stream_t stream);
@@ -366,8 +369,9 @@ int cdx_optimizer_step(const cdx_adam* cfg, const cdx_opt_buffers* buf, int64_t 
 /* --------------------------------------------------------------- TorchSDF -------
  * Replaces torchsdf._C.unbatched_triangle_distance_forward_cuda / _backward_cuda
  * (thirdparty/TorchSDF/torchsdf/csrc/bindings.cpp:22-27, kernels
- * unbatched_triangle_distance_cuda.cu:176-270).  float32 only (the dtype the reference
- * path uses, optimize_pregrasp.py:165-168).  Outputs are caller-allocated.
+ * unbatched_triangle_distance_cuda.cu:176-270).  float32 (the dtype the reference path uses,
+ * optimize_pregrasp.py:165-168) and, through the _f64 entry points, float64 (the reference's
+ * double dispatch, .cu:32-41 / :282).  Outputs are caller-allocated.
  * points [P*3], faces [F*9] → sqdist [P], sign [P] (±1), normals [P*3], clst [P*3],
  * face_idx [P] (argmin face, first minimum; nullable). */
 int cdx_sdf_forward(const float* points, int64_t P, const float* faces, int64_t F,
@@ -376,6 +380,14 @@ int cdx_sdf_forward(const float* points, int64_t P, const float* faces, int64_t 
 /* grad_points = 2·grad_dist·(p − clst) (unbatched_triangle_distance_cuda.cu:256-270). */
 int cdx_sdf_backward(const float* grad_dist, const float* points, const float* clst, int64_t P,
                      float* grad_points, cdx_stream_t stream);
+/* float64 points / faces: the reference's double instantiation — double arithmetic except the
+ * float edge parameter of point_at (.cu:171-173) and the float squared distance (.cu:237), so
+ * sqdist holds float values; brute force with the reference's 512-face tile rule. */
+int cdx_sdf_forward_f64(const double* points, int64_t P, const double* faces, int64_t F,
+                        double* sqdist, int32_t* sign, double* normals, double* clst,
+                        int32_t* face_idx, cdx_stream_t stream);
+int cdx_sdf_backward_f64(const double* grad_dist, const double* points, const double* clst, int64_t P,
+                         double* grad_points, cdx_stream_t stream);
 
 /* Library identification (gfx arch string compiled in). */
 const char* cdx_version(void);

