@@ -56,3 +56,22 @@ def test_sdf_normal_invariant_cpu():
     grad = _sdf_oracle.backward(np.ones_like(d), pts, c)
     direct = n * 2 * np.sqrt(d)[:, None]
     assert np.abs(direct - grad).max() < 5e-7
+
+
+def test_sdf_double_oracle_invariants_cpu():
+    """The C oracle's double instantiation (unbatched_triangle_distance_cuda.cu:282 with scalar_t =
+    double): squared distances are float values (the kernel's `float dist`, .cu:237), the TorchSDF
+    normal.py invariant holds, and on float32-representable inputs its distance agrees with the float
+    instantiation's to float rounding, with the same sign wherever both pick the same face (points
+    nearest a shared vertex or edge tie between faces, and the two precisions break ties apart)."""
+    rng = np.random.default_rng(3)
+    faces = np.load(os.path.join(DATA, "meshes", "sphere42_faces.npy"))
+    pts = (rng.random((2000, 3)) * 2 - 1).astype(np.float32)
+    d, s, n, c, f = _sdf_oracle.forward_f64(pts.astype(np.float64), faces.astype(np.float64))
+    assert d.dtype == np.float64 and np.array_equal(d, d.astype(np.float32).astype(np.float64))
+    grad = _sdf_oracle.backward_f64(np.ones_like(d), pts.astype(np.float64), c)
+    assert np.abs(n * 2 * np.sqrt(d)[:, None] - grad).max() < 5e-7
+    d32, s32, _, _, f32 = _sdf_oracle.forward(pts, faces)
+    same = f == f32
+    assert same.mean() > 0.9 and np.array_equal(s[same], s32[same])
+    assert np.abs(d - d32).max() <= 1e-6 * max(1.0, np.abs(d32).max())

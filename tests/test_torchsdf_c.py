@@ -60,17 +60,59 @@ def test_shim_rejects_like_the_reference():
 
 
 @pytest.mark.gpu
-def test_shim_rejects_double_and_noncontiguous():
+def test_shim_rejects_half_and_noncontiguous():
+    """The dispatch's AT_ERROR for a dtype it does not instantiate (.cu:32-41: float and double only),
+    CHECK_CONTIGUOUS for a transposed view."""
     import compliancedex_amd.torchsdf_c as _C
-    pts = torch.zeros(4, 3, device="cuda", dtype=torch.float64)
-    faces = torch.zeros(2, 3, 3, device="cuda", dtype=torch.float64)
-    outs = (torch.zeros(4, device="cuda", dtype=torch.float64), torch.zeros(4, device="cuda", dtype=torch.int32),
-            torch.zeros(4, 3, device="cuda", dtype=torch.float64), torch.zeros(4, 3, device="cuda", dtype=torch.float64))
-    with pytest.raises(RuntimeError, match="not implemented for 'Float64'"):
+    pts = torch.zeros(4, 3, device="cuda", dtype=torch.float16)
+    faces = torch.zeros(2, 3, 3, device="cuda", dtype=torch.float16)
+    outs = (torch.zeros(4, device="cuda", dtype=torch.float16), torch.zeros(4, device="cuda", dtype=torch.int32),
+            torch.zeros(4, 3, device="cuda", dtype=torch.float16), torch.zeros(4, 3, device="cuda", dtype=torch.float16))
+    with pytest.raises(RuntimeError, match="not implemented for 'Float16'"):
         _C.unbatched_triangle_distance_forward_cuda(pts, faces, *outs)
     with pytest.raises(RuntimeError, match="contiguous"):
         _C.unbatched_triangle_distance_forward_cuda(torch.zeros(3, 4, device="cuda").t(), faces.float(),
-                                                    *(o.float() if o.dtype == torch.float64 else o for o in outs))
+                                                    *(o.float() if o.dtype == torch.float16 else o for o in outs))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh", ["cube", "sphere42", "banana"])
+def test_shim_double_dispatch_vs_oracle_bitwise(mesh):
+    """float64 points / faces through the reference's calling sequence (sdf.py:42-64 on the shim): the
+    double instantiation (cdx_sdf_forward_f64 — double arithmetic except the float edge parameter and
+    float squared distance the reference's kernel names, .cu:171-173, :237) bit-identical to the C
+    oracle's double restatement in distance, sign, normal, closest point, argmin face and backward;
+    compute_sdf (autograd) gives the same; the TorchSDF normal.py invariant holds in double."""
+    import os
+    import numpy as np
+    import compliancedex_amd.torchsdf_c as _C
+    from compliancedex_amd import compute_sdf, compute_sdf_with_faces
+    from tests import _sdf_oracle
+    from tests._helpers import DATA
+    faces = np.load(os.path.join(DATA, "meshes", f"{mesh}_faces.npy")).astype(np.float64)
+    if mesh == "banana":
+        faces = faces[:3000]
+    rng = np.random.default_rng(5)
+    lo, hi = faces.reshape(-1, 3).min(0), faces.reshape(-1, 3).max(0)
+    pts = lo - 0.2 * (hi - lo) + 1.4 * (hi - lo) * rng.random((1500, 3))
+    pts[:20] = faces[:20, 0]
+    ft = torch.from_numpy(faces).cuda()
+    pt = torch.from_numpy(pts).cuda().requires_grad_(True)
+    a = _reference_sdf_py(_C, pt.detach(), ft)
+    d, sg, n, c = compute_sdf(pt, ft)
+    (d * torch.arange(1500, device="cuda", dtype=torch.float64)).sum().backward()
+    face = compute_sdf_with_faces(pt.detach(), ft)[4].cpu().numpy()
+    torch.cuda.synchronize()
+    o = _sdf_oracle.forward_f64(pts, faces)
+    og = _sdf_oracle.backward_f64(np.arange(1500, dtype=np.float64), pts, o[3])
+    assert np.array_equal(sg.cpu().numpy(), o[1]) and np.array_equal(face, o[4])
+    for x, y in zip((d, n, c, pt.grad), (o[0], o[2], o[3], og)):
+        assert np.array_equal(x.detach().cpu().numpy().view(np.uint64), y.view(np.uint64))
+    for x, y in zip(a, (d.detach(), sg, n, c)):
+        assert torch.equal(x, y)
+    assert np.array_equal(o[0], o[0].astype(np.float32).astype(np.float64))  # float squared distances (.cu:237)
+    g2 = torch.autograd.grad(compute_sdf(pt, ft)[0].sum(), pt)[0]
+    assert torch.allclose(n * 2 * d.detach().sqrt().unsqueeze(1), g2, atol=5e-7)
 
 
 @pytest.mark.gpu
