@@ -88,9 +88,14 @@ def pack_survivors(capacity, object_id, rank, cand_offset, best_loss, margin, q,
 
 
 def unpack_records(gathered):
-    """Concatenates the valid rows of every rank's buffer → [n_total, W]."""
-    rows = [g[1:1 + int(g[0, 0])] for g in gathered]
-    return torch.cat(rows, dim=0) if rows else gathered[0][1:1]
+    """Concatenates the valid rows of every rank's buffer → [n_total, W] (one host read of the
+    stored counts: the headers of all ranks in one copy)."""
+    if len(gathered) == 1:
+        g = gathered[0]
+        return g[1:1 + int(g[0, 0])]
+    counts = torch.stack([g[0, 0] for g in gathered]).tolist()
+    rows = [g[1:1 + int(n)] for g, n in zip(gathered, counts)]
+    return torch.cat(rows, dim=0)
 
 
 def overflow(gathered):

@@ -95,7 +95,8 @@ def test_shim_double_dispatch_vs_oracle_bitwise(mesh):
     rng = np.random.default_rng(5)
     lo, hi = faces.reshape(-1, 3).min(0), faces.reshape(-1, 3).max(0)
     pts = lo - 0.2 * (hi - lo) + 1.4 * (hi - lo) * rng.random((1500, 3))
-    pts[:20] = faces[:20, 0]
+    k = min(20, len(faces))
+    pts[:k] = faces[:k, 0]
     ft = torch.from_numpy(faces).cuda()
     pt = torch.from_numpy(pts).cuda().requires_grad_(True)
     a = _reference_sdf_py(_C, pt.detach(), ft)
