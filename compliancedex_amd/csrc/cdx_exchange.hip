@@ -6,9 +6,10 @@
 // all-gatherv).  Row 0 is the header [stored, survived, capacity, 0, …]; rows 1.. are the
 // survivors in candidate order:
 //   [object_id, rank, candidate_id, best_loss, 1, margin[T], q[D], comp[T], target[3T], palm[6]]
-// One workgroup, no host synchronisation: thread t owns the contiguous candidates [t·C, t·C + C),
-// C = ceil(E/1024); one block scan of the per-thread survivor counts gives each its first row;
-// rows past the stored count are zeroed, so the buffer is a pure function of the inputs.
+// No host synchronisation: the buffer is zeroed (hipMemsetAsync: rows past the stored count stay
+// zero, so the buffer is a pure function of the inputs), then one workgroup — thread t owns the
+// contiguous candidates [t·C, t·C + C), C = ceil(E/1024) — scans the per-thread survivor counts and
+// writes each survivor's row and the header.
 #include <hip/hip_runtime.h>
 
 #include "cdx.h"
@@ -65,9 +66,11 @@ __global__ __launch_bounds__(PACK_THREADS) void pack_survivors_kernel(
     for (int i = 0; i < 6; ++i) o[c++] = palm[e * 6 + i];
     ++r;
   }
-  const int64_t stored = total < capacity ? total : capacity;
-  for (int64_t i = (stored + 1) * W + t; i < (capacity + 1) * W; i += PACK_THREADS) buf[i] = 0.0;
-  if (t < W) buf[t] = t == 0 ? (double)stored : t == 1 ? (double)total : t == 2 ? (double)capacity : 0.0;
+  if (t == 0) {
+    buf[0] = (double)(total < capacity ? total : capacity);
+    buf[1] = (double)total;
+    buf[2] = (double)capacity;
+  }
 }
 
 }  // namespace
@@ -79,7 +82,10 @@ extern "C" int cdx_pack_survivors(int64_t E, int32_t n_tips, int32_t n_dofs, con
   if (E < 0 || capacity < 0 || n_tips < 1 || n_tips > CDX_MAX_TIPS || n_dofs < 0 || n_dofs > CDX_MAX_DOFS || !buf)
     return CDX_EINVAL;
   if (E > 0 && (!margin || !best_loss || !q || !comp || !target || !palm)) return CDX_EINVAL;
-  hipLaunchKernelGGL(pack_survivors_kernel, dim3(1), dim3(PACK_THREADS), 0, reinterpret_cast<hipStream_t>(stream), E,
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int W = 5 + n_tips + n_dofs + n_tips + 3 * n_tips + 6;
+  if (hipMemsetAsync(buf, 0, (size_t)(capacity + 1) * W * sizeof(double), s) != hipSuccess) return CDX_ELAUNCH;
+  hipLaunchKernelGGL(pack_survivors_kernel, dim3(1), dim3(PACK_THREADS), 0, s, E,
                      (int)n_tips, (int)n_dofs, margin, best_loss, q, comp, target, palm, object_id, rank, cand_offset,
                      capacity, buf);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;

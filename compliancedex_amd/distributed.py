@@ -49,6 +49,8 @@ def default_capacity(total, world):
 
 
 def _f64(t, shape):
+    if t.dtype is torch.float64 and t.is_contiguous() and tuple(t.shape) == tuple(shape):
+        return t.detach()  # already the layout the pack reads (no extra dispatch on the exit path)
     return t.detach().to(torch.float64).reshape(shape).contiguous()
 
 
@@ -61,7 +63,8 @@ def pack_survivors(capacity, object_id, rank, cand_offset, best_loss, margin, q,
     dev = margin.device
     capacity = int(capacity)
     buf = torch.empty(capacity + 1, W, dtype=torch.float64, device=dev)
-    ins = [_f64(margin, (E, T)), _f64(best_loss, (E,)), _f64(q, (E, D)), _f64(comp, (E, T)), _f64(target, (E, 3 * T)),
+    tgt = target if (target.dim() == 2 and target.is_contiguous()) else target.reshape(E, 3 * T)
+    ins = [_f64(margin, (E, T)), _f64(best_loss, (E,)), _f64(q, (E, D)), _f64(comp, (E, T)), _f64(tgt, (E, 3 * T)),
            _f64(palm, (E, 6))]
     if dev.type == "cuda":
         from . import _native as N

@@ -239,3 +239,19 @@ def test_optimize_sharded_one_object_per_rank_gloo_world2():
         assert shapes == [(12, record_width(16, 4))] * 2
         assert ovf == [0, 0]
         assert np.array_equal(rec, full)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("E,cap", [(4096, 4096), (4096, 7), (1, 3), (0, 5), (3000, 1500)])
+def test_native_pack_equals_cpu_layout(E, cap):
+    """cdx_pack_survivors (the GPU pack: one launch, header counts written on the device, no host
+    sync) produces bit for bit the buffer of the CPU (torch-ops) layout: survivors in candidate order,
+    overflow counted in the header, unused rows zero; NaN margins do not survive."""
+    d = _local(3, E=E)
+    if E:
+        d["margin"][0, 0] = float("nan")
+    cpu = pack_survivors(cap, 5, 1, 10, **d)
+    gpu = pack_survivors(cap, 5, 1, 10, **{k: v.cuda() for k, v in d.items()})
+    torch.cuda.synchronize()
+    assert torch.equal(gpu.cpu(), cpu)
+    assert torch.equal(unpack_records([gpu]).cpu(), unpack_records([cpu]))
