@@ -510,8 +510,22 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
 // device.
 struct SideStream {
   hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;  // main → side before mean A, side → main after it
+  hipEvent_t gate = nullptr, joinB = nullptr; // main → side after the ∇std pass, side → main after mean B
 };
+
+// The forked mean is split (CDX_MEAN_SPLIT, default 1): part A — the all-tip and target rows, which
+// the level kernel reads — runs beside the selection / exact pass as before; part B — the pregrasp
+// and palm rows, read only by the combine kernel — is gated behind the ∇std pass, so it runs beside
+// the latency-bound level kernel (3E lanes: ≈ 1/5 of the SIMDs) instead of competing with the GEMM
+// passes for CUs.  0 = one mean launch at the fork point.
+bool mean_split() {
+  static const bool on = [] {
+    const char* e = getenv("CDX_MEAN_SPLIT");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
 
 bool side_stream(SideStream& out) {
   static SideStream per_dev[64];
@@ -546,9 +560,27 @@ bool side_stream(SideStream& out) {
       (void)hipGetLastError();
       return false;
     }
+    hipEvent_t c, d;
+    if (hipEventCreateWithFlags(&c, hipEventDisableTiming) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+      (void)hipStreamDestroy(st);
+      (void)hipGetLastError();
+      return false;
+    }
+    if (hipEventCreateWithFlags(&d, hipEventDisableTiming) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+      (void)hipEventDestroy(c);
+      (void)hipStreamDestroy(st);
+      (void)hipGetLastError();
+      return false;
+    }
     ss.s = st;
     ss.fork = a;
     ss.join = b;
+    ss.gate = c;
+    ss.joinB = d;
   }
   out = ss;
   return true;
@@ -672,6 +704,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   const bool scr = screen_on(p, E);
   SideStream ss;
   const bool fork = scr && fork_mean() && side_stream(ss);
+  const SideStream* pending_b = nullptr;  // mean B still to be joined before the combine kernel
   int rc;
   if (!fork) {
     rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
@@ -690,16 +723,28 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     // under capture an unjoined fork invalidates the graph, and eagerly the mean would keep writing
     // the workspace after the error return.  (A join recorded before a failed launch_fork only waits
     // on the event's previous record.)
-    bool forked = false;
+    bool forked = false, forkedB = false;
+    const int64_t MqA = mean_split() ? (int64_t)(p->n_query_levels + 1) * E * T : Mq;  // rows of mean A
+    const cdx_stream_t side = reinterpret_cast<cdx_stream_t>(ss.s);
     auto launch_fork = [&]() -> int {
       forked = true;
       if (hipEventRecord(ss.fork, s) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess) return CDX_ELAUNCH;
-      const int r = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, reinterpret_cast<cdx_stream_t>(ss.s));
+      const int r = cdx_gpis_mean(&p->gpis, w.X, MqA, w.mean, w.gmean, w.normal, side);
       if (r) return r;
       return hipEventRecord(ss.join, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
     };
+    auto launch_b = [&]() -> int {  // mean B, gated behind the work already on `s`
+      if (MqA >= Mq) return CDX_OK;
+      forkedB = true;
+      if (hipEventRecord(ss.gate, s) != hipSuccess || hipStreamWaitEvent(ss.s, ss.gate, 0) != hipSuccess) return CDX_ELAUNCH;
+      const int r = cdx_gpis_mean(&p->gpis, w.X + 3 * MqA, Mq - MqA, w.mean + MqA, w.gmean + 3 * MqA,
+                                  w.normal + 3 * MqA, side);
+      if (r) return r;
+      return hipEventRecord(ss.joinB, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
+    };
     auto joined = [&](int r) -> int {
       if (forked && hipStreamWaitEvent(s, ss.join, 0) != hipSuccess && !r) r = CDX_ELAUNCH;
+      if (forkedB && hipStreamWaitEvent(s, ss.joinB, 0) != hipSuccess && !r) r = CDX_ELAUNCH;
       return r;
     };
     if (fork && fork_point() == 1 && (rc = launch_fork())) return joined(rc);
@@ -719,7 +764,14 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                                    w.Xg, w.vrow, w.stats, s);
     if (rc) return joined(rc);
     rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V, w.vrow);
-    rc = joined(rc);
+    if (rc) return joined(rc);
+    if (fork && (rc = launch_b())) return joined(rc);
+    // mean A before the level kernel; mean B is joined before the combine kernel below
+    if (forked && hipStreamWaitEvent(s, ss.join, 0) != hipSuccess) {
+      forked = false;
+      return joined(CDX_ELAUNCH);
+    }
+    if (forkedB) pending_b = &ss;
   } else {
     const cdx::VarSelect vs{p->chain.n_tips, w.sel, w.Xg};
     rc = cdx::gpis_var_launch(p->gpis, w.X, Ms, w.std_, w.var, w.var_ws, s, w.V, &vs);
@@ -743,7 +795,11 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     else
       hipLaunchKernelGGL((closure_level_kernel<0, -1>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
                          kabsch_noise, seed, gv, w.lvl, flip);
-    if (hipGetLastError() != hipSuccess) return CDX_ELAUNCH;
+    if (hipGetLastError() != hipSuccess) {
+      if (pending_b) (void)hipStreamWaitEvent(s, pending_b->joinB, 0);
+      return CDX_ELAUNCH;
+    }
+    if (pending_b && hipStreamWaitEvent(s, pending_b->joinB, 0) != hipSuccess) return CDX_ELAUNCH;
     const bool sh = shallow_chain(p->chain);
     const dim3 cb(COMBINE_BLOCK);
     if (p->chain.n_tips <= 4) {
