@@ -514,15 +514,15 @@ struct SideStream {
   hipEvent_t gate = nullptr, joinB = nullptr; // main → side after the ∇std pass, side → main after mean B
 };
 
-// The forked mean is split (CDX_MEAN_SPLIT, default 1): part A — the all-tip and target rows, which
-// the level kernel reads — runs beside the selection / exact pass as before; part B — the pregrasp
-// and palm rows, read only by the combine kernel — is gated behind the ∇std pass, so it runs beside
-// the latency-bound level kernel (3E lanes: ≈ 1/5 of the SIMDs) instead of competing with the GEMM
-// passes for CUs.  0 = one mean launch at the fork point.
+// CDX_MEAN_SPLIT=1 splits the forked mean: part A — the all-tip and target rows, which the level
+// kernel reads — at the fork point; part B — the pregrasp and palm rows, read only by the combine
+// kernel — gated behind the ∇std pass, beside the latency-bound level kernel (3E lanes, ≈ 1/5 of the
+// SIMDs).  Off by default: 1.135–1.154 vs 1.095–1.110 ms per closure (profiles/r03e_mean_split_ab.jsonl)
+// — mean B's waves share SIMDs with the level kernel's long dependent chains and stretch them.
 bool mean_split() {
   static const bool on = [] {
     const char* e = getenv("CDX_MEAN_SPLIT");
-    return !e || atoi(e) != 0;
+    return e && atoi(e) != 0;
   }();
   return on;
 }
@@ -878,9 +878,11 @@ int cdx_closure_screen_reset(const cdx_problem* p, int64_t E, void* workspace, c
   if (E == 0 || !screen_on(p, E)) return CDX_OK;
   if (!workspace) return CDX_EINVAL;
   ClosureWs w = closure_ws_layout(p, E, static_cast<char*>(workspace));
-  return hipMemsetAsync(w.stats + cdx::SS_CUM, 0, (cdx::SS_WORDS - cdx::SS_CUM) * sizeof(int),
-                        reinterpret_cast<hipStream_t>(stream)) == hipSuccess
-             ? CDX_OK : CDX_ELAUNCH;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(w.stats + cdx::SS_CUM, 0, (cdx::SS_WORDS - cdx::SS_CUM) * sizeof(int), s) != hipSuccess)
+    return CDX_ELAUNCH;
+  const int64_t Ms = (int64_t)p->n_query_levels * E * p->chain.n_tips;
+  return cdx::gpis_refine_reset(p->gpis, Ms, w.refine_ws, s);
 }
 
 const char* cdx_version(void) { return "compliancedex_amd 0.1 gfx950"; }

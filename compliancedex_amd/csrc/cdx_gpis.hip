@@ -250,7 +250,9 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 //   cut into gridDim.x equal pieces of the concatenated K-sequence of all (query tile, stripe)
 //   pairs: a piece's segments that cover a whole stripe finish their epilogue in place, a stripe
 //   cut by piece boundaries leaves partial V tiles in rl.slots (slot 0: the piece's first segment,
-//   1: its last) that gpis_var_merge sums in piece order.
+//   1: its last); the last of the unit's pieces to finish (a per-unit arrival counter) sums them in
+//   piece order — the same order, hence the same bits, as the separate gpis_var_merge kernel it
+//   replaces (CDX_MERGE_KERNEL builds that for A/B).
 enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2, MODE_VARL = 3 };
 
 struct RefineList {
@@ -258,6 +260,8 @@ struct RefineList {
   const int* extra;   // device count of positions past the G primary ones
   int G;
   double* slots;      // [gridDim.x][2][ST_BM][ST_BN] partial V tiles of cut stripes
+  int* cnt;           // [Nt][mt_cap] arrival counters of cut units (zero between launches)
+  int mt_cap;         // query tiles the list can hold
 };
 
 // Whitened pass A operand: K* generated on chip per stripe (default), or read from a buffer
@@ -328,6 +332,60 @@ __device__ inline int refine_pieces(int64_t total, int G) {
 // XCD); with fewer, piece b (blocks spread round-robin over the XCDs).
 __device__ inline int refine_piece(int b, int G, int pieces) {
   return pieces == G && (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b;
+}
+
+// Piece holding K-sequence position x (pieces cut [0, total) at total·p/pieces).
+__device__ inline int refine_piece_of(int64_t x, int64_t total, int pieces) {
+  int p = (int)(x * pieces / total);
+  while (p + 1 < pieces && total * (p + 1) / pieces <= x) ++p;
+  while (p > 0 && total * p / pieces > x) --p;
+  return p;
+}
+
+// A cut unit (stripe nt, query tile mt, K-sequence [S0, S1)): V = its pieces' partial tiles summed in
+// piece order, stored at the list positions, and Σ V² per row into partial[nt][position] — 8 waves,
+// 4 columns per lane, MERGE_RB rows per batch so a batch's loads are in flight together.
+constexpr int MERGE_THREADS = 512, MERGE_RB = 8;
+__device__ inline void refine_merge_unit(const cdx_gpis& g, const RefineList& rl, int64_t M_pad, double* partial,
+                                         double* vout, int nt, int mt, int64_t S0, int64_t S1, int64_t total,
+                                         int pieces, int tid) {
+  const int Np = g.N_pad;
+  const int pf = refine_piece_of(S0, total, pieces), pl = refine_piece_of(S1 - 1, total, pieces);
+  auto qof = [&](int pp) { return total * pp / pieces; };
+  const int lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = MERGE_THREADS / 64;
+  for (int r0 = wave * MERGE_RB; r0 < ST_BM; r0 += NW * MERGE_RB) {
+    double v[MERGE_RB][4] = {};
+    for (int pp = pf; pp <= pl; ++pp) {
+      // this stripe's segment in piece pp; slot 0 if it is the piece's first segment, else 1
+      const int64_t a = max(qof(pp), S0), e = min(qof(pp + 1), S1);
+      if (a >= e) continue;
+      const int slot = 2 * pp + (a == qof(pp) ? 0 : 1);
+      const double* src = rl.slots + ((int64_t)slot * ST_BM + r0) * ST_BN + 4 * lane;
+#pragma unroll
+      for (int rr = 0; rr < MERGE_RB; ++rr)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[rr][c] += src[rr * ST_BN + c];
+    }
+    double sq[MERGE_RB];
+#pragma unroll
+    for (int rr = 0; rr < MERGE_RB; ++rr) {
+      double* dst = vout + ((int64_t)mt * ST_BM + r0 + rr) * Np + nt * ST_BN + 4 * lane;
+      sq[rr] = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        dst[c] = v[rr][c];
+        sq[rr] = fma(v[rr][c], v[rr][c], sq[rr]);
+      }
+    }
+#pragma unroll
+    for (int w = 1; w < 64; w <<= 1)
+#pragma unroll
+      for (int rr = 0; rr < MERGE_RB; ++rr) sq[rr] += __shfl_xor(sq[rr], w);
+    if (lane == 0)
+#pragma unroll
+      for (int rr = 0; rr < MERGE_RB; ++rr) partial[(int64_t)nt * M_pad + (int64_t)mt * ST_BM + r0 + rr] = sq[rr];
+  }
 }
 
 #if defined(CDX_DIAG_WGTIME)
@@ -706,6 +764,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     if (pc >= pieces) return;
     const int64_t q0 = total * pc / pieces, q1 = total * (pc + 1) / pieces;
     bool first = true;
+    __shared__ int s_last;
     for (int64_t q = q0; q < q1;) {
       int nt, mt;
       int64_t S0, S1;
@@ -717,6 +776,25 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
       if (!first) __syncthreads();  // the previous segment's epilogue used the stage buffers
       first = false;
       tile(mt, nt, kbeg, kend, full ? nt : 2 * pc + (q == q0 ? 0 : 1), full);
+#if !defined(CDX_MERGE_KERNEL)
+      if (!full) {
+        // release this piece's partial tile, count the arrival; the unit's last piece merges it
+        __threadfence();
+        __syncthreads();
+        if (tid == 0) {
+          const int n = refine_piece_of(S1 - 1, total, pieces) - refine_piece_of(S0, total, pieces) + 1;
+          int* c = rl.cnt + (int64_t)nt * rl.mt_cap + mt;
+          const int old = atomicAdd(c, 1);
+          s_last = old == n - 1;
+          if (old == n - 1) *c = 0;  // ready for the next launch
+        }
+        __syncthreads();
+        if (s_last) {
+          __threadfence();  // acquire: the other pieces' tiles
+          refine_merge_unit(g, rl, M_pad, partial, vout, nt, mt, S0, S1, total, pieces, tid);
+        }
+      }
+#endif
       q = e;
     }
     return;
@@ -914,11 +992,9 @@ __global__ __launch_bounds__(256) void gpis_var_splitk_finalize(cdx_gpis g, cons
   }
 }
 
-// Refine pass (MODE_VARL), cut stripes: workgroup p finishes the stripe whose K-range ends inside
-// piece p after starting in an earlier one — V = its partial tiles summed in piece order, stored at
-// the list positions, and Σ V² per row into partial[nt][position] (8 waves, 4 columns per lane,
-// MERGE_RB rows per batch so a batch's loads are in flight together).
-constexpr int MERGE_THREADS = 512, MERGE_RB = 8;
+#if defined(CDX_MERGE_KERNEL)
+// A/B build: the cut units merged by a separate kernel after the refine pass — workgroup p finishes
+// the unit whose K-range ends inside piece p after starting in an earlier one.
 __global__ __launch_bounds__(MERGE_THREADS) void gpis_var_merge(cdx_gpis g, RefineList rl, int64_t M_pad,
                                                       double* __restrict__ partial, double* __restrict__ vout) {
   const int Np = g.N_pad, Nt = Np / ST_BN;
@@ -929,51 +1005,15 @@ __global__ __launch_bounds__(MERGE_THREADS) void gpis_var_merge(cdx_gpis g, Refi
   const int64_t total = (int64_t)MtL * W;
   const int pieces = refine_pieces(total, gridDim.x), p = blockIdx.x;
   if (p >= pieces) return;
-  auto qof = [&](int pp) { return total * pp / pieces; };
-  const int64_t q0 = qof(p), q1 = qof(p + 1);
+  const int64_t q0 = total * p / pieces, q1 = total * (p + 1) / pieces;
   if (q0 >= q1 || q0 >= total) return;
   int nt, mt;
   int64_t S0, S1;
   refine_locate(q0, MtL, g.N, Np, nt, mt, S0, S1);
   if (!(S0 < q0 && S1 <= q1)) return;
-  int pf = p;
-  while (pf > 0 && qof(pf) > S0) --pf;  // the stripe's first piece (possibly an empty one before it)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int NW = MERGE_THREADS / 64;
-  for (int r0 = wave * MERGE_RB; r0 < ST_BM; r0 += NW * MERGE_RB) {
-    double v[MERGE_RB][4] = {};
-    for (int pp = pf; pp <= p; ++pp) {
-      // this stripe's segment in piece pp (empty pieces — fewer K-steps than pieces — hold none);
-      // slot 0 if it is the piece's first segment, else 1 (gpis_std_kernel<VARL>'s rule)
-      const int64_t a = max(qof(pp), S0), e = min(qof(pp + 1), S1);
-      if (a >= e) continue;
-      const int slot = 2 * pp + (a == qof(pp) ? 0 : 1);
-      const double* src = rl.slots + ((int64_t)slot * ST_BM + r0) * ST_BN + 4 * lane;
-#pragma unroll
-      for (int rr = 0; rr < MERGE_RB; ++rr)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[rr][c] += src[rr * ST_BN + c];
-    }
-    double sq[MERGE_RB];
-#pragma unroll
-    for (int rr = 0; rr < MERGE_RB; ++rr) {
-      double* dst = vout + ((int64_t)mt * ST_BM + r0 + rr) * Np + nt * ST_BN + 4 * lane;
-      sq[rr] = 0.0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        dst[c] = v[rr][c];
-        sq[rr] = fma(v[rr][c], v[rr][c], sq[rr]);
-      }
-    }
-#pragma unroll
-    for (int w = 1; w < 64; w <<= 1)
-#pragma unroll
-      for (int rr = 0; rr < MERGE_RB; ++rr) sq[rr] += __shfl_xor(sq[rr], w);
-    if (lane == 0)
-#pragma unroll
-      for (int rr = 0; rr < MERGE_RB; ++rr) partial[(int64_t)nt * M_pad + (int64_t)mt * ST_BM + r0 + rr] = sq[rr];
-  }
+  refine_merge_unit(g, rl, M_pad, partial, vout, nt, mt, S0, S1, total, pieces, threadIdx.x);
 }
+#endif
 
 // Partial slots a ∇std launch wrote, in increasing order (host-computed, passed by value).
 constexpr int GRAD_MAX_SLOTS = 512;
@@ -1192,10 +1232,22 @@ int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_
 // Pieces of the refine pass: one per CU.
 constexpr int REFINE_PIECES = 256;
 
+// [stripe partials][cut-unit partial tiles][arrival counters]
+static size_t refine_part_bytes(const cdx_gpis& g, int64_t Mcap) {
+  return ((size_t)(g.N_pad / ST_BN) * (size_t)round_up(Mcap, ST_BM) * sizeof(double) + 255) / 256 * 256;
+}
+static size_t refine_slot_bytes() { return (size_t)REFINE_PIECES * 2 * ST_BM * ST_BN * sizeof(double); }
+static size_t refine_cnt_bytes(const cdx_gpis& g, int64_t Mcap) {
+  return ((size_t)(g.N_pad / ST_BN) * (size_t)(round_up(Mcap, ST_BM) / ST_BM) * sizeof(int) + 255) / 256 * 256;
+}
+
 size_t gpis_refine_ws_bytes(const cdx_gpis& g, int64_t Mcap) {
-  const size_t part = (size_t)(g.N_pad / ST_BN) * (size_t)round_up(Mcap, ST_BM) * sizeof(double);
-  const size_t slots = (size_t)REFINE_PIECES * 2 * ST_BM * ST_BN * sizeof(double);
-  return (part + 255) / 256 * 256 + slots;
+  return refine_part_bytes(g, Mcap) + refine_slot_bytes() + refine_cnt_bytes(g, Mcap);
+}
+
+int gpis_refine_reset(const cdx_gpis& g, int64_t Mcap, void* ws, hipStream_t s) {
+  char* c = static_cast<char*>(ws) + refine_part_bytes(g, Mcap) + refine_slot_bytes();
+  return hipMemsetAsync(c, 0, refine_cnt_bytes(g, Mcap), s) == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
 template <int KT>
@@ -1205,7 +1257,9 @@ static void refine_launch_kt(const cdx_gpis& g, const double* X, int64_t Mcap, c
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VARL>), dim3(REFINE_PIECES), dim3(ST_THREADS), 0, s, g, X, Mcap, partial,
                      M_pad, 0, g.N_pad / ST_BN, vout, nullptr, nullptr, 0, rl);
   prof_mark(PROF_GPIS_STD, false, s);
+#if defined(CDX_MERGE_KERNEL)
   hipLaunchKernelGGL(gpis_var_merge, dim3(REFINE_PIECES), dim3(MERGE_THREADS), 0, s, g, rl, M_pad, partial, vout);
+#endif
 }
 
 int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
@@ -1213,8 +1267,9 @@ int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, cons
   if (Mcap <= 0 || G <= 0 || G > Mcap) return CDX_EINVAL;
   const int64_t M_pad = round_up(Mcap, ST_BM);
   double* partial = static_cast<double*>(ws);
-  const size_t part = (size_t)(g.N_pad / ST_BN) * (size_t)M_pad * sizeof(double);
-  RefineList rl{rows, extra, G, reinterpret_cast<double*>(static_cast<char*>(ws) + (part + 255) / 256 * 256)};
+  char* slots = static_cast<char*>(ws) + refine_part_bytes(g, Mcap);
+  RefineList rl{rows, extra, G, reinterpret_cast<double*>(slots), reinterpret_cast<int*>(slots + refine_slot_bytes()),
+                (int)(M_pad / ST_BM)};
   switch (g.kernel) {
     case CDX_KERNEL_TPS: refine_launch_kt<CDX_KERNEL_TPS>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
     case CDX_KERNEL_RBF: refine_launch_kt<CDX_KERNEL_RBF>(g, X, Mcap, rl, partial, M_pad, vout, s); break;

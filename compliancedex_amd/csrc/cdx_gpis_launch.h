@@ -34,6 +34,9 @@ int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_
 // CU) whatever the count; V rows go to vout at the list positions ([round_up(Mcap, 128), N_pad]),
 // Σ V² per (stripe, position) to the returned partial [N_pad/256][*M_pad_out].
 size_t gpis_refine_ws_bytes(const cdx_gpis& g, int64_t Mcap);
+// Zeroes the refine workspace's cut-unit arrival counters (once after allocation; every launch
+// leaves them zero).
+int gpis_refine_reset(const cdx_gpis& g, int64_t Mcap, void* ws, hipStream_t s);
 int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
                        void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out);
 }  // namespace cdx

@@ -267,7 +267,8 @@ typedef struct {
 /* Reads the record (an async copy on `stream`, then a wait on that stream). */
 int cdx_closure_screen_report(const cdx_problem* p, int64_t E, const void* workspace, cdx_screen_report* out,
                               cdx_stream_t stream);
-/* Zeroes the cumulative fields (stream-ordered); a no-op when the closure does not screen. */
+/* Zeroes the cumulative fields and the exact pass's arrival counters (stream-ordered; REQUIRED once
+ * after allocating a workspace for a screened closure); a no-op when the closure does not screen. */
 int cdx_closure_screen_reset(const cdx_problem* p, int64_t E, void* workspace, cdx_stream_t stream);
 
 /* ------------------------------------------------------------ survivor exchange ------
