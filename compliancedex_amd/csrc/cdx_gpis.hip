@@ -250,9 +250,10 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 //   cut into gridDim.x equal pieces of the concatenated K-sequence of all (query tile, stripe)
 //   pairs: a piece's segments that cover a whole stripe finish their epilogue in place, a stripe
 //   cut by piece boundaries leaves partial V tiles in rl.slots (slot 0: the piece's first segment,
-//   1: its last); the last of the unit's pieces to finish (a per-unit arrival counter) sums them in
-//   piece order — the same order, hence the same bits, as the separate gpis_var_merge kernel it
-//   replaces (CDX_MERGE_KERNEL builds that for A/B).
+//   1: its last) that gpis_var_merge sums in piece order.  (CDX_MERGE_FUSED instead lets the last of a
+//   unit's pieces to finish — a per-unit arrival counter — sum them, in the same order: bit-identical,
+//   but 1.22 vs 1.11 ms per closure, profiles/r03f_merge_fused_ab.jsonl: the agent-scope release
+//   fence each cut piece needs writes back its XCD's whole L2.)
 enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2, MODE_VARL = 3 };
 
 struct RefineList {
@@ -776,7 +777,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
       if (!first) __syncthreads();  // the previous segment's epilogue used the stage buffers
       first = false;
       tile(mt, nt, kbeg, kend, full ? nt : 2 * pc + (q == q0 ? 0 : 1), full);
-#if !defined(CDX_MERGE_KERNEL)
+#if defined(CDX_MERGE_FUSED)
       if (!full) {
         // release this piece's partial tile, count the arrival; the unit's last piece merges it
         __threadfence();
@@ -992,9 +993,9 @@ __global__ __launch_bounds__(256) void gpis_var_splitk_finalize(cdx_gpis g, cons
   }
 }
 
-#if defined(CDX_MERGE_KERNEL)
-// A/B build: the cut units merged by a separate kernel after the refine pass — workgroup p finishes
-// the unit whose K-range ends inside piece p after starting in an earlier one.
+#if !defined(CDX_MERGE_FUSED)
+// The cut units merged by a separate kernel after the refine pass — workgroup p finishes the unit
+// whose K-range ends inside piece p after starting in an earlier one.
 __global__ __launch_bounds__(MERGE_THREADS) void gpis_var_merge(cdx_gpis g, RefineList rl, int64_t M_pad,
                                                       double* __restrict__ partial, double* __restrict__ vout) {
   const int Np = g.N_pad, Nt = Np / ST_BN;
@@ -1257,7 +1258,7 @@ static void refine_launch_kt(const cdx_gpis& g, const double* X, int64_t Mcap, c
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VARL>), dim3(REFINE_PIECES), dim3(ST_THREADS), 0, s, g, X, Mcap, partial,
                      M_pad, 0, g.N_pad / ST_BN, vout, nullptr, nullptr, 0, rl);
   prof_mark(PROF_GPIS_STD, false, s);
-#if defined(CDX_MERGE_KERNEL)
+#if !defined(CDX_MERGE_FUSED)
   hipLaunchKernelGGL(gpis_var_merge, dim3(REFINE_PIECES), dim3(MERGE_THREADS), 0, s, g, rl, M_pad, partial, vout);
 #endif
 }
