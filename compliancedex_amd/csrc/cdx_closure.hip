@@ -527,6 +527,14 @@ bool mean_split() {
   return on;
 }
 
+// Fork/join events: no timing, and (CDX_SIDE_EVENT_FENCE unset) no system-scope fence — they order
+// two streams of one device, whose kernels see each other's writes at kernel boundaries anyway.
+unsigned side_event_flags() {
+  static const unsigned f = getenv("CDX_SIDE_EVENT_FENCE") ? hipEventDisableTiming
+                                                           : (hipEventDisableTiming | hipEventDisableSystemFence);
+  return f;
+}
+
 bool side_stream(SideStream& out) {
   static SideStream per_dev[64];
   int dev = 0;
@@ -549,26 +557,26 @@ bool side_stream(SideStream& out) {
       (void)hipGetLastError();
       return false;
     }
-    if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&a, side_event_flags()) != hipSuccess) {
       (void)hipStreamDestroy(st);
       (void)hipGetLastError();
       return false;
     }
-    if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&b, side_event_flags()) != hipSuccess) {
       (void)hipEventDestroy(a);
       (void)hipStreamDestroy(st);
       (void)hipGetLastError();
       return false;
     }
     hipEvent_t c, d;
-    if (hipEventCreateWithFlags(&c, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&c, side_event_flags()) != hipSuccess) {
       (void)hipEventDestroy(a);
       (void)hipEventDestroy(b);
       (void)hipStreamDestroy(st);
       (void)hipGetLastError();
       return false;
     }
-    if (hipEventCreateWithFlags(&d, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&d, side_event_flags()) != hipSuccess) {
       (void)hipEventDestroy(a);
       (void)hipEventDestroy(b);
       (void)hipEventDestroy(c);
