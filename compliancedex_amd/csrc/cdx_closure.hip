@@ -527,11 +527,14 @@ bool mean_split() {
   return on;
 }
 
-// Fork/join events: no timing, and (CDX_SIDE_EVENT_FENCE unset) no system-scope fence — they order
+// Fork/join events: no timing, and (CDX_SIDE_EVENT_FENCE=0 / unset) no system-scope fence — they order
 // two streams of one device, whose kernels see each other's writes at kernel boundaries anyway.
 unsigned side_event_flags() {
-  static const unsigned f = getenv("CDX_SIDE_EVENT_FENCE") ? hipEventDisableTiming
-                                                           : (hipEventDisableTiming | hipEventDisableSystemFence);
+  static const unsigned f = [] {
+    const char* e = getenv("CDX_SIDE_EVENT_FENCE");
+    return (e && atoi(e) != 0) ? (unsigned)hipEventDisableTiming
+                               : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
+  }();
   return f;
 }
 
