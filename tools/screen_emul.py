@@ -112,12 +112,16 @@ def main():
     results = {name: emul(As, Bs) + off * colsum for name, (As, off) in variants.items()}
     results["fp16 x2 (kernel)"] = (emul(split2h(Af16, 1.0, f16rtz), split2h(Lit, SB, f16), pairs=((0, 0), (0, 1), (1, 0)))
                                    / (SA * SB) + colsum)
+    A2, B2 = split2h(Af16, 1.0, f16rtz), split2h(Lit, SB, f16)
+    results["fp16 x1 (a0·b0)"] = emul(A2, B2, pairs=((0, 0),)) / (SA * SB) + colsum
+    results["fp16 a0·(b0+b1)"] = emul(A2, B2, pairs=((0, 0), (0, 1))) / (SA * SB) + colsum
+    results["fp16 (a0+a1)·b0"] = emul(A2, B2, pairs=((0, 0), (1, 0))) / (SA * SB) + colsum
     for name, Ve in results.items():
         s2e = k0 - (Ve * Ve).sum(1)
         err = np.abs(s2e - s2) / k0
         msg = f"{name:18s} |Δstd²|/k0 max {err.max():.2e} p99 {np.percentile(err, 99):.2e}"
         s2e4 = s2e.reshape(-1, 4)
-        for mult in (4, 8, 16):
+        for mult in (2, 4, 8, 16):
             delta = mult * err.max() * k0
             cand = (s2e4 + delta) >= (s2e4 - delta).max(1, keepdims=True)
             ok = cand[np.arange(len(amax)), amax].all()

@@ -28,7 +28,11 @@ VARIANTS = {"base": BASE,
             "diag_nomfma": BASE + ("CDX_SC_DIAG_NOMFMA",),
             "diag_nogen_nomfma": BASE + ("CDX_SC_DIAG_NOGEN", "CDX_SC_DIAG_NOMFMA")}
 # measured and dropped (profiles/r02j_screen_variants.jsonl): sched_group_barrier 1 MFMA : 6 VALU
-# interleave (+10 %), s_setprio 1 around the MFMA block (+6 %)
+# interleave (+10 %), s_setprio 1 around the MFMA block (+6 %).  Round 3 (profiles/r03j-l_*): B staged
+# through VGPRs + ds_write instead of LDS-DMA (+1 %); row-block order with A-fragment prefetch (+2 %);
+# X1 rows loaded one sub-step ahead (+4 %); both with a 1 MFMA : 4 VALU sched_group_barrier pipeline
+# (+4..9 %); X1 rows not loaded at all (diagnostic, ±0); a register-A kernel (each wave 32 rows × 256
+# columns, Ã generated in registers, only B through LDS, B ring of 2/3/4 by asm LDS-DMA) +4..6 %.
 if os.environ.get("CDX_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CDX_VARIANTS"].split(",")}
 
@@ -74,7 +78,9 @@ def child(lib, E):
     est0 = st.screen_var(X)
     err = float((est0 - exact_var(st, X)).abs().max()) / float(g.R) ** 3
     repeat_equal = all(torch.equal(est0, st.screen_var(X)) for _ in range(20))
-    print(json.dumps({"lib": os.path.basename(lib), "M": M, "screen_ms": ms, "max_err_over_k0": err, "bitwise_repeatable": repeat_equal,
+    import hashlib
+    digest = hashlib.sha256(est0.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(json.dumps({"lib": os.path.basename(lib), "M": M, "screen_ms": ms, "max_err_over_k0": err, "bitwise_repeatable": repeat_equal, "estimate_sha256": digest,
                       "f16_tflops": 3 * M * 2000 * 2001 / ms / 1e9}), flush=True)
 
 
