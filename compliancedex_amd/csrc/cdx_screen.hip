@@ -48,13 +48,17 @@ constexpr int SC_BM = 256;                 // query rows per workgroup
 #define CDX_SC_WAVES 8
 #endif
 // 8 waves (two per SIMD): 2 (rows) × 4 (columns), 128 × 64 outputs each; 4 waves (one per SIMD,
-// accumulators in AGPRs): 2 × 2, 128 × 128 outputs each (half the fragment reads per MFMA)
+// accumulators in AGPRs): 2 × 2, 128 × 128 outputs each (half the fragment reads per MFMA);
+// 16 waves (four per SIMD, ≤ 128 registers): 4 × 4, 64 × 64 outputs each
 constexpr int SC_W = CDX_SC_WAVES;
-static_assert(SC_W == 8 || SC_W == 4, "8 or 4 waves per workgroup");
+static_assert(SC_W == 8 || SC_W == 4 || SC_W == 16, "4, 8 or 16 waves per workgroup");
 constexpr int SC_THREADS = 64 * SC_W;
-constexpr int SC_WC = SC_W == 8 ? 64 : 128;  // columns per wave
-constexpr int SC_NJ = SC_WC / 32;            // 32-column accumulator blocks per wave
-constexpr int SC_GKH = SC_W == 8 ? 1 : 2;    // k-halves generated per thread per sub-step
+constexpr int SC_WC = SC_W == 4 ? 128 : 64;   // columns per wave
+constexpr int SC_WR = SC_W == 16 ? 64 : 128;  // rows per wave
+constexpr int SC_NJ = SC_WC / 32;             // 32-column accumulator blocks per wave
+constexpr int SC_NI = SC_WR / 32;             // 32-row accumulator blocks per wave
+constexpr int SC_GKH = SC_W == 4 ? 2 : 1;     // k-halves generated per thread per sub-step
+// 16 waves: each thread generates one (sub-step, k-half) chunk of the next stage
 constexpr int SC_REG = 4 * 256;            // 16-byte LDS units of one 16-K sub-step: [slice][khalf][256]
 #ifndef CDX_SC_SUB
 #define CDX_SC_SUB 2
@@ -74,11 +78,16 @@ static_assert(SC_SUB == 1 || SC_SUB == 2, "stage = 16 or 32 K rows");
 // other half each generates one 16-K sub-step of the next stage's A and DMAs its B.
 constexpr bool SC_PP = CDX_SC_PP;
 static_assert(!SC_PP || (SC_W == 8 && SC_SUB == 2 && SC_RING == 2), "ping-pong: 8 waves, 32-K stages, B ring of 2");
-constexpr int SC_LDT = 264;               // fp32 row pitch of the epilogue's accumulator image (4 rows ≡ 32 banks)
-// LDS: A stages (generated, 2 buffers) | B stages (LDS-DMA ring)
+// Epilogue image of one row half of the tile: fp32 rows of pitch SC_LDE ≡ 4 (mod 32), the e-th
+// 64-column share of a row rotated by 16·e dwords (sc_tcol): the accumulators' ds_write_b128 (8
+// consecutive rows per lane group) and the summing threads' ds_read_b128 (4 shares × 4 rows per
+// lane group) are both conflict-free.  Then the stripe's (cscale, csum) pairs, pair c at c + (c >> 6).
+constexpr int SC_LDE = 260;
+constexpr int SC_EPI_CF = 128 * SC_LDE * 4;
+constexpr int SC_EPI = SC_EPI_CF + (SC_BN + SC_BN / 64) * 16;
+// LDS: A stages (generated, 2 buffers) | B stages (LDS-DMA ring); after the loop, the epilogue
 constexpr int SC_A_OFF = 0, SC_B_OFF = 2 * SC_SUB * SC_REG * 16;
-constexpr int SC_SMEM = std::max(SC_B_OFF + SC_RING * SC_SUB * SC_REG * 16,  // stage buffers
-                                 128 * SC_LDT * 4);                          // epilogue: one row half of the tile
+constexpr int SC_SMEM = std::max(SC_B_OFF + SC_RING * SC_SUB * SC_REG * 16, SC_EPI);
 static_assert(SC_SMEM <= 160 * 1024, "screen stage buffers exceed the CU's LDS");
 
 // K-steps (16 rows of L⁻ᵀ) of stripe nt: rows [0, min(N, (nt+1)·256 − shift)) as in the fp64 pass.
@@ -111,7 +120,7 @@ __device__ __forceinline__ void split2(float xa, float xb, unsigned& h0, unsigne
 // One workgroup per (query tile of 256 rows, stripe of 256 columns); stripes paired heavy+light per
 // XCD as in gpis_std_kernel<VAR>.  partial[nt][m] = Σ over the stripe's columns of (Ã·L⁻ᵀ + c)².
 template <int KT>
-__global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
+__global__ __launch_bounds__(SC_THREADS, SC_W / 4) void gpis_screen_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
                                                                     double* __restrict__ partial, int64_t M_pad, int Mt,
                                                                     int Nt) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[SC_SMEM];
@@ -144,7 +153,8 @@ __global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_ker
 
   // generation: thread → query row grow, k-halves gkh .. gkh + SC_GKH − 1 (wave-uniform), 8 entries each
   const int grow = tid & (SC_BM - 1);
-  const int gkh = SC_W == 8 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;
+  const int gkh = SC_W == 4 ? 0 : __builtin_amdgcn_readfirstlane((tid >> 8) & 1);
+  const int gsub = SC_W == 16 ? __builtin_amdgcn_readfirstlane(tid >> 9) : 0;
   float qx, qy, qz;
   {
     const int64_t m = std::min(m0 + grow, M - 1);  // pad rows replicate a valid query
@@ -162,15 +172,16 @@ __global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_ker
 
   // wave → 128 × SC_WC output sub-tile; with 8 waves, waves w and w+4 share a SIMD and take
   // complementary columns
-  const int cwave = SC_W == 8 ? (wave < 4 ? wave : 7 - wave) : (wave & 1);
-  const int wr = (SC_W == 8 ? (wave >> 2) : (wave >> 1)) * 128;
+  // (16 waves: waves w, w+4, w+8, w+12 share a SIMD and take all four column quarters)
+  const int cwave = SC_W == 16 ? (((wave & 3) + (wave >> 2)) & 3) : SC_W == 8 ? (wave < 4 ? wave : 7 - wave) : (wave & 1);
+  const int wr = (SC_W == 16 ? (wave >> 2) : SC_W == 8 ? (wave >> 2) : (wave >> 1)) * SC_WR;
   const int wc = cwave * SC_WC;
   // B rows past this wave's last column are zero (upper-triangular L⁻ᵀ, shifted columns)
   const int kend_w = __builtin_amdgcn_readfirstlane(n0 + wc + SC_WC - shift);
 
-  f32x16 acc[4][SC_NJ];
+  f32x16 acc[SC_NI][SC_NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < SC_NI; ++i)
 #pragma unroll
     for (int j = 0; j < SC_NJ; ++j)
 #pragma unroll
@@ -233,7 +244,8 @@ __global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_ker
     }
   };
   // one sub-step's 12·SC_NJ MFMAs: lane → (row/col l&31, k-half l>>5); B slices of the wave's column
-  // blocks, A slice by slice (products of slice-index sum ≤ 1, smallest first)
+  // blocks, A slice by slice (products of slice-index sum ≤ 1, smallest first); each MFMA takes the
+  // B slice as its A operand (Ṽᵀ blocks: see the epilogue)
   auto mfma_sub = [&](int abuf, int bslot, int sub, auto more_c) {
     constexpr bool MORE = decltype(more_c)::value;
     const u32x4* a4 = sA4 + (abuf * SC_SUB + sub) * SC_REG;
@@ -250,9 +262,9 @@ __global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_ker
 #endif
 #pragma unroll
     for (int sa = 1; sa >= 0; --sa) {
-      f16x8 fa[4];
+      f16x8 fa[SC_NI];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < SC_NI; ++i)
 #if defined(CDX_SC_DIAG_NOREAD)
         fa[i] = __builtin_bit_cast(f16x8, u32x4{(unsigned)lane, (unsigned)i, (unsigned)sa, (unsigned)abuf});
 #else
@@ -261,13 +273,13 @@ __global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_ker
 #pragma unroll
       for (int sb = 1 - sa; sb >= 0; --sb)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < SC_NI; ++i)
 #pragma unroll
           for (int j = 0; j < SC_NJ; ++j)
 #if defined(CDX_SC_DIAG_NOMFMA)  // timing-only diagnostic build: outputs are wrong
             acc[i][j][0] += (float)fa[i][0] * (float)fb[sb][j][0];
 #else
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[sb][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[sb][j], fa[i], acc[i][j], 0, 0, 0);
 #endif
       if (!MORE) __builtin_amdgcn_sched_barrier(0);  // tail step: no fragment hoisting past a slice group
     }
@@ -279,8 +291,13 @@ __global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_ker
   // prologue: B stages 0 .. SC_RING−2 landed, A of stage 0 generated
 #pragma unroll
   for (int st = 0; st < SC_RING - 1; ++st) issue(st);
+  if constexpr (SC_W == 16) {
+    gen_a(0, gsub, gkh);
+    write_a(0, gsub, gkh);
+  } else {
 #pragma unroll
-  for (int u = 0; u < SC_SUB; ++u) gen_write(0, 0, u);
+    for (int u = 0; u < SC_SUB; ++u) gen_write(0, 0, u);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -296,7 +313,11 @@ __global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_ker
     if (SC_RING > 2 || s + 1 < nS) issue(s + SC_RING - 1);
 #pragma unroll
     for (int u = 0; u < SC_SUB; ++u) {
-      if (SC_GKH == 1) {
+      if constexpr (SC_W == 16) {
+        if (MORE && u == 0) gen_a(s + 1, gsub, gkh);
+        if (u < NLIVE) mfma_sub(s & 1, s % SC_RING, u, more_c);
+        if (MORE && u == 0) write_a((s + 1) & 1, gsub, gkh);
+      } else if (SC_GKH == 1) {
         if (MORE) gen_a(s + 1, u, gkh);
         if (u < NLIVE) mfma_sub(s & 1, s % SC_RING, u, more_c);
         if (MORE) write_a((s + 1) & 1, u, gkh);
@@ -372,45 +393,64 @@ __global__ __launch_bounds__(SC_THREADS, SC_W == 8 ? 2 : 1) void gpis_screen_ker
   __syncthreads();
 
   // Epilogue: per row Σ over the stripe's 256 columns of (Ṽ + c)² in f64.  The accumulators go
-  // through LDS one row half at a time ([128][SC_LDT] fp32, the stage buffers are free after the
-  // loop), then SC_THREADS/128 threads per row sum a share of its columns each and combine by
-  // xor-shuffles.  (Summing
-  // in registers needs the f64 squares of a whole row block live next to the accumulators and
-  // made the allocator spill.)  C map (32x32x16): reg r of lane l is row (r&3) + 8(r>>2) + 4(l>>5),
-  // column l&31.
+  // through LDS one row half at a time (the stage buffers are free after the loop), then EP threads
+  // per row sum a share of its columns each, in column order, and combine by xor-shuffles; the
+  // columns' (cscale, csum) come from LDS too (staged once: read from global memory per thread, they
+  // cost a quarter of the kernel).  (Summing in registers needs the f64 squares of a whole row block
+  // live next to the accumulators and made the allocator spill.)  The MFMAs compute Ṽᵀ (L⁻ᵀ slice
+  // as the A operand, Ã as B), so reg r of lane l holds query row l&31, column (r&3) + 8(r>>2) +
+  // 4(l>>5): four consecutive columns per register quad, one ds_write_b128.
+#if defined(CDX_SC_DIAG_NOEPI)  // timing-only diagnostic build: outputs are wrong
+  {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < SC_NI; ++i)
+#pragma unroll
+      for (int j = 0; j < SC_NJ; ++j) t += acc[i][j][0] + acc[i][j][15];
+    if (lane == 0) partial[(int64_t)nt * M_pad + m0 + wave] = t;
+    return;
+  }
+#endif
   float* T = reinterpret_cast<float*>(smem);
-  constexpr int EP = SC_THREADS / 128, ECOL = SC_BN / EP;  // threads per row, columns per thread
+  double2* CF = reinterpret_cast<double2*>(smem + SC_EPI_CF);
+  constexpr int EP = SC_W == 4 ? 2 : 4, ECOL = SC_BN / EP;  // threads per row, columns per thread
   const int erow = tid / EP, epart = tid % EP;
+  auto tcol = [](int c) { return (c & ~63) + (((c & 63) + 16 * (c >> 6)) & 63); };
+  if (tid < SC_BN) CF[tid + (tid >> 6)] = make_double2(sv.cscale[n0 + tid], sv.csum[n0 + tid]);
 #pragma unroll
   for (int ph = 0; ph < 2; ++ph) {
     if (ph) __syncthreads();  // phase 0's readers are done with T
-    if (wr == 128 * ph) {
+    if ((wr >> 7) == ph) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < SC_NI; ++i)
 #pragma unroll
         for (int j = 0; j < SC_NJ; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            T[(32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * SC_LDT + wc + 32 * j + (lane & 31)] = acc[i][j][r];
+          for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<float4*>(T + ((wr & 127) + 32 * i + (lane & 31)) * SC_LDE + tcol(wc + 32 * j + 8 * q + 4 * (lane >> 5))) =
+                make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
     }
     __syncthreads();
-    const float4* Tr = reinterpret_cast<const float4*>(T + erow * SC_LDT + ECOL * epart);
-    const double* cs = sv.csum + n0 + ECOL * epart;
-    const double* cf = sv.cscale + n0 + ECOL * epart;
-    double sum = 0.0;
+    if (tid < 128 * EP) {  // 16 waves: the first 8 sum (the same column split and order)
+      const float* Tr = T + erow * SC_LDE;
+      double sum = 0.0;
 #pragma unroll 4
-    for (int c = 0; c < ECOL / 4; ++c) {
-      const float4 v = Tr[c];
-      const double x0 = fma((double)v.x, cf[4 * c], cs[4 * c]), x1 = fma((double)v.y, cf[4 * c + 1], cs[4 * c + 1]),
-                   x2 = fma((double)v.z, cf[4 * c + 2], cs[4 * c + 2]), x3 = fma((double)v.w, cf[4 * c + 3], cs[4 * c + 3]);
-      sum = fma(x0, x0, sum);
-      sum = fma(x1, x1, sum);
-      sum = fma(x2, x2, sum);
-      sum = fma(x3, x3, sum);
-    }
+      for (int c = 0; c < ECOL / 4; ++c) {
+        const int c0 = ECOL * epart + 4 * c;  // 4 columns inside one 64-column share
+        const float4 v = *reinterpret_cast<const float4*>(Tr + tcol(c0));
+        const double2* p = CF + c0 + (c0 >> 6);
+        const double2 p0 = p[0], p1 = p[1], p2 = p[2], p3 = p[3];
+        const double x0 = fma((double)v.x, p0.x, p0.y), x1 = fma((double)v.y, p1.x, p1.y),
+                     x2 = fma((double)v.z, p2.x, p2.y), x3 = fma((double)v.w, p3.x, p3.y);
+        sum = fma(x0, x0, sum);
+        sum = fma(x1, x1, sum);
+        sum = fma(x2, x2, sum);
+        sum = fma(x3, x3, sum);
+      }
 #pragma unroll
-    for (int w = 1; w < EP; w <<= 1) sum += __shfl_xor(sum, w);
-    if (epart == 0) partial[(int64_t)nt * M_pad + m0 + 128 * ph + erow] = sum;
+      for (int w = 1; w < EP; w <<= 1) sum += __shfl_xor(sum, w);
+      if (epart == 0) partial[(int64_t)nt * M_pad + m0 + 128 * ph + erow] = sum;
+    }
   }
 }
 

@@ -21,12 +21,19 @@ VARIANTS = {"base": BASE,
             "pp": BASE + ("CDX_SC_PP=1",),  # ping-pong: the two waves of a SIMD multiply in alternate half-stages
             "w4": BASE + ("CDX_SC_WAVES=4",),  # 4 waves of 128 x 128 (one per SIMD, AGPR accumulators)
             "w4_sub1": BASE + ("CDX_SC_WAVES=4", "CDX_SC_SUB=1"),
+            "w16": BASE + ("CDX_SC_WAVES=16",),  # 16 waves of 64 x 64 (four per SIMD, <= 128 registers)
+            "w16_ring3": BASE + ("CDX_SC_WAVES=16", "CDX_SC_RING=3"),
             "diag_noread": BASE + ("CDX_SC_DIAG_NOREAD",),      # MFMAs on fragments read once per stage
             "diag_nobar": BASE + ("CDX_SC_DIAG_NOBAR",),        # no s_barrier in the loop (races)
             "diag_nodma": BASE + ("CDX_SC_DIAG_NODMA",),        # no B DMAs in the loop
             "diag_nogen": BASE + ("CDX_SC_DIAG_NOGEN",),
             "diag_nomfma": BASE + ("CDX_SC_DIAG_NOMFMA",),
-            "diag_nogen_nomfma": BASE + ("CDX_SC_DIAG_NOGEN", "CDX_SC_DIAG_NOMFMA")}
+            "diag_nogen_nomfma": BASE + ("CDX_SC_DIAG_NOGEN", "CDX_SC_DIAG_NOMFMA"),
+            # MFMAs only: fragments from lane ids, no generation, no B DMA, no barrier
+            "diag_mfma_only": BASE + ("CDX_SC_DIAG_NOREAD", "CDX_SC_DIAG_NOGEN", "CDX_SC_DIAG_NODMA", "CDX_SC_DIAG_NOBAR"),
+            "diag_noepi": BASE + ("CDX_SC_DIAG_NOEPI",),  # no epilogue (Σ (Ṽ + c)² through LDS)
+            "diag_noread_nogen": BASE + ("CDX_SC_DIAG_NOREAD", "CDX_SC_DIAG_NOGEN"),
+            "diag_noread_nodma": BASE + ("CDX_SC_DIAG_NOREAD", "CDX_SC_DIAG_NODMA")}
 # measured and dropped (profiles/r02j_screen_variants.jsonl): sched_group_barrier 1 MFMA : 6 VALU
 # interleave (+10 %), s_setprio 1 around the MFMA block (+6 %).  Round 3 (profiles/r03j-l_*): B staged
 # through VGPRs + ds_write instead of LDS-DMA (+1 %); row-block order with A-fragment prefetch (+2 %);
