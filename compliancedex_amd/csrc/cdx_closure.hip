@@ -237,14 +237,20 @@ __global__ __launch_bounds__(64) void force_eq_backward_kernel(
   }
 }
 
-template <int NT, int G>
+template <int NT, int G, bool PRE = false>
 __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_t E, const double* __restrict__ q,
                                                            const double* __restrict__ comp,
                                                            const double* __restrict__ target,
                                                            const double* __restrict__ X,
                                                            const double* __restrict__ noise, uint64_t seed,
                                                            GpisView gv, double* __restrict__ lvl,
-                                                           int32_t* __restrict__ flip) {
+                                                           int32_t* __restrict__ flip,
+                                                           const double* __restrict__ krot) {
+#if defined(CDX_LEVEL_PRIO)
+  // latency-bound dependent chains: issue first whenever ready, so that the GPIS mean's part B on
+  // the side stream (CDX_MEAN_SPLIT) fills the issue slots the chains leave without stretching them
+  __builtin_amdgcn_s_setprio(CDX_LEVEL_PRIO);
+#endif
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int K = P.n_levels;
   if (t >= K * E) return;
@@ -269,12 +275,13 @@ __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_
   }
   in.noise = nz;
   in.noise_stride = 0;
+  in.rot = krot ? krot + t * cdx::ForceEq<NT, G>::KABSCH_RECORD : nullptr;
   double dq[CDX_MAX_DOFS];
   const double qnorm = cdx::ref_dist(P, in.q, dq);
   GpisView g = gv;
   g.e = e;
   cdx::LevelOut lo;
-  cdx::level_fwd_bwd<NT, GpisView, G>(P, k, in, tip, qnorm, g, lo);
+  cdx::level_fwd_bwd<NT, GpisView, G, PRE>(P, k, in, tip, qnorm, g, lo);
   double* r = lvl + t * level_record_width(T);
   r[0] = lo.l;
   for (int f = 0; f < T; ++f) {
@@ -286,6 +293,45 @@ __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_
     }
   }
   if (flip) flip[t] = lo.flip;
+}
+
+// Per-(level, candidate) thread: the Kabsch stage of force_eq_reward (:49-69) — the weighted
+// cross-covariance of the level's all-tip points and the targets, its 3×3 SVD and the rotation — as a
+// record the level kernel loads instead of running the SVD itself (ForceEq::save_rotation).  Its inputs
+// are the query points, compliances, targets and the Kabsch noise only (not the GPIS results), so the
+// screened closure runs it on the side stream after the screen kernel, beside the latency-bound
+// selection and compaction, and takes the SVD (≈ 21 of the level kernel's 45 µs at E = 4096,
+// CDX_DIAG_NOSVD build) off the critical path.  Same
+// arithmetic as the inline path (both are ForceEq::rotation on the same values): bit-identical records.
+template <int NT, int G>
+__global__ __launch_bounds__(64) void closure_kabsch_kernel(cdx_problem P, int64_t E, const double* __restrict__ comp,
+                                                            const double* __restrict__ target,
+                                                            const double* __restrict__ X,
+                                                            const double* __restrict__ noise, uint64_t seed,
+                                                            double* __restrict__ krot) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int K = P.n_levels;
+  if (t >= K * E) return;
+  const int k = (int)(t / E);
+  const int64_t e = t - (int64_t)k * E;
+  const int T = NT > 0 ? NT : P.chain.n_tips, Lq = P.n_query_levels;
+  constexpr int NTA = cdx::ForceEq<NT, G>::NTA;
+  double a[NTA][3];
+  const double* tg = target + e * T * 3;
+  for (int f = 0; f < T; ++f) {
+    const double c = (double)P.coeff[k][f];  // the all-tip point exactly as level_fwd_bwd forms it
+    for (int i = 0; i < 3; ++i) a[f][i] = tg[3 * f + i] + c * (X[3 * cdx::q_pre(Lq, e, f, E, T) + i] - tg[3 * f + i]);
+  }
+  double nz[9];
+  if (noise) {
+    for (int i = 0; i < 9; ++i) nz[i] = noise[t * 9 + i];
+  } else {
+    device_noise(P.loop ? seed ^ splitmix64(P.loop->seed) : seed, t, nz);
+  }
+  cdx::ForceEq<NT, G> fe;
+  fe.setup(cdx::force_eq_params(P), T, a, tg, comp + e * T, nullptr);
+  fe.rotation(nz);
+  fe.save_rotation(krot + t * cdx::ForceEq<NT, G>::KABSCH_RECORD);
 }
 
 // Per-candidate group of GS lanes, lane f = fingertip f: sums the levels, adds the pregrasp
@@ -412,6 +458,7 @@ size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 struct ClosureWs {
   double *X, *mean, *gmean, *normal, *std_, *var, *gstd, *Xg, *lvl, *V;
+  double* krot;  // Kabsch records [n_levels·E][KABSCH_RECORD] (screened closure: computed on the side stream)
   int64_t* sel;
   void *var_ws, *grad_ws;
   // split-precision screening (screen_on): estimates, list positions, the kept-row list, per-group
@@ -494,6 +541,7 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   w.screen_ws = scr ? take(cdx::screen_ws_bytes(p->gpis, Ms)) : nullptr;
   w.refine_ws = scr ? take(cdx::gpis_refine_ws_bytes(p->gpis, Ms)) : nullptr;
   w.lvl = (double*)take((size_t)p->n_levels * E * level_record_width(p->chain.n_tips) * sizeof(double));
+  w.krot = scr ? (double*)take((size_t)p->n_levels * E * cdx::ForceEq<0>::KABSCH_RECORD * sizeof(double)) : nullptr;
 #if !defined(CDX_GRAD_EXPLICIT)
   w.V = (double*)take(cdx::gpis_v_bytes(p->gpis, Ms));
 #else
@@ -527,6 +575,18 @@ bool mean_split() {
   return on;
 }
 
+// Kabsch records computed ahead of the level kernel (closure_kabsch_kernel), CDX_KABSCH_AHEAD: 1
+// (default) on the side stream ahead of the mean, one fork after the screen kernel; 0 the level kernel
+// runs the SVD itself.  (A stream of their own, with their own fork / join events, measured 1.24–1.26
+// vs 1.05 ms per closure — the refine pass slowed 0.34 → 0.58 ms; profiles/r03t_kabsch_ab.jsonl.)
+int kabsch_mode() {
+  static const int m = [] {
+    const char* e = getenv("CDX_KABSCH_AHEAD");
+    return e && atoi(e) == 0 ? 0 : 1;
+  }();
+  return m;
+}
+
 // Fork/join events: no timing, and (CDX_SIDE_EVENT_FENCE=0 / unset) no system-scope fence — they order
 // two streams of one device, whose kernels see each other's writes at kernel boundaries anyway.
 unsigned side_event_flags() {
@@ -545,7 +605,6 @@ bool side_stream(SideStream& out) {
   SideStream& ss = per_dev[dev];
   if (!ss.s) {
     hipStream_t st;
-    hipEvent_t a, b;
     // CDX_SIDE_PRIO: < 0 creates the side stream at the device's lowest priority, > 0 at its
     // highest (the CP prefers a higher-priority queue's dispatches), 0 (default) normal.
     const char* pe = getenv("CDX_SIDE_PRIO");
@@ -560,38 +619,20 @@ bool side_stream(SideStream& out) {
       (void)hipGetLastError();
       return false;
     }
-    if (hipEventCreateWithFlags(&a, side_event_flags()) != hipSuccess) {
-      (void)hipStreamDestroy(st);
-      (void)hipGetLastError();
-      return false;
-    }
-    if (hipEventCreateWithFlags(&b, side_event_flags()) != hipSuccess) {
-      (void)hipEventDestroy(a);
-      (void)hipStreamDestroy(st);
-      (void)hipGetLastError();
-      return false;
-    }
-    hipEvent_t c, d;
-    if (hipEventCreateWithFlags(&c, side_event_flags()) != hipSuccess) {
-      (void)hipEventDestroy(a);
-      (void)hipEventDestroy(b);
-      (void)hipStreamDestroy(st);
-      (void)hipGetLastError();
-      return false;
-    }
-    if (hipEventCreateWithFlags(&d, side_event_flags()) != hipSuccess) {
-      (void)hipEventDestroy(a);
-      (void)hipEventDestroy(b);
-      (void)hipEventDestroy(c);
-      (void)hipStreamDestroy(st);
-      (void)hipGetLastError();
-      return false;
+    hipEvent_t ev[4];
+    for (int i = 0; i < 4; ++i) {
+      if (hipEventCreateWithFlags(&ev[i], side_event_flags()) != hipSuccess) {
+        for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
+        (void)hipStreamDestroy(st);
+        (void)hipGetLastError();
+        return false;
+      }
     }
     ss.s = st;
-    ss.fork = a;
-    ss.join = b;
-    ss.gate = c;
-    ss.joinB = d;
+    ss.fork = ev[0];
+    ss.join = ev[1];
+    ss.gate = ev[2];
+    ss.joinB = ev[3];
   }
   out = ss;
   return true;
@@ -716,6 +757,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   SideStream ss;
   const bool fork = scr && fork_mean() && side_stream(ss);
   const SideStream* pending_b = nullptr;  // mean B still to be joined before the combine kernel
+  const double* krot = nullptr;           // Kabsch records computed ahead (else the level kernel's own SVD)
   int rc;
   if (!fork) {
     rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
@@ -737,9 +779,34 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     bool forked = false, forkedB = false;
     const int64_t MqA = mean_split() ? (int64_t)(p->n_query_levels + 1) * E * T : Mq;  // rows of mean A
     const cdx_stream_t side = reinterpret_cast<cdx_stream_t>(ss.s);
+    // The Kabsch records (closure_kabsch_kernel, kabsch_mode() 1): first on the side stream, right
+    // after the screen kernel (the screen's waves leave too few registers for them to run beside it;
+    // after it they share the chip with the latency-bound selection and compaction), then mean A on
+    // the same stream — one fork, one join: every event record / wait on `s` costs ≈ 5 µs of stream
+    // time (profiles/r03s_*).  The mean is effectively serial after the refine pass anyway (it cannot
+    // share a CU with it), so queueing it behind the records costs nothing.
+    const int kmode = fork ? kabsch_mode() : 0;
+    auto launch_records = [&](hipStream_t st) {
+      const int64_t KE = (int64_t)p->n_levels * E;
+      const dim3 kg((unsigned)((KE + 63) / 64));
+      if (T == 4 && p->gravity)
+        hipLaunchKernelGGL((closure_kabsch_kernel<4, 1>), kg, dim3(64), 0, st, *p, E, comp, target, w.X, kabsch_noise,
+                           seed, w.krot);
+      else if (T == 4)
+        hipLaunchKernelGGL((closure_kabsch_kernel<4, 0>), kg, dim3(64), 0, st, *p, E, comp, target, w.X, kabsch_noise,
+                           seed, w.krot);
+      else
+        hipLaunchKernelGGL((closure_kabsch_kernel<0, -1>), kg, dim3(64), 0, st, *p, E, comp, target, w.X,
+                           kabsch_noise, seed, w.krot);
+      return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+    };
     auto launch_fork = [&]() -> int {
       forked = true;
       if (hipEventRecord(ss.fork, s) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess) return CDX_ELAUNCH;
+      if (kmode == 1) {
+        const int r = launch_records(ss.s);
+        if (r) return r;
+      }
       const int r = cdx_gpis_mean(&p->gpis, w.X, MqA, w.mean, w.gmean, w.normal, side);
       if (r) return r;
       return hipEventRecord(ss.join, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
@@ -758,30 +825,33 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
       if (forkedB && hipStreamWaitEvent(s, ss.joinB, 0) != hipSuccess && !r) r = CDX_ELAUNCH;
       return r;
     };
-    if (fork && fork_point() == 1 && (rc = launch_fork())) return joined(rc);
+    // the mean's fork point (kabsch_mode 1 forks once, after the screen, whatever fork_point says)
+    const int fp = kmode == 1 ? 4 : (fork ? fork_point() : 0);
+    if (fp == 1 && (rc = launch_fork())) return joined(rc);
     auto fork_cb = [](void* c) { return (*static_cast<decltype(launch_fork)*>(c))(); };
-    const bool fork_after_screen = fork && fork_point() == 4;
     rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.stats,
-                                   s, fork_after_screen ? +fork_cb : nullptr, &launch_fork);
+                                   s, fp == 4 ? +fork_cb : nullptr, &launch_fork);
     if (rc) return joined(rc);
-    if (fork && fork_point() == 2 && (rc = launch_fork())) return joined(rc);
+    if (fp == 2 && (rc = launch_fork())) return joined(rc);
     double* rpart = nullptr;
     int64_t rpad = 0;
     rc = cdx::gpis_refine_launch(p->gpis, w.X, w.rows, w.stats + cdx::SS_EXTRA, (int)Mg, Ms, w.refine_ws, w.V, s, &rpart,
                                  &rpad);
     if (rc) return joined(rc);
-    if (fork && fork_point() == 3 && (rc = launch_fork())) return joined(rc);
+    if (fp == 3 && (rc = launch_fork())) return joined(rc);
     rc = cdx::refine_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.sv2, w.vpos, w.keep, w.std_, w.var, w.sel,
                                    w.Xg, w.vrow, w.stats, s);
     if (rc) return joined(rc);
     rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V, w.vrow);
     if (rc) return joined(rc);
     if (fork && (rc = launch_b())) return joined(rc);
-    // mean A before the level kernel; mean B is joined before the combine kernel below
+    // mean A (and the Kabsch records of mode 1) before the level kernel; mean B is joined before the
+    // combine kernel below
     if (forked && hipStreamWaitEvent(s, ss.join, 0) != hipSuccess) {
       forked = false;
       return joined(CDX_ELAUNCH);
     }
+    if (kmode == 1 && forked) krot = w.krot;
     if (forkedB) pending_b = &ss;
   } else {
     const cdx::VarSelect vs{p->chain.n_tips, w.sel, w.Xg};
@@ -797,15 +867,18 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   {
     const int64_t KE = (int64_t)p->n_levels * E;
     const dim3 lgrid((unsigned)((KE + 63) / 64));
-    if (p->chain.n_tips == 4 && p->gravity)
+    if (p->chain.n_tips == 4 && p->gravity && krot)
+      hipLaunchKernelGGL((closure_level_kernel<4, 1, true>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
+                         kabsch_noise, seed, gv, w.lvl, flip, krot);
+    else if (p->chain.n_tips == 4 && p->gravity)
       hipLaunchKernelGGL((closure_level_kernel<4, 1>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gv, w.lvl, flip);
+                         kabsch_noise, seed, gv, w.lvl, flip, krot);
     else if (p->chain.n_tips == 4)
       hipLaunchKernelGGL((closure_level_kernel<4, 0>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gv, w.lvl, flip);
+                         kabsch_noise, seed, gv, w.lvl, flip, krot);
     else
       hipLaunchKernelGGL((closure_level_kernel<0, -1>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gv, w.lvl, flip);
+                         kabsch_noise, seed, gv, w.lvl, flip, krot);
     if (hipGetLastError() != hipSuccess) {
       if (pending_b) (void)hipStreamWaitEvent(s, pending_b->joinB, 0);
       return CDX_ELAUNCH;

@@ -39,6 +39,11 @@ CDX_HD void svd3_cswap(double* s, double* A, double* V, int j) {
 // with high relative accuracy for the small singular values the rank-1-plus-noise
 // Kabsch matrices of the reference's initial configuration have.
 CDX_HD void svd3(const double* H, double* U, double* S, double* V) {
+#if defined(CDX_DIAG_NOSVD)  // timing-only diagnostic build (outputs wrong): the level kernel without its SVD
+  for (int i = 0; i < 9; ++i) { U[i] = V[i] = (i % 4 == 0) ? 1.0 : 0.0; }
+  S[0] = 3.0 + H[0]; S[1] = 2.0 + H[4]; S[2] = 1.0 + H[8];
+  return;
+#endif
   double A[9];
   for (int i = 0; i < 9; ++i) { A[i] = H[i]; V[i] = (i % 4 == 0) ? 1.0 : 0.0; }
   for (int sweep = 0; sweep < 12; ++sweep) {
@@ -219,6 +224,7 @@ struct CandidateIn {
   const double *q, *comp, *target, *palm_pos, *palm_ori;  // this candidate's rows
   const double* noise;                                     // [K][9] for this candidate (stride via noise_stride)
   int64_t noise_stride;                                    // doubles between levels
+  const double* rot = nullptr;  // this level's Kabsch record (ForceEq::save_rotation), or null: SVD inline
 };
 
 struct CandidateOut {
@@ -274,8 +280,9 @@ struct ForceEq {
   double reward;
   int flip;
 
-  CDX_HDM void forward(const ForceEqParams& fp, int T_, const double (*tip)[3], const double* target,
-                      const double* comp, const double (*nrm)[3], const double* noise) {
+  // The points, weights and centroids of the weighted Kabsch fit (everything before the SVD).
+  CDX_HDM void setup(const ForceEqParams& fp, int T_, const double (*tip)[3], const double* target, const double* comp,
+                     const double (*nrm)[3]) {
     T_rt = T_;
     const int T = NT > 0 ? NT : T_;
     const bool grav = G >= 0 ? G != 0 : fp.gravity != 0;
@@ -283,7 +290,7 @@ struct ForceEq {
     const int NP = (NT > 0 && G >= 0) ? (G ? NT + 1 : NT) : NP_rt;
 #pragma unroll
     for (int f = 0; f < T; ++f) {
-      for (int i = 0; i < 3; ++i) { S1[f][i] = tip[f][i]; S2[f][i] = target[3 * f + i]; n[f][i] = nrm[f][i]; }
+      for (int i = 0; i < 3; ++i) { S1[f][i] = tip[f][i]; S2[f][i] = target[3 * f + i]; n[f][i] = nrm ? nrm[f][i] : 0.0; }
       w[f] = comp[f];
     }
     if (grav) {
@@ -297,6 +304,11 @@ struct ForceEq {
     for (int i = 0; i < NP; ++i)
       for (int j = 0; j < 3; ++j) { c1[j] += S1[i][j]; c2[j] += S2[i][j]; }
     for (int j = 0; j < 3; ++j) { c1[j] /= NP; c2[j] /= NP; }
+  }
+
+  // H = Σ w_i (S1_i − c1)(w_i (S2_i − c2))ᵀ, then the rotation and its tape (R = V·D·Uᵀ of H + 1e-6·noise).
+  CDX_HDM void rotation(const double* noise) {
+    const int NP = (NT > 0 && G >= 0) ? (G ? NT + 1 : NT) : NP_rt;
     double H[9];
     {
       double Pm[NTA + 1][3], Qm[NTA + 1][3];
@@ -318,6 +330,26 @@ struct ForceEq {
       kabsch_rotation(H, noise, t_, R);
       tp = t_;
     }
+  }
+
+  // The rotation stage as a record of KABSCH_RECORD doubles [U, S, V, d, R] (closure_kabsch_kernel
+  // computes it ahead of the level kernel) and back.
+  static constexpr int KABSCH_RECORD = 32;
+  CDX_HDM void save_rotation(double* rec) const {
+    for (int i = 0; i < 9; ++i) { rec[i] = tp.U[i]; rec[12 + i] = tp.V[i]; rec[22 + i] = R[i]; }
+    for (int i = 0; i < 3; ++i) rec[9 + i] = tp.S[i];
+    rec[21] = tp.d;
+  }
+  CDX_HDM void load_rotation(const double* rec) {
+    for (int i = 0; i < 9; ++i) { tp.U[i] = rec[i]; tp.V[i] = rec[12 + i]; R[i] = rec[22 + i]; }
+    for (int i = 0; i < 3; ++i) tp.S[i] = rec[9 + i];
+    tp.d = rec[21];
+  }
+
+  // Everything after the rotation: translation, equilibrium residuals, friction margins, reward.
+  CDX_HDM void finish(const ForceEqParams& fp, const double* comp) {
+    const int T = NT > 0 ? NT : T_rt;
+    const int NP = (NT > 0 && G >= 0) ? (G ? NT + 1 : NT) : NP_rt;
     flip = tp.d < 0 ? 1 : 0;
     W = 0.0;
     double num[3] = {0, 0, 0};
@@ -343,6 +375,17 @@ struct ForceEq {
       fn[f] = sqrt(dot3(force, force));
       reward += 0.2 * log(ang[f] + 1) + 0.8 * log(margin[f] + 1);
     }
+  }
+
+  // rot: a record save_rotation wrote for the same inputs, or null (the SVD runs here).
+  CDX_HDM void forward(const ForceEqParams& fp, int T_, const double (*tip)[3], const double* target,
+                      const double* comp, const double (*nrm)[3], const double* noise, const double* rot = nullptr) {
+    setup(fp, T_, tip, target, comp, nrm);
+    if (rot)
+      load_rotation(rot);
+    else
+      rotation(noise);
+    finish(fp, comp);
   }
 
   // diff_f = R·S1_f + t − target_f (S2_f holds target_f)
@@ -452,7 +495,7 @@ struct LevelOut {
   int flip;
 };
 
-template <int NT, typename GpisAt, int G = -1>
+template <int NT, typename GpisAt, int G = -1, bool PRE = false>
 CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, const double (*tip)[3], double qnorm,
                           GpisAt gp, LevelOut& o) {
   constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
@@ -476,7 +519,13 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
     td[f] = gp(1, 0, f).mean;
   }
   ForceEq<NT, G> fe;
-  fe.forward(force_eq_params(P), T, a, in.target, in.comp, n, in.noise + k * in.noise_stride);
+  if constexpr (PRE) {  // the Kabsch record is given (in.rot): no SVD code in this instantiation
+    fe.setup(force_eq_params(P), T, a, in.target, in.comp, n);
+    fe.load_rotation(in.rot);
+    fe.finish(force_eq_params(P), in.comp);
+  } else {
+    fe.forward(force_eq_params(P), T, a, in.target, in.comp, n, in.noise + k * in.noise_stride, in.rot);
+  }
   o.flip = fe.flip;
   // contact margin (unclamped), from the copies ForceEq keeps (fe.S1 = a, fe.S2 = target, fe.n = n):
   // the backward recomputes it the same way, so a and n need not stay live through the SVD

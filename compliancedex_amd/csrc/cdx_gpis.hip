@@ -629,6 +629,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     // partial[pslot = chunk][M_pad][N_pad] instead; gpis_var_splitk_finalize sums the chunks.
     double* red = smem;  // [ST_WN][ST_BM]
     if (LIST && !full) {  // a cut stripe: this segment's partial V tile to its slot
+#if !defined(CDX_DIAG_NOVSTORE)  // timing-only diagnostic build (outputs wrong): no V / partial-tile stores
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -637,6 +638,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
 #pragma unroll
           for (int j = 0; j < 4; ++j) vr[16 * j] = acc[i][j][r];
         }
+#endif
       return;
     }
     if (!LIST && parts > 0) {
@@ -651,7 +653,11 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
         }
       return;
     }
+#if defined(CDX_DIAG_NOVSTORE)
+    if (vout && !LIST) {
+#else
     if (vout) {
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll

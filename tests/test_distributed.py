@@ -242,16 +242,23 @@ def test_optimize_sharded_one_object_per_rank_gloo_world2():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("E,cap", [(4096, 4096), (4096, 7), (1, 3), (0, 5), (3000, 1500)])
+@pytest.mark.parametrize("E,cap", [(4096, 4096), (4096, 7), (1, 3), (0, 5), (3000, 1500), (5000, 2100), (2049, 9000),
+                                   (1024, 0)])
 def test_native_pack_equals_cpu_layout(E, cap):
     """cdx_pack_survivors (the GPU pack: one launch, header counts written on the device, no host
-    sync) produces bit for bit the buffer of the CPU (torch-ops) layout: survivors in candidate order,
-    overflow counted in the header, unused rows zero; NaN margins do not survive."""
+    sync, no memset) produces bit for bit the buffer of the CPU (torch-ops) layout: survivors in
+    candidate order, overflow counted in the header, unused rows zero — also when the buffer was dirty
+    before (the kernel zeroes them itself); NaN margins do not survive.  Ragged sizes cross the
+    kernel's 1024-candidate tiles with the capacity cut inside a tile."""
     d = _local(3, E=E)
     if E:
         d["margin"][0, 0] = float("nan")
     cpu = pack_survivors(cap, 5, 1, 10, **d)
-    gpu = pack_survivors(cap, 5, 1, 10, **{k: v.cuda() for k, v in d.items()})
+    dg = {k: v.cuda() for k, v in d.items()}
+    dirty = torch.full(((cap + 1) * record_width(d["q"].shape[1], d["margin"].shape[1]),), float("nan"),
+                       dtype=torch.float64, device="cuda")
+    del dirty  # the caching allocator hands the NaN-filled block to the pack's buffer
+    gpu = pack_survivors(cap, 5, 1, 10, **dg)
     torch.cuda.synchronize()
     assert torch.equal(gpu.cpu(), cpu)
     assert torch.equal(unpack_records([gpu]).cpu(), unpack_records([cpu]))

@@ -376,3 +376,59 @@ def test_screened_graph_first_capture_creates_side_stream():
     r = subprocess.run([sys.executable, "-c", _FIRST_CAPTURE.format(repo=REPO)], capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and "first-capture ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
+_KABSCH_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {repo!r})
+from compliancedex_amd import ProbabilisticGraspOptimizer
+from compliancedex_amd.urdf import load_robot
+from compliancedex_amd.workloads import prob_inputs, synthetic_banana_gpis
+cfg = load_robot("allegro")["config"]
+g = synthetic_banana_gpis(2000, device="cuda")
+q, comp, target, palm = prob_inputs(cfg["ref_q"], 4096, seed=321, spread=True)
+out = {{}}
+for mode in ("given", "device"):
+    opt = ProbabilisticGraspOptimizer("allegro", cfg["ee_link_name"], cfg["ee_link_offset"], palm_offset=palm,
+                                      ref_q=cfg["ref_q"], optimize_target=True, optimize_palm=True, device="cuda",
+                                      seed=77)
+    t = [torch.from_numpy(np.ascontiguousarray(a)).cuda().requires_grad_(True)
+         for a in (q, comp, target, palm[:, :3], palm[:, 3:])]
+    noise = (torch.from_numpy(np.random.default_rng(7).random((3 * 4096, 3, 3))).cuda() if mode == "given" else None)
+    opt.closure(*t, 1, g, 4096, kabsch_noise=noise)
+    torch.cuda.synchronize()
+    out[mode + "_loss"] = opt.total_loss.cpu().numpy()
+    out[mode + "_margin"] = opt.total_margin.cpu().numpy()
+    out[mode + "_flip"] = opt.kabsch_flip.cpu().numpy()
+    for i, x in enumerate(t):
+        out[mode + "_g%d" % i] = x.grad.cpu().numpy()
+np.savez({path!r}, **out)
+print("kabsch child ok")
+"""
+
+
+def test_kabsch_records_ahead_bit_identical(tmp_path):
+    """The screened closure computes the Kabsch records (SVD of the weighted cross-covariance) on a
+    side stream ahead of the level kernel (closure_kabsch_kernel, ahead of the mean on its stream); with
+    CDX_KABSCH_AHEAD=0 the level kernel runs the SVD itself.  Both give bit-identical losses, margins, Kabsch masks and gradients, with
+    the Kabsch noise given and drawn on the device.  (The switch is read once per process: one child
+    per setting.)"""
+    import os
+    import subprocess
+    import sys
+    from tests.conftest import REPO
+    res = {}
+    for ahead in ("1", "0"):
+        path = str(tmp_path / f"k{ahead}.npz")
+        env = dict(os.environ, CDX_KABSCH_AHEAD=ahead)
+        r = subprocess.run([sys.executable, "-c", _KABSCH_CHILD.format(repo=REPO, path=path)], capture_output=True,
+                           text=True, timeout=240, env=env)
+        assert r.returncode == 0 and "kabsch child ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+        res[ahead] = np.load(path)
+    a = res["0"]
+    for mode in ("1",):
+        b = res[mode]
+        assert set(a.files) == set(b.files)
+        for k in a.files:
+            assert np.array_equal(a[k], b[k], equal_nan=True), (mode, k)
+    assert np.isfinite(a["given_loss"]).sum() > 4000
