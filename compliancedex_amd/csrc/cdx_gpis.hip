@@ -772,6 +772,9 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     const int64_t q0 = total * pc / pieces, q1 = total * (pc + 1) / pieces;
     bool first = true;
     __shared__ int s_last;
+#if defined(CDX_DIAG_WGTIME)
+    int n_seg = 0;
+#endif
     for (int64_t q = q0; q < q1;) {
       int nt, mt;
       int64_t S0, S1;
@@ -803,7 +806,19 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
       }
 #endif
       q = e;
+#if defined(CDX_DIAG_WGTIME)
+      ++n_seg;
+#endif
     }
+#if defined(CDX_DIAG_WGTIME)  // the piece's [start, end], HW ids, (segments, K-steps)
+    if (tid == 0 && b < 16384) {
+      cdx_wgtime[b][0] = t_start;
+      cdx_wgtime[b][1] = __builtin_amdgcn_s_memrealtime();
+      cdx_wgtime[b][2] = ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32) |
+                         (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+      cdx_wgtime[b][3] = ((unsigned long long)n_seg << 32) | (unsigned)(q1 - q0);
+    }
+#endif
     return;
   }
   if (MODE == MODE_GRADV) {

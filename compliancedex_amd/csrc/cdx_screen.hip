@@ -74,6 +74,9 @@ static_assert(SC_SUB == 1 || SC_SUB == 2, "stage = 16 or 32 K rows");
 #ifndef CDX_SC_PP
 #define CDX_SC_PP 0
 #endif
+#ifndef CDX_SC_EPI_REG  // epilogue from the accumulator registers (1, default) or through an LDS image (0)
+#define CDX_SC_EPI_REG 1
+#endif
 // Ping-pong: the two waves of a SIMD (waves w, w+4) multiply in alternate half-stages; in the
 // other half each generates one 16-K sub-step of the next stage's A and DMAs its B.
 constexpr bool SC_PP = CDX_SC_PP;
@@ -392,14 +395,15 @@ __global__ __launch_bounds__(SC_THREADS, SC_W / 4) void gpis_screen_kernel(cdx_g
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // Epilogue: per row Σ over the stripe's 256 columns of (Ṽ + c)² in f64.  The accumulators go
-  // through LDS one row half at a time (the stage buffers are free after the loop), then EP threads
-  // per row sum a share of its columns each, in column order, and combine by xor-shuffles; the
-  // columns' (cscale, csum) come from LDS too (staged once: read from global memory per thread, they
-  // cost a quarter of the kernel).  (Summing in registers needs the f64 squares of a whole row block
-  // live next to the accumulators and made the allocator spill.)  The MFMAs compute Ṽᵀ (L⁻ᵀ slice
-  // as the A operand, Ã as B), so reg r of lane l holds query row l&31, column (r&3) + 8(r>>2) +
-  // 4(l>>5): four consecutive columns per register quad, one ds_write_b128.
+  // Epilogue: per row Σ over the stripe's 256 columns of (Ṽ + c)² in f64.  The MFMAs compute Ṽᵀ (L⁻ᵀ
+  // slice as the A operand, Ã as B), so reg r of lane l holds query row l&31, column (r&3) + 8(r>>2) +
+  // 4(l>>5).  Default (CDX_SC_EPI_REG=1): each lane sums its own columns straight from the accumulators
+  // into one f64 per row block (below; 0.175 vs 0.181 ms per screen in the closure, standalone 0.207–0.211
+  // vs 0.218 ms against 0.200–0.204 with no epilogue at all, profiles/r03u_screen_epilogue_ab.jsonl).
+  // CDX_SC_EPI_REG=0: the accumulators go through LDS one row half at a time (four consecutive columns
+  // per register quad, one ds_write_b128, rotated conflict-free image), then EP threads per row sum a
+  // share of its columns each, in column order, and combine by xor-shuffles.  Both stage the columns'
+  // (cscale, csum) in LDS once (read from global memory per thread, they cost a quarter of the kernel).
 #if defined(CDX_SC_DIAG_NOEPI)  // timing-only diagnostic build: outputs are wrong
   {
     float t = 0.f;
@@ -408,6 +412,45 @@ __global__ __launch_bounds__(SC_THREADS, SC_W / 4) void gpis_screen_kernel(cdx_g
 #pragma unroll
       for (int j = 0; j < SC_NJ; ++j) t += acc[i][j][0] + acc[i][j][15];
     if (lane == 0) partial[(int64_t)nt * M_pad + m0 + wave] = t;
+    return;
+  }
+#endif
+#if CDX_SC_EPI_REG
+  // Register epilogue: each lane sums (Ṽ·cscale + csum)² over its own 32 columns of its rows straight
+  // from the accumulators (columns in (j, r) order, the (cscale, csum) pairs broadcast from LDS), the
+  // two column halves of a lane pair combine by one xor-shuffle, and the column waves of a row through
+  // LDS in column-wave order — no accumulator image in LDS and one barrier instead of three.
+  {
+    double2* CF = reinterpret_cast<double2*>(smem);                          // [SC_BN] (cscale, csum)
+    double* red = reinterpret_cast<double*>(smem + SC_BN * sizeof(double2));  // [SC_BN / SC_WC][SC_BM]
+    if (tid < SC_BN) CF[tid] = make_double2(sv.cscale[n0 + tid], sv.csum[n0 + tid]);
+    __syncthreads();
+    double sum[SC_NI];
+#pragma unroll
+    for (int i = 0; i < SC_NI; ++i) sum[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < SC_NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const double2 cf = CF[wc + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
+#pragma unroll
+        for (int i = 0; i < SC_NI; ++i) {
+          const double x = fma((double)acc[i][j][r], cf.x, cf.y);
+          sum[i] = fma(x, x, sum[i]);
+        }
+      }
+#pragma unroll
+    for (int i = 0; i < SC_NI; ++i) {
+      sum[i] += __shfl_xor(sum[i], 32);
+      if (lane < 32) red[cwave * SC_BM + wr + 32 * i + lane] = sum[i];
+    }
+    __syncthreads();
+    if (tid < SC_BM) {
+      double t = 0.0;
+#pragma unroll
+      for (int c = 0; c < SC_BN / SC_WC; ++c) t += red[c * SC_BM + tid];
+      partial[(int64_t)nt * M_pad + m0 + tid] = t;
+    }
     return;
   }
 #endif

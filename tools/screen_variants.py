@@ -32,6 +32,8 @@ VARIANTS = {"base": BASE,
             # MFMAs only: fragments from lane ids, no generation, no B DMA, no barrier
             "diag_mfma_only": BASE + ("CDX_SC_DIAG_NOREAD", "CDX_SC_DIAG_NOGEN", "CDX_SC_DIAG_NODMA", "CDX_SC_DIAG_NOBAR"),
             "diag_noepi": BASE + ("CDX_SC_DIAG_NOEPI",),  # no epilogue (Σ (Ṽ + c)² through LDS)
+            "epireg": BASE + ("CDX_SC_EPI_REG=1",),  # epilogue summed from the accumulator registers
+            "epilds": BASE + ("CDX_SC_EPI_REG=0",),  # epilogue through the LDS image
             "diag_noread_nogen": BASE + ("CDX_SC_DIAG_NOREAD", "CDX_SC_DIAG_NOGEN"),
             "diag_noread_nodma": BASE + ("CDX_SC_DIAG_NOREAD", "CDX_SC_DIAG_NODMA")}
 # measured and dropped (profiles/r02j_screen_variants.jsonl): sched_group_barrier 1 MFMA : 6 VALU
@@ -92,7 +94,7 @@ def child(lib, E):
 
 
 def run(E):
-    for name in VARIANTS:
+    for name in list(VARIANTS) * int(os.environ.get("CDX_VARIANT_ROUNDS", "1")):
         lib = os.path.join(REPO, "compliancedex_amd", "lib", f"libcdx_sc_{name}.so")
         if os.path.exists(lib):
             subprocess.run([sys.executable, __file__, "child", lib, str(E)], check=False, timeout=300)
