@@ -133,6 +133,13 @@ struct GpisView {
   int T, Lq;
   __device__ cdx::GpisPoint operator()(int kind, int u, int f) const;
   int64_t e;
+  // ∇std folded into the level kernel (screened closure): the kernel sums its group's ∇std from the pass's
+  // piece partials once (cdx::grad_fold_gstd with sel / var) into gsv, the value of all-tip row gq
+  cdx::GradFold fold;
+  const double* var = nullptr;
+  const int64_t* sel = nullptr;
+  int64_t gq = -1;
+  double gsv[3] = {0, 0, 0};
 };
 
 __device__ cdx::GpisPoint GpisView::operator()(int kind, int u, int f) const {
@@ -146,7 +153,12 @@ __device__ cdx::GpisPoint GpisView::operator()(int kind, int u, int f) const {
   for (int i = 0; i < 3; ++i) p.gmean[i] = gmean[3 * qi + i];
   if (kind == 0) {
     p.std = std_[qi];
-    for (int i = 0; i < 3; ++i) { p.gstd[i] = gstd[3 * qi + i]; p.normal[i] = normal[3 * qi + i]; }
+    for (int i = 0; i < 3; ++i) p.normal[i] = normal[3 * qi + i];
+    // (only the group's selected row — the variance cost's argmax — has a ∇std; level_fwd_bwd reads no other)
+    if (fold.partial)
+      for (int i = 0; i < 3; ++i) p.gstd[i] = qi == gq ? gsv[i] : 0.0;
+    else
+      for (int i = 0; i < 3; ++i) p.gstd[i] = gstd[3 * qi + i];
   } else {
     p.std = 0;
     for (int i = 0; i < 3; ++i) { p.gstd[i] = 0; p.normal[i] = 0; }
@@ -280,6 +292,12 @@ __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_
   const double qnorm = cdx::ref_dist(P, in.q, dq);
   GpisView g = gv;
   g.e = e;
+  if (gv.fold.partial) {  // this level's group: its selected row and ∇std (the finalize, folded; read
+    // from the kernel argument itself: its cost table stays in scalar registers)
+    const int64_t m = (int64_t)P.level_query[k] * E + e;
+    g.gq = gv.sel[m];
+    cdx::grad_fold_gstd(gv.fold, m, gv.var[g.gq], g.gsv);
+  }
   cdx::LevelOut lo;
   cdx::level_fwd_bwd<NT, GpisView, G, PRE>(P, k, in, tip, qnorm, g, lo);
   double* r = lvl + t * level_record_width(T);
@@ -587,6 +605,16 @@ int kabsch_mode() {
   return m;
 }
 
+// CDX_GRAD_FOLD=0 keeps the ∇std finalize kernel (A/B); default: the screened closure's level kernel
+// sums the ∇std pieces of its group itself (GpisView::fold) — one launch fewer.
+bool grad_fold() {
+  static const bool on = [] {
+    const char* e = getenv("CDX_GRAD_FOLD");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
 // Fork/join events: no timing, and (CDX_SIDE_EVENT_FENCE=0 / unset) no system-scope fence — they order
 // two streams of one device, whose kernels see each other's writes at kernel boundaries anyway.
 unsigned side_event_flags() {
@@ -758,6 +786,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   const bool fork = scr && fork_mean() && side_stream(ss);
   const SideStream* pending_b = nullptr;  // mean B still to be joined before the combine kernel
   const double* krot = nullptr;           // Kabsch records computed ahead (else the level kernel's own SVD)
+  cdx::GradFold fold;                      // ∇std finalize folded into the level kernel (screened closure)
   int rc;
   if (!fork) {
     rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
@@ -842,7 +871,8 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     rc = cdx::refine_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.sv2, w.vpos, w.keep, w.std_, w.var, w.sel,
                                    w.Xg, w.vrow, w.stats, s);
     if (rc) return joined(rc);
-    rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V, w.vrow);
+    rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V, w.vrow,
+                               grad_fold() ? &fold : nullptr);
     if (rc) return joined(rc);
     if (fork && (rc = launch_b())) return joined(rc);
     // mean A (and the Kabsch records of mode 1) before the level kernel; mean B is joined before the
@@ -863,22 +893,26 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   GpisView gv;
   gv.mean = w.mean; gv.gmean = w.gmean; gv.normal = w.normal; gv.std_ = w.std_; gv.gstd = w.gstd;
   gv.E = E; gv.T = p->chain.n_tips; gv.Lq = p->n_query_levels; gv.e = 0;
+  GpisView gvl = gv;  // the level kernel's view: ∇std from the pass's pieces when folded
+  gvl.fold = fold;
+  gvl.var = w.var;
+  gvl.sel = w.sel;
   cdx::prof_mark(cdx::PROF_COST, true, s);
   {
     const int64_t KE = (int64_t)p->n_levels * E;
     const dim3 lgrid((unsigned)((KE + 63) / 64));
     if (p->chain.n_tips == 4 && p->gravity && krot)
       hipLaunchKernelGGL((closure_level_kernel<4, 1, true>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gv, w.lvl, flip, krot);
+                         kabsch_noise, seed, gvl, w.lvl, flip, krot);
     else if (p->chain.n_tips == 4 && p->gravity)
       hipLaunchKernelGGL((closure_level_kernel<4, 1>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gv, w.lvl, flip, krot);
+                         kabsch_noise, seed, gvl, w.lvl, flip, krot);
     else if (p->chain.n_tips == 4)
       hipLaunchKernelGGL((closure_level_kernel<4, 0>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gv, w.lvl, flip, krot);
+                         kabsch_noise, seed, gvl, w.lvl, flip, krot);
     else
       hipLaunchKernelGGL((closure_level_kernel<0, -1>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gv, w.lvl, flip, krot);
+                         kabsch_noise, seed, gvl, w.lvl, flip, krot);
     if (hipGetLastError() != hipSuccess) {
       if (pending_b) (void)hipStreamWaitEvent(s, pending_b->joinB, 0);
       return CDX_ELAUNCH;

@@ -256,6 +256,8 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 //   fence each cut piece needs writes back its XCD's whole L2.)
 enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2, MODE_VARL = 3 };
 
+constexpr int RC_MAX_NT = 16;  // stripes with host unit costs (N_pad ≤ 4096); beyond: equal K-step cuts
+static_assert(RC_MAX_NT == cdx::GC_MAX_NT, "the ∇std pass's stripe costs travel in RefineList::uc");
 struct RefineList {
   const int* rows;    // query index per list position
   const int* extra;   // device count of positions past the G primary ones
@@ -263,6 +265,9 @@ struct RefineList {
   double* slots;      // [gridDim.x][2][ST_BM][ST_BN] partial V tiles of cut stripes
   int* cnt;           // [Nt][mt_cap] arrival counters of cut units (zero between launches)
   int mt_cap;         // query tiles the list can hold
+  int64_t* cuts;      // [gridDim.x + 1] piece bounds in the K-sequence (written by the refine kernel)
+  int n_uc;           // stripes with unit costs below (= N_pad/256), 0: equal K-step cuts
+  int64_t uc[RC_MAX_NT];  // cost of one (stripe, query tile) unit per stripe (var_unit_cost, host)
 };
 
 // Whitened pass A operand: K* generated on chip per stripe (default), or read from a buffer
@@ -335,12 +340,111 @@ __device__ inline int refine_piece(int b, int G, int pieces) {
   return pieces == G && (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b;
 }
 
-// Piece holding K-sequence position x (pieces cut [0, total) at total·p/pieces).
-__device__ inline int refine_piece_of(int64_t x, int64_t total, int pieces) {
-  int p = (int)(x * pieces / total);
-  while (p + 1 < pieces && total * (p + 1) / pieces <= x) ++p;
-  while (p > 0 && total * p / pieces > x) --p;
-  return p;
+// Cost-balanced cuts of the refine sequence.  A K-step's time is not uniform: in the last 16–20 K-steps
+// of a unit (the stripe's diagonal block) the waves past their own columns skip their MFMAs, so the
+// light stripes' short units are cheaper per K-step.  Measured per piece (CDX_DIAG_WGTIME build,
+// tools/refine_pieces.py, profiles/r03v_refine_pieces.json): time ≈ 2.8 µs per K-step + 0.27 µs per
+// 16-column MFMA block of the busiest SIMD (8 in a full step); equal K-step cuts left the heavy-stripe
+// pieces 366 µs against 295 µs for the light ones (end times 292 … 385 µs).  The cuts balance
+// RC_FIX + RC_BLK·blocks per K-step instead (integer costs: the same cuts on every workgroup and in the
+// merge); CDX_REFINE_UNIFORM builds the equal-K-step cuts for the A/B.
+#if defined(CDX_REFINE_UNIFORM)
+constexpr int RC_FIX = 1, RC_BLK = 0;
+#else
+constexpr int RC_FIX = 21, RC_BLK = 2;
+#endif
+// MFMA blocks (16 columns × one wave) of the busiest SIMD in K-step s of a stripe-nt unit: wave cwave c
+// (columns 64c … 64c+63 of the stripe, shifted by vsh) issues 4 blocks up to its diagonal block, then
+// 3, 2, 1, 0 (gpis_std_kernel's VAR step variants); SIMDs hold the column waves (c, 3 − c).
+__device__ __host__ inline int var_step_blocks(int nt, int s, int vsh16) {
+  int b[4];
+  for (int c = 0; c < 4; ++c) {
+    const int d = s - (16 * nt + 4 * c - vsh16);
+    b[c] = d <= 0 ? 4 : (d >= 4 ? 0 : 4 - d);
+  }
+  return max(b[0] + b[3], b[1] + b[2]);
+}
+// Piece p of the refine sequence is [cut(p), cut(p+1)).  The per-stripe unit costs depend on (N, N_pad)
+// only: the launcher computes them on the host (RefineList::uc); each refine workgroup computes its own
+// two bounds from them and the device-side row count (a few scalar steps), and writes its start to
+// RefineList::cuts for the merge kernel.
+__device__ __host__ inline int64_t var_unit_cost(int nt, int N, int Np) {
+  const int vsh16 = var_shift(N, Np) / ST_BK, ks = var_ksteps(nt, N, Np);
+  const int sd = min(ks, max(0, 16 * nt - vsh16 + 1));  // steps before the first one below 8 blocks
+  int64_t c = (int64_t)sd * (RC_FIX + 8 * RC_BLK);
+  for (int s = sd; s < ks; ++s) c += RC_FIX + RC_BLK * var_step_blocks(nt, s, vsh16);
+  return c;
+}
+// ⌊a / b⌋ for 0 ≤ a < 2⁵³, b > 0 through a double division and an exact integer correction
+__device__ inline int64_t floordiv_i64(int64_t a, int64_t b) {
+  int64_t q = (int64_t)((double)a / (double)b);
+  while (q > 0 && q * b > a) --q;
+  while ((q + 1) * b <= a) ++q;
+  return q;
+}
+struct RefineCuts {
+  int MtL, N, Np, Nt, pieces, vsh16;
+  int64_t total;  // K-steps of the sequence
+  // start of piece p: the first K-sequence position x whose preceding cost reaches ctot·p/pieces, from
+  // the unit costs uc[nt] (a kernel-argument array, indexed statically) and ctot = Σ MtL·uc[nt]
+  // (use_uc false: equal K-step cuts)
+  template <class UC>
+  __device__ __forceinline__ int64_t cut(int p, const UC& uc, bool use_uc, int64_t ctot) const {
+    if (p <= 0) return 0;
+    if (p >= pieces) return total;
+    if (!use_uc) return total * p / pieces;
+    const int64_t target = ctot * p;  // compare cost·pieces against ctot·p (exact integers)
+    int64_t acc = 0, pos = 0;
+#pragma unroll
+    for (int nt = 0; nt < RC_MAX_NT; ++nt) {  // static indices into uc (a kernel argument): no scratch copy
+      if (nt >= Nt) break;
+      const int ks = var_ksteps(nt, N, Np);
+      const int64_t sc = (int64_t)MtL * uc[nt];
+      if ((acc + sc) * pieces < target) {
+        acc += sc;
+        pos += (int64_t)MtL * ks;
+        continue;
+      }
+      const int64_t r = target - acc * pieces;  // > 0, ≤ sc·pieces
+      const int64_t mt = floordiv_i64(r - 1, uc[nt] * pieces);
+      const int64_t need = r - mt * uc[nt] * pieces;  // cost·pieces still to cover inside unit mt
+      const int sd = min(ks, max(0, 16 * nt - vsh16 + 1));
+      const int64_t full = (RC_FIX + 8 * RC_BLK) * (int64_t)pieces;
+      int64_t st;
+      if (need <= (int64_t)sd * full) {
+        st = floordiv_i64(need + full - 1, full);
+      } else {
+        int64_t cum = (int64_t)sd * full;
+        st = sd;
+        while (st < ks && cum < need) cum += (RC_FIX + RC_BLK * var_step_blocks(nt, (int)st++, vsh16)) * (int64_t)pieces;
+      }
+      return pos + mt * ks + st;
+    }
+    return total;
+  }
+};
+__device__ inline RefineCuts refine_cuts(const cdx_gpis& g, int64_t Mrows, int G) {
+  RefineCuts rc;
+  rc.MtL = (int)((Mrows + ST_BM - 1) / ST_BM);
+  rc.N = g.N;
+  rc.Np = g.N_pad;
+  rc.Nt = g.N_pad / ST_BN;
+  rc.vsh16 = var_shift(g.N, g.N_pad) / ST_BK;
+  int W = 0;
+  for (int t = 0; t < rc.Nt; ++t) W += var_ksteps(t, g.N, g.N_pad);
+  rc.total = (int64_t)rc.MtL * W;
+  rc.pieces = refine_pieces(rc.total, G);
+  return rc;
+}
+// piece holding K-sequence position x: the largest p with cuts[p] ≤ x
+__device__ inline int refine_piece_of(int64_t x, const int64_t* cuts, int pieces) {
+  int lo = 0, hi = pieces - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (cuts[mid] <= x) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
 }
 
 // A cut unit (stripe nt, query tile mt, K-sequence [S0, S1)): V = its pieces' partial tiles summed in
@@ -348,11 +452,10 @@ __device__ inline int refine_piece_of(int64_t x, int64_t total, int pieces) {
 // 4 columns per lane, MERGE_RB rows per batch so a batch's loads are in flight together.
 constexpr int MERGE_THREADS = 512, MERGE_RB = 8;
 __device__ inline void refine_merge_unit(const cdx_gpis& g, const RefineList& rl, int64_t M_pad, double* partial,
-                                         double* vout, int nt, int mt, int64_t S0, int64_t S1, int64_t total,
-                                         int pieces, int tid) {
+                                         double* vout, int nt, int mt, int64_t S0, int64_t S1, int pieces, int tid) {
   const int Np = g.N_pad;
-  const int pf = refine_piece_of(S0, total, pieces), pl = refine_piece_of(S1 - 1, total, pieces);
-  auto qof = [&](int pp) { return total * pp / pieces; };
+  const int pf = refine_piece_of(S0, rl.cuts, pieces), pl = refine_piece_of(S1 - 1, rl.cuts, pieces);
+  auto qof = [&](int pp) { return rl.cuts[pp]; };
   const int lane = tid & 63, wave = tid >> 6;
   constexpr int NW = MERGE_THREADS / 64;
   for (int r0 = wave * MERGE_RB; r0 < ST_BM; r0 += NW * MERGE_RB) {
@@ -762,14 +865,20 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
 
   if constexpr (LIST) {
     // pieces of the concatenated K-sequence of all (stripe, query tile) units (refine_locate)
-    const int MtL = (int)((Mrows + ST_BM - 1) / ST_BM);
-    int W = 0;
-    for (int t = 0; t < Nt; ++t) W += var_ksteps(t, g.N, Np);
-    const int64_t total = (int64_t)MtL * W;
-    const int pieces = refine_pieces(total, gridDim.x);
+    const RefineCuts rc = refine_cuts(g, Mrows, gridDim.x);
+    const int MtL = rc.MtL, pieces = rc.pieces;
     const int pc = refine_piece(b, gridDim.x, pieces);
     if (pc >= pieces) return;
-    const int64_t q0 = total * pc / pieces, q1 = total * (pc + 1) / pieces;
+    const bool use_uc = rl.n_uc == rc.Nt && rc.total >= 32 * (int64_t)pieces;  // short pieces: equal K-steps
+    int64_t ctot = 0;
+#pragma unroll
+    for (int nt = 0; nt < RC_MAX_NT; ++nt)
+      if (nt < rc.Nt) ctot += (int64_t)MtL * rl.uc[nt];
+    const int64_t q0 = rc.cut(pc, rl.uc, use_uc, ctot), q1 = rc.cut(pc + 1, rl.uc, use_uc, ctot);
+    if (tid == 0) {  // the piece table for the merge kernel
+      rl.cuts[pc] = q0;
+      if (pc == pieces - 1) rl.cuts[pieces] = q1;
+    }
     bool first = true;
     __shared__ int s_last;
 #if defined(CDX_DIAG_WGTIME)
@@ -792,7 +901,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
         __threadfence();
         __syncthreads();
         if (tid == 0) {
-          const int n = refine_piece_of(S1 - 1, total, pieces) - refine_piece_of(S0, total, pieces) + 1;
+          const int n = refine_piece_of(S1 - 1, rl.cuts, pieces) - refine_piece_of(S0, rl.cuts, pieces) + 1;
           int* c = rl.cnt + (int64_t)nt * rl.mt_cap + mt;
           const int old = atomicAdd(c, 1);
           s_last = old == n - 1;
@@ -801,7 +910,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
         __syncthreads();
         if (s_last) {
           __threadfence();  // acquire: the other pieces' tiles
-          refine_merge_unit(g, rl, M_pad, partial, vout, nt, mt, S0, S1, total, pieces, tid);
+          refine_merge_unit(g, rl, M_pad, partial, vout, nt, mt, S0, S1, pieces, tid);
         }
       }
 #endif
@@ -827,7 +936,9 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     const int p = t / Mt, mt = t - p * Mt;
     int W = 0;
     for (int nt = 0; nt < Nt; ++nt) W += gradv_ksteps(nt, g.N);
-    const int q0 = (int)((int64_t)W * p / parts), q1 = (int)((int64_t)W * (p + 1) / parts);
+    // cost-balanced cuts from the launcher's per-stripe costs (carried in rl.uc, RC_MAX_NT = GC_MAX_NT)
+    const int q0 = cdx::gradv_cut(p, parts, W, g.N, Nt, rl.uc, rl.n_uc),
+              q1 = cdx::gradv_cut(p + 1, parts, W, g.N, Nt, rl.uc, rl.n_uc);
     bool first = true;
     for (int nt = 0, s0 = 0; nt < Nt; ++nt) {
       const int s1 = s0 + gradv_ksteps(nt, g.N);
@@ -1019,22 +1130,19 @@ __global__ __launch_bounds__(256) void gpis_var_splitk_finalize(cdx_gpis g, cons
 // whose K-range ends inside piece p after starting in an earlier one.
 __global__ __launch_bounds__(MERGE_THREADS) void gpis_var_merge(cdx_gpis g, RefineList rl, int64_t M_pad,
                                                       double* __restrict__ partial, double* __restrict__ vout) {
-  const int Np = g.N_pad, Nt = Np / ST_BN;
   const int64_t Mrows = (int64_t)rl.G + *rl.extra;
-  const int MtL = (int)((Mrows + ST_BM - 1) / ST_BM);
-  int W = 0;
-  for (int t = 0; t < Nt; ++t) W += var_ksteps(t, g.N, Np);
-  const int64_t total = (int64_t)MtL * W;
-  const int pieces = refine_pieces(total, gridDim.x), p = blockIdx.x;
-  if (p >= pieces) return;
-  const int64_t q0 = total * p / pieces, q1 = total * (p + 1) / pieces;
-  if (q0 >= q1 || q0 >= total) return;
+  const RefineCuts rc = refine_cuts(g, Mrows, gridDim.x);
+  const int p = blockIdx.x;
+  if (p >= rc.pieces) return;
+  const int64_t q0 = rl.cuts[p], q1 = rl.cuts[p + 1];
+  if (q0 >= q1 || q0 >= rc.total) return;
   int nt, mt;
   int64_t S0, S1;
-  refine_locate(q0, MtL, g.N, Np, nt, mt, S0, S1);
+  refine_locate(q0, rc.MtL, g.N, g.N_pad, nt, mt, S0, S1);
   if (!(S0 < q0 && S1 <= q1)) return;
-  refine_merge_unit(g, rl, M_pad, partial, vout, nt, mt, S0, S1, total, pieces, threadIdx.x);
+  refine_merge_unit(g, rl, M_pad, partial, vout, nt, mt, S0, S1, rc.pieces, threadIdx.x);
 }
+
 #endif
 
 // Partial slots a ∇std launch wrote, in increasing order (host-computed, passed by value).
@@ -1183,17 +1291,27 @@ static void var_launch_kt(const cdx_gpis& g, const double* X, int64_t M, double*
 template <int KT>
 static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const int64_t* sel, const double* var,
                            double* gstd, double* partial, int64_t M_pad, int Mt, int n_tiles, const double* vin,
-                           hipStream_t s, const int64_t* vrow) {
+                           hipStream_t s, const int64_t* vrow, GradFold* fold) {
   prof_mark(PROF_GPIS_GRAD, true, s);
   GradSlots slots;
   slots.n = 0;
   if (vin) {
     const int parts = gradv_parts(g, Mt);
+    // cost-balanced pieces (gradv_cut): per-stripe costs to the kernel through the list's cost table
+    GradCosts gc;
+    RefineList rl{};
+#if defined(CDX_GRAD_COSTCUT)  // off: 0.295 vs 0.286 ms for the ∇std pass (profiles/r03w_cuts_ab.jsonl)
+    if (n_tiles <= GC_MAX_NT && n_tiles <= RC_MAX_NT) {
+      gc.n = rl.n_uc = n_tiles;
+      for (int nt = 0; nt < n_tiles; ++nt) gc.uc[nt] = rl.uc[nt] = gradv_unit_cost(nt, g.N);
+    }
+#endif
     // slot p + nt per (piece, stripe) segment the kernel runs (same cut as gpis_std_kernel<GRADV>)
     int W = 0;
     for (int nt = 0; nt < n_tiles; ++nt) W += gradv_ksteps(nt, g.N);
     for (int p = 0; p < parts; ++p) {
-      const int q0 = (int)((int64_t)W * p / parts), q1 = (int)((int64_t)W * (p + 1) / parts);
+      const int q0 = gradv_cut(p, parts, W, g.N, n_tiles, gc.uc, gc.n),
+                q1 = gradv_cut(p + 1, parts, W, g.N, n_tiles, gc.uc, gc.n);
       for (int nt = 0, s0 = 0; nt < n_tiles; ++nt) {
         const int s1 = s0 + gradv_ksteps(nt, g.N);
         if (std::max(q0, s0) < std::min(q1, s1) && slots.n < GRAD_MAX_SLOTS) slots.t[slots.n++] = (unsigned short)(p + nt);
@@ -1201,7 +1319,18 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
       }
     }
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRADV>), dim3((unsigned)(Mt * parts)), dim3(ST_THREADS), 0,
-                       s, g, X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, vrow ? vrow : sel, parts, RefineList{});
+                       s, g, X, M, partial, M_pad, Mt, n_tiles, nullptr, vin, vrow ? vrow : sel, parts, rl);
+    if (fold) {  // the consumer sums the pieces itself (same slots in the same order as the list above)
+      prof_mark(PROF_GPIS_GRAD, false, s);
+      fold->partial = partial;
+      fold->M_pad = M_pad;
+      fold->parts = parts;
+      fold->W = W;
+      fold->Nt = n_tiles;
+      fold->N = g.N;
+      fold->gc = gc;
+      return;
+    }
   } else {
     for (int nt = 0; nt < n_tiles && nt < GRAD_MAX_SLOTS; ++nt) slots.t[slots.n++] = (unsigned short)nt;
     hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_GRAD>), dim3((unsigned)(Mt * n_tiles)), dim3(ST_THREADS), 0, s, g,
@@ -1234,8 +1363,9 @@ int gpis_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* std_o
 }
 
 int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_t* sel, const double* var,
-                     double* gstd, void* ws, hipStream_t s, const double* vin, const int64_t* vrow) {
+                     double* gstd, void* ws, hipStream_t s, const double* vin, const int64_t* vrow, GradFold* fold) {
   if (vin && !g.Linv) return CDX_EINVAL;
+  if (fold && !vin) return CDX_EINVAL;
   if (M <= 0) return CDX_OK;
   const int64_t M_pad = round_up(M, ST_BM);
   const int n_tiles = g.N_pad / ST_BN;
@@ -1244,9 +1374,9 @@ int gpis_grad_launch(const cdx_gpis& g, const double* X, int64_t M, const int64_
   const int Mt = (int)(M_pad / ST_BM);
   double* partial = static_cast<double*>(ws);
   switch (g.kernel) {
-    case CDX_KERNEL_TPS: grad_launch_kt<CDX_KERNEL_TPS>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s, vrow); break;
-    case CDX_KERNEL_RBF: grad_launch_kt<CDX_KERNEL_RBF>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s, vrow); break;
-    default: grad_launch_kt<CDX_KERNEL_JOINT>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s, vrow); break;
+    case CDX_KERNEL_TPS: grad_launch_kt<CDX_KERNEL_TPS>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s, vrow, fold); break;
+    case CDX_KERNEL_RBF: grad_launch_kt<CDX_KERNEL_RBF>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s, vrow, fold); break;
+    default: grad_launch_kt<CDX_KERNEL_JOINT>(g, X, M, sel, var, gstd, partial, M_pad, Mt, n_tiles, vin, s, vrow, fold); break;
   }
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
@@ -1263,8 +1393,10 @@ static size_t refine_cnt_bytes(const cdx_gpis& g, int64_t Mcap) {
   return ((size_t)(g.N_pad / ST_BN) * (size_t)(round_up(Mcap, ST_BM) / ST_BM) * sizeof(int) + 255) / 256 * 256;
 }
 
+static size_t refine_cuts_bytes() { return ((REFINE_PIECES + 1) * sizeof(int64_t) + 255) / 256 * 256; }
+
 size_t gpis_refine_ws_bytes(const cdx_gpis& g, int64_t Mcap) {
-  return refine_part_bytes(g, Mcap) + refine_slot_bytes() + refine_cnt_bytes(g, Mcap);
+  return refine_part_bytes(g, Mcap) + refine_slot_bytes() + refine_cnt_bytes(g, Mcap) + refine_cuts_bytes();
 }
 
 int gpis_refine_reset(const cdx_gpis& g, int64_t Mcap, void* ws, hipStream_t s) {
@@ -1291,7 +1423,13 @@ int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, cons
   double* partial = static_cast<double*>(ws);
   char* slots = static_cast<char*>(ws) + refine_part_bytes(g, Mcap);
   RefineList rl{rows, extra, G, reinterpret_cast<double*>(slots), reinterpret_cast<int*>(slots + refine_slot_bytes()),
-                (int)(M_pad / ST_BM)};
+                (int)(M_pad / ST_BM),
+                reinterpret_cast<int64_t*>(slots + refine_slot_bytes() + refine_cnt_bytes(g, Mcap)), 0, {}};
+  const int Nt = g.N_pad / ST_BN;
+  if (Nt <= RC_MAX_NT) {
+    rl.n_uc = Nt;
+    for (int nt = 0; nt < Nt; ++nt) rl.uc[nt] = var_unit_cost(nt, g.N, g.N_pad);
+  }
   switch (g.kernel) {
     case CDX_KERNEL_TPS: refine_launch_kt<CDX_KERNEL_TPS>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
     case CDX_KERNEL_RBF: refine_launch_kt<CDX_KERNEL_RBF>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
