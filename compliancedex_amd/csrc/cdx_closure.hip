@@ -249,7 +249,7 @@ __global__ __launch_bounds__(64) void force_eq_backward_kernel(
   }
 }
 
-template <int NT, int G, bool PRE = false>
+template <int NT, int G, bool PRE = false, bool VL = false>
 __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_t E, const double* __restrict__ q,
                                                            const double* __restrict__ comp,
                                                            const double* __restrict__ target,
@@ -292,14 +292,14 @@ __global__ __launch_bounds__(64) void closure_level_kernel(cdx_problem P, int64_
   const double qnorm = cdx::ref_dist(P, in.q, dq);
   GpisView g = gv;
   g.e = e;
-  if (gv.fold.partial) {  // this level's group: its selected row and ∇std (the finalize, folded; read
+  if (!VL && gv.fold.partial) {  // this level's group: its selected row and ∇std (the finalize, folded; read
     // from the kernel argument itself: its cost table stays in scalar registers)
     const int64_t m = (int64_t)P.level_query[k] * E + e;
     g.gq = gv.sel[m];
     cdx::grad_fold_gstd(gv.fold, m, gv.var[g.gq], g.gsv);
   }
   cdx::LevelOut lo;
-  cdx::level_fwd_bwd<NT, GpisView, G, PRE>(P, k, in, tip, qnorm, g, lo);
+  cdx::level_fwd_bwd<NT, GpisView, G, PRE, !VL>(P, k, in, tip, qnorm, g, lo);
   double* r = lvl + t * level_record_width(T);
   r[0] = lo.l;
   for (int f = 0; f < T; ++f) {
@@ -356,8 +356,16 @@ __global__ __launch_bounds__(64) void closure_kabsch_kernel(cdx_problem P, int64
 // and palm GPIS terms (:757-763), the palm/euler backward and the fingertip's FK VJP, then
 // reduces the shared gradients: palm terms with xor-shuffles, the per-DOF FK contributions
 // through LDS ([dof][thread], summed in the same pairwise order over the group's lanes).
-constexpr int COMBINE_BLOCK = 256;
-template <int GS, int MAXD>
+// VL (var_late): the level records hold no variance cost; lane f adds it here for the levels whose group
+// maximum (sel, the first maximum of log(100·std) as level_fwd_bwd takes it) is fingertip f — loss
+// w_k·(l_k + uncertainty·log(100·std)) and, through the all-tip interpolation a = target + c·(tip −
+// target), c·g and g − c·g of g = w_k·uncertainty/std·∇std into the tip and target gradients; ∇std
+// summed from the pass's pieces here when folded (once per distinct level, by that fingertip's lane).
+#if !defined(CDX_COMBINE_BLOCK)
+#define CDX_COMBINE_BLOCK 64
+#endif
+constexpr int COMBINE_BLOCK = CDX_COMBINE_BLOCK;  // 64: E = 4096 spreads over 256 workgroups, one per CU
+template <int GS, int MAXD, bool VL = false>
 __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
     cdx_problem P, int64_t E, const double* __restrict__ q, const double* __restrict__ palm_pos,
     const double* __restrict__ palm_ori, GpisView gv, const double* __restrict__ lvl, double* __restrict__ total_loss,
@@ -378,11 +386,37 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
 
   double gt[3] = {0, 0, 0}, gtar[3] = {0, 0, 0}, gcomp = 0, marg = 0;
   if (live) {
+    int ulast = -1;
+    int64_t qsel = -1;
+    double gs3[3] = {0, 0, 0}, ssel = 0;
     for (int k = 0; k < K; ++k) {
       const double* r = lvl + ((int64_t)k * E + e) * LW;
       marg += P.weight[k] * r[1 + f];
       gcomp += r[1 + 7 * T + f];
       for (int i = 0; i < 3; ++i) { gt[i] += r[1 + T + 3 * f + i]; gtar[i] += r[1 + 4 * T + 3 * f + i]; }
+      if constexpr (VL) {
+        const int u = P.level_query[k];
+        if (u != ulast) {  // this distinct level's group maximum and (on its lane) its ∇std
+          ulast = u;
+          const int64_t m = (int64_t)u * E + e;
+          qsel = gv.sel[m];
+          ssel = gv.std_[qsel];
+          if (qsel == cdx::q_alltip(u, e, f, E, T)) {
+            if (gv.fold.partial)
+              cdx::grad_fold_gstd(gv.fold, m, gv.var[qsel], gs3);
+            else
+              for (int i = 0; i < 3; ++i) gs3[i] = gv.gstd[3 * qsel + i];
+          }
+        }
+        if (qsel == cdx::q_alltip(u, e, f, E, T)) {
+          const double gs = P.weight[k] * P.uncertainty / ssel, c = (double)P.coeff[k][f];
+          for (int i = 0; i < 3; ++i) {
+            const double ga = gs * gs3[i];
+            gt[i] += c * ga;
+            gtar[i] += ga - c * ga;
+          }
+        }
+      }
     }
     const cdx::GpisPoint gpp = g(2, 0, f);
     for (int i = 0; i < 3; ++i) gt[i] += -5.0 * gpp.gmean[i];
@@ -436,7 +470,11 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
   }
   if (f != 0) return;
   double total = 0.0;
-  for (int k = 0; k < K; ++k) total += P.weight[k] * lvl[((int64_t)k * E + e) * LW];
+  for (int k = 0; k < K; ++k) {
+    double l = lvl[((int64_t)k * E + e) * LW];
+    if constexpr (VL) l = l + P.uncertainty * log(100 * gv.std_[gv.sel[(int64_t)P.level_query[k] * E + e]]);
+    total += P.weight[k] * l;
+  }
   double pre_sum = 0.0;
   for (int ff = 0; ff < T; ++ff) pre_sum += g(2, 0, ff).mean;
   total = total - pre_sum * 5.0;
@@ -675,6 +713,66 @@ bool problem_ok(const cdx_problem* p) {
   return true;
 }
 
+// The level kernel (per (level, candidate)) and the combine kernel (per candidate and fingertip) of a
+// closure, dispatched on the fingertip count, gravity, Kabsch records (krot) and chain depth.
+template <bool VL>
+int launch_level(const cdx_problem* p, int64_t E, const double* q, const double* comp, const double* target,
+                 const double* kabsch_noise, uint64_t seed, const ClosureWs& w, const GpisView& gv, int32_t* flip,
+                 const double* krot, hipStream_t s) {
+  const int64_t KE = (int64_t)p->n_levels * E;
+  const dim3 lgrid((unsigned)((KE + 63) / 64));
+  if (p->chain.n_tips == 4 && p->gravity && krot)
+    hipLaunchKernelGGL((closure_level_kernel<4, 1, true, VL>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
+                       kabsch_noise, seed, gv, w.lvl, flip, krot);
+  else if (p->chain.n_tips == 4 && p->gravity)
+    hipLaunchKernelGGL((closure_level_kernel<4, 1, false, VL>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
+                       kabsch_noise, seed, gv, w.lvl, flip, krot);
+  else if (p->chain.n_tips == 4)
+    hipLaunchKernelGGL((closure_level_kernel<4, 0, false, VL>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
+                       kabsch_noise, seed, gv, w.lvl, flip, krot);
+  else
+    hipLaunchKernelGGL((closure_level_kernel<0, -1, false, VL>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
+                       kabsch_noise, seed, gv, w.lvl, flip, krot);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+template <bool VL>
+int launch_combine(const cdx_problem* p, int64_t E, const double* q, const double* palm_pos, const double* palm_ori,
+                   const GpisView& gv, const ClosureWs& w, double* total_loss, double* total_margin, double* g_q,
+                   double* g_comp, double* g_target, double* g_palm_pos, double* g_palm_ori, hipStream_t s) {
+  const bool sh = shallow_chain(p->chain);
+  const dim3 cb(COMBINE_BLOCK);
+  if (p->chain.n_tips <= 4) {
+    const dim3 cg((unsigned)((E * 4 + COMBINE_BLOCK - 1) / COMBINE_BLOCK));
+    if (sh)
+      hipLaunchKernelGGL((closure_combine_kernel<4, 8, VL>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv, w.lvl,
+                         total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
+    else
+      hipLaunchKernelGGL((closure_combine_kernel<4, CDX_MAX_DEPTH, VL>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv,
+                         w.lvl, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
+  } else {
+    const dim3 cg((unsigned)((E * 8 + COMBINE_BLOCK - 1) / COMBINE_BLOCK));
+    if (sh)
+      hipLaunchKernelGGL((closure_combine_kernel<8, 8, VL>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv, w.lvl,
+                         total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
+    else
+      hipLaunchKernelGGL((closure_combine_kernel<8, CDX_MAX_DEPTH, VL>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv,
+                         w.lvl, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
+  }
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+// The variance cost added by the combine kernel instead of the level kernel (CDX_VAR_LATE, default 1; 0 for
+// the A/B): the level kernel then reads no std, and the screened closure with the forked mean runs it on the
+// side stream right after the mean — beside the merge / exact selection / ∇std passes instead of after them.
+bool var_late() {
+  static const bool on = [] {
+    const char* e = getenv("CDX_VAR_LATE");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
 }  // namespace
 
 extern "C" {
@@ -786,7 +884,9 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   const bool fork = scr && fork_mean() && side_stream(ss);
   const SideStream* pending_b = nullptr;  // mean B still to be joined before the combine kernel
   const double* krot = nullptr;           // Kabsch records computed ahead (else the level kernel's own SVD)
-  cdx::GradFold fold;                      // ∇std finalize folded into the level kernel (screened closure)
+  cdx::GradFold fold;                      // ∇std finalize folded into the level (or combine) kernel (screened)
+  const bool vlate = var_late();
+  bool level_early = false;                // the level kernel already queued (side stream, after the mean)
   int rc;
   if (!fork) {
     rc = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, stream);
@@ -836,8 +936,17 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
         const int r = launch_records(ss.s);
         if (r) return r;
       }
-      const int r = cdx_gpis_mean(&p->gpis, w.X, MqA, w.mean, w.gmean, w.normal, side);
+      int r = cdx_gpis_mean(&p->gpis, w.X, MqA, w.mean, w.gmean, w.normal, side);
       if (r) return r;
+      if (vlate) {  // the level kernel reads the mean A rows, the Kabsch records and no std
+        GpisView gv0;
+        gv0.mean = w.mean; gv0.gmean = w.gmean; gv0.normal = w.normal; gv0.std_ = w.std_; gv0.gstd = w.gstd;
+        gv0.E = E; gv0.T = T; gv0.Lq = p->n_query_levels; gv0.e = 0;
+        r = launch_level<true>(p, E, q, comp, target, kabsch_noise, seed, w, gv0, flip, kmode == 1 ? w.krot : nullptr,
+                               ss.s);
+        if (r) return r;
+        level_early = true;
+      }
       return hipEventRecord(ss.join, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
     };
     auto launch_b = [&]() -> int {  // mean B, gated behind the work already on `s`
@@ -893,51 +1002,25 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   GpisView gv;
   gv.mean = w.mean; gv.gmean = w.gmean; gv.normal = w.normal; gv.std_ = w.std_; gv.gstd = w.gstd;
   gv.E = E; gv.T = p->chain.n_tips; gv.Lq = p->n_query_levels; gv.e = 0;
-  GpisView gvl = gv;  // the level kernel's view: ∇std from the pass's pieces when folded
+  GpisView gvl = gv;  // ∇std from the pass's pieces when folded (the level kernel's view, or the combine's: vlate)
   gvl.fold = fold;
   gvl.var = w.var;
   gvl.sel = w.sel;
   cdx::prof_mark(cdx::PROF_COST, true, s);
-  {
-    const int64_t KE = (int64_t)p->n_levels * E;
-    const dim3 lgrid((unsigned)((KE + 63) / 64));
-    if (p->chain.n_tips == 4 && p->gravity && krot)
-      hipLaunchKernelGGL((closure_level_kernel<4, 1, true>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gvl, w.lvl, flip, krot);
-    else if (p->chain.n_tips == 4 && p->gravity)
-      hipLaunchKernelGGL((closure_level_kernel<4, 1>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gvl, w.lvl, flip, krot);
-    else if (p->chain.n_tips == 4)
-      hipLaunchKernelGGL((closure_level_kernel<4, 0>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gvl, w.lvl, flip, krot);
-    else
-      hipLaunchKernelGGL((closure_level_kernel<0, -1>), lgrid, dim3(64), 0, s, *p, E, q, comp, target, w.X,
-                         kabsch_noise, seed, gvl, w.lvl, flip, krot);
-    if (hipGetLastError() != hipSuccess) {
+  if (!level_early) {
+    rc = vlate ? launch_level<true>(p, E, q, comp, target, kabsch_noise, seed, w, gv, flip, krot, s)
+               : launch_level<false>(p, E, q, comp, target, kabsch_noise, seed, w, gvl, flip, krot, s);
+    if (rc) {
       if (pending_b) (void)hipStreamWaitEvent(s, pending_b->joinB, 0);
-      return CDX_ELAUNCH;
-    }
-    if (pending_b && hipStreamWaitEvent(s, pending_b->joinB, 0) != hipSuccess) return CDX_ELAUNCH;
-    const bool sh = shallow_chain(p->chain);
-    const dim3 cb(COMBINE_BLOCK);
-    if (p->chain.n_tips <= 4) {
-      const dim3 cg((unsigned)((E * 4 + COMBINE_BLOCK - 1) / COMBINE_BLOCK));
-      if (sh)
-        hipLaunchKernelGGL((closure_combine_kernel<4, 8>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv, w.lvl,
-                           total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
-      else
-        hipLaunchKernelGGL((closure_combine_kernel<4, CDX_MAX_DEPTH>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv,
-                           w.lvl, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
-    } else {
-      const dim3 cg((unsigned)((E * 8 + COMBINE_BLOCK - 1) / COMBINE_BLOCK));
-      if (sh)
-        hipLaunchKernelGGL((closure_combine_kernel<8, 8>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv, w.lvl,
-                           total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
-      else
-        hipLaunchKernelGGL((closure_combine_kernel<8, CDX_MAX_DEPTH>), cg, cb, 0, s, *p, E, q, palm_pos, palm_ori, gv,
-                           w.lvl, total_loss, total_margin, g_q, g_comp, g_target, g_palm_pos, g_palm_ori);
+      return rc;
     }
   }
+  if (pending_b && hipStreamWaitEvent(s, pending_b->joinB, 0) != hipSuccess) return CDX_ELAUNCH;
+  rc = vlate ? launch_combine<true>(p, E, q, palm_pos, palm_ori, gvl, w, total_loss, total_margin, g_q, g_comp, g_target,
+                                    g_palm_pos, g_palm_ori, s)
+             : launch_combine<false>(p, E, q, palm_pos, palm_ori, gv, w, total_loss, total_margin, g_q, g_comp, g_target,
+                                     g_palm_pos, g_palm_ori, s);
+  if (rc) return rc;
   cdx::prof_mark(cdx::PROF_COST, false, s);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }

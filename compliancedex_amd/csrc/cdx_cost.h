@@ -495,7 +495,11 @@ struct LevelOut {
   int flip;
 };
 
-template <int NT, typename GpisAt, int G = -1, bool PRE = false>
+// VAR = false leaves the variance cost out of l and of the gradients (its loss term is the last operand of
+// l's left-to-right sum, so adding uncertainty·lmax to the record later gives l bit for bit): the closure's
+// combine kernel adds it once ∇std is known, so this level kernel needs neither std nor ∇std and can run
+// beside the std passes (cdx_closure.hip, var_late()).
+template <int NT, typename GpisAt, int G = -1, bool PRE = false, bool VAR = true>
 CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, const double (*tip)[3], double qnorm,
                           GpisAt gp, LevelOut& o) {
   constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
@@ -557,16 +561,18 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
   fcost = -fcost;
   // variance cost: uncertainty · max_f log(100 std)
   int fmax = 0;
-  double lmax = log(100 * s[0]);
-  for (int f = 1; f < T; ++f) {
-    const double lv = log(100 * s[f]);
-    if (lv > lmax) { lmax = lv; fmax = f; }
+  double lmax = 0.0;
+  if constexpr (VAR) {
+    lmax = log(100 * s[0]);
+    for (int f = 1; f < T; ++f) {
+      const double lv = log(100 * s[f]);
+      if (lv > lmax) { lmax = lv; fmax = f; }
+    }
   }
   double dcost = 0.0, tcost = 0.0;
   for (int f = 0; f < T; ++f) { dcost += fabs(d[f]); tcost += td[f]; }
-  const double l = -fe.reward * 200.0 + 1000 * dcost + 20 * tcost + (-creward * 200.0) + fcost + qnorm * 10.0 +
-                   P.uncertainty * lmax;
-  o.l = l;
+  const double l0 = -fe.reward * 200.0 + 1000 * dcost + 20 * tcost + (-creward * 200.0) + fcost + qnorm * 10.0;
+  o.l = VAR ? l0 + P.uncertainty * lmax : l0;
   for (int f = 0; f < T; ++f) o.margin[f] = fe.margin[f];
 
   // ---- backward of this level with dL/dl = wk
@@ -581,7 +587,7 @@ CDX_HD void level_fwd_bwd(const cdx_problem& P, int k, const CandidateIn& in, co
     const GpisPoint& gt = gp(1, 0, f);
     for (int i = 0; i < 3; ++i) o.g_target[f][i] += wk * 20.0 * gt.gmean[i];
   }
-  {
+  if constexpr (VAR) {
     // (fmax is data-dependent: the update is selected per fingertip so g_a keeps static indices)
     const GpisPoint& ga = gp(0, u, fmax);
     const double gs = wk * P.uncertainty / ga.std;
