@@ -385,15 +385,17 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
   g.e = ec;
 
   double gt[3] = {0, 0, 0}, gtar[3] = {0, 0, 0}, gcomp = 0, marg = 0;
+  double total = 0.0;  // Σ_k w_k·l_k (lane 0's)
   if (live) {
     int ulast = -1;
     int64_t qsel = -1;
-    double gs3[3] = {0, 0, 0}, ssel = 0;
+    double gs3[3] = {0, 0, 0}, ssel = 0, lsel = 0;
     for (int k = 0; k < K; ++k) {
       const double* r = lvl + ((int64_t)k * E + e) * LW;
       marg += P.weight[k] * r[1 + f];
       gcomp += r[1 + 7 * T + f];
       for (int i = 0; i < 3; ++i) { gt[i] += r[1 + T + 3 * f + i]; gtar[i] += r[1 + 4 * T + 3 * f + i]; }
+      double l = r[0];
       if constexpr (VL) {
         const int u = P.level_query[k];
         if (u != ulast) {  // this distinct level's group maximum and (on its lane) its ∇std
@@ -401,6 +403,7 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
           const int64_t m = (int64_t)u * E + e;
           qsel = gv.sel[m];
           ssel = gv.std_[qsel];
+          lsel = log(100 * ssel);  // the level loss's max_f log(100·std_f)
           if (qsel == cdx::q_alltip(u, e, f, E, T)) {
             if (gv.fold.partial)
               cdx::grad_fold_gstd(gv.fold, m, gv.var[qsel], gs3);
@@ -416,7 +419,9 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
             gtar[i] += ga - c * ga;
           }
         }
+        l = l + P.uncertainty * lsel;
       }
+      total += P.weight[k] * l;
     }
     const cdx::GpisPoint gpp = g(2, 0, f);
     for (int i = 0; i < 3; ++i) gt[i] += -5.0 * gpp.gmean[i];
@@ -469,12 +474,6 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
     for (int i = 0; i < 3; ++i) g_target[(e * T + f) * 3 + i] = gtar[i];
   }
   if (f != 0) return;
-  double total = 0.0;
-  for (int k = 0; k < K; ++k) {
-    double l = lvl[((int64_t)k * E + e) * LW];
-    if constexpr (VL) l = l + P.uncertainty * log(100 * gv.std_[gv.sel[(int64_t)P.level_query[k] * E + e]]);
-    total += P.weight[k] * l;
-  }
   double pre_sum = 0.0;
   for (int ff = 0; ff < T; ++ff) pre_sum += g(2, 0, ff).mean;
   total = total - pre_sum * 5.0;

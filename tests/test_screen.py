@@ -432,3 +432,64 @@ def test_kabsch_records_ahead_bit_identical(tmp_path):
         for k in a.files:
             assert np.array_equal(a[k], b[k], equal_nan=True), (mode, k)
     assert np.isfinite(a["given_loss"]).sum() > 4000
+
+
+_VARLATE_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {repo!r})
+from compliancedex_amd import ProbabilisticGraspOptimizer
+from compliancedex_amd.urdf import load_robot
+from compliancedex_amd.workloads import prob_inputs, synthetic_banana_gpis
+cfg = load_robot("allegro")["config"]
+g = synthetic_banana_gpis(2000, device="cuda")
+out = {{}}
+for E in (4096, 256):  # screened (side-stream level kernel) and unscreened (below the screen's row threshold)
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=321, spread=True)
+    opt = ProbabilisticGraspOptimizer("allegro", cfg["ee_link_name"], cfg["ee_link_offset"], palm_offset=palm,
+                                      ref_q=cfg["ref_q"], optimize_target=True, optimize_palm=True, device="cuda",
+                                      seed=77)
+    t = [torch.from_numpy(np.ascontiguousarray(a)).cuda().requires_grad_(True)
+         for a in (q, comp, target, palm[:, :3], palm[:, 3:])]
+    opt.closure(*t, 1, g, E)
+    torch.cuda.synchronize()
+    out["e%d_loss" % E] = opt.total_loss.cpu().numpy()
+    out["e%d_margin" % E] = opt.total_margin.cpu().numpy()
+    out["e%d_flip" % E] = opt.kabsch_flip.cpu().numpy()
+    for i, x in enumerate(t):
+        out["e%d_g%d" % (E, i)] = x.grad.cpu().numpy()
+np.savez({path!r}, **out)
+print("varlate child ok")
+"""
+
+
+def test_variance_cost_in_combine_matches_level_kernel(tmp_path):
+    """CDX_VAR_LATE (default 1): the level kernel leaves the variance cost uncertainty·max_f log(100·std_f)
+    (optimize_pregrasp.py:733) out and the combine kernel adds it — loss term and, through the all-tip
+    interpolation, its ∇std gradient — so that the level kernel can run beside the std passes.  Against
+    CDX_VAR_LATE=0 (the level kernel adds it, round-2 arithmetic): losses, margins and Kabsch masks
+    bit-identical (the variance term is the last operand of the level loss's left-to-right sum); the tip
+    and target gradients differ only by the order of one addition (c·(a + b) vs c·a + c·b): 1e-13 of the
+    largest entry.  Screened E = 4096 (level kernel on the side stream) and unscreened E = 256."""
+    import os
+    import subprocess
+    import sys
+    from tests.conftest import REPO
+    res = {}
+    for vl in ("1", "0"):
+        path = str(tmp_path / f"v{vl}.npz")
+        env = dict(os.environ, CDX_VAR_LATE=vl)
+        r = subprocess.run([sys.executable, "-c", _VARLATE_CHILD.format(repo=REPO, path=path)], capture_output=True,
+                           text=True, timeout=240, env=env)
+        assert r.returncode == 0 and "varlate child ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+        res[vl] = np.load(path)
+    a, b = res["0"], res["1"]
+    assert set(a.files) == set(b.files)
+    for k in a.files:
+        if k.endswith(("_loss", "_margin", "_flip")):
+            assert np.array_equal(a[k], b[k], equal_nan=True), k
+        else:
+            fin = np.isfinite(a[k])
+            assert np.array_equal(fin, np.isfinite(b[k])), k
+            scale = max(np.abs(a[k][fin]).max(), 1e-300)
+            assert np.abs(a[k][fin] - b[k][fin]).max() <= 1e-13 * scale, (k, np.abs(a[k][fin] - b[k][fin]).max() / scale)
+    assert np.isfinite(a["e4096_loss"]).sum() > 3000
