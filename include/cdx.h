@@ -277,7 +277,8 @@ int cdx_closure_screen_reset(const cdx_problem* p, int64_t E, void* workspace, c
  * go to buf [(capacity + 1) * W] f64, W = 5 + n_tips + n_dofs + n_tips + 3·n_tips + 6: row 0 the header
  * [stored, survived, capacity, 0, …], rows 1.. the first `capacity` survivors in candidate order as
  * [object_id, rank, cand_offset + e, best_loss, 1, margin[T], q[D], comp[T], target[3T], palm[6]],
- * the remaining rows zero.  One launch, no host synchronisation; the buffer feeds one all_gather. */
+ * the remaining rows zero.  Two launches over 64-candidate tiles (counts, then rows), no host
+ * synchronisation; the buffer feeds one all_gather. */
 int cdx_pack_survivors(int64_t E, int32_t n_tips, int32_t n_dofs, const double* margin, const double* best_loss,
                        const double* q, const double* comp, const double* target, const double* palm,
                        double object_id, double rank, int64_t cand_offset, int64_t capacity, double* buf,

@@ -243,13 +243,13 @@ def test_optimize_sharded_one_object_per_rank_gloo_world2():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("E,cap", [(4096, 4096), (4096, 7), (1, 3), (0, 5), (3000, 1500), (5000, 2100), (2049, 9000),
-                                   (1024, 0)])
+                                   (1024, 0), (130, 70), (65, 64)])
 def test_native_pack_equals_cpu_layout(E, cap):
-    """cdx_pack_survivors (the GPU pack: one launch, header counts written on the device, no host
-    sync, no memset) produces bit for bit the buffer of the CPU (torch-ops) layout: survivors in
+    """cdx_pack_survivors (the GPU pack: per-tile counts, then the rows — two launches over the chip,
+    header counts written on the device, no host sync, no memset) produces bit for bit the buffer of the CPU (torch-ops) layout: survivors in
     candidate order, overflow counted in the header, unused rows zero — also when the buffer was dirty
     before (the kernel zeroes them itself); NaN margins do not survive.  Ragged sizes cross the
-    kernel's 1024-candidate tiles with the capacity cut inside a tile."""
+    kernel's 64-candidate tiles with the capacity cut inside a tile."""
     d = _local(3, E=E)
     if E:
         d["margin"][0, 0] = float("nan")
