@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 for r in $(seq 1 "$R"); do
   for SPEC in "$@"; do
     IFS=+ read -r L ENVS <<< "$SPEC"
-    unset CDX_MEAN_SPLIT CDX_FORK_MEAN
+    for v in $(compgen -e | grep '^CDX_'); do unset "$v"; done  # each spec starts from the defaults
     if [ -n "$ENVS" ]; then for kv in ${ENVS//+/ }; do export "$kv"; done; fi
     if [ "$L" = base ]; then export CDX_LIB=$ROOT/compliancedex_amd/lib/libcdx.so; else export CDX_LIB=$ROOT/compliancedex_amd/lib/libcdx_$L.so; fi
     timeout -k 10 200 python3 "$ROOT/bench.py" --steps 50 --warmup 20 --no-cpu-baseline > "$OUT/run.log" 2>&1

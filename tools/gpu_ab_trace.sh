@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 # a spec may carry environment settings: name+VAR=VAL+VAR2=VAL2 (e.g. base+CDX_MEAN_SPLIT=1)
 for SPEC in "$@"; do
   IFS=+ read -r L ENVS <<< "$SPEC"
-  unset CDX_MEAN_SPLIT CDX_FORK_MEAN
+  for v in $(compgen -e | grep '^CDX_'); do unset "$v"; done  # each spec starts from the defaults
   if [ -n "$ENVS" ]; then for kv in ${ENVS//+/ }; do export "$kv"; done; fi
   if [ "$L" = base ]; then export CDX_LIB=$ROOT/compliancedex_amd/lib/libcdx.so; else export CDX_LIB=$ROOT/compliancedex_amd/lib/libcdx_$L.so; fi
   L=${SPEC//=/-}
