@@ -14,6 +14,7 @@
 //                               and the five parameter gradients        — :713-769, :49-118
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 
 #include "cdx_collision.h"
@@ -761,6 +762,16 @@ int launch_combine(const cdx_problem* p, int64_t E, const double* q, const doubl
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
+// Test hook (cdx_debug_fail_next_closure): the next screened closure returns CDX_ELAUNCH at injection
+// point `stage` (1: after the screen / selection and the side-stream fork, 2: after the exact pass,
+// 3: after the ∇std pass), through the same error path as a failed launch — one-shot.
+std::atomic<int> g_fail_stage{0};
+bool inject_fail(int stage) {
+  int want = stage;
+  return g_fail_stage.load(std::memory_order_relaxed) == stage &&
+         g_fail_stage.compare_exchange_strong(want, 0, std::memory_order_relaxed);
+}
+
 // The variance cost added by the combine kernel instead of the level kernel (CDX_VAR_LATE, default 1; 0 for
 // the A/B): the level kernel then reads no std, and the screened closure with the forked mean runs it on the
 // side stream right after the mean — beside the merge / exact selection / ∇std passes instead of after them.
@@ -968,12 +979,14 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     auto fork_cb = [](void* c) { return (*static_cast<decltype(launch_fork)*>(c))(); };
     rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.stats,
                                    s, fp == 4 ? +fork_cb : nullptr, &launch_fork);
+    if (!rc && inject_fail(1)) rc = CDX_ELAUNCH;
     if (rc) return joined(rc);
     if (fp == 2 && (rc = launch_fork())) return joined(rc);
     double* rpart = nullptr;
     int64_t rpad = 0;
     rc = cdx::gpis_refine_launch(p->gpis, w.X, w.rows, w.stats + cdx::SS_EXTRA, (int)Mg, Ms, w.refine_ws, w.V, s, &rpart,
                                  &rpad);
+    if (!rc && inject_fail(2)) rc = CDX_ELAUNCH;
     if (rc) return joined(rc);
     if (fp == 3 && (rc = launch_fork())) return joined(rc);
     rc = cdx::refine_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.sv2, w.vpos, w.keep, w.std_, w.var, w.sel,
@@ -981,6 +994,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     if (rc) return joined(rc);
     rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V, w.vrow,
                                grad_fold() ? &fold : nullptr);
+    if (!rc && inject_fail(3)) rc = CDX_ELAUNCH;
     if (rc) return joined(rc);
     if (fork && (rc = launch_b())) return joined(rc);
     // mean A (and the Kabsch records of mode 1) before the level kernel; mean B is joined before the
@@ -1022,6 +1036,12 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   if (rc) return rc;
   cdx::prof_mark(cdx::PROF_COST, false, s);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+int cdx_debug_fail_next_closure(int32_t stage) {
+  if (stage < 0 || stage > 3) return CDX_EINVAL;
+  g_fail_stage.store(stage, std::memory_order_relaxed);
+  return CDX_OK;
 }
 
 int cdx_closure_screen_stats(const cdx_problem* p, int64_t E, const void* workspace, int32_t* out) {

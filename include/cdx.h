@@ -270,6 +270,10 @@ int cdx_closure_screen_report(const cdx_problem* p, int64_t E, const void* works
 /* Zeroes the cumulative fields and the exact pass's arrival counters (stream-ordered; REQUIRED once
  * after allocating a workspace for a screened closure); a no-op when the closure does not screen. */
 int cdx_closure_screen_reset(const cdx_problem* p, int64_t E, void* workspace, cdx_stream_t stream);
+/* Test hook: the next screened cdx_closure returns CDX_ELAUNCH at injection point `stage` (1: after the
+ * screen / selection and the side-stream fork, 2: after the exact pass, 3: after the ∇std pass; 0 clears),
+ * through the error path of a failed launch — which joins the side stream before returning. */
+int cdx_debug_fail_next_closure(int32_t stage);
 
 /* ------------------------------------------------------------ survivor exchange ------
  * Multi-GPU record pack (no reference counterpart — the reference is single-GPU):

@@ -493,3 +493,50 @@ def test_variance_cost_in_combine_matches_level_kernel(tmp_path):
             scale = max(np.abs(a[k][fin]).max(), 1e-300)
             assert np.abs(a[k][fin] - b[k][fin]).max() <= 1e-13 * scale, (k, np.abs(a[k][fin] - b[k][fin]).max() / scale)
     assert np.isfinite(a["e4096_loss"]).sum() > 3000
+
+
+def test_injected_error_joins_side_stream(banana2000):
+    """Every error return after the screened closure has forked its side stream (Kabsch records, mean,
+    level kernel) joins it first (cdx_closure.hip: joined()).  cdx_debug_fail_next_closure makes the next
+    closure fail at one of three points — after the screen / selection / fork, after the exact pass,
+    after the ∇std pass — through the failed-launch error path.  Eagerly: the call raises, the stream
+    drains, and the next closure gives the unfailed results bit for bit.  Under hipGraph capture: the
+    call raises and the capture still ends cleanly (an unjoined fork would make capture_end fail with
+    its own error instead of the closure's)."""
+    from compliancedex_amd import _native as N
+    from compliancedex_amd.workloads import prob_inputs
+    cfg, opt = _opt()
+    E = 1024  # 4096 all-tip rows: screened, side stream forked
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=41, spread=True)
+    opt.palm_offset = torch.from_numpy(palm).to(DEV)
+    t = [torch.from_numpy(np.ascontiguousarray(x)).to(DEV) for x in (q, comp, target, palm[:, :3], palm[:, 3:])]
+    noise = torch.from_numpy(np.random.default_rng(5).random((3 * E, 3, 3))).to(DEV)
+    lib = N.load()
+
+    def run():
+        opt.closure(*t, 1, banana2000, E, kabsch_noise=noise)
+        return [x.detach().cpu().numpy().copy() for x in (opt.total_loss, opt.total_margin, opt.kabsch_flip)]
+
+    ref = run()
+    torch.cuda.synchronize()
+    for stage in (1, 2, 3):
+        N.check(lib.cdx_debug_fail_next_closure(stage), "cdx_debug_fail_next_closure")
+        with pytest.raises(RuntimeError, match="cdx_closure failed"):
+            opt.closure(*t, 1, banana2000, E, kabsch_noise=noise)
+        torch.cuda.synchronize()
+        for a, b in zip(run(), ref):
+            assert np.array_equal(a, b, equal_nan=True), stage
+        N.check(lib.cdx_debug_fail_next_closure(stage), "cdx_debug_fail_next_closure")
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with pytest.raises(RuntimeError, match="cdx_closure failed"):
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side):
+                    opt.closure(*t, 1, banana2000, E, kabsch_noise=noise)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        del g
+        for a, b in zip(run(), ref):
+            assert np.array_equal(a, b, equal_nan=True), stage
+    N.check(lib.cdx_debug_fail_next_closure(0), "cdx_debug_fail_next_closure")
