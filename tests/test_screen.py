@@ -540,3 +540,4 @@ def test_injected_error_joins_side_stream(banana2000):
         for a, b in zip(run(), ref):
             assert np.array_equal(a, b, equal_nan=True), stage
     N.check(lib.cdx_debug_fail_next_closure(0), "cdx_debug_fail_next_closure")
+
