@@ -17,6 +17,8 @@
 // latency-bound on one CU.)
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include "cdx.h"
 
 namespace {
@@ -104,13 +106,16 @@ __global__ __launch_bounds__(PACK_TILE) void pack_survivors_kernel(
       buf[c] = c == 0 ? (double)stored : (c == 1 ? (double)total : (c == 2 ? (double)capacity : 0.0));
 }
 
-// Per-device scratch for the tile counts (grown on demand; a grown-out array is not freed, since a pack
-// still queued on some stream may read it).
+// Per-device scratch for the tile counts (grown on demand under a lock; a grown-out array is not freed,
+// since a pack still queued on some stream may read it).  One scratch per device: packs on one device are
+// expected one at a time in stream order (one exchange per optimise loop), not on several streams at once.
 int* pack_scratch(int64_t tiles) {
+  static std::mutex mu;
   static int* per_dev[64] = {};
   static int64_t cap[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
   if (cap[dev] < tiles) {
     const int64_t want = tiles < 4096 ? 4096 : tiles;
     void* p = nullptr;

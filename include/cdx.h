@@ -282,7 +282,8 @@ int cdx_debug_fail_next_closure(int32_t stage);
  * [stored, survived, capacity, 0, …], rows 1.. the first `capacity` survivors in candidate order as
  * [object_id, rank, cand_offset + e, best_loss, 1, margin[T], q[D], comp[T], target[3T], palm[6]],
  * the remaining rows zero.  Two launches over 64-candidate tiles (counts, then rows), no host
- * synchronisation; the buffer feeds one all_gather. */
+ * synchronisation; the buffer feeds one all_gather.  The tile counts use a per-device scratch array: packs on
+ * one device run one at a time in stream order (not concurrently on several streams). */
 int cdx_pack_survivors(int64_t E, int32_t n_tips, int32_t n_dofs, const double* margin, const double* best_loss,
                        const double* q, const double* comp, const double* target, const double* palm,
                        double object_id, double rank, int64_t cand_offset, int64_t capacity, double* buf,
