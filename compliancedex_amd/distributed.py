@@ -19,8 +19,9 @@ Every rank must pass an equal-shaped buffer to ``all_gather`` (RCCL sizes its re
 the local one), so the default capacity is the same on every rank: ⌈total / world⌉ for a sharded
 batch, the largest per-rank candidate count (one all_reduce) for one object per rank.
 
-On the GPU the pack is one kernel (cdx_pack_survivors: block-scan compaction in candidate order,
-header counts written on the device, no host synchronisation); CPU tensors (the gloo tests) take
+On the GPU the pack is cdx_pack_survivors (two chip-wide launches over 64-candidate tiles: survivor
+counts, then each tile's rows at the prefix of the earlier tiles' counts — compaction in candidate
+order, header counts written on the device, no host synchronisation); CPU tensors (the gloo tests) take
 the same layout through torch ops.  Reading the gathered headers (``unpack_records``) is the one
 host synchronisation of the exchange.
 """
