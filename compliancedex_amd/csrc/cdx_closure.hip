@@ -671,10 +671,13 @@ bool side_stream(SideStream& out) {
   SideStream& ss = per_dev[dev];
   if (!ss.s) {
     hipStream_t st;
-    // CDX_SIDE_PRIO: < 0 creates the side stream at the device's lowest priority, > 0 at its
-    // highest (the CP prefers a higher-priority queue's dispatches), 0 (default) normal.
+    // CDX_SIDE_PRIO: < 0 creates the side stream at the device's lowest priority, > 0 (default, round 3)
+    // at its highest (the CP prefers a higher-priority queue's dispatches: the mean and the level kernel,
+    // which gate the ∇std pass, over the merge; 1.009–1.013 vs 1.012–1.016 ms per closure over 3
+    // interleaved rounds, profiles/r03zi_side_prio_ab.jsonl; as the default 1.017–1.023 vs 1.017–1.030,
+    // r03zj_side_prio_default_ab.jsonl), 0 normal.
     const char* pe = getenv("CDX_SIDE_PRIO");
-    const int want = pe ? atoi(pe) : 0;
+    const int want = pe ? atoi(pe) : 1;
     int least = 0, greatest = 0;
     hipError_t ce;
     if (want != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
