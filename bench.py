@@ -161,22 +161,32 @@ def main():
         qt.grad = ct.grad = tt.grad = pp.grad = po.grad = None
         opt.closure(qt, ct, tt, pp, po, 1, gpis, E)
 
-    def exchange():
+    def exchange(check_shape=True):
         """Surviving grasps of this rank's object → one all_gather of fixed-capacity records
-        (capacity E on every rank; the header keeps the true count)."""
+        (capacity E on every rank; the header keeps the true count).  The buffer shapes are checked
+        equal across ranks (one all_reduce) on the warm-up exchange; the timed one reuses that shape."""
         buf = D.pack_survivors(E, rank, rank, 0, opt.total_loss, opt.total_margin, qt.detach(), ct.detach(),
                                tt.detach(), torch.cat([pp, po], 1).detach())
         if world > 1:
-            records, bufs = D.all_gather_survivors(buf if args.backend == "nccl" else buf.cpu(), return_buffers=True)
+            records, bufs = D.all_gather_survivors(buf if args.backend == "nccl" else buf.cpu(), return_buffers=True,
+                                                   check_shape=check_shape)
         else:
             records, bufs = D.unpack_records([buf]), [buf]
         return buf, records, bufs
 
-    for _ in range(args.warmup):
-        step()
-    exchange()  # warms the pack kernels and the communicator (RCCL sets up its rings on first use)
     lib = N.load()
     import ctypes
+    # Host-side setup that idles the GPU goes BEFORE the warm-up steps, so the timed steps start at the
+    # clock the warm-up reached: the profiling event pool (cdx_profile_enable creates 49 152 events on
+    # first use) and the exchange's first run (pack kernels, communicator setup, one host read), here on
+    # the parameters with zero losses / margins (no survivors; the same buffer shapes).
+    N.check(lib.cdx_profile_enable((1 << N.PROF_STAGES) - 1), "cdx_profile_enable")
+    N.check(lib.cdx_profile_enable(0), "cdx_profile_enable")
+    opt.total_loss = torch.zeros(E, dtype=torch.float64, device=dev)
+    opt.total_margin = torch.zeros(E, ct.shape[1], dtype=torch.float64, device=dev)
+    exchange()  # warms the pack kernels and the communicator (RCCL sets up its rings on first use)
+    for _ in range(args.warmup):
+        step()
     # HIP events only around the two roofline kernels inside the timed region (each event record
     # costs ≈ 5 µs of stream time); the other stages are timed in a separate pass afterwards
     # (each record costs stream time: only the dominant kernel's — the exact-pass refine, whose roofline
@@ -187,15 +197,23 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-step stream times (the clock ramp): one event between steps on the closure's stream
+    # (CDX_BENCH_STEP_EVENTS=0 drops them for an A/B of their cost)
+    step_events = os.environ.get("CDX_BENCH_STEP_EVENTS", "1") != "0"
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if step_events else []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    if evs:
+        evs[0].record()
+    for i in range(args.steps):
         step()
+        if evs:
+            evs[i + 1].record()
     # the exchange is queued right behind the last step (no host sync in between, as an optimise loop
     # would run it); its time is the stream time from the last step's end to the exchange's end
     # (pack + all_gather + the header read), from events on the step's stream
     eg0, eg1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     eg0.record()
-    buf, records, bufs = exchange()
+    buf, records, bufs = exchange(check_shape=False)
     n_records = int(records.shape[0])
     eg1.record()
     torch.cuda.synchronize()
@@ -234,6 +252,7 @@ def main():
         elapsed, gather_s = float(t[0]), float(t[1])
     nan_candidates = int((~torch.isfinite(opt.total_loss)).sum())
 
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)] if evs else []
     ms_per_step = 1e3 * elapsed / args.steps
     value = E * world / (elapsed / args.steps)
     stage_names = ["queries", "gpis_mean", "gpis_std_var", "cost_bwd", "gpis_std_grad", "gpis_screen"]
@@ -284,6 +303,11 @@ def main():
                                  "from the last step's end to the exchange's end); ms_repeat_median: the same "
                                  "exchange repeated after the timed region, host wall time with a sync before each "
                                  "(informational)"},
+            "step_ms": ({"min": min(step_ms), "median": statistics.median(step_ms), "max": max(step_ms),
+                         "first5_mean": statistics.fmean(step_ms[:5]), "last5_mean": statistics.fmean(step_ms[-5:]),
+                         "note": "rank 0's stream time per timed step (HIP events between steps): the clock ramp "
+                                 "shows as first5_mean > last5_mean"} if step_ms else None),
+            "native": N.build_info(),
             "stage_ms": stage_ms,
             "stage_ms_note": "gpis_std_var (the refine kernel, the headline roofline): HIP events over "
                               "the timed steps; the other stages from a 10-step all-stage pass after the timed "
@@ -325,11 +349,17 @@ def main():
                                                   "audit_misses", "audit_flips", "faults", "max_ratio",
                                                   "max_ratio_audit", "cum_closures", "cum_audited_rows",
                                                   "cum_bound_misses", "cum_audit_misses", "cum_audit_flips",
-                                                  "cum_faults", "cum_max_ratio", "cum_max_ratio_audit")}
+                                                  "cum_faults", "cum_max_ratio", "cum_max_ratio_audit", "repaired",
+                                                  "discarded_rows", "min_gap", "audit_cut", "cum_repairs",
+                                                  "cum_discarded_rows", "cum_min_gap")}
+            out["screen"] = {k: (None if isinstance(v, float) and not np.isfinite(v) else v)  # strict JSON: no inf
+                             for k, v in out["screen"].items()}
             out["screen"]["delta_over_k0"] = gpis.native_state().desc.screen_delta / float(gpis.R) ** 3
-            out["screen"]["note"] = ("every closure re-checks its kept rows and an audit sample of discarded rows "
-                                     "with the exact fp64 pass; max_ratio = max |estimate − exact| / margin; cum_* "
-                                     "over all closures of this run")
+            out["screen"]["note"] = ("every closure re-checks its kept rows and the discarded rows nearest the keep "
+                                     "threshold (smallest z = margins below the group's floor) with the exact fp64 "
+                                     "pass and repairs itself (every row exact) if a check fails; max_ratio = max "
+                                     "|estimate − exact| / margin; min_gap = smallest z left unaudited; cum_* over all "
+                                     "closures of this run")
         # the dominant kernel (longest per launch) is the headline roofline
         # the headline roofline: the longest-per-launch kernel among those timed live in the timed steps
         stage_of = {"roofline_refine": 2, "roofline_grad": 4, "roofline_screen": 5}

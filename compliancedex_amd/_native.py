@@ -83,7 +83,10 @@ class CdxScreenReport(C.Structure):
                [("max_ratio", C.c_double), ("max_ratio_audit", C.c_double)] + \
                [(n, C.c_int64) for n in ("cum_closures", "cum_audited_rows", "cum_bound_misses", "cum_audit_misses",
                                          "cum_audit_flips", "cum_faults")] + \
-               [("cum_max_ratio", C.c_double), ("cum_max_ratio_audit", C.c_double)]
+               [("cum_max_ratio", C.c_double), ("cum_max_ratio_audit", C.c_double)] + \
+               [("repaired", C.c_int32), ("discarded_rows", C.c_int32), ("min_gap", C.c_double),
+                ("audit_cut", C.c_double), ("cum_repairs", C.c_int64), ("cum_discarded_rows", C.c_int64),
+                ("cum_min_gap", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -163,8 +166,19 @@ def load():
                 C.sizeof(CdxScreenReport)]
         if list(sizes) != mine:
             raise ImportError(f"ABI struct size mismatch: library {list(sizes)} vs binding {mine}")
+        info = build_info()
+        if not info["matches"] and "CDX_LIB" not in os.environ:
+            import warnings
+            warnings.warn(f"{path} was not built from this tree's csrc/ (stamp {info['lib_sha16']}, sources "
+                          f"{info['src_sha16']}): rebuild with `python -m compliancedex_amd.build`")
         _lib = lib
         return lib
+
+
+def build_info():
+    """Source digest of the tree vs the one libcdx.so was built from (build.stamp_info)."""
+    from .build import stamp_info
+    return stamp_info(lib_path())
 
 
 def check(rc, what):

@@ -43,12 +43,45 @@ def _deps():
 DEFAULT_DEFINES = ("CDX_FAST_SQRT", "CDX_STD_SCHED")
 
 
+def source_digest(defines=DEFAULT_DEFINES):
+    """sha256 of what libcdx.so is compiled from: every file of csrc/ and include/cdx.h (by name and
+    bytes, sorted), the -D switches and the offload arch."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted(_deps()):
+        h.update(os.path.relpath(p, REPO).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    h.update(("|".join(defines) + "|" + ARCH).encode())
+    return h.hexdigest()
+
+
+def _write_stamp(out, defines):
+    with open(out + ".srcsha", "w") as f:
+        f.write(source_digest(defines) + "\n")
+
+
+def stamp_info(out=None, defines=DEFAULT_DEFINES):
+    """{"src_sha16": digest of the tree's sources, "lib_sha16": the digest the library was built from
+    (its .srcsha stamp, None if absent), "matches": both equal} — the library a run loads was built
+    from exactly these sources (the GPU box runs the pushed binary without building)."""
+    out = out or os.path.join(LIB, "libcdx.so")
+    cur = source_digest(defines)
+    try:
+        with open(out + ".srcsha") as f:
+            built = f.read().strip()
+    except OSError:
+        built = None
+    return {"src_sha16": cur[:16], "lib_sha16": built[:16] if built else None, "matches": built == cur}
+
+
 def build_device(force=False, defines=DEFAULT_DEFINES, out_name="libcdx.so"):
     os.makedirs(LIB, exist_ok=True)
     out = os.path.join(LIB, out_name)
     if not force and not _stale(out, _deps()):
         return out
-    objs = []
+    cmds, objs = [], []
     for src in HIP_SOURCES:
         obj = os.path.join(LIB, out_name + "." + src.replace(".hip", ".o"))
         # -Wno-pass-failed: `#pragma unroll` on loops whose trip count is only known at run time in the
@@ -61,9 +94,15 @@ def build_device(force=False, defines=DEFAULT_DEFINES, out_name="libcdx.so"):
         # collision cost's 1/d near the floor amplifies a contracted f32 FK to 1e-4)
         if src in ("cdx_sdf.hip", "cdx_closure.hip"):
             flags.append("-ffp-contract=off")
-        _run([HIPCC, *flags, "-c", os.path.join(CSRC, src), "-o", obj])
+        cmds.append([HIPCC, *flags, "-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)
+    # one hipcc per translation unit, a few at a time (each holds ~1-2 GB while compiling)
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(len(cmds), int(os.environ.get("CDX_BUILD_JOBS", "4"))))
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(_run, cmds))
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out])
+    _write_stamp(out, defines)
     for o in objs:
         os.remove(o)
     return out

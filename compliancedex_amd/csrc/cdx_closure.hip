@@ -521,6 +521,7 @@ struct ClosureWs {
   // keep / audit masks, statistics (cdx::ScreenStat), ∇std V rows, screen / refine scratch
   double* sv2;
   int *vpos, *rows, *stats;
+  unsigned* zkey;  // discarded rows' normalised gap z (float bits) for the audit
   unsigned short* keep;
   int64_t* vrow;
   void *screen_ws, *refine_ws;
@@ -592,6 +593,7 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   w.vpos = scr ? (int*)take(Ms * sizeof(int)) : nullptr;
   w.rows = scr ? (int*)take(Ms * sizeof(int)) : nullptr;
   w.stats = scr ? (int*)take(cdx::SS_WORDS * sizeof(int)) : nullptr;
+  w.zkey = scr ? (unsigned*)take(Ms * sizeof(unsigned)) : nullptr;
   w.keep = scr ? (unsigned short*)take(Mg * sizeof(unsigned short)) : nullptr;
   w.vrow = scr ? (int64_t*)take(Mg * sizeof(int64_t)) : nullptr;
   w.screen_ws = scr ? take(cdx::screen_ws_bytes(p->gpis, Ms)) : nullptr;
@@ -773,6 +775,19 @@ bool inject_fail(int stage) {
   int want = stage;
   return g_fail_stage.load(std::memory_order_relaxed) == stage &&
          g_fail_stage.compare_exchange_strong(want, 0, std::memory_order_relaxed);
+}
+
+// The screened closure's repair pass (CDX_SCREEN_REPAIR, default 1; 0 only for the cost A/B): when any
+// check of the closure failed — a kept or audited estimate off by more than its margin, an audited row
+// that is its group's exact maximum, a maximum on an unrun row — every all-tip row runs the exact pass
+// and the groups select as the unscreened closure does, inside the same closure (gated launches: no
+// host sync, hipGraph-capturable).
+bool screen_repair() {
+  static const bool on = [] {
+    const char* e = getenv("CDX_SCREEN_REPAIR");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
 }
 
 // The variance cost added by the combine kernel instead of the level kernel (CDX_VAR_LATE, default 1; 0 for
@@ -980,8 +995,8 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     const int fp = kmode == 1 ? 4 : (fork ? fork_point() : 0);
     if (fp == 1 && (rc = launch_fork())) return joined(rc);
     auto fork_cb = [](void* c) { return (*static_cast<decltype(launch_fork)*>(c))(); };
-    rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.stats,
-                                   s, fp == 4 ? +fork_cb : nullptr, &launch_fork);
+    rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.zkey,
+                                   w.stats, s, fp == 4 ? +fork_cb : nullptr, &launch_fork);
     if (!rc && inject_fail(1)) rc = CDX_ELAUNCH;
     if (rc) return joined(rc);
     if (fp == 2 && (rc = launch_fork())) return joined(rc);
@@ -995,6 +1010,16 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     rc = cdx::refine_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.sv2, w.vpos, w.keep, w.std_, w.var, w.sel,
                                    w.Xg, w.vrow, w.stats, s);
     if (rc) return joined(rc);
+    if (screen_repair()) {
+      // the repair pass, gated on this closure's checks (a no-op launch pair otherwise): every all-tip row
+      // through the exact pass (identity list) and the unscreened selection — no screened result that
+      // failed a check leaves the closure, whichever entry point called it
+      rc = cdx::gpis_refine_launch(p->gpis, w.X, nullptr, nullptr, (int)Ms, Ms, w.refine_ws, w.V, s, nullptr, nullptr,
+                                   w.stats, false);
+      if (!rc)
+        rc = cdx::repair_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.std_, w.var, w.sel, w.Xg, w.vrow, w.stats, s);
+      if (rc) return joined(rc);
+    }
     rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V, w.vrow,
                                grad_fold() ? &fold : nullptr);
     if (!rc && inject_fail(3)) rc = CDX_ELAUNCH;
@@ -1093,6 +1118,14 @@ int cdx_closure_screen_report(const cdx_problem* p, int64_t E, const void* works
   out->cum_faults = (uint32_t)st[c + cdx::SS_FAULT];
   out->cum_max_ratio = ratio(c + cdx::SS_RATIO);
   out->cum_max_ratio_audit = ratio(c + cdx::SS_RATIO_AUDIT);
+  out->repaired = st[cdx::SS_REPAIR];
+  out->discarded_rows = st[cdx::SS_DISCARD];
+  out->min_gap = ratio(cdx::SS_GAP);
+  out->audit_cut = ratio(cdx::SS_AUDIT_CUT);
+  out->cum_repairs = (uint32_t)st[c + cdx::SS_REPAIR];
+  out->cum_discarded_rows = (uint32_t)st[c + cdx::SS_DISCARD];
+  const unsigned cg = (unsigned)st[c + cdx::SS_GAP];  // 0xFFFFFFFF − bits of the smallest gap, 0: none
+  out->cum_min_gap = cg ? (double)__builtin_bit_cast(float, 0xFFFFFFFFu - cg) : INFINITY;
   return CDX_OK;
 }
 

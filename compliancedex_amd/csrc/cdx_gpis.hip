@@ -21,6 +21,7 @@
 #include "cdx_gpis.h"
 #include "cdx_gpis_launch.h"
 #include "cdx_prof.h"
+#include "cdx_screen.h"
 
 using cdx::gpis_k;
 using cdx::gpis_k0;
@@ -259,8 +260,8 @@ enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2, MODE_VARL = 3 };
 constexpr int RC_MAX_NT = 16;  // stripes with host unit costs (N_pad ≤ 4096); beyond: equal K-step cuts
 static_assert(RC_MAX_NT == cdx::GC_MAX_NT, "the ∇std pass's stripe costs travel in RefineList::uc");
 struct RefineList {
-  const int* rows;    // query index per list position
-  const int* extra;   // device count of positions past the G primary ones
+  const int* rows;    // query index per list position (null: the identity)
+  const int* extra;   // device count of positions past the G primary ones (nullable: 0)
   int G;
   double* slots;      // [gridDim.x][2][ST_BM][ST_BN] partial V tiles of cut stripes
   int* cnt;           // [Nt][mt_cap] arrival counters of cut units (zero between launches)
@@ -268,7 +269,14 @@ struct RefineList {
   int64_t* cuts;      // [gridDim.x + 1] piece bounds in the K-sequence (written by the refine kernel)
   int n_uc;           // stripes with unit costs below (= N_pad/256), 0: equal K-step cuts
   int64_t uc[RC_MAX_NT];  // cost of one (stripe, query tile) unit per stripe (var_unit_cost, host)
+  const int* gate;    // nullable: screen statistics; the launch has no rows unless cdx::screen_failed
 };
+
+// Rows of a refine launch (device-side count; 0 when gated off).
+__device__ inline int64_t refine_rows(const RefineList& rl) {
+  if (rl.gate && !cdx::screen_failed(rl.gate)) return 0;
+  return (int64_t)rl.G + (rl.extra ? *rl.extra : 0);
+}
 
 // Whitened pass A operand: K* generated on chip per stripe (default), or read from a buffer
 // gpis_kstar_kernel wrote (CDX_VAR_KLOAD).  On chip, each K* entry is regenerated by every stripe
@@ -520,7 +528,8 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   double* xq = smem + ST_NBUF * (ST_TILE + ST_BTILE);
   double* xs = xq + ST_BM * 3;  // [2][ST_XS]: X1 rows of the stage generated next
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t Mrows = LIST ? (int64_t)rl.G + *rl.extra : M;  // rows of this launch (list: device count)
+  const int64_t Mrows = LIST ? refine_rows(rl) : M;  // rows of this launch (list: device count)
+  if (LIST && Mrows == 0) return;                     // a gated repair pass with nothing to repair
 #if defined(CDX_DIAG_WGTIME)
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -555,7 +564,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   const double* vrow = nullptr;  // MODE_GRADV: this thread's row of the stored V
   {
     int64_t m = min(m0 + gm, Mrows - 1);  // pad rows replicate a valid query
-    if (LIST) m = rl.rows[m];
+    if (LIST && rl.rows) m = rl.rows[m];
     qx = X[3 * m]; qy = X[3 * m + 1]; qz = X[3 * m + 2];
     if (tid < ST_BM) { xq[3 * tid] = qx; xq[3 * tid + 1] = qy; xq[3 * tid + 2] = qz; }
     if (!GEN) vrow = vin + (vsel ? vsel[m] : m) * (int64_t)Np;
@@ -1130,7 +1139,8 @@ __global__ __launch_bounds__(256) void gpis_var_splitk_finalize(cdx_gpis g, cons
 // whose K-range ends inside piece p after starting in an earlier one.
 __global__ __launch_bounds__(MERGE_THREADS) void gpis_var_merge(cdx_gpis g, RefineList rl, int64_t M_pad,
                                                       double* __restrict__ partial, double* __restrict__ vout) {
-  const int64_t Mrows = (int64_t)rl.G + *rl.extra;
+  const int64_t Mrows = refine_rows(rl);
+  if (Mrows == 0) return;
   const RefineCuts rc = refine_cuts(g, Mrows, gridDim.x);
   const int p = blockIdx.x;
   if (p >= rc.pieces) return;
@@ -1406,34 +1416,35 @@ int gpis_refine_reset(const cdx_gpis& g, int64_t Mcap, void* ws, hipStream_t s) 
 
 template <int KT>
 static void refine_launch_kt(const cdx_gpis& g, const double* X, int64_t Mcap, const RefineList& rl, double* partial,
-                             int64_t M_pad, double* vout, hipStream_t s) {
-  prof_mark(PROF_GPIS_STD, true, s);
+                             int64_t M_pad, double* vout, hipStream_t s, bool prof) {
+  if (prof) prof_mark(PROF_GPIS_STD, true, s);
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VARL>), dim3(REFINE_PIECES), dim3(ST_THREADS), 0, s, g, X, Mcap, partial,
                      M_pad, 0, g.N_pad / ST_BN, vout, nullptr, nullptr, 0, rl);
-  prof_mark(PROF_GPIS_STD, false, s);
+  if (prof) prof_mark(PROF_GPIS_STD, false, s);
 #if !defined(CDX_MERGE_FUSED)
   hipLaunchKernelGGL(gpis_var_merge, dim3(REFINE_PIECES), dim3(MERGE_THREADS), 0, s, g, rl, M_pad, partial, vout);
 #endif
 }
 
 int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
-                       void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out) {
+                       void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out, const int* gate,
+                       bool prof) {
   if (Mcap <= 0 || G <= 0 || G > Mcap) return CDX_EINVAL;
   const int64_t M_pad = round_up(Mcap, ST_BM);
   double* partial = static_cast<double*>(ws);
   char* slots = static_cast<char*>(ws) + refine_part_bytes(g, Mcap);
   RefineList rl{rows, extra, G, reinterpret_cast<double*>(slots), reinterpret_cast<int*>(slots + refine_slot_bytes()),
                 (int)(M_pad / ST_BM),
-                reinterpret_cast<int64_t*>(slots + refine_slot_bytes() + refine_cnt_bytes(g, Mcap)), 0, {}};
+                reinterpret_cast<int64_t*>(slots + refine_slot_bytes() + refine_cnt_bytes(g, Mcap)), 0, {}, gate};
   const int Nt = g.N_pad / ST_BN;
   if (Nt <= RC_MAX_NT) {
     rl.n_uc = Nt;
     for (int nt = 0; nt < Nt; ++nt) rl.uc[nt] = var_unit_cost(nt, g.N, g.N_pad);
   }
   switch (g.kernel) {
-    case CDX_KERNEL_TPS: refine_launch_kt<CDX_KERNEL_TPS>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
-    case CDX_KERNEL_RBF: refine_launch_kt<CDX_KERNEL_RBF>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
-    default: refine_launch_kt<CDX_KERNEL_JOINT>(g, X, Mcap, rl, partial, M_pad, vout, s); break;
+    case CDX_KERNEL_TPS: refine_launch_kt<CDX_KERNEL_TPS>(g, X, Mcap, rl, partial, M_pad, vout, s, prof); break;
+    case CDX_KERNEL_RBF: refine_launch_kt<CDX_KERNEL_RBF>(g, X, Mcap, rl, partial, M_pad, vout, s, prof); break;
+    default: refine_launch_kt<CDX_KERNEL_JOINT>(g, X, Mcap, rl, partial, M_pad, vout, s, prof); break;
   }
   if (partial_out) *partial_out = partial;
   if (M_pad_out) *M_pad_out = M_pad;

@@ -141,10 +141,14 @@ __device__ inline void grad_fold_gstd(const GradFold& f, int64_t m, double v, do
 // rows rows[0 .. G + *extra) of X (device-side count, at most Mcap), cut into pieces of equal estimated
 // cost (one per CU) whatever the count; V rows go to vout at the list positions ([round_up(Mcap, 128),
 // N_pad]), Σ V² per (stripe, position) to the returned partial [N_pad/256][*M_pad_out].
+// rows null: the identity list (rows 0 .. G + *extra; extra nullable = 0).  gate (nullable): the
+// closure's screen statistics — the launch runs only when a check failed (cdx::screen_failed), else every
+// workgroup returns at once (the closure's repair pass).  prof: mark the launch for cdx_profile_read.
 size_t gpis_refine_ws_bytes(const cdx_gpis& g, int64_t Mcap);
 // Zeroes the refine workspace's cut-unit arrival counters (once after allocation; every launch
 // leaves them zero).
 int gpis_refine_reset(const cdx_gpis& g, int64_t Mcap, void* ws, hipStream_t s);
 int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
-                       void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out);
+                       void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out,
+                       const int* gate = nullptr, bool prof = true);
 }  // namespace cdx

@@ -66,9 +66,15 @@ int screen_var_launch(const cdx_gpis& g, const double* X, int64_t M, double* var
 
 // Screening statistics in the closure workspace (int32 words; "ratio" words hold the float bits of
 // max |estimate − exact| / Δ_f over the rows checked, finite rows only).  Per closure (reset by the
-// compaction kernel): the rows checked are every kept row and the audit sample (a deterministic
-// pseudo-random draw of discarded rows, run through the exact pass as well).  Cumulative (reset only
-// by cdx_closure_screen_reset): the same events summed over closures.
+// compaction kernel): the rows checked are every kept row and the audited rows — the discarded rows
+// nearest the keep threshold (smallest normalised gap z, below).  Cumulative (reset only by
+// cdx_closure_screen_reset): the same events summed over closures.
+//
+// Normalised gap of a discarded row f of a group: z_f = (lo − a_f)/Δ_f with lo = max_g (a_g − Δ_g), the
+// margins between its estimate and the group's keep floor (> 1 for every discarded row).  The row g
+// attaining lo is kept, so its exact value is known: f can hold the group's true maximum only if f's
+// own estimate is off by more than z_f·Δ_f (+ (1 − ratio_g)·Δ_g).  The audit runs the rows of
+// smallest z exactly; every row left out has z ≥ SS_GAP.
 enum ScreenStat {
   SS_EXTRA = 0,        // rows in the exact-pass list past the G group leaders (kept + audited)
   SS_MISS = 1,         // kept rows whose finite estimate missed the exact value by more than Δ_f
@@ -78,22 +84,45 @@ enum ScreenStat {
   SS_FAULT = 5,        // groups whose maximum fell on a row the exact pass did not run (safe fallback)
   SS_RATIO = 6,        // max error ratio over kept rows (float bits)
   SS_RATIO_AUDIT = 7,  // max error ratio over audited rows (float bits)
-  SS_CUM = 8,          // cumulative block: closures, then SS_MISS .. SS_RATIO_AUDIT summed / maxed
-  SS_WORDS = 16
+  SS_REPAIR = 8,       // 1: a check above failed and the closure re-ran every all-tip row exactly
+  SS_GAP = 9,          // smallest z over the discarded rows left unaudited (float bits; +inf: none)
+  SS_AUDIT_CUT = 10,   // the audit's cut: every discarded row with z below it was audited (float bits)
+  SS_DISCARD = 11,     // discarded rows (audited or not)
+  SS_CUM = 16,         // cumulative block: [SS_CUM] closures, [SS_CUM + k] event k summed (counts),
+                       // maxed (ratios) — SS_GAP as the max of 0xFFFFFFFF − bits (0: no value)
+  SS_WORDS = 32
 };
 
-// Audited discarded rows per closure (expected count; 0 disables the audit): CDX_SCREEN_AUDIT.
+// Any check of this closure failed (the repair pass runs when it did).
+__device__ __host__ inline bool screen_failed(const int* st) {
+  return (st[SS_MISS] | st[SS_AUDIT_MISS] | st[SS_AUDIT_FLIP] | st[SS_FAULT]) != 0;
+}
+
+// The audit's row budget per closure (CDX_SCREEN_AUDIT, default 64; 0 disables the audit): the
+// discarded rows are binned by z (8 bins per octave from z = 1) and the lowest bins are audited while
+// their count stays ≤ the budget, plus the bin that crosses it when the total stays ≤ 4× the budget.
 int screen_audit_rows();
+constexpr int AUDIT_BINS = 256;
+constexpr unsigned Z_NONE = 0xFFFFFFFFu;  // zkey of a kept / leader row (not an audit candidate)
+__device__ __host__ inline int audit_bin(unsigned key) {
+  if (key <= 0x3F800000u) return 0;  // z ≤ 1 (rounding at the keep threshold)
+  const unsigned b = (key - 0x3F800000u) >> 20;
+  return b < (unsigned)AUDIT_BINS ? (int)b : AUDIT_BINS - 1;
+}
+__device__ __host__ inline unsigned audit_bin_floor(int b) {  // float bits of the smallest z of bin b
+  return b >= AUDIT_BINS ? 0x7F800000u : 0x3F800000u + ((unsigned)b << 20);
+}
 
 // Closure screening of the all-tip rows (G groups of T, M = G·T): screen partials in ws
 // (screen_ws_bytes(g, M)), per-row estimate sv2, rows kept for the exact pass listed in rows[0 .. G +
 // stats[SS_EXTRA]) (the G group leaders first, at position = group, then the other kept rows and the
 // audited rows in group order), vpos[q] = list position or −1 (then std_[q] = the estimate), keep [G]
-// masks (low byte kept, high byte audited).  The audit draw is a hash of the rows' query points.
+// masks (low byte kept, high byte audited), zkey [M] the discarded rows' z (float bits; Z_NONE
+// otherwise) from which the compaction picks the audited rows.
 // after_screen(ctx), when given, runs on the host between the screen kernel's launch and the
 // selection's (the closure forks its side stream there); its nonzero return is returned.
 int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, void* ws, double* sv2, double* std_,
-                         int* vpos, int* rows, unsigned short* keep, int* stats, hipStream_t s,
+                         int* vpos, int* rows, unsigned short* keep, unsigned* zkey, int* stats, hipStream_t s,
                          int (*after_screen)(void*) = nullptr, void* ctx = nullptr);
 // After the refine pass (gpis_refine_launch): exact std/var of the kept and audited rows, then per
 // group the ∇std row (sel = query, Xg = point, vrow = V row, always a row the exact pass ran) and the
@@ -101,5 +130,10 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
 int refine_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, const double* rpartial, int64_t M_pad,
                          const double* sv2, const int* vpos, const unsigned short* keep, double* std_, double* var,
                          int64_t* sel, double* Xg, int64_t* vrow, int* stats, hipStream_t s);
+// The repair (only when screen_failed(stats)): after a refine pass over EVERY all-tip row (identity list,
+// gated on the same stats), exact std/var of all rows and each group's first maximum of log(100·std) as
+// the ∇std row — the unscreened closure's selection; sets SS_REPAIR and counts it.  A no-op otherwise.
+int repair_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, const double* rpartial, int64_t M_pad,
+                         double* std_, double* var, int64_t* sel, double* Xg, int64_t* vrow, int* stats, hipStream_t s);
 
 }  // namespace cdx

@@ -523,25 +523,17 @@ constexpr int SEL_BLOCK = 64;
 
 using cdx::screen_margin;
 
-__device__ __forceinline__ uint64_t audit_mix(uint64_t x) {  // splitmix64 finaliser
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
-// Per group: estimates, leader, kept rows, and the audit draw — a discarded row q joins the exact
-// pass as an audited row when the high word of a hash of (q, its query point's bits) is below
-// audit_thresh (expected count CDX_SCREEN_AUDIT per closure).  Keyed by the inputs, not by a
-// counter: the same inputs give the same exact-pass list, hence bit-identical results (the refine
-// pass's K-split depends on the list length), and every optimiser step draws a new sample.
+// Per group: estimates, leader, kept rows, and each discarded row's normalised gap z (cdx_screen.h) for
+// the audit, which the compaction kernel picks: the discarded rows nearest the keep threshold.  A
+// function of the inputs only: the same inputs give the same exact-pass list, hence bit-identical results
+// (the refine pass's K-split depends on the list length).
 template <int KT>
 __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const double* __restrict__ partial,
                                                             int64_t M_pad, int Nt, int64_t G, int T,
                                                             double* __restrict__ sv2, double* __restrict__ std_,
                                                             int* __restrict__ vpos, int* __restrict__ rows,
                                                             unsigned short* __restrict__ keep,
-                                                            const double* __restrict__ X, unsigned audit_thresh) {
+                                                            unsigned* __restrict__ zkey, const double* __restrict__ X) {
   const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= G) return;
   const double k0 = cdx::gpis_k0<KT>(g.R), delta = g.screen_delta;
@@ -565,39 +557,87 @@ __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const do
   unsigned mask = 0;
   for (int f = 0; f < T; ++f) {
     const int64_t q = gi * T + f;
+    unsigned z = cdx::Z_NONE;
     if (f == lead) {
       vpos[q] = (int)gi;
       rows[gi] = (int)q;
     } else if (!finite || a[f] + d[f] >= lo) {
       mask |= 1u << f;  // kept: position assigned by screen_compact_kernel
-    } else if (audit_thresh &&
-               (unsigned)(audit_mix(audit_mix((uint64_t)q) ^ audit_mix(__double_as_longlong(X[3 * q])) ^
-                                    audit_mix(__double_as_longlong(X[3 * q + 1]) + 1) ^
-                                    audit_mix(__double_as_longlong(X[3 * q + 2]) + 2)) >> 32) < audit_thresh) {
-      mask |= 0x100u << f;  // discarded by the screen, audited by the exact pass
     } else {
-      vpos[q] = -1;
+      vpos[q] = -1;  // discarded (the compaction may still list it as audited)
       std_[q] = sqrt(a[f]);
+      z = __float_as_uint((float)((lo - a[f]) / d[f]));
     }
+    zkey[q] = z;
   }
   keep[gi] = (unsigned short)mask;
 }
 
 // Deterministic compaction of the kept non-leader fingertips and the audited rows behind the G
 // leaders (group order, fingertip order): one workgroup; thread t owns the contiguous groups [t·C,
-// t·C + C), C = ceil(G/1024); one scan of the per-thread counts (wave shuffles, then the 16 wave
-// totals through LDS: two barriers in all).  Resets the per-closure statistics and counts the closure
-// and its audited rows in the cumulative block.
-__global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, const unsigned short* __restrict__ keep,
+// t·C + C), C = ceil(G/1024).  First the audit: an LDS histogram of the discarded rows' z bins and one
+// wave's scan of it give the cut (cdx_screen.h audit_bin: the lowest bins within the row budget A, plus
+// the bin that crosses A while the total stays ≤ 4A); the discarded rows below the cut are audited, i.e.
+// listed for the exact pass like the kept ones.  Then one scan of the per-thread counts (wave shuffles,
+// then the 16 wave totals through LDS).  Resets the per-closure statistics and counts the closure and its
+// audited rows in the cumulative block; records the smallest z left unaudited.
+__global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, unsigned short* __restrict__ keep,
+                                                              const unsigned* __restrict__ zkey,
                                                               int* __restrict__ vpos, int* __restrict__ rows,
-                                                              int* __restrict__ stats) {
-  __shared__ int wsum[16], wsa[16];
+                                                              int* __restrict__ stats, int A) {
+  __shared__ int hist[cdx::AUDIT_BINS], wsum[16], wsa[16], s_cut;
+  __shared__ unsigned wmin[16];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t C = (G + 1023) / 1024;
   const int64_t g0 = (int64_t)t * C, g1 = g0 + C < G ? g0 + C : G;
+  if (t < cdx::AUDIT_BINS) hist[t] = 0;
+  if (t == 0) s_cut = A > 0 ? cdx::AUDIT_BINS : 0;
+  __syncthreads();
+  int nd = 0;  // discarded rows of this thread
+  if (A > 0) {
+    for (int64_t gi = g0; gi < g1; ++gi)
+      for (int f = 0; f < T; ++f) {
+        const unsigned z = zkey[gi * T + f];
+        if (z != cdx::Z_NONE) {
+          atomicAdd(&hist[cdx::audit_bin(z)], 1);
+          ++nd;
+        }
+      }
+  } else {
+    for (int64_t gi = g0; gi < g1; ++gi)
+      for (int f = 0; f < T; ++f) nd += zkey[gi * T + f] != cdx::Z_NONE;
+  }
+  __syncthreads();
+  if (A > 0 && wave == 0) {  // the cut: lane l scans bins 4l .. 4l + 3
+    constexpr int PB = cdx::AUDIT_BINS / 64;
+    int h[PB], s = 0;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) s += (h[i] = hist[PB * lane + i]);
+    int inc = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(inc, d);
+      if (lane >= d) inc += v;
+    }
+    int c = inc - s;  // rows in the bins below this lane's
+    if (c < A && inc >= A) {  // the lane holding the first bin whose cumulative count reaches A
+      int b = 0;
+      while (c + h[b] < A) c += h[b++];
+      s_cut = PB * lane + b + (c + h[b] <= 4 * A ? 1 : 0);
+    }
+  }
+  __syncthreads();
+  const int cut = s_cut;
   int n = 0, na = 0;
+  unsigned zmin = 0x7F800000u;  // +inf
   for (int64_t gi = g0; gi < g1; ++gi) {
-    const unsigned m = keep[gi];
+    unsigned m = keep[gi];
+    for (int f = 0; f < T; ++f) {
+      const unsigned z = zkey[gi * T + f];
+      if (z == cdx::Z_NONE) continue;
+      if (cdx::audit_bin(z) < cut) m |= 0x100u << f;
+      else zmin = min(zmin, z);
+    }
     n += __popc(m);
     na += __popc(m >> 8);
   }
@@ -607,23 +647,40 @@ __global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, 
     const int v = __shfl_up(inc, d);
     if (lane >= d) inc += v;
   }
-  int wa = na;
+  int wa = na, wd = nd;
+  unsigned wz = zmin;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) wa += __shfl_xor(wa, d);
+  for (int d = 1; d < 64; d <<= 1) {
+    wa += __shfl_xor(wa, d);
+    wd += __shfl_xor(wd, d);
+    wz = min(wz, (unsigned)__shfl_xor((int)wz, d));
+  }
   if (lane == 63) wsum[wave] = inc;
-  if (lane == 0) wsa[wave] = wa;
+  if (lane == 0) {
+    wsa[wave] = wa;
+    wmin[wave] = wz;
+    hist[wave] = wd;  // (the histogram is no longer read)
+  }
   __syncthreads();
-  int before = 0, total = 0, total_a = 0;
+  int before = 0, total = 0, total_a = 0, total_d = 0;
+  unsigned zm = 0x7F800000u;
 #pragma unroll
   for (int w = 0; w < 16; ++w) {
     const int s = wsum[w];
     before += w < wave ? s : 0;
     total += s;
     total_a += wsa[w];
+    total_d += hist[w];
+    zm = min(zm, wmin[w]);
   }
   int pos = (int)G + before + inc - n;
   for (int64_t gi = g0; gi < g1; ++gi) {
-    const unsigned m = keep[gi];
+    unsigned m = keep[gi];
+    for (int f = 0; f < T; ++f) {
+      const unsigned z = zkey[gi * T + f];
+      if (z != cdx::Z_NONE && cdx::audit_bin(z) < cut) m |= 0x100u << f;
+    }
+    keep[gi] = (unsigned short)m;
     for (int f = 0; f < T; ++f)
       if (((m >> f) | (m >> (8 + f))) & 1u) {
         const int64_t q = gi * T + f;
@@ -635,10 +692,17 @@ __global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, 
   if (t == 0) {
     stats[cdx::SS_EXTRA] = total;
     stats[cdx::SS_AUDIT] = total_a;
-    for (int k = cdx::SS_MISS; k < cdx::SS_CUM; ++k)
-      if (k != cdx::SS_AUDIT) stats[k] = 0;
+    stats[cdx::SS_GAP] = (int)zm;
+    stats[cdx::SS_AUDIT_CUT] = (int)cdx::audit_bin_floor(cut);
+    stats[cdx::SS_DISCARD] = total_d;
+    for (int k : {cdx::SS_MISS, cdx::SS_AUDIT_MISS, cdx::SS_AUDIT_FLIP, cdx::SS_FAULT, cdx::SS_RATIO,
+                  cdx::SS_RATIO_AUDIT, cdx::SS_REPAIR})
+      stats[k] = 0;
     stats[cdx::SS_CUM] += 1;
     stats[cdx::SS_CUM + cdx::SS_AUDIT] += total_a;
+    stats[cdx::SS_CUM + cdx::SS_DISCARD] += total_d;
+    unsigned* cz = reinterpret_cast<unsigned*>(stats + cdx::SS_CUM + cdx::SS_GAP);
+    *cz = max(*cz, 0xFFFFFFFFu - zm);
   }
 }
 
@@ -740,6 +804,43 @@ __global__ __launch_bounds__(256) void refine_select_kernel(cdx_gpis g, const do
       atomicMax(&us[cdx::SS_CUM + cdx::SS_RATIO_AUDIT], __float_as_uint(ra));
     }
   }
+}
+
+// The repair's selection (gated: a no-op unless a check of this closure failed, cdx::screen_failed).  The
+// refine pass has just run every all-tip row at list position = row (identity list): exact std / var of
+// every row, the group's first maximum of log(100·std) — as gpis_var_finalize_select and level_fwd_bwd
+// take it — its query, point and V row.
+template <int KT>
+__global__ __launch_bounds__(256) void repair_select_kernel(cdx_gpis g, const double* __restrict__ rpartial,
+                                                            int64_t M_pad, int Nt, int64_t G, int T,
+                                                            const double* __restrict__ X, double* __restrict__ std_,
+                                                            double* __restrict__ var, int64_t* __restrict__ sel,
+                                                            double* __restrict__ Xg, int64_t* __restrict__ vrow,
+                                                            int* __restrict__ stats) {
+  if (!cdx::screen_failed(stats)) return;
+  const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi == 0) {  // (SS_REPAIR is not among the words screen_failed reads)
+    stats[cdx::SS_REPAIR] = 1;
+    stats[cdx::SS_CUM + cdx::SS_REPAIR] += 1;
+  }
+  if (gi >= G) return;
+  const double k0 = cdx::gpis_k0<KT>(g.R);
+  int fmax = 0;
+  double lmax = 0;
+  for (int f = 0; f < T; ++f) {
+    const int64_t q = gi * T + f;
+    double acc = 0;
+    for (int t = 0; t < Nt; ++t) acc += rpartial[(int64_t)t * M_pad + q];
+    const double v = k0 - acc, sd = sqrt(fabs(v));
+    std_[q] = sd;
+    var[q] = v;
+    const double lv = log(100 * sd);
+    if (f == 0 || lv > lmax) { lmax = lv; fmax = f; }
+  }
+  const int64_t qi = gi * T + fmax;
+  sel[gi] = qi;
+  vrow[gi] = qi;
+  for (int i = 0; i < 3; ++i) Xg[3 * gi + i] = X[3 * qi + i];
 }
 
 // ------------------------------------------------------------------ preparation (once per state)
@@ -892,7 +993,7 @@ int screen_audit_rows() {
 }
 
 int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, void* ws, double* sv2, double* std_,
-                         int* vpos, int* rows, unsigned short* keep, int* stats, hipStream_t s,
+                         int* vpos, int* rows, unsigned short* keep, unsigned* zkey, int* stats, hipStream_t s,
                          int (*after_screen)(void*), void* ctx) {
   const int64_t Ms = G * T;
   if (G <= 0 || T <= 0 || T > CDX_MAX_TIPS) return CDX_EINVAL;
@@ -902,11 +1003,6 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
   const int Mt = (int)(M_pad / SC_BM);
   double* partial = static_cast<double*>(ws);
   const dim3 grid((unsigned)(Mt * Nt)), sgrid((unsigned)((G + SEL_BLOCK - 1) / SEL_BLOCK));
-  // audit draw: P(row audited) = A / ((T − 1)·G), about A of the (T − 1)·G non-leader rows
-  const int64_t cand = (int64_t)(T - 1) * G;
-  const int A = screen_audit_rows();
-  const unsigned thresh = (A <= 0 || cand <= 0) ? 0u
-                          : (unsigned)std::min<double>(4294967295.0, std::ceil(4294967296.0 * A / (double)cand));
   switch (g.kernel) {
     case CDX_KERNEL_TPS:
       prof_mark(PROF_SCREEN, true, s);
@@ -915,7 +1011,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, X, thresh);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, zkey, X);
       break;
     case CDX_KERNEL_RBF:
       prof_mark(PROF_SCREEN, true, s);
@@ -924,7 +1020,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, X, thresh);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, zkey, X);
       break;
     default:
       prof_mark(PROF_SCREEN, true, s);
@@ -933,10 +1029,11 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, X, thresh);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, zkey, X);
       break;
   }
-  hipLaunchKernelGGL(screen_compact_kernel, dim3(1), dim3(1024), 0, s, G, T, (const unsigned short*)keep, vpos, rows, stats);
+  hipLaunchKernelGGL(screen_compact_kernel, dim3(1), dim3(1024), 0, s, G, T, keep, (const unsigned*)zkey, vpos, rows, stats,
+                     screen_audit_rows());
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
@@ -954,6 +1051,24 @@ int refine_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, c
       break;
     default:
       hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
+      break;
+  }
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+int repair_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, const double* rpartial, int64_t M_pad,
+                         double* std_, double* var, int64_t* sel, double* Xg, int64_t* vrow, int* stats, hipStream_t s) {
+  const int Nt = g.N_pad / SC_BN;
+  const dim3 sgrid((unsigned)((G + SEL_BLOCK - 1) / SEL_BLOCK));
+  switch (g.kernel) {
+    case CDX_KERNEL_TPS:
+      hipLaunchKernelGGL(repair_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, X, std_, var, sel, Xg, vrow, stats);
+      break;
+    case CDX_KERNEL_RBF:
+      hipLaunchKernelGGL(repair_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, X, std_, var, sel, Xg, vrow, stats);
+      break;
+    default:
+      hipLaunchKernelGGL(repair_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, X, std_, var, sel, Xg, vrow, stats);
       break;
   }
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;

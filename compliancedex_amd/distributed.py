@@ -107,10 +107,27 @@ def overflow(gathered):
     return [int(g[0, 1]) - int(g[0, 0]) for g in gathered]
 
 
-def all_gather_survivors(buf, group=None, return_buffers=False):
+def check_equal_shapes(buf, group=None):
+    """Raises ValueError on EVERY rank when the ranks' buffers differ in shape (one all_reduce of
+    [rows, cols, −rows, −cols] with MAX): an all_gather of unequal buffers would hang or corrupt
+    RCCL's receive buffers instead of failing."""
+    dev = buf.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    r, c = int(buf.shape[0]), int(buf.shape[1])
+    t = torch.tensor([r, c, -r, -c], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    hi_r, hi_c, lo_r, lo_c = t.tolist()
+    if (hi_r, hi_c, -lo_r, -lo_c) != (r, c, r, c):
+        raise ValueError(f"survivor buffers differ across ranks: rows {-lo_r}..{hi_r}, cols {-lo_c}..{hi_c} "
+                         f"(this rank {r}x{c}); pass one capacity on every rank (default_capacity / agreed_capacity)")
+
+
+def all_gather_survivors(buf, group=None, return_buffers=False, check_shape=True):
     """One collective: every rank receives every rank's fixed-capacity buffer (all ranks must
-    pass the same shape — see ``default_capacity``)."""
+    pass the same shape — see ``default_capacity``).  ``check_shape`` (default) verifies that first
+    with one all_reduce (check_equal_shapes); a caller that already checked this shape may skip it."""
     world = dist.get_world_size(group)
+    if check_shape and world > 1:
+        check_equal_shapes(buf, group)
     out = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(out, buf.contiguous(), group=group)
     return (unpack_records(out), out) if return_buffers else unpack_records(out)

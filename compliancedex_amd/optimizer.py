@@ -108,7 +108,8 @@ class ProbabilisticGraspOptimizer:
         self._ws = None
         self._last_ws = None  # workspace of the most recent closure (the optimiser's or a graph's own)
         self._seed = int(seed)
-        self.screen_fallbacks = 0  # optimise loops re-run unscreened after a failed screen check
+        self.screen_repairs = 0  # screened closures of optimise loops that repaired themselves (failed a check)
+        self.last_screen_report = None
         self._graphs = {}
         self.optim = None
 
@@ -158,8 +159,9 @@ class ProbabilisticGraspOptimizer:
     def screen_report(self, gpis, E, friction_mu=1):
         """Verification record of the last closure over E candidates (cdx_closure_screen_report, one
         stream-ordered device→host copy): exact / audited rows, margin misses, audit flips, faults,
-        the largest estimate error in units of its margin, and the same summed since the workspace's
-        last reset — or None when the closure ran the full fp64 pass."""
+        whether the closure repaired itself, the largest estimate error in units of its margin, the
+        smallest normalised gap left unaudited, and the same summed since the workspace's last reset —
+        or None when the closure ran the full fp64 pass."""
         if self._last_ws is None:
             return None
         rep = N.CdxScreenReport()
@@ -173,7 +175,7 @@ class ProbabilisticGraspOptimizer:
         if r is None:
             return None
         return {k: r[k] for k in ("exact_rows", "bound_misses", "screened_rows", "audited_rows", "audit_misses",
-                                  "audit_flips", "faults", "max_ratio", "max_ratio_audit")}
+                                  "audit_flips", "faults", "max_ratio", "max_ratio_audit", "repaired", "min_gap")}
 
     def _reset_screen(self, p, E, ws):
         N.check(N.load().cdx_closure_screen_reset(p, E, N.ptr(ws), N.stream_ptr(ws.device)), "cdx_closure_screen_reset")
@@ -295,6 +297,9 @@ class ProbabilisticGraspOptimizer:
         opt_value = torch.inf * torch.ones(num_envs, dtype=torch.float64, device=joint_angles.device)
         opt_margin = torch.zeros(num_envs, 4, dtype=torch.float64, device=joint_angles.device)
         opt_palm_poses = self.palm_offset.clone()
+        p = self.problem(gpis, friction_mu)  # the loop's cumulative screen record starts at zero
+        self._ensure_ws(p, num_envs, joint_angles.device)
+        self._reset_screen(p, num_envs, self._ws)
         for s in range(self.num_iters):
             noise = noise_tape[s] if noise_tape is not None else None
             self.closure(joint_angles, compliance, target_pose, palm_poses, palm_oris, friction_mu, gpis, num_envs,
@@ -316,6 +321,7 @@ class ProbabilisticGraspOptimizer:
         self.best_loss = opt_value
         if verbose:
             print("Margin:", opt_margin)
+        self.last_screen_report = self.screen_report(gpis, num_envs, friction_mu) if self.num_iters else None
         return opt_joint_angle, opt_compliance, opt_target_pose, opt_palm_poses, opt_margin
 
     def adam_config(self):
@@ -342,30 +348,18 @@ class ProbabilisticGraspOptimizer:
         the same whether launched eagerly or replayed from a captured hipGraph (``graph=True``;
         captured once per (E, problem), replayed on later calls).
 
-        Screened closures verify themselves (cdx_screen_report): the loop's cumulative record is
-        read once at the end (one host sync), and if any closure missed a margin or took the fault
-        fallback, the whole loop is run again without the screen (``screen_fallbacks`` counts it), so
-        the returned results are those of the full fp64 path either way."""
-        seed0 = self._seed
+        Screened closures verify and, when a check fails, repair themselves on the device (cdx_closure:
+        every all-tip row through the exact pass, the unscreened selection), so every step is the full
+        fp64 path's; the loop's cumulative record is read once at the end (one host sync) into
+        ``last_screen_report``, and ``screen_repairs`` counts the repaired closures."""
         res = self._optimize_fused_once(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
                                         noise_tape, graph, step_hook)
         rep = self.screen_report(gpis, init_joint_angles.shape[0], friction_mu)
         self.last_screen_report = rep
-        if rep is not None and (rep["cum_bound_misses"] or rep["cum_audit_misses"] or rep["cum_faults"]
-                                or rep["cum_audit_flips"]):
-            warnings.warn(f"screened optimise loop failed its checks ({rep}); re-running it unscreened")
-            self.screen_fallbacks += 1
-            p = self.problem(gpis, friction_mu)
-            delta = p.gpis.screen_delta
-            p.gpis.screen_delta = 0.0
-            seed_after = self._seed
-            self._seed = seed0  # the same noise keys: the re-run is the screened loop's exact counterpart
-            try:
-                res = self._optimize_fused_once(init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,
-                                                noise_tape, False, step_hook)
-            finally:
-                p.gpis.screen_delta = delta
-                self._seed = seed_after
+        if rep is not None and rep["cum_repairs"]:
+            self.screen_repairs += rep["cum_repairs"]
+            warnings.warn(f"{rep['cum_repairs']} of {rep['cum_closures']} screened closures failed a check and "
+                          f"repaired themselves (exact pass over every row)")
         return res
 
     def _optimize_fused_once(self, init_joint_angles, target_pose, compliance, friction_mu, gpis, verbose,

@@ -235,14 +235,18 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
 int cdx_closure_screen_stats(const cdx_problem* p, int64_t E, const void* workspace, int32_t* out3);
 
 /* The screened closure's verification record.  Every screened closure runs the exact fp64 pass for
- * each group's leader, every fingertip the selection keeps, and an AUDIT sample of the fingertips it
- * discards (a hash of the rows' query points — the same inputs draw the same sample, each optimiser
- * step a new one; CDX_SCREEN_AUDIT rows expected, default 64), and checks each of those estimates
- * against its margin Δ_f.  The maximum of each group is taken over
- * exact values; an audited row that turns out to be its group's maximum is used (audit_flips), and a
- * maximum on a row the exact pass did not run (possible only after a margin failure) takes the best
- * exact row instead and is counted as a fault.  Fields cum_* accumulate over closures since the last
- * cdx_closure_screen_reset (call it once after allocating the workspace). */
+ * each group's leader, every fingertip the selection keeps, and an AUDIT of the fingertips it discards
+ * nearest the keep threshold — smallest normalised gap z = (lo − a_f)/Δ_f, lo = max_g (a_g − Δ_g), the
+ * margins by which the row's estimate sits below its group's keep floor (CDX_SCREEN_AUDIT rows, default
+ * 64: the lowest 1/8-octave z bins within that budget) — and checks each of those estimates against its
+ * margin Δ_f.  The maximum of each group is taken over exact values.  If any check fails (a kept or
+ * audited estimate off by more than Δ_f, an audited row that is its group's exact maximum, a maximum on
+ * a row the exact pass did not run) the same closure REPAIRS itself: every all-tip row runs the exact
+ * pass and the groups select as the unscreened closure does (repaired = 1), so no entry point returns a
+ * screened result that failed a check.  A discarded row left unaudited (z ≥ min_gap) can hold its
+ * group's true maximum only if its estimate is off by more than z·Δ_f; the checked rows' largest error
+ * is max_ratio·Δ_f.  Fields cum_* accumulate over closures since the last cdx_closure_screen_reset (call
+ * it once after allocating the workspace). */
 typedef struct {
   int32_t screened;        /* 1 if the last closure on this workspace screened (else all fields 0) */
   int32_t screened_rows;   /* all-tip rows estimated by the screen */
@@ -262,6 +266,13 @@ typedef struct {
   int64_t cum_faults;
   double cum_max_ratio;
   double cum_max_ratio_audit;
+  int32_t repaired;        /* 1 if a check failed and the closure re-ran every row exactly */
+  int32_t discarded_rows;  /* rows the screen discarded (audited or not) */
+  double min_gap;          /* smallest z among discarded rows left unaudited (+inf: none) */
+  double audit_cut;        /* every discarded row with z below this was audited */
+  int64_t cum_repairs;
+  int64_t cum_discarded_rows;
+  double cum_min_gap;      /* smallest min_gap over the closures (+inf: none) */
 } cdx_screen_report;
 
 /* Reads the record (an async copy on `stream`, then a wait on that stream). */

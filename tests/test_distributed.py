@@ -87,6 +87,36 @@ def test_all_gather_survivors_gloo_world2():
     assert set(full[:, 1]) <= {0.0, 1.0}
 
 
+def _unequal_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    d = _local(rank)
+    buf = pack_survivors(16 + 4 * rank, 7, rank, 0, **d)  # rank 1's capacity differs: a config-3 run gone wrong
+    try:
+        all_gather_survivors(buf)
+        q.put((rank, "gathered"))
+    except ValueError as e:
+        q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+def test_all_gather_unequal_capacity_fails_on_every_rank():
+    """Buffers of different shape must fail loudly on every rank (one all_reduce before the all_gather),
+    not hang or scramble the collective."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_unequal_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        assert "differ across ranks" in res[r] and "rows 17..21" in res[r], res
+
+
 def test_pack_header_counts_overflow():
     d = _local(0, E=40)
     n_surv = int((d["margin"] > 0).all(1).sum())

@@ -43,12 +43,14 @@ def _opt(hand="allegro"):
                                             optimize_target=True, optimize_palm=True, device=DEV)
 
 
-def _closure(opt, gpis, inputs, screen=True):
+def _closure(opt, gpis, inputs, screen=True, delta_scale=1.0):
     q, comp, target, palm = inputs
     p = opt.problem(gpis, 1)
     delta = p.gpis.screen_delta
     if not screen:
         p.gpis.screen_delta = 0.0
+    elif delta_scale != 1.0:  # debug margins (the closure's own descriptor copy): forces failed checks
+        p.gpis.screen_delta = delta * delta_scale
     try:
         t = [torch.from_numpy(np.ascontiguousarray(a)).to(DEV).requires_grad_(True)
              for a in (q, comp, target, palm[:, :3], palm[:, 3:])]
@@ -210,21 +212,24 @@ def _report(opt, gpis, E):
 
 
 def test_screen_report_audits_discarded_rows(banana2000):
-    """Every screened closure verifies itself (cdx_closure_screen_report): the exact pass also runs an
-    audit sample of the rows the screen discards (≈ CDX_SCREEN_AUDIT = 64 expected), and every kept and
-    audited estimate is checked against its margin Δ_f.  On the bench workload: no miss, no audited
-    row that turned out to be its group's maximum, no fault, and the worst estimate error a small
-    fraction of its margin; the cumulative block counts the closures."""
+    """Every screened closure verifies itself (cdx_closure_screen_report): the exact pass also runs the
+    discarded rows nearest the keep threshold — smallest normalised gap z = (lo − a_f)/Δ_f, the lowest
+    1/8-octave z bins within CDX_SCREEN_AUDIT = 64 rows (≤ 4× that with the crossing bin) — and every
+    kept and audited estimate is checked against its margin Δ_f.  On the bench workload: no miss, no
+    audited row that turned out to be its group's maximum, no fault, no repair, the worst estimate error a
+    small fraction of its margin, and every unaudited discarded row at least min_gap ≥ audit_cut > 1
+    margins below its group's floor; the cumulative block counts the closures."""
     from compliancedex_amd.workloads import prob_inputs
     cfg, opt = _opt()
     inputs = prob_inputs(cfg["ref_q"], 4096, seed=1000, spread=True)
     _closure(opt, banana2000, inputs)
     r = _report(opt, banana2000, 4096)
     assert r["screened"] == 1 and r["screened_rows"] == 4 * 4096
-    assert 16 <= r["audited_rows"] <= 200, r
-    assert r["exact_rows"] >= 4096 + r["audited_rows"]
-    assert r["bound_misses"] == r["audit_misses"] == r["audit_flips"] == r["faults"] == 0, r
+    assert 0 < r["audited_rows"] <= 4 * 64 and r["audited_rows"] <= r["discarded_rows"], r
+    assert r["exact_rows"] == 4 * 4096 - r["discarded_rows"] + r["audited_rows"], r
+    assert r["bound_misses"] == r["audit_misses"] == r["audit_flips"] == r["faults"] == r["repaired"] == 0, r
     assert 0 < r["max_ratio"] < 0.5 and 0 < r["max_ratio_audit"] < 0.5, r
+    assert r["min_gap"] >= r["audit_cut"] > 1.0, r  # the audit took the nearest rows
     n0 = r["cum_closures"]
     _closure(opt, banana2000, inputs)
     r2 = _report(opt, banana2000, 4096)
@@ -270,7 +275,7 @@ def test_optimize_trajectory_screened_equals_unscreened_every_step(banana2000):
     step the closure's loss, margins and five gradients equal the unscreened fp64 closure's on the
     same parameters and Kabsch noise to TOL_TRAJ (NaN candidates identical), and the loop's
     cumulative screen record shows no
-    miss, fault or audit flip (so no fallback re-run).
+    miss, fault or audit flip (so no closure repaired itself).
     (Two separately run trajectories are not compared: the screened and unscreened exact passes sum
     V in different K-splits — 1e-16 relative — and 200 Adam steps amplify that to 1e-9 by step 26.)"""
     from compliancedex_amd import ProbabilisticGraspOptimizer
@@ -311,8 +316,8 @@ def test_optimize_trajectory_screened_equals_unscreened_every_step(banana2000):
 
     opt.optimize(*args, 1, banana2000, verbose=False, noise_tape=Tape(), step_hook=hook)
     rep = opt.last_screen_report
-    assert steps == list(range(200)) and opt.screen_fallbacks == 0
-    assert rep["cum_closures"] == 200 and rep["cum_bound_misses"] == rep["cum_faults"] == 0, rep
+    assert steps == list(range(200)) and opt.screen_repairs == 0
+    assert rep["cum_closures"] == 200 and rep["cum_bound_misses"] == rep["cum_faults"] == rep["cum_repairs"] == 0, rep
     assert rep["cum_audit_misses"] == rep["cum_audit_flips"] == 0 and rep["cum_audited_rows"] > 200 * 16, rep
     w = worst.cpu().numpy()
     assert (w <= TOL_TRAJ).all(), dict(zip(keys, w))
@@ -541,3 +546,89 @@ def test_injected_error_joins_side_stream(banana2000):
             assert np.array_equal(a, b, equal_nan=True), stage
     N.check(lib.cdx_debug_fail_next_closure(0), "cdx_debug_fail_next_closure")
 
+
+
+@pytest.mark.parametrize("scale", [1e-3, 1e-9])
+def test_failed_checks_repair_the_closure(scale, banana2000):
+    """Injected screen misses: the closure's margins shrunk to scale × Δ (1e-3: kept and audited rows
+    miss it; 1e-9: groups keep only their leader and the true maximum is often discarded).  Every check
+    that fails makes the same closure repair itself — every all-tip row through the exact pass, the
+    unscreened selection — so the reference-API closure() returns the unscreened fp64 closure's loss,
+    margins, Kabsch masks and five gradients (TOL_EQ), and the report says it repaired."""
+    from compliancedex_amd.workloads import prob_inputs
+    cfg, opt = _opt()
+    E = 4096
+    inputs = prob_inputs(cfg["ref_q"], E, seed=1000, spread=True)
+    a, _ = _closure(opt, banana2000, inputs, screen=True, delta_scale=scale)
+    r = _report(opt, banana2000, E)
+    b, _ = _closure(opt, banana2000, inputs, screen=False)
+    assert r["repaired"] == 1 and r["cum_repairs"] >= 1, r
+    assert r["bound_misses"] + r["audit_misses"] + r["audit_flips"] + r["faults"] > 0, r
+    assert np.array_equal(a["flip"], b["flip"])
+    for k in OUTS:
+        assert rel_err(a[k], b[k]) <= TOL_EQ, (k, rel_err(a[k], b[k]))
+    c, _ = _closure(opt, banana2000, inputs, screen=True)  # the calibrated margins again: no repair
+    r2 = _report(opt, banana2000, E)
+    assert r2["repaired"] == 0, r2
+    for k in OUTS:
+        assert rel_err(c[k], b[k]) <= TOL_EQ, (k, rel_err(c[k], b[k]))
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_optimize_with_failed_checks_equals_unscreened(fused, banana2000):
+    """A 30-iteration optimise loop with injected misses (margins 1e-3 × Δ), through the fused loop and
+    the reference loop (fused=False, torch.optim.Adam): every closure repairs itself on the device (no
+    host sync per step), cum_repairs = 30, and at every step (fused) / at the end (both) the results
+    equal the unscreened loop's on the same noise to the K-split rounding (per step TOL_EQ; the final
+    best iterate 1e-8 after 30 Adam steps)."""
+    from compliancedex_amd import ProbabilisticGraspOptimizer
+    from compliancedex_amd.workloads import prob_inputs
+    cfg, opt = _opt()
+    opt.num_iters = 30
+    E = 4096
+    q, comp, target, palm = prob_inputs(cfg["ref_q"], E, seed=78, spread=True)
+    args = [torch.from_numpy(np.ascontiguousarray(x)).to(DEV) for x in (q, target, comp)]
+
+    def run(o, delta_scale, hook=None):
+        o.palm_offset = torch.from_numpy(palm).to(DEV)
+        p = o.problem(banana2000, 1)
+        d0 = p.gpis.screen_delta
+        p.gpis.screen_delta = d0 * delta_scale
+        g = torch.Generator(device=DEV).manual_seed(99)
+        tape = [torch.rand(3 * E, 3, 3, generator=g, device=DEV, dtype=torch.float64) for _ in range(30)]
+        try:
+            res = o.optimize(*[x.clone() for x in args], 1, banana2000, verbose=False, noise_tape=tape, fused=fused,
+                             step_hook=hook)
+        finally:
+            p.gpis.screen_delta = d0
+        return [x.detach().cpu().numpy() for x in res]
+
+    ref = ProbabilisticGraspOptimizer("allegro", cfg["ee_link_name"], cfg["ee_link_offset"], ref_q=cfg["ref_q"],
+                                      optimize_target=True, optimize_palm=True, device=DEV)
+    ref.num_iters = 30
+    p_ref = ref.problem(banana2000, 1)
+    keys = ("total_loss", "total_margin", "g_q", "g_comp", "g_target", "g_palm_pos", "g_palm_ori")
+    worst = [0.0]
+
+    def hook(s, out, st):
+        d0 = p_ref.gpis.screen_delta
+        p_ref.gpis.screen_delta = 0.0
+        o2 = ref._outputs(E, 4, 16, 3, torch.device(DEV))
+        ref._closure_into(p_ref, st["q"], st["comp"], st["target"], st["pp"], st["po"], st["noise"], o2, seed=0)
+        p_ref.gpis.screen_delta = d0
+        for k in keys:
+            x, y = out[k], o2[k]
+            fin = torch.isfinite(y)
+            assert torch.equal(torch.isfinite(x), fin), (s, k)
+            e = float(torch.where(fin, (x - y).abs(), 0).max() / torch.where(fin, y.abs(), 0).max().clamp(min=1e-300))
+            worst[0] = max(worst[0], e)
+
+    got = run(opt, 1e-3, hook if fused else None)
+    rep = opt.last_screen_report
+    assert rep["cum_closures"] == 30 and rep["cum_repairs"] == 30, rep
+    assert worst[0] <= TOL_EQ, worst
+    want = run(ref, 0.0)
+    for x, y in zip(got, want):
+        fin = np.isfinite(y)
+        assert np.array_equal(np.isfinite(x), fin)
+        assert np.abs(x[fin] - y[fin]).max() <= 1e-8 * max(np.abs(y[fin]).max(), 1e-300)

@@ -1,4 +1,4 @@
-"""Per-closure kernel timeline from a rocprofv3 kernel trace (tools/gpu_round.sh's prof_TAG).
+"""Per-closure kernel timeline from a rocprofv3 kernel trace (tools/gpu.sh's prof_TAG).
 
   python tools/closure_timeline.py gpurun_out/prof_TAG/run_kernel_trace.csv [n_closures]
 

@@ -1,4 +1,4 @@
-"""Summarises rocprofv3 outputs of tools/gpu_round.sh into profiles/.
+"""Summarises rocprofv3 outputs of tools/gpu.sh into profiles/.
 
   python tools/pmc_summary.py TAG [E N]
 Reads gpurun_out/prof_TAG (kernel-trace stats), gpurun_out/pmc_FETCH_SIZE_TAG and
