@@ -37,6 +37,12 @@ constexpr float PT_LIM = 1e4f;      // |p| bound of the culled path (face_may_na
 
 struct Sphere { float cx, cy, cz, r, alpha, cnorm, _p0, _p1; };
 
+// Diagnostic counters (cdx_sdf_stats): [0] (point, face) pairs the culled kernel evaluated — faces of
+// every chunk a wave evaluates × its live lanes —, [1] pairs of the brute-force scans (exact path),
+// [2] points queried.  Counted only while enabled (one atomic per wave).
+__device__ unsigned long long g_sdf_stats[3];
+bool g_sdf_count = false;
+
 __device__ inline unsigned fkey(float f) {
   const unsigned u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -211,7 +217,7 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled_kernel(
     const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
     int64_t F, const cdx::FaceRec* __restrict__ rec, const Sphere* __restrict__ sph, int C,
     const unsigned* __restrict__ ws, float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
-    float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face) {
+    float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face, int count) {
   if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
   __shared__ float s_val[4][64];
   __shared__ int s_idx[4][64];
@@ -224,6 +230,8 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled_kernel(
   const bool ok = fabsf(p.x) <= PT_LIM && fabsf(p.y) <= PT_LIM && fabsf(p.z) <= PT_LIM;
   if (!__all(ok)) {  // same points in every wave: uniform over the workgroup
     if (w == 0) exact_point(p, faces, F, pi, out_dist, out_sign, out_nrm, out_clst, out_face, live);
+    if (count && w == 0 && lane == 0)
+      atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(__ballot(live)));
     return;
   }
   const float pnorm = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
@@ -246,6 +254,7 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled_kernel(
   // pass 2: exact distances over the chunks some lane cannot rule out
   float best = INFINITY;
   int bidx = 0x7fffffff;
+  unsigned evaluated = 0;  // faces of the chunks this wave evaluated (diagnostic count)
   for (int c = w; c < C; c += 4) {
     const Sphere s = sph[c];
     const float dx = p.x - s.cx, dy = p.y - s.cy, dz = p.z - s.cz;
@@ -255,10 +264,18 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled_kernel(
     if (!__any(need)) continue;
     const int f0 = c * CHUNK;
     const int nf = (int)min((int64_t)CHUNK, F - f0);
+    evaluated += nf;
     for (int k = 0; k < nf; ++k) {
       const cdx::FaceRec& r = rec[f0 + k];
       const float d = cdx::face_dist2(p, r);
       if (d < best || (d == best && r.idx < bidx)) { best = d; bidx = r.idx; }
+    }
+  }
+  if (count) {
+    const unsigned long long nl = __popcll(__ballot(live));
+    if (lane == 0) {
+      atomicAdd(&g_sdf_stats[0], (unsigned long long)evaluated * nl);
+      if (w == 0) atomicAdd(&g_sdf_stats[2], nl);
     }
   }
   s_val[w][lane] = best;
@@ -290,11 +307,18 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_exact_kernel(const float* __res
                                                               const unsigned* __restrict__ ws,
                                                               float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
                                                               float* __restrict__ out_nrm, float* __restrict__ out_clst,
-                                                              int32_t* __restrict__ out_face) {
+                                                              int32_t* __restrict__ out_face, int count) {
   if (ws && !ws[6]) return;
   __shared__ float sf[SDF_TILE * 9];
   const int64_t pi = (int64_t)blockIdx.x * SDF_BLOCK + threadIdx.x;
   const bool live = pi < P;
+  if (count) {
+    const unsigned long long nl = __popcll(__ballot(live));
+    if ((threadIdx.x & 63) == 0 && nl) {
+      atomicAdd(&g_sdf_stats[1], (unsigned long long)F * nl);
+      atomicAdd(&g_sdf_stats[2], nl);
+    }
+  }
   cdx::F3 p = cdx::f3(0.f, 0.f, 0.f);
   if (live) p = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
   float best = 0.f;
@@ -412,7 +436,7 @@ int cdx_sdf_forward(const float* points, int64_t P, const float* faces, int64_t 
   const unsigned pblocks = (unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK);
   if (sdf_mode() == 1) {
     hipLaunchKernelGGL(sdf_exact_kernel, dim3(pblocks), dim3(SDF_BLOCK), 0, s, points, P, faces, F,
-                       (const unsigned*)nullptr, sqdist, sign, normals, clst, face_idx);
+                       (const unsigned*)nullptr, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
     return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
   }
   const int n = (int)F, m = (int)P;
@@ -457,12 +481,30 @@ int cdx_sdf_forward(const float* points, int64_t P, const float* faces, int64_t 
                      (const int*)(fv + n), rec, sph, ws);
   hipLaunchKernelGGL(sdf_culled_kernel, dim3((unsigned)((P + 63) / 64)), dim3(SDF_BLOCK), 0, s, points, P,
                      (const int*)(pv + m), faces, F, (const cdx::FaceRec*)rec, (const Sphere*)sph, C,
-                     (const unsigned*)ws, sqdist, sign, normals, clst, face_idx);
+                     (const unsigned*)ws, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
   hipLaunchKernelGGL(sdf_exact_kernel, dim3(pblocks), dim3(SDF_BLOCK), 0, s, points, P, faces, F,
-                     (const unsigned*)ws, sqdist, sign, normals, clst, face_idx);
+                     (const unsigned*)ws, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
   ok = ok && hipGetLastError() == hipSuccess;
   ok = (hipFreeAsync(base, s) == hipSuccess) && ok;
   return ok ? CDX_OK : CDX_ELAUNCH;
+}
+
+int cdx_sdf_stats(int32_t enable, uint64_t* out3, cdx_stream_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (out3) {
+    if (hipMemcpyFromSymbolAsync(out3, HIP_SYMBOL(g_sdf_stats), sizeof(g_sdf_stats), 0, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return CDX_ELAUNCH;
+  }
+  if (enable >= 0) {
+    const unsigned long long z[3] = {0, 0, 0};
+    if (enable && hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sdf_stats), z, sizeof(z), 0, hipMemcpyHostToDevice, s) != hipSuccess)
+      return CDX_ELAUNCH;
+    if (enable && hipStreamSynchronize(s) != hipSuccess) return CDX_ELAUNCH;
+    g_sdf_count = enable != 0;
+  }
+  return CDX_OK;
 }
 
 int cdx_sdf_backward(const float* grad_dist, const float* points, const float* clst, int64_t P, float* grad_points,

@@ -161,10 +161,45 @@ def case_c4(dev):
         sum(o[0].sum() for o in outs).backward()
     sdf_s = timed(sdf, 5, warm=1)
     pairs = 3 * 4 * E * faces.shape[0]
+    # forward alone (HIP events on the stream: the whole cdx_sdf_forward launch sequence) and the
+    # culled kernel's work counters (cdx_sdf_stats): pairs evaluated after culling vs brute force
+    import ctypes
+    from compliancedex_amd import _native as N
+    lib = N.load()
+    st = (ctypes.c_uint64 * 3)()
+    N.check(lib.cdx_sdf_stats(1, None, N.stream_ptr(dev)), "cdx_sdf_stats")
+    with torch.no_grad():
+        for i, f in enumerate((deflated, faces, faces)):
+            compute_sdf(pts[i].detach(), f)
+    N.check(lib.cdx_sdf_stats(0, st, N.stream_ptr(dev)), "cdx_sdf_stats")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    reps = 10
+    with torch.no_grad():
+        for i, f in enumerate((deflated, faces, faces)):
+            compute_sdf(pts[i].detach(), f)
+        ev[0].record()
+        for _ in range(reps):
+            for i, f in enumerate((deflated, faces, faces)):
+                compute_sdf(pts[i].detach(), f)
+        ev[1].record()
+    torch.cuda.synchronize()
+    fwd_ms = ev[0].elapsed_time(ev[1]) / reps
+    evaluated, brute_exact, n_pts = int(st[0]), int(st[1]), int(st[2])
+    flops_pair = 46  # f32 flops of face_dist2 on its usual branch (cdx_sdf.h; 3 IEEE divisions counted as 1 each)
+    achieved = (evaluated + brute_exact) * flops_pair / (fwd_ms * 1e-3) / 1e12
     print(json.dumps({"case": "config4_primitives", "E": E, "fk_fwd_bwd_ms": fk_s * 1e3,
                       "fk_evals_per_s": E / fk_s, "sdf_3calls_fwd_bwd_ms": sdf_s * 1e3,
                       "sdf_point_face_pairs_per_s": pairs / sdf_s, "faces": int(faces.shape[0]),
-                      "sdf_evals_per_s": E / sdf_s}), flush=True)
+                      "sdf_evals_per_s": E / sdf_s,
+                      "roofline_sdf": {"bound": "valu", "kernel": "sdf_culled_kernel (+ Morton sorts, chunk build)",
+                                       "fwd_3calls_ms": fwd_ms, "points": n_pts, "brute_force_pairs": pairs,
+                                       "pairs_evaluated": evaluated, "pairs_exact_path": brute_exact,
+                                       "evaluated_over_brute_force": (evaluated + brute_exact) / pairs,
+                                       "flops_per_pair": flops_pair, "achieved": achieved, "peak": 157.3,
+                                       "unit": "TFLOP/s (f32 vector)", "frac": achieved / 157.3,
+                                       "note": "achieved counts only the evaluated pairs' face_dist2 flops over the "
+                                               "whole forward (sorts, culling tests, winner recompute included)"}}),
+          flush=True)
 
 
 def case_c4loop(dev):
@@ -204,6 +239,29 @@ def case_c4loop(dev):
     iters = 20  # amortises the per-call setup (mesh upload, face-chunk culling structure)
     kin = KinGraspOptimizer("iiwa7_allegro", links, offs, palm_offset=[0.0, 0.0, 0.0], num_iters=iters,
                             optimize_target=True, ref_q=ref_q)
+    qf = (0.3 * torch.randn(E, D, device=dev)).float()
+    tg = torch.from_numpy(target).to(dev).float()
+    cp = torch.from_numpy(comp).to(dev).float()
+
+    def loop():
+        kin.optimize(qf, tg, cp, 1, TriangleMesh(mesh.vertices, mesh.triangles), verbose=False)
+    sec = timed(loop, 3, warm=1)
+    print(json.dumps({"case": "config4_kin_sdf_loop", "E": E, "iterations": iters, "faces": int(len(mesh.triangles)),
+                      "ms_per_iteration": sec / iters * 1e3, "evals_per_s": E * iters / sec}), flush=True)
+
+
+def case_c4kin(dev):
+    """The SDF/Kin-mode loop alone (for a per-kernel rocprof split of one iteration)."""
+    from compliancedex_amd import KinGraspOptimizer, TriangleMesh
+    from compliancedex_amd.urdf import load_robot
+    from compliancedex_amd.workloads import prob_inputs
+    E, D, iters = 16384, 23, int(os.environ.get("CDX_C4KIN_ITERS", "20"))
+    links = load_robot("iiwa7_allegro")["config"]["ee_link_name"]
+    offs = [[0.0, -0.04, 0.015]] * 3 + [[0.0, -0.05, -0.015]]
+    _, comp, target, _ = prob_inputs([0.0] * D, E, seed=8, spread=True)
+    mesh = TriangleMesh.from_npz(os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_mesh.npz"))
+    kin = KinGraspOptimizer("iiwa7_allegro", links, offs, palm_offset=[0.0, 0.0, 0.0], num_iters=iters,
+                            optimize_target=True, ref_q=[0.0] * D)
     qf = (0.3 * torch.randn(E, D, device=dev)).float()
     tg = torch.from_numpy(target).to(dev).float()
     cp = torch.from_numpy(comp).to(dev).float()
