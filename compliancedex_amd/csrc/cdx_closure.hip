@@ -618,7 +618,31 @@ struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;  // main → side before mean A, side → main after it
   hipEvent_t gate = nullptr, joinB = nullptr; // main → side after the ∇std pass, side → main after mean B
+  // the split mean schedule (mean_sched() 2): a second side stream for the mean chunks
+  hipStream_t s2 = nullptr;
+  hipEvent_t g1 = nullptr, g2 = nullptr, e2a = nullptr, jb = nullptr;
 };
+
+// Mean schedule of the screened closure (CDX_MEAN_SCHED): 1 (default) the whole mean on the side stream
+// after the Kabsch records; 2 the mean in two chunks on a second side stream, each in a window where the
+// main stream runs latency- or bandwidth-bound kernels: rows [0, M1) (CDX_MEAN_CHUNK1 of them, default 0.3)
+// beside the selection / compaction — the refine pass waits for them —, the rest beside the merge and the
+// exact selection after the refine pass; the level kernel follows the all-tip and target rows.
+int mean_sched() {
+  static const int m = [] {
+    const char* e = getenv("CDX_MEAN_SCHED");
+    return e ? atoi(e) : 1;
+  }();
+  return m;
+}
+double mean_chunk1() {
+  static const double f = [] {
+    const char* e = getenv("CDX_MEAN_CHUNK1");
+    const double v = e ? atof(e) : 0.3;
+    return v < 0 ? 0.0 : (v > 1 ? 1.0 : v);
+  }();
+  return f;
+}
 
 // CDX_MEAN_SPLIT=1 splits the forked mean: part A — the all-tip and target rows, which the level
 // kernel reads — at the fork point; part B — the pregrasp and palm rows, read only by the combine
@@ -704,6 +728,35 @@ bool side_stream(SideStream& out) {
     ss.join = ev[1];
     ss.gate = ev[2];
     ss.joinB = ev[3];
+  }
+  if (mean_sched() == 2 && !ss.s2) {
+    // CDX_SIDEB_PRIO: the mean chunks' stream priority (0 normal, default: the merge's workgroups are
+    // dispatched first and the mean fills the CUs around them; > 0 highest, < 0 lowest)
+    const char* pe = getenv("CDX_SIDEB_PRIO");
+    const int want = pe ? atoi(pe) : 0;
+    int least = 0, greatest = 0;
+    hipStream_t st;
+    hipError_t ce;
+    if (want != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      ce = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, want < 0 ? least : greatest);
+    else
+      ce = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    hipEvent_t ev[4];
+    int made = 0;
+    if (ce == hipSuccess)
+      for (; made < 4; ++made)
+        if (hipEventCreateWithFlags(&ev[made], side_event_flags()) != hipSuccess) break;
+    if (ce != hipSuccess || made < 4) {
+      for (int j = 0; j < made; ++j) (void)hipEventDestroy(ev[j]);
+      if (ce == hipSuccess) (void)hipStreamDestroy(st);
+      (void)hipGetLastError();
+      return false;
+    }
+    ss.s2 = st;
+    ss.g1 = ev[0];
+    ss.g2 = ev[1];
+    ss.e2a = ev[2];
+    ss.jb = ev[3];
   }
   out = ss;
   return true;
@@ -986,7 +1039,56 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
       if (r) return r;
       return hipEventRecord(ss.joinB, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
     };
+    // The split mean schedule (mean_sched 2; needs the records ahead, the variance cost in the combine and
+    // no mean A/B split): side A = ss.s runs the Kabsch records and the level kernel, side B = ss.s2 the
+    // mean chunks.  Phase 1 at the fork point: A records; B rows [0, M1), then g1 (the refine pass waits
+    // for it).  Phase 2 right after the refine kernel (g2 recorded between it and the merge): B the
+    // remaining all-tip / target rows, e2a, the pregrasp / palm rows; A waits e2a, runs the level kernel and
+    // records join; B waits join and records jb, which the main stream waits for before the combine.
+    const bool sched2 = fork && kabsch_mode() == 1 && vlate && !mean_split() && mean_sched() == 2 && ss.s2;
+    const int64_t M01 = (int64_t)(p->n_query_levels + 1) * E * T;  // all-tip + target rows (the level kernel's)
+    const int64_t M1 = sched2 ? std::min<int64_t>(Mq, (int64_t)(mean_chunk1() * (double)Mq)) : 0;
+    bool forked2 = false;
+    const cdx_stream_t sideB = reinterpret_cast<cdx_stream_t>(ss.s2);
+    auto mean_rows = [&](int64_t a, int64_t b, cdx_stream_t st) -> int {
+      if (b <= a) return CDX_OK;
+      return cdx_gpis_mean(&p->gpis, w.X + 3 * a, b - a, w.mean + a, w.gmean + 3 * a, w.normal + 3 * a, st);
+    };
+    auto launch_fork2 = [&]() -> int {
+      forked = forked2 = true;
+      if (hipEventRecord(ss.fork, s) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess ||
+          hipStreamWaitEvent(ss.s2, ss.fork, 0) != hipSuccess)
+        return CDX_ELAUNCH;
+      int r = launch_records(ss.s);
+      if (!r) r = mean_rows(0, M1, sideB);
+      if (!r && hipEventRecord(ss.g1, ss.s2) != hipSuccess) r = CDX_ELAUNCH;
+      return r;
+    };
+    auto launch_phase2 = [&]() -> int {  // after the main stream recorded g2
+      if (hipStreamWaitEvent(ss.s2, ss.g2, 0) != hipSuccess) return CDX_ELAUNCH;
+      int r = mean_rows(M1, std::max(M1, M01), sideB);
+      if (!r && hipEventRecord(ss.e2a, ss.s2) != hipSuccess) r = CDX_ELAUNCH;
+      if (!r) r = mean_rows(std::max(M1, M01), Mq, sideB);
+      if (r) return r;
+      if (hipStreamWaitEvent(ss.s, ss.e2a, 0) != hipSuccess) return CDX_ELAUNCH;
+      GpisView gv0;
+      gv0.mean = w.mean; gv0.gmean = w.gmean; gv0.normal = w.normal; gv0.std_ = w.std_; gv0.gstd = w.gstd;
+      gv0.E = E; gv0.T = T; gv0.Lq = p->n_query_levels; gv0.e = 0;
+      r = launch_level<true>(p, E, q, comp, target, kabsch_noise, seed, w, gv0, flip, w.krot, ss.s);
+      if (r) return r;
+      level_early = true;
+      if (hipEventRecord(ss.join, ss.s) != hipSuccess || hipStreamWaitEvent(ss.s2, ss.join, 0) != hipSuccess ||
+          hipEventRecord(ss.jb, ss.s2) != hipSuccess)
+        return CDX_ELAUNCH;
+      return CDX_OK;
+    };
     auto joined = [&](int r) -> int {
+      if (forked2) {  // both side streams' queued work, whichever phase failed
+        if ((hipEventRecord(ss.join, ss.s) != hipSuccess || hipEventRecord(ss.jb, ss.s2) != hipSuccess ||
+             hipStreamWaitEvent(s, ss.join, 0) != hipSuccess || hipStreamWaitEvent(s, ss.jb, 0) != hipSuccess) && !r)
+          r = CDX_ELAUNCH;
+        return r;
+      }
       if (forked && hipStreamWaitEvent(s, ss.join, 0) != hipSuccess && !r) r = CDX_ELAUNCH;
       if (forkedB && hipStreamWaitEvent(s, ss.joinB, 0) != hipSuccess && !r) r = CDX_ELAUNCH;
       return r;
@@ -995,18 +1097,23 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     const int fp = kmode == 1 ? 4 : (fork ? fork_point() : 0);
     if (fp == 1 && (rc = launch_fork())) return joined(rc);
     auto fork_cb = [](void* c) { return (*static_cast<decltype(launch_fork)*>(c))(); };
-    rc = cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep, w.zkey,
-                                   w.stats, s, fp == 4 ? +fork_cb : nullptr, &launch_fork);
+    auto fork2_cb = [](void* c) { return (*static_cast<decltype(launch_fork2)*>(c))(); };
+    rc = sched2 ? cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep,
+                                            w.zkey, w.stats, s, +fork2_cb, &launch_fork2)
+                : cdx::screen_select_launch(p->gpis, w.X, Mg, T, w.screen_ws, w.sv2, w.std_, w.vpos, w.rows, w.keep,
+                                            w.zkey, w.stats, s, fp == 4 ? +fork_cb : nullptr, &launch_fork);
     if (!rc && inject_fail(1)) rc = CDX_ELAUNCH;
     if (rc) return joined(rc);
-    if (fp == 2 && (rc = launch_fork())) return joined(rc);
+    if (!sched2 && fp == 2 && (rc = launch_fork())) return joined(rc);
+    if (sched2 && hipStreamWaitEvent(s, ss.g1, 0) != hipSuccess) return joined(CDX_ELAUNCH);
     double* rpart = nullptr;
     int64_t rpad = 0;
     rc = cdx::gpis_refine_launch(p->gpis, w.X, w.rows, w.stats + cdx::SS_EXTRA, (int)Mg, Ms, w.refine_ws, w.V, s, &rpart,
-                                 &rpad);
+                                 &rpad, nullptr, true, sched2 ? ss.g2 : nullptr);
+    if (!rc && sched2) rc = launch_phase2();
     if (!rc && inject_fail(2)) rc = CDX_ELAUNCH;
     if (rc) return joined(rc);
-    if (fp == 3 && (rc = launch_fork())) return joined(rc);
+    if (!sched2 && fp == 3 && (rc = launch_fork())) return joined(rc);
     rc = cdx::refine_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.sv2, w.vpos, w.keep, w.std_, w.var, w.sel,
                                    w.Xg, w.vrow, w.stats, s);
     if (rc) return joined(rc);
@@ -1024,11 +1131,11 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                                grad_fold() ? &fold : nullptr);
     if (!rc && inject_fail(3)) rc = CDX_ELAUNCH;
     if (rc) return joined(rc);
-    if (fork && (rc = launch_b())) return joined(rc);
+    if (fork && !sched2 && (rc = launch_b())) return joined(rc);
     // mean A (and the Kabsch records of mode 1) before the level kernel; mean B is joined before the
-    // combine kernel below
-    if (forked && hipStreamWaitEvent(s, ss.join, 0) != hipSuccess) {
-      forked = false;
+    // combine kernel below (sched2: jb follows both side streams)
+    if (forked && hipStreamWaitEvent(s, sched2 ? ss.jb : ss.join, 0) != hipSuccess) {
+      forked = forked2 = false;
       return joined(CDX_ELAUNCH);
     }
     if (kmode == 1 && forked) krot = w.krot;

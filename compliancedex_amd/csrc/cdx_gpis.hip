@@ -257,6 +257,26 @@ typedef double dbl2v __attribute__((ext_vector_type(2)));
 //   fence each cut piece needs writes back its XCD's whole L2.)
 enum { MODE_GRAD = 0, MODE_VAR = 1, MODE_GRADV = 2, MODE_VARL = 3 };
 
+// Streaming V (A/B switches): CDX_NT_VSTORE stores V rows and the refine's partial tiles non-temporally,
+// CDX_NT_VLOAD loads the ∇std pass's V rows non-temporally — streamed once, they then do not evict the
+// L⁻ᵀ / L⁻¹ stripes each XCD's L2 re-reads for every query tile.
+template <class T>
+__device__ __forceinline__ void v_store(T* p, T v) {
+#if defined(CDX_NT_VSTORE)
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+template <class T>
+__device__ __forceinline__ T v_load(const T* p) {
+#if defined(CDX_NT_VLOAD)
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 constexpr int RC_MAX_NT = 16;  // stripes with host unit costs (N_pad ≤ 4096); beyond: equal K-step cuts
 static_assert(RC_MAX_NT == cdx::GC_MAX_NT, "the ∇std pass's stripe costs travel in RefineList::uc");
 struct RefineList {
@@ -486,7 +506,7 @@ __device__ inline void refine_merge_unit(const cdx_gpis& g, const RefineList& rl
       sq[rr] = 0.0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        dst[c] = v[rr][c];
+        v_store(dst + c, v[rr][c]);
         sq[rr] = fma(v[rr][c], v[rr][c], sq[rr]);
       }
     }
@@ -590,7 +610,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     }
     if (!GEN) {  // GRADV: V at shifted columns; VAR: K* rows
 #pragma unroll
-      for (int i = 0; i < GEN_PER; ++i) kv[i] = vrow[kb + gk + i + (VAR ? 0 : vsh)];
+      for (int i = 0; i < GEN_PER; ++i) kv[i] = v_load(vrow + kb + gk + i + (VAR ? 0 : vsh));
     }
   };
   auto gen = [&](const double* x1, int i) {  // K* entry (gm, gk + i) from the X1 rows at x1
@@ -748,7 +768,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
         for (int r = 0; r < 4; ++r) {
           double* vr = rl.slots + ((int64_t)pslot * ST_BM + wr + 16 * i + (lane >> 4) + 4 * r) * ST_BN + wc + (lane & 15);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) vr[16 * j] = acc[i][j][r];
+          for (int j = 0; j < 4; ++j) v_store(vr + 16 * j, acc[i][j][r]);
         }
 #endif
       return;
@@ -776,7 +796,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
         for (int r = 0; r < 4; ++r) {
           double* vr = vout + (m0 + wr + 16 * i + (lane >> 4) + 4 * r) * (int64_t)Np + n0 + wc + (lane & 15);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) vr[16 * j] = acc[i][j][r];
+          for (int j = 0; j < 4; ++j) v_store(vr + 16 * j, acc[i][j][r]);
         }
     }
 #pragma unroll
@@ -1416,11 +1436,12 @@ int gpis_refine_reset(const cdx_gpis& g, int64_t Mcap, void* ws, hipStream_t s) 
 
 template <int KT>
 static void refine_launch_kt(const cdx_gpis& g, const double* X, int64_t Mcap, const RefineList& rl, double* partial,
-                             int64_t M_pad, double* vout, hipStream_t s, bool prof) {
+                             int64_t M_pad, double* vout, hipStream_t s, bool prof, hipEvent_t after) {
   if (prof) prof_mark(PROF_GPIS_STD, true, s);
   hipLaunchKernelGGL((gpis_std_kernel<KT, MODE_VARL>), dim3(REFINE_PIECES), dim3(ST_THREADS), 0, s, g, X, Mcap, partial,
                      M_pad, 0, g.N_pad / ST_BN, vout, nullptr, nullptr, 0, rl);
   if (prof) prof_mark(PROF_GPIS_STD, false, s);
+  if (after) (void)hipEventRecord(after, s);
 #if !defined(CDX_MERGE_FUSED)
   hipLaunchKernelGGL(gpis_var_merge, dim3(REFINE_PIECES), dim3(MERGE_THREADS), 0, s, g, rl, M_pad, partial, vout);
 #endif
@@ -1428,7 +1449,7 @@ static void refine_launch_kt(const cdx_gpis& g, const double* X, int64_t Mcap, c
 
 int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
                        void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out, const int* gate,
-                       bool prof) {
+                       bool prof, hipEvent_t after_refine) {
   if (Mcap <= 0 || G <= 0 || G > Mcap) return CDX_EINVAL;
   const int64_t M_pad = round_up(Mcap, ST_BM);
   double* partial = static_cast<double*>(ws);
@@ -1442,9 +1463,9 @@ int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, cons
     for (int nt = 0; nt < Nt; ++nt) rl.uc[nt] = var_unit_cost(nt, g.N, g.N_pad);
   }
   switch (g.kernel) {
-    case CDX_KERNEL_TPS: refine_launch_kt<CDX_KERNEL_TPS>(g, X, Mcap, rl, partial, M_pad, vout, s, prof); break;
-    case CDX_KERNEL_RBF: refine_launch_kt<CDX_KERNEL_RBF>(g, X, Mcap, rl, partial, M_pad, vout, s, prof); break;
-    default: refine_launch_kt<CDX_KERNEL_JOINT>(g, X, Mcap, rl, partial, M_pad, vout, s, prof); break;
+    case CDX_KERNEL_TPS: refine_launch_kt<CDX_KERNEL_TPS>(g, X, Mcap, rl, partial, M_pad, vout, s, prof, after_refine); break;
+    case CDX_KERNEL_RBF: refine_launch_kt<CDX_KERNEL_RBF>(g, X, Mcap, rl, partial, M_pad, vout, s, prof, after_refine); break;
+    default: refine_launch_kt<CDX_KERNEL_JOINT>(g, X, Mcap, rl, partial, M_pad, vout, s, prof, after_refine); break;
   }
   if (partial_out) *partial_out = partial;
   if (M_pad_out) *M_pad_out = M_pad;

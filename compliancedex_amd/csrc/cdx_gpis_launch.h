@@ -144,11 +144,12 @@ __device__ inline void grad_fold_gstd(const GradFold& f, int64_t m, double v, do
 // rows null: the identity list (rows 0 .. G + *extra; extra nullable = 0).  gate (nullable): the
 // closure's screen statistics — the launch runs only when a check failed (cdx::screen_failed), else every
 // workgroup returns at once (the closure's repair pass).  prof: mark the launch for cdx_profile_read.
+// after_refine (nullable): recorded on s between the refine kernel and its merge.
 size_t gpis_refine_ws_bytes(const cdx_gpis& g, int64_t Mcap);
 // Zeroes the refine workspace's cut-unit arrival counters (once after allocation; every launch
 // leaves them zero).
 int gpis_refine_reset(const cdx_gpis& g, int64_t Mcap, void* ws, hipStream_t s);
 int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
                        void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out,
-                       const int* gate = nullptr, bool prof = true);
+                       const int* gate = nullptr, bool prof = true, hipEvent_t after_refine = nullptr);
 }  // namespace cdx
