@@ -128,6 +128,9 @@ _SIGS = {
     "cdx_sdf_forward_f64": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "cdx_sdf_backward_f64": (C.c_int, [_P, _P, _P, _I64, _P, _P]),
     "cdx_sdf_stats": (C.c_int, [C.c_int32, C.POINTER(C.c_uint64), _P]),
+    "cdx_sdf_mesh_bytes": (C.c_size_t, [_I64]),
+    "cdx_sdf_mesh_prepare": (C.c_int, [_P, _I64, _P, _P]),
+    "cdx_sdf_query": (C.c_int, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "cdx_version": (C.c_char_p, []),
     "cdx_abi_sizes": (None, [C.POINTER(C.c_size_t)]),
     "cdx_selftest_mfma_f64": (C.c_int, [_P, _P, _P, _P]),

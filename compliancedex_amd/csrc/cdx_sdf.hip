@@ -422,6 +422,89 @@ int sdf_mode() {  // CDX_SDF_MODE=exact forces the brute-force kernel (benchmark
   return m;
 }
 
+// Prepared mesh: [ws words: bbox min keys ×3, max keys ×3, may-NaN flag, 0][records: C·CHUNK FaceRec][spheres]
+size_t mesh_rec_off() { return align256(8 * sizeof(unsigned)); }
+size_t mesh_sph_off(int64_t C) { return mesh_rec_off() + align256((size_t)C * CHUNK * sizeof(cdx::FaceRec)); }
+size_t mesh_bytes(int64_t F) {
+  const int64_t C = (F + CHUNK - 1) / CHUNK;
+  return mesh_sph_off(C) + align256((size_t)C * sizeof(Sphere));
+}
+
+// Face records and chunk spheres in Morton order of the bounding box of the faces (and of the points,
+// when given: the one-shot cdx_sdf_forward keeps its point-inclusive frame).  The order only steers the
+// culling (ties resolve by face index), so any frame gives identical outputs.
+int mesh_build(const float* faces, int64_t F, const float* points, int64_t P, char* mesh, hipStream_t s) {
+  const int n = (int)F;
+  const int C = (n + CHUNK - 1) / CHUNK;
+  size_t tf = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tf, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
+                                         (int*)nullptr, n, 0, 30, s) != hipSuccess)
+    return CDX_ELAUNCH;
+  size_t off = 0;
+  const size_t o_fk = off; off = align256(off + 2 * (size_t)n * sizeof(unsigned));
+  const size_t o_fv = off; off = align256(off + 2 * (size_t)n * sizeof(int));
+  const size_t o_tmp = off; off = align256(off + tf);
+  char* base = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&base), off, s) != hipSuccess) return CDX_ELAUNCH;
+  unsigned* ws = reinterpret_cast<unsigned*>(mesh);
+  unsigned* fk = reinterpret_cast<unsigned*>(base + o_fk);
+  int* fv = reinterpret_cast<int*>(base + o_fv);
+  hipLaunchKernelGGL(sdf_init_kernel, dim3(1), dim3(64), 0, s, ws);
+  const int64_t nbb = P + 3 * F;
+  const unsigned bbb = (unsigned)std::min<int64_t>((nbb + 255) / 256, 1024);
+  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(bbb), dim3(256), 0, s, points, P, faces, F, ws);
+  hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((F + 255) / 256)), dim3(256), 0, s, (const float*)nullptr,
+                     (int64_t)0, faces, F, (const unsigned*)ws, fk, fv, (unsigned*)nullptr, (int*)nullptr);
+  size_t t1 = tf;
+  bool ok = hipcub::DeviceRadixSort::SortPairs(base + o_tmp, t1, fk, fk + n, fv, fv + n, n, 0, 30, s) == hipSuccess;
+  hipLaunchKernelGGL(sdf_chunk_kernel, dim3((unsigned)((C * CHUNK + 255) / 256)), dim3(256), 0, s, faces, F,
+                     (const int*)(fv + n), reinterpret_cast<cdx::FaceRec*>(mesh + mesh_rec_off()),
+                     reinterpret_cast<Sphere*>(mesh + mesh_sph_off(C)), ws);
+  ok = ok && hipGetLastError() == hipSuccess;
+  ok = (hipFreeAsync(base, s) == hipSuccess) && ok;
+  return ok ? CDX_OK : CDX_ELAUNCH;
+}
+
+// Points in Morton order of the mesh's frame (a wave then holds nearby points), the culled kernel, and
+// the brute-force tile rule when the mesh may produce NaN distances (decided on the device).
+int mesh_query(const char* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
+               int32_t* sign, float* normals, float* clst, int32_t* face_idx, hipStream_t s) {
+  const int m = (int)P;
+  const int C = (int)((F + CHUNK - 1) / CHUNK);
+  size_t tp = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tp, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
+                                         (int*)nullptr, m, 0, 30, s) != hipSuccess)
+    return CDX_ELAUNCH;
+  size_t off = 0;
+  const size_t o_pk = off; off = align256(off + 2 * (size_t)m * sizeof(unsigned));
+  const size_t o_pv = off; off = align256(off + 2 * (size_t)m * sizeof(int));
+  const size_t o_tmp = off; off = align256(off + tp);
+  char* base = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&base), off, s) != hipSuccess) return CDX_ELAUNCH;
+  const unsigned* ws = reinterpret_cast<const unsigned*>(mesh);
+  unsigned* pk = reinterpret_cast<unsigned*>(base + o_pk);
+  int* pv = reinterpret_cast<int*>(base + o_pv);
+  hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P,
+                     (const float*)nullptr, (int64_t)0, ws, (unsigned*)nullptr, (int*)nullptr, pk, pv);
+  size_t t2 = tp;
+  bool ok = hipcub::DeviceRadixSort::SortPairs(base + o_tmp, t2, pk, pk + m, pv, pv + m, m, 0, 30, s) == hipSuccess;
+  hipLaunchKernelGGL(sdf_culled_kernel, dim3((unsigned)((P + 63) / 64)), dim3(SDF_BLOCK), 0, s, points, P,
+                     (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
+                     reinterpret_cast<const Sphere*>(mesh + mesh_sph_off(C)), C, ws, sqdist, sign, normals, clst,
+                     face_idx, (int)g_sdf_count);
+  hipLaunchKernelGGL(sdf_exact_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0, s, points,
+                     P, faces, F, ws, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
+  ok = ok && hipGetLastError() == hipSuccess;
+  ok = (hipFreeAsync(base, s) == hipSuccess) && ok;
+  return ok ? CDX_OK : CDX_ELAUNCH;
+}
+
+bool sdf_args_ok(int64_t P, const float* points, const float* faces, int64_t F, const float* sqdist,
+                 const int32_t* sign, const float* normals, const float* clst) {
+  return !(F == 0 || !points || !faces || !sqdist || !sign || !normals || !clst) && P <= INT32_MAX &&
+         F <= INT32_MAX / 9;
+}
+
 }  // namespace
 
 extern "C" {
@@ -430,63 +513,37 @@ int cdx_sdf_forward(const float* points, int64_t P, const float* faces, int64_t 
                     float* normals, float* clst, int32_t* face_idx, cdx_stream_t stream) {
   if (P < 0 || F < 0) return CDX_EINVAL;
   if (P == 0) return CDX_OK;
-  if (F == 0 || !points || !faces || !sqdist || !sign || !normals || !clst) return CDX_EINVAL;
-  if (P > INT32_MAX || F > INT32_MAX / 9) return CDX_EINVAL;
+  if (!sdf_args_ok(P, points, faces, F, sqdist, sign, normals, clst)) return CDX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const unsigned pblocks = (unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK);
   if (sdf_mode() == 1) {
-    hipLaunchKernelGGL(sdf_exact_kernel, dim3(pblocks), dim3(SDF_BLOCK), 0, s, points, P, faces, F,
-                       (const unsigned*)nullptr, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
+    hipLaunchKernelGGL(sdf_exact_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0, s,
+                       points, P, faces, F, (const unsigned*)nullptr, sqdist, sign, normals, clst, face_idx,
+                       (int)g_sdf_count);
     return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
   }
-  const int n = (int)F, m = (int)P;
-  const int C = (n + CHUNK - 1) / CHUNK;
-  size_t tf = 0, tp = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tf, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
-                                         (int*)nullptr, n, 0, 30, s) != hipSuccess ||
-      hipcub::DeviceRadixSort::SortPairs(nullptr, tp, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
-                                         (int*)nullptr, m, 0, 30, s) != hipSuccess)
-    return CDX_ELAUNCH;
-  // workspace: ws words | face keys/vals ×2 | point keys/vals ×2 | records | spheres | cub temp
-  size_t off = 0;
-  const size_t o_ws = off; off = align256(off + 8 * sizeof(unsigned));
-  const size_t o_fk = off; off = align256(off + 2 * (size_t)n * sizeof(unsigned));
-  const size_t o_fv = off; off = align256(off + 2 * (size_t)n * sizeof(int));
-  const size_t o_pk = off; off = align256(off + 2 * (size_t)m * sizeof(unsigned));
-  const size_t o_pv = off; off = align256(off + 2 * (size_t)m * sizeof(int));
-  const size_t o_rec = off; off = align256(off + (size_t)C * CHUNK * sizeof(cdx::FaceRec));
-  const size_t o_sph = off; off = align256(off + (size_t)C * sizeof(Sphere));
-  const size_t o_tmp = off; off = align256(off + (tf > tp ? tf : tp));
-  char* base = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void**>(&base), off, s) != hipSuccess) return CDX_ELAUNCH;
-  unsigned* ws = reinterpret_cast<unsigned*>(base + o_ws);
-  unsigned* fk = reinterpret_cast<unsigned*>(base + o_fk);
-  int* fv = reinterpret_cast<int*>(base + o_fv);
-  unsigned* pk = reinterpret_cast<unsigned*>(base + o_pk);
-  int* pv = reinterpret_cast<int*>(base + o_pv);
-  cdx::FaceRec* rec = reinterpret_cast<cdx::FaceRec*>(base + o_rec);
-  Sphere* sph = reinterpret_cast<Sphere*>(base + o_sph);
-  void* tmp = base + o_tmp;
+  char* mesh = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&mesh), mesh_bytes(F), s) != hipSuccess) return CDX_ELAUNCH;
+  int rc = mesh_build(faces, F, points, P, mesh, s);
+  if (!rc) rc = mesh_query(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, s);
+  if (hipFreeAsync(mesh, s) != hipSuccess && !rc) rc = CDX_ELAUNCH;
+  return rc;
+}
 
-  hipLaunchKernelGGL(sdf_init_kernel, dim3(1), dim3(64), 0, s, ws);
-  const int64_t nbb = P + 3 * F;
-  const unsigned bbb = (unsigned)std::min<int64_t>((nbb + 255) / 256, 1024);
-  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(bbb), dim3(256), 0, s, points, P, faces, F, ws);
-  hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((F + P + 255) / 256)), dim3(256), 0, s, points, P, faces, F,
-                     (const unsigned*)ws, fk, fv, pk, pv);
-  size_t t1 = tf, t2 = tp;
-  bool ok = hipcub::DeviceRadixSort::SortPairs(tmp, t1, fk, fk + n, fv, fv + n, n, 0, 30, s) == hipSuccess;
-  ok = ok && hipcub::DeviceRadixSort::SortPairs(tmp, t2, pk, pk + m, pv, pv + m, m, 0, 30, s) == hipSuccess;
-  hipLaunchKernelGGL(sdf_chunk_kernel, dim3((unsigned)((C * CHUNK + 255) / 256)), dim3(256), 0, s, faces, F,
-                     (const int*)(fv + n), rec, sph, ws);
-  hipLaunchKernelGGL(sdf_culled_kernel, dim3((unsigned)((P + 63) / 64)), dim3(SDF_BLOCK), 0, s, points, P,
-                     (const int*)(pv + m), faces, F, (const cdx::FaceRec*)rec, (const Sphere*)sph, C,
-                     (const unsigned*)ws, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
-  hipLaunchKernelGGL(sdf_exact_kernel, dim3(pblocks), dim3(SDF_BLOCK), 0, s, points, P, faces, F,
-                     (const unsigned*)ws, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
-  ok = ok && hipGetLastError() == hipSuccess;
-  ok = (hipFreeAsync(base, s) == hipSuccess) && ok;
-  return ok ? CDX_OK : CDX_ELAUNCH;
+size_t cdx_sdf_mesh_bytes(int64_t F) { return F > 0 ? mesh_bytes(F) : 0; }
+
+int cdx_sdf_mesh_prepare(const float* faces, int64_t F, void* mesh, cdx_stream_t stream) {
+  if (F <= 0 || F > INT32_MAX / 9 || !faces || !mesh) return CDX_EINVAL;
+  return mesh_build(faces, F, nullptr, 0, static_cast<char*>(mesh), reinterpret_cast<hipStream_t>(stream));
+}
+
+int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
+                  int32_t* sign, float* normals, float* clst, int32_t* face_idx, cdx_stream_t stream) {
+  if (P < 0 || F < 0 || !mesh) return CDX_EINVAL;
+  if (P == 0) return CDX_OK;
+  if (!sdf_args_ok(P, points, faces, F, sqdist, sign, normals, clst)) return CDX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (sdf_mode() == 1) return cdx_sdf_forward(points, P, faces, F, sqdist, sign, normals, clst, face_idx, stream);
+  return mesh_query(static_cast<const char*>(mesh), faces, F, points, P, sqdist, sign, normals, clst, face_idx, s);
 }
 
 int cdx_sdf_stats(int32_t enable, uint64_t* out3, cdx_stream_t stream) {

@@ -2,7 +2,8 @@
 
 ``compute_sdf(points, face_vertices) -> (sqdist, sign, normals, clst_points)``: squared
 distance (autograd w.r.t. points), int32 sign, unit (p − c) normal and closest point
-(sdf.py:34-64), computed by cdx_sdf_forward / cdx_sdf_backward (float32, the culled path) or
+(sdf.py:34-64), computed by cdx_sdf_query on a cached prepared mesh / cdx_sdf_backward (float32, the
+culled path) or
 cdx_sdf_forward_f64 / cdx_sdf_backward_f64 (float64, the reference's double instantiation,
 unbatched_triangle_distance_cuda.cu:282).  ``compute_sdf_with_faces`` additionally returns the
 argmin face index.
@@ -33,6 +34,33 @@ def _check(points, faces):
         raise RuntimeError(f"face_vertices must have shape [F, 3, 3], got {tuple(faces.shape)}")
 
 
+class _MeshCache:
+    """Prepared float32 meshes (cdx_sdf_mesh_prepare) of the face tensors queried last: the optimisers
+    query the same two meshes every iteration, so the face records / chunk spheres are built once.
+    Keyed by the face tensor's storage, shape, device and version counter (an in-place change bumps
+    it); an entry holds its face tensor, so the storage cannot be reused while cached."""
+
+    def __init__(self, size=8):
+        self.size, self.entries = size, {}
+
+    def get(self, faces):
+        key = (faces.data_ptr(), tuple(faces.shape), faces.device.index, faces._version)
+        hit = self.entries.pop(key, None)
+        if hit is None:
+            lib = N.load()
+            buf = torch.empty(lib.cdx_sdf_mesh_bytes(faces.shape[0]), dtype=torch.uint8, device=faces.device)
+            N.check(lib.cdx_sdf_mesh_prepare(N.ptr(faces), faces.shape[0], N.ptr(buf), N.stream_ptr(faces.device)),
+                    "cdx_sdf_mesh_prepare")
+            hit = (faces, buf)
+            if len(self.entries) >= self.size:
+                self.entries.pop(next(iter(self.entries)))
+        self.entries[key] = hit  # most recent last
+        return hit[1]
+
+
+_meshes = _MeshCache()
+
+
 def _forward(points, faces, want_face):
     _check(points, faces)
     lib = N.load()
@@ -44,6 +72,11 @@ def _forward(points, faces, want_face):
     normals = torch.zeros(P, 3, dtype=points.dtype, device=points.device)
     clst = torch.zeros(P, 3, dtype=points.dtype, device=points.device)
     face = torch.zeros(P, dtype=torch.int32, device=points.device) if want_face else None
+    if points.dtype == torch.float32 and P > 0 and faces.shape[0] > 0:
+        N.check(lib.cdx_sdf_query(N.ptr(_meshes.get(faces)), N.ptr(faces), faces.shape[0], N.ptr(points), P, N.ptr(dist),
+                                  N.ptr(sign), N.ptr(normals), N.ptr(clst), N.ptr(face), N.stream_ptr(points.device)),
+                "cdx_sdf_query")
+        return dist, sign, normals, clst, face
     fwd = lib.cdx_sdf_forward if points.dtype == torch.float32 else lib.cdx_sdf_forward_f64
     N.check(fwd(N.ptr(points), P, N.ptr(faces), faces.shape[0], N.ptr(dist), N.ptr(sign), N.ptr(normals), N.ptr(clst),
                 N.ptr(face), N.stream_ptr(points.device)), "cdx_sdf_forward")

@@ -401,17 +401,28 @@ int cdx_sdf_backward(const float* grad_dist, const float* points, const float* c
 /* float64 points / faces: the reference's double instantiation — double arithmetic except the
  * float edge parameter of point_at (.cu:171-173) and the float squared distance (.cu:237), so
  * sqdist holds float values; brute force with the reference's 512-face tile rule. */
+int cdx_sdf_forward_f64(const double* points, int64_t P, const double* faces, int64_t F,
+                        double* sqdist, int32_t* sign, double* normals, double* clst,
+                        int32_t* face_idx, cdx_stream_t stream);
+int cdx_sdf_backward_f64(const double* grad_dist, const double* points, const double* clst, int64_t P,
+                         double* grad_points, cdx_stream_t stream);
+
+/* A prepared mesh for repeated float32 queries (the SDF optimisers query the same meshes every
+ * iteration): the face records in Morton order, their 32-face chunks' bounding spheres and the
+ * may-NaN flag of cdx_sdf_forward's culled path, built once.  cdx_sdf_query is cdx_sdf_forward on it —
+ * identical outputs (the face order only steers the culling; ties resolve by face index).  faces must
+ * stay the ones prepared (the exact path of a NaN-capable mesh scans them).  mesh: cdx_sdf_mesh_bytes(F)
+ * caller-owned device bytes. */
+size_t cdx_sdf_mesh_bytes(int64_t F);
+int cdx_sdf_mesh_prepare(const float* faces, int64_t F, void* mesh, cdx_stream_t stream);
+int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
+                  int32_t* sign, float* normals, float* clst, int32_t* face_idx, cdx_stream_t stream);
 /* Diagnostic work counters of cdx_sdf_forward (float path): out3 (nullable, host) = [(point, face) pairs
  * the culled kernel evaluated — every face of each chunk a wave could not rule out, times its live
  * lanes —, pairs of brute-force scans (the exact path), points queried]; read before `enable` applies.
  * enable 1: zero the counters and count from now on (one atomic per wave); 0: stop counting; −1: only
  * read.  Against P·F per call this is the culling's work saving. */
 int cdx_sdf_stats(int32_t enable, uint64_t* out3, cdx_stream_t stream);
-int cdx_sdf_forward_f64(const double* points, int64_t P, const double* faces, int64_t F,
-                        double* sqdist, int32_t* sign, double* normals, double* clst,
-                        int32_t* face_idx, cdx_stream_t stream);
-int cdx_sdf_backward_f64(const double* grad_dist, const double* points, const double* clst, int64_t P,
-                         double* grad_points, cdx_stream_t stream);
 
 /* Library identification (gfx arch string compiled in). */
 const char* cdx_version(void);

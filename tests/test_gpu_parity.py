@@ -437,6 +437,35 @@ def test_sdf_culled_near_surface_bitwise():
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+def test_sdf_prepared_mesh_equals_one_shot():
+    """compute_sdf queries a cached prepared mesh (cdx_sdf_mesh_prepare once, cdx_sdf_query per call,
+    the face frame only) and the _C shim the one-shot cdx_sdf_forward (the points ∪ faces frame): the
+    Morton frame only steers the culling, so the outputs are bit-identical; an in-place change of the
+    face tensor invalidates the cached mesh (its version counter)."""
+    from compliancedex_amd import _native as N
+    from compliancedex_amd import compute_sdf_with_faces
+    lib = N.load()
+    faces = torch.from_numpy(np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))).to(DEV)
+    rng = np.random.default_rng(17)
+    lo, hi = faces.reshape(-1, 3).min(0)[0], faces.reshape(-1, 3).max(0)[0]
+    pts = (lo - 0.3 + (hi - lo + 0.6) * torch.from_numpy(rng.random((5000, 3))).to(DEV).float()).contiguous()
+
+    def one_shot(f):
+        P = pts.shape[0]
+        o = [torch.zeros(P, device=DEV), torch.zeros(P, dtype=torch.int32, device=DEV), torch.zeros(P, 3, device=DEV),
+             torch.zeros(P, 3, device=DEV), torch.zeros(P, dtype=torch.int32, device=DEV)]
+        N.check(lib.cdx_sdf_forward(N.ptr(pts), P, N.ptr(f), f.shape[0], *(N.ptr(t) for t in o), N.stream_ptr(DEV)), "fwd")
+        return [t.cpu().numpy() for t in o]
+
+    for step in range(2):
+        got = [t.cpu().numpy() for t in compute_sdf_with_faces(pts, faces)]
+        again = [t.cpu().numpy() for t in compute_sdf_with_faces(pts, faces)]  # cache hit
+        want = one_shot(faces)
+        for a, b, c in zip(got, again, want):
+            assert _bitwise_equal_nan_aware(a, c) and _bitwise_equal_nan_aware(b, c), step
+        faces.mul_(1.1)  # in place: the next query must re-prepare
+
+
 def test_sdf_nonfinite_points_take_exact_path():
     """A workgroup holding a NaN / inf / |p| > 1e4 point runs the reference tile rule."""
     from compliancedex_amd import compute_sdf_with_faces
