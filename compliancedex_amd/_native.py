@@ -61,6 +61,10 @@ class CdxForceEq(C.Structure):
                 ("dummy_comp", C.c_float), ("n_tips", C.c_int32)]
 
 
+class CdxKinParams(C.Structure):
+    _fields_ = [("fe", CdxForceEq), ("ref_q", C.c_float * MAX_DOFS)]
+
+
 class CdxAdam(C.Structure):
     _fields_ = [("lr", C.c_double * 5), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double),
                 ("comp_min", C.c_double), ("target_lb", C.c_double * (MAX_TIPS * 3)),
@@ -128,6 +132,8 @@ _SIGS = {
     "cdx_sdf_forward_f64": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "cdx_sdf_backward_f64": (C.c_int, [_P, _P, _P, _I64, _P, _P]),
     "cdx_sdf_stats": (C.c_int, [C.c_int32, C.POINTER(C.c_uint64), _P]),
+    "cdx_kin_cost": (C.c_int, [C.POINTER(CdxChain), C.POINTER(CdxKinParams), _I64] + [_P] * 15 + [C.c_uint64] +
+                     [_P] * 7),
     "cdx_sdf_mesh_bytes": (C.c_size_t, [_I64]),
     "cdx_sdf_mesh_prepare": (C.c_int, [_P, _I64, _P, _P]),
     "cdx_sdf_query": (C.c_int, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),

@@ -19,7 +19,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "lib")
 ARCH = os.environ.get("CDX_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["cdx_gpis.hip", "cdx_screen.hip", "cdx_fit.hip", "cdx_closure.hip", "cdx_sdf.hip", "cdx_optim.hip", "cdx_exchange.hip"]
+HIP_SOURCES = ["cdx_gpis.hip", "cdx_screen.hip", "cdx_fit.hip", "cdx_closure.hip", "cdx_sdf.hip", "cdx_optim.hip", "cdx_exchange.hip", "cdx_kin.hip"]
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
 
@@ -92,7 +92,7 @@ def build_device(force=False, defines=DEFAULT_DEFINES, out_name="libcdx.so"):
         # no FMA contraction in the per-candidate code (FK, Kabsch, costs) and TorchSDF: the
         # device then rounds like the reference's CPU float ops and like libcdx_host.so (the
         # collision cost's 1/d near the floor amplifies a contracted f32 FK to 1e-4)
-        if src in ("cdx_sdf.hip", "cdx_closure.hip"):
+        if src in ("cdx_sdf.hip", "cdx_closure.hip", "cdx_kin.hip"):
             flags.append("-ffp-contract=off")
         cmds.append([HIPCC, *flags, "-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)

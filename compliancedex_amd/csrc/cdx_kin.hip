@@ -1,0 +1,178 @@
+// Kin-mode (KinGraspOptimizer, optimize_pregrasp.py:121-227) cost assembly and backward for gfx950: one
+// lane per candidate takes the iteration's fingertips (FK + palm offset), the three TorchSDF queries'
+// outputs and the parameters, and returns the loss l, the force-closure margins, the blended contact
+// normals and the gradients of l w.r.t. the joint angles, targets and compliances — the reference's
+// ~30 elementwise ops, its force_eq_reward and the autograd backward through them, TorchSDF and the FK
+// chain (:183-208), in one launch.
+//
+//   normal_f   = normalize(½·s1_f·n1_f + ½·s2_f·n2_f)          (tips vs deflated / true mesh, :186-187; f32)
+//   l          = −5·reward + 1000·Σ√d_f + 10·Σ ts_f·√td_f + 10·|mean tip − mean target|
+//                − Σ clamp(fn_f·softmin(fn)_f, max = 1) + 10·|q − ref_q|          (:195-205)
+//   ∂√d/∂tip   = ½/√d · 2(tip − clst)                          (TorchSDF backward, .cu:256-270)
+// The per-candidate arithmetic is f64 (the force-equilibrium reward is ForceEq, shared with the closure);
+// the normals are formed in f32 as the reference forms them; the FK backward runs in f32 like the
+// reference's autograd through compute_forward_kinematics.
+#include <hip/hip_runtime.h>
+
+#include "cdx_cost.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+__device__ __forceinline__ uint64_t kin_mix(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+template <int NT, int MAXD>
+__global__ __launch_bounds__(64) void kin_cost_kernel(
+    cdx_chain chain, cdx_kin_params p, int64_t E, const float* __restrict__ q, const float* __restrict__ tip,
+    const float* __restrict__ target, const float* __restrict__ comp, const int32_t* __restrict__ sign1,
+    const float* __restrict__ n1, const float* __restrict__ sqd, const int32_t* __restrict__ sign2,
+    const float* __restrict__ n2, const float* __restrict__ clst, const float* __restrict__ tsqd,
+    const int32_t* __restrict__ tsign, const float* __restrict__ tclst, const double* __restrict__ noise, uint64_t seed,
+    double* __restrict__ loss, double* __restrict__ margin, float* __restrict__ normal_out, float* __restrict__ g_q,
+    float* __restrict__ g_target, float* __restrict__ g_comp) {
+  constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int T = NT > 0 ? NT : chain.n_tips, D = chain.n_dofs;
+  double tp[NTA][3], tg[NTA * 3], cp[NTA], nr[NTA][3];
+  for (int f = 0; f < T; ++f) {
+    const int64_t r = e * T + f;
+    // ½·s1·n1 + ½·s2·n2 and its norm, in float32 (the reference's tensors are float32)
+    float n[3];
+    const float a1 = 0.5f * (float)sign1[r], a2 = 0.5f * (float)sign2[r];
+    for (int i = 0; i < 3; ++i) n[i] = a1 * n1[3 * r + i] + a2 * n2[3 * r + i];
+    const float nn = sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    for (int i = 0; i < 3; ++i) {
+      const float v = n[i] / nn;
+      nr[f][i] = (double)v;
+      if (normal_out) normal_out[3 * r + i] = v;
+      tp[f][i] = (double)tip[3 * r + i];
+      tg[3 * f + i] = (double)target[3 * r + i];
+    }
+    cp[f] = (double)comp[r];
+  }
+  double nz[9];
+  if (noise) {
+    for (int i = 0; i < 9; ++i) nz[i] = noise[e * 9 + i];
+  } else {
+    for (int i = 0; i < 9; ++i) nz[i] = (double)(kin_mix(seed ^ kin_mix((uint64_t)(e * 9 + i))) >> 11) * 0x1.0p-53;
+  }
+  cdx::ForceEqParams fp;
+  fp.cos_mu = (double)p.fe.cos_mu;
+  fp.gravity = p.fe.gravity;
+  for (int i = 0; i < 3; ++i) fp.com[i] = (double)p.fe.com[i];
+  fp.dummy_target_z = (double)p.fe.dummy_target_z;
+  fp.dummy_comp = (double)p.fe.dummy_comp;
+  cdx::ForceEq<NT> fe;
+  fe.forward(fp, T, tp, tg, cp, nr, nz);
+
+  // ---- forward
+  double ct[3] = {0, 0, 0}, cg[3] = {0, 0, 0};
+  for (int f = 0; f < T; ++f)
+    for (int i = 0; i < 3; ++i) { ct[i] += tp[f][i]; cg[i] += tg[3 * f + i]; }
+  double cd[3];
+  for (int i = 0; i < 3; ++i) cd[i] = ct[i] / T - cg[i] / T;
+  const double cn = sqrt(cd[0] * cd[0] + cd[1] * cd[1] + cd[2] * cd[2]);
+  double dq2 = 0.0;
+  for (int i = 0; i < D; ++i) {
+    const double d = (double)q[e * D + i] - (double)p.ref_q[i];
+    dq2 += d * d;
+  }
+  const double qn = sqrt(dq2);
+  double dcost = 0.0, tcost = 0.0, sd[NTA], std_[NTA];
+  for (int f = 0; f < T; ++f) {
+    const int64_t r = e * T + f;
+    sd[f] = sqrt((double)sqd[r]);
+    std_[f] = sqrt((double)tsqd[r]);
+    dcost += sd[f];
+    tcost += (double)tsign[r] * std_[f];
+  }
+  const double* fn = fe.fn;
+  double zmax = -fn[0];
+  for (int f = 1; f < T; ++f) zmax = -fn[f] > zmax ? -fn[f] : zmax;
+  double ez[NTA], esum = 0.0;
+  for (int f = 0; f < T; ++f) { ez[f] = exp(-fn[f] - zmax); esum += ez[f]; }
+  double sm[NTA], v[NTA], fcost = 0.0;
+  for (int f = 0; f < T; ++f) {
+    sm[f] = ez[f] / esum;
+    v[f] = fn[f] * sm[f];
+    fcost += v[f] > 1.0 ? 1.0 : v[f];
+  }
+  loss[e] = -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost + qn * 10.0;
+  for (int f = 0; f < T; ++f) margin[e * T + f] = fe.margin[f];
+
+  // ---- backward (dl = 1)
+  double gt[NTA][3], gg[NTA][3], gc[NTA];
+  for (int f = 0; f < T; ++f) {
+    const int64_t r = e * T + f;
+    gc[f] = 0.0;
+    const double gd = 1000.0 * 0.5 / sd[f], gtd = 10.0 * (double)tsign[r] * 0.5 / std_[f];
+    for (int i = 0; i < 3; ++i) {
+      const double gcen = cn > 0 ? 10.0 * cd[i] / cn / T : 0.0;
+      gt[f][i] = 2.0 * gd * (tp[f][i] - (double)clst[3 * r + i]) + gcen;
+      gg[f][i] = 2.0 * gtd * (tg[3 * f + i] - (double)tclst[3 * r + i]) - gcen;
+    }
+  }
+  double g_fn[NTA], g_sm[NTA], gsm_dot = 0.0;
+  for (int f = 0; f < T; ++f) {
+    const double gv = v[f] <= 1.0 ? -1.0 : 0.0;
+    g_fn[f] = gv * sm[f];
+    g_sm[f] = gv * fn[f];
+    gsm_dot += g_sm[f] * sm[f];
+  }
+  for (int f = 0; f < T; ++f) g_fn[f] += -(sm[f] * (g_sm[f] - gsm_dot));
+  fe.backward(-5.0, g_fn, cp, gt, gg, gc);
+  float gq[CDX_MAX_DOFS];
+  for (int i = 0; i < D; ++i) {
+    const double d = (double)q[e * D + i] - (double)p.ref_q[i];
+    gq[i] = qn > 0 ? (float)(10.0 * d / qn) : 0.f;
+  }
+  float fk_g[CDX_MAX_DOFS];
+  for (int i = 0; i < D; ++i) fk_g[i] = 0.f;
+  for (int f = 0; f < T; ++f) {
+    const float gpos[3] = {(float)gt[f][0], (float)gt[f][1], (float)gt[f][2]};
+    cdx::fk_tip_bwd<MAXD>(chain, f, q + e * D, gpos, cdx::GqAdd{fk_g});
+  }
+  for (int i = 0; i < D; ++i) g_q[e * D + i] = gq[i] + fk_g[i];
+  for (int f = 0; f < T; ++f) {
+    g_comp[e * T + f] = (float)gc[f];
+    for (int i = 0; i < 3; ++i) g_target[(e * T + f) * 3 + i] = (float)gg[f][i];
+  }
+}
+
+}  // namespace
+
+extern "C" int cdx_kin_cost(const cdx_chain* chain, const cdx_kin_params* p, int64_t E, const float* q, const float* tip,
+                            const float* target, const float* comp, const int32_t* sign1, const float* n1,
+                            const float* sqdist, const int32_t* sign2, const float* n2, const float* clst,
+                            const float* tsqdist, const int32_t* tsign, const float* tclst, const double* noise,
+                            uint64_t seed, double* loss, double* margin, float* normal, float* g_q, float* g_target,
+                            float* g_comp, cdx_stream_t stream) {
+  if (!chain || !p || chain->n_tips < 1 || chain->n_tips > CDX_MAX_TIPS || chain->n_dofs < 0 ||
+      chain->n_dofs > CDX_MAX_DOFS || chain->n_bodies < 1 || chain->n_bodies > CDX_MAX_BODIES || p->fe.n_tips != chain->n_tips)
+    return CDX_EINVAL;
+  if (E < 0) return CDX_EINVAL;
+  if (E == 0) return CDX_OK;
+  if (!q || !tip || !target || !comp || !sign1 || !n1 || !sqdist || !sign2 || !n2 || !clst || !tsqdist || !tsign ||
+      !tclst || !loss || !margin || !g_q || !g_target || !g_comp)
+    return CDX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)((E + 63) / 64));
+  const bool shallow = cdx::chain_max_depth(*chain) <= 8;
+#define CDX_KIN_LAUNCH(NT, MAXD)                                                                                      \
+  hipLaunchKernelGGL((kin_cost_kernel<NT, MAXD>), grid, dim3(64), 0, s, *chain, *p, E, q, tip, target, comp, sign1, n1, \
+                     sqdist, sign2, n2, clst, tsqdist, tsign, tclst, noise, seed, loss, margin, normal, g_q, g_target,    \
+                     g_comp)
+  if (chain->n_tips == 4 && shallow) CDX_KIN_LAUNCH(4, 8);
+  else if (chain->n_tips == 4) CDX_KIN_LAUNCH(4, CDX_MAX_DEPTH);
+  else if (shallow) CDX_KIN_LAUNCH(0, 8);
+  else CDX_KIN_LAUNCH(0, CDX_MAX_DEPTH);
+#undef CDX_KIN_LAUNCH
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}

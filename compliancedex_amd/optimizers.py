@@ -20,9 +20,11 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .force_eq import force_eq_reward
+from . import _native as N
+from .force_eq import force_eq_descriptor, force_eq_reward
 from .optimizer import EE_OFFSETS, FINGERTIP_LB, FINGERTIP_UB, WRIST_OFFSET
 from .robot_model import DifferentiableRobotModel
+from .torchsdf import _forward as _sdf_query
 from .torchsdf import compute_sdf
 
 
@@ -126,8 +128,13 @@ class KinGraspOptimizer:
         return (tips.view(-1, 3) + self.palm_offset).view(-1, 3)
 
     def optimize(self, joint_angles, target_pose, compliance, friction_mu, object_mesh, verbose=True,
-                 kabsch_noise=None, trace_rows=False):
-        """``trace_rows``: also keep every iteration's per-candidate loss in ``loss_rows`` (device)."""
+                 kabsch_noise=None, trace_rows=False, fused=True):
+        """``trace_rows``: also keep every iteration's per-candidate loss in ``loss_rows`` (device).
+        ``fused`` (default): per iteration one FK launch, the three TorchSDF queries on cached prepared
+        meshes and ONE cost-and-backward kernel (cdx_kin_cost: force_eq_reward, the six cost terms and the
+        backward through them, TorchSDF and the FK chain) writing the parameters' gradients — no autograd
+        graph; ``fused=False``: the same loop through the autograd drop-ins (compute_sdf, force_eq_reward,
+        the FK module) and torch tensor ops, as the reference writes it."""
         self.loss_history = []
         self.loss_rows = []
         joint_angles = joint_angles.clone().requires_grad_(True)
@@ -143,6 +150,9 @@ class KinGraspOptimizer:
             optim = torch.optim.Adam([{"params": joint_angles, "lr": 1e-2}, {"params": compliance, "lr": 0.2}])
         E, T = target_pose.shape[0], target_pose.shape[1]
         best = _Best(torch.float32, E, T, self.device, q=joint_angles, comp=compliance, target=target_pose)
+        if fused:
+            return self._optimize_fused(joint_angles, target_pose, compliance, friction_mu, faces, faces_deflate,
+                                        optim, best, verbose, kabsch_noise, trace_rows)
         for s in range(self.num_iters):
             optim.zero_grad()
             all_tip = self.forward_kinematics(joint_angles)
@@ -171,6 +181,61 @@ class KinGraspOptimizer:
             print(best.margin, best.normal)
         self.best_loss = best.value
         return best.params["q"], best.params["comp"], best.params["target"], best.flag()
+
+    def _optimize_fused(self, joint_angles, target_pose, compliance, friction_mu, faces, faces_deflate, optim, best,
+                        verbose, kabsch_noise, trace_rows):
+        lib = N.load()
+        dev = self.device
+        E, T = target_pose.shape[0], target_pose.shape[1]
+        chain = self.robot_model._descriptor(self.ee_link_names, self.ee_link_offsets)
+        D = chain.n_dofs
+        prm = N.CdxKinParams()
+        prm.fe = force_eq_descriptor(T, friction_mu, self.mass, 10.0 if self.gravity else None, 2.0, self.com)
+        for i, v in enumerate(self.ref_q.float().tolist()):
+            prm.ref_q[i] = v
+        f32 = dict(dtype=torch.float32, device=dev)
+        tips = torch.empty(E * T, 3, **f32)
+        loss = torch.empty(E, dtype=torch.float64, device=dev)
+        margin = torch.empty(E, T, dtype=torch.float64, device=dev)
+        normal = torch.empty(E * T, 3, **f32)
+        g_q, g_target, g_comp = torch.empty(E, D, **f32), torch.empty(E, T, 3, **f32), torch.empty(E, T, **f32)
+        offset = self.palm_offset.float()
+        stream = N.stream_ptr(dev)
+        for s in range(self.num_iters):
+            q = joint_angles.detach()
+            if not q.is_contiguous() or q.dtype != torch.float32:
+                raise ValueError("KinGraspOptimizer: joint angles must be a contiguous float32 tensor")
+            N.check(lib.cdx_fk_forward(chain, N.ptr(q), E, N.ptr(tips), None, stream), "cdx_fk_forward")
+            tips.add_(offset)  # FK + palm offset (:148)
+            tgt = target_pose.detach().reshape(-1, 3).contiguous()
+            _, sign1, n1, _, _ = _sdf_query(tips, faces_deflate, False)
+            dist, sign2, n2, clst, _ = _sdf_query(tips, faces, False)
+            tdist, tsign, _, tclst, _ = _sdf_query(tgt, faces, False)
+            nz = _noise(kabsch_noise, s)
+            nz = None if nz is None else nz.detach().to(device=dev, dtype=torch.float64).contiguous()
+            comp = compliance.detach().contiguous()
+            N.check(lib.cdx_kin_cost(chain, prm, E, N.ptr(q), N.ptr(tips), N.ptr(tgt), N.ptr(comp), N.ptr(sign1),
+                                     N.ptr(n1), N.ptr(dist), N.ptr(sign2), N.ptr(n2), N.ptr(clst), N.ptr(tdist),
+                                     N.ptr(tsign), N.ptr(tclst), N.ptr(nz), next(_kin_seeds), N.ptr(loss), N.ptr(margin),
+                                     N.ptr(normal), N.ptr(g_q), N.ptr(g_target), N.ptr(g_comp), stream), "cdx_kin_cost")
+            joint_angles.grad = g_q.clone()
+            compliance.grad = g_comp.clone()
+            if self.optimize_target:
+                target_pose.grad = g_target.clone()
+            self.loss_history.append(loss.sum())  # device scalar, no sync
+            if trace_rows:
+                self.loss_rows.append(loss.clone())
+            if verbose:
+                print("Loss:", float(loss.sum()), compliance)
+            best.update(loss, margin, normal.clone(), q=joint_angles, comp=compliance, target=target_pose)
+            optim.step()
+        if verbose:
+            print(best.margin, best.normal)
+        self.best_loss = best.value
+        return best.params["q"], best.params["comp"], best.params["target"], best.flag()
+
+
+_kin_seeds = __import__("itertools").count(0x6B1)
 
 
 class SDFGraspOptimizer:

@@ -328,6 +328,26 @@ int cdx_force_eq_backward(const cdx_force_eq* p, int64_t B, const double* tip, c
                           const double* g_reward, const double* g_force_norm, double* g_tip,
                           double* g_target, double* g_comp, cdx_stream_t stream);
 
+/* ------------------------------------------------------------ Kin-mode iteration ------
+ * KinGraspOptimizer's per-iteration cost and its backward (optimize_pregrasp.py:183-208) for E
+ * candidates, one lane each, after the iteration's FK (tip = FK(q) + palm offset, float32 [E*T*3]) and
+ * its three TorchSDF queries: tips vs the deflated mesh (sign1, n1), tips vs the mesh (sqdist, sign2,
+ * n2, clst), targets vs the mesh (tsqdist, tsign, tclst; tsign read as [E, T]).  Returns loss [E] and
+ * the force-closure margins [E*T] (f64), the blended normals [E*T*3] (nullable) and the gradients of the
+ * loss w.r.t. q [E*D], target [E*T*3] and compliance [E*T] (float32, the parameters' dtype) — through
+ * force_eq_reward (noise [E*9] = its rand_like draw, or NULL: drawn on device from seed), the TorchSDF
+ * backward and the FK chain (float32, like the reference's autograd). */
+typedef struct {
+  cdx_force_eq fe;            /* force_eq_reward constants (mass, COM, gravity spring, friction) */
+  float ref_q[CDX_MAX_DOFS];  /* ref_cost = 10·|q − ref_q| */
+} cdx_kin_params;
+int cdx_kin_cost(const cdx_chain* chain, const cdx_kin_params* p, int64_t E, const float* q, const float* tip,
+                 const float* target, const float* comp, const int32_t* sign1, const float* n1,
+                 const float* sqdist, const int32_t* sign2, const float* n2, const float* clst,
+                 const float* tsqdist, const int32_t* tsign, const float* tclst, const double* noise,
+                 uint64_t seed, double* loss, double* margin, float* normal, float* g_q, float* g_target,
+                 float* g_comp, cdx_stream_t stream);
+
 /* ------------------------------------------------------------ collision loss -------
  * Replaces ProbabilisticGraspOptimizer.compute_collision_loss (optimize_pregrasp.py:671-701):
  * anchor links by f32 FK (:674-676), palm transform R(euler XYZ)·a + palm_pos (:677-678), then

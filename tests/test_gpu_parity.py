@@ -630,6 +630,56 @@ def test_other_optimisers_vs_reference(name):
     assert bool(out[3]) == bool(d["flag"])
 
 
+def test_kin_optimiser_autograd_path_vs_reference():
+    """KinGraspOptimizer(fused=False): the reference-shaped loop through the autograd drop-ins (the fused
+    cdx_kin_cost loop is test_other_optimisers_vs_reference[mode_kin]) against the same reference run."""
+    name = [n for n in golden_names("mode_") if "kin" in n and "gpis" not in n]
+    assert name
+    d = golden(name[0])
+    o, args = _mode_opt(d)
+    noise = [torch.from_numpy(n).to(DEV) for n in d["noise"]]
+    out = o.optimize(*args, verbose=False, kabsch_noise=noise, fused=False)
+    trace = torch.stack(o.loss_history).cpu().numpy()
+    assert np.abs(trace - d["loss_trace"]).max() <= 1e-4 * np.abs(d["loss_trace"]).max(), (trace, d["loss_trace"])
+    for i in range(3):
+        assert rel_err(out[i].detach().double().cpu(), d[f"out{i}"]) < 1e-4, i
+
+
+def test_kin_optimiser_fused_equals_autograd_at_size():
+    """The fused Kin iteration (FK, three TorchSDF queries, cdx_kin_cost) against the autograd loop on
+    2 048 Allegro candidates around the banana mesh, 8 iterations with the same Kabsch noise: per-iteration
+    per-candidate losses within 1e-4 of the largest (the autograd glue runs in float32 like the reference,
+    the fused kernel in f64; the difference compounds through Adam), NaN candidates identical, final joint
+    angles / compliances / targets 1e-4."""
+    from compliancedex_amd import KinGraspOptimizer, TriangleMesh
+    from compliancedex_amd.urdf import load_robot
+    from compliancedex_amd.workloads import prob_inputs
+    cfg = load_robot("allegro")["config"]
+    E, iters = 2048, 8
+    q, comp, target, _ = prob_inputs(cfg["ref_q"], E, seed=12, spread=True)
+    mesh = TriangleMesh.from_npz(os.path.join(DATA, "meshes", "banana_mesh.npz"))
+    center = np.load(os.path.join(DATA, "banana_center.npy"))
+    g = torch.Generator(device=DEV).manual_seed(5)
+    noise = [torch.rand(E, 3, 3, generator=g, device=DEV, dtype=torch.float64) for _ in range(iters)]
+    res = {}
+    for fused in (True, False):
+        o = KinGraspOptimizer("allegro", cfg["ee_link_name"], cfg["ee_link_offset"],
+                              palm_offset=center.tolist(), num_iters=iters,
+                              optimize_target=True, ref_q=cfg["ref_q"])
+        out = o.optimize(*(torch.from_numpy(np.ascontiguousarray(a)).to(DEV).float() for a in (q, target, comp)),
+                         1, TriangleMesh(mesh.vertices, mesh.triangles), verbose=False, kabsch_noise=noise,
+                         trace_rows=True, fused=fused)
+        res[fused] = ([r.double().cpu().numpy() for r in o.loss_rows], [x.detach().double().cpu().numpy() for x in out[:3]])
+    (ra, oa), (rb, ob) = res[True], res[False]
+    for s, (a, b) in enumerate(zip(ra, rb)):
+        fin = np.isfinite(b)
+        assert np.array_equal(np.isfinite(a), fin), s
+        assert np.abs(a[fin] - b[fin]).max() <= 1e-4 * np.abs(b[fin]).max(), (s, np.abs(a[fin] - b[fin]).max())
+    assert np.isfinite(rb[-1]).sum() > E // 2
+    for x, y in zip(oa, ob):
+        assert rel_err(x, y) < 1e-4
+
+
 def test_optimize_graph_replay_matches_eager():
     """The fused loop keeps its noise key and Adam step in device counters (cdx_loop), so the
     hipGraph-captured loop and the eager loop are the same computation: bit-identical results,
