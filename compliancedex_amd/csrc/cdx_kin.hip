@@ -27,7 +27,7 @@ __device__ __forceinline__ uint64_t kin_mix(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-template <int NT, int MAXD>
+template <int NT, int MAXD, bool FK>
 __global__ __launch_bounds__(64) void kin_cost_kernel(
     cdx_chain chain, cdx_kin_params p, int64_t E, const float* __restrict__ q, const float* __restrict__ tip,
     const float* __restrict__ target, const float* __restrict__ comp, const int32_t* __restrict__ sign1,
@@ -35,11 +35,11 @@ __global__ __launch_bounds__(64) void kin_cost_kernel(
     const float* __restrict__ n2, const float* __restrict__ clst, const float* __restrict__ tsqd,
     const int32_t* __restrict__ tsign, const float* __restrict__ tclst, const double* __restrict__ noise, uint64_t seed,
     double* __restrict__ loss, double* __restrict__ margin, float* __restrict__ normal_out, float* __restrict__ g_q,
-    float* __restrict__ g_target, float* __restrict__ g_comp) {
+    float* __restrict__ g_target, float* __restrict__ g_comp, float* __restrict__ g_tip, int T_rt) {
   constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E) return;
-  const int T = NT > 0 ? NT : chain.n_tips, D = chain.n_dofs;
+  const int T = NT > 0 ? NT : T_rt, D = FK ? chain.n_dofs : 0;
   double tp[NTA][3], tg[NTA * 3], cp[NTA], nr[NTA][3];
   for (int f = 0; f < T; ++f) {
     const int64_t r = e * T + f;
@@ -104,7 +104,9 @@ __global__ __launch_bounds__(64) void kin_cost_kernel(
     v[f] = fn[f] * sm[f];
     fcost += v[f] > 1.0 ? 1.0 : v[f];
   }
-  loss[e] = -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost + qn * 10.0;
+  // Kin mode adds the joint-space ref_cost last (:205); SDF mode (no chain) has none (:218)
+  loss[e] = FK ? -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost + qn * 10.0
+               : -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost;
   for (int f = 0; f < T; ++f) margin[e * T + f] = fe.margin[f];
 
   // ---- backward (dl = 1)
@@ -128,18 +130,23 @@ __global__ __launch_bounds__(64) void kin_cost_kernel(
   }
   for (int f = 0; f < T; ++f) g_fn[f] += -(sm[f] * (g_sm[f] - gsm_dot));
   fe.backward(-5.0, g_fn, cp, gt, gg, gc);
-  float gq[CDX_MAX_DOFS];
-  for (int i = 0; i < D; ++i) {
-    const double d = (double)q[e * D + i] - (double)p.ref_q[i];
-    gq[i] = qn > 0 ? (float)(10.0 * d / qn) : 0.f;
+  if constexpr (FK) {
+    float gq[CDX_MAX_DOFS];
+    for (int i = 0; i < D; ++i) {
+      const double d = (double)q[e * D + i] - (double)p.ref_q[i];
+      gq[i] = qn > 0 ? (float)(10.0 * d / qn) : 0.f;
+    }
+    float fk_g[CDX_MAX_DOFS];
+    for (int i = 0; i < D; ++i) fk_g[i] = 0.f;
+    for (int f = 0; f < T; ++f) {
+      const float gpos[3] = {(float)gt[f][0], (float)gt[f][1], (float)gt[f][2]};
+      cdx::fk_tip_bwd<MAXD>(chain, f, q + e * D, gpos, cdx::GqAdd{fk_g});
+    }
+    for (int i = 0; i < D; ++i) g_q[e * D + i] = gq[i] + fk_g[i];
   }
-  float fk_g[CDX_MAX_DOFS];
-  for (int i = 0; i < D; ++i) fk_g[i] = 0.f;
-  for (int f = 0; f < T; ++f) {
-    const float gpos[3] = {(float)gt[f][0], (float)gt[f][1], (float)gt[f][2]};
-    cdx::fk_tip_bwd<MAXD>(chain, f, q + e * D, gpos, cdx::GqAdd{fk_g});
-  }
-  for (int i = 0; i < D; ++i) g_q[e * D + i] = gq[i] + fk_g[i];
+  if (g_tip)
+    for (int f = 0; f < T; ++f)
+      for (int i = 0; i < 3; ++i) g_tip[(e * T + f) * 3 + i] = (float)gt[f][i];
   for (int f = 0; f < T; ++f) {
     g_comp[e * T + f] = (float)gc[f];
     for (int i = 0; i < 3; ++i) g_target[(e * T + f) * 3 + i] = (float)gg[f][i];
@@ -153,26 +160,31 @@ extern "C" int cdx_kin_cost(const cdx_chain* chain, const cdx_kin_params* p, int
                             const float* sqdist, const int32_t* sign2, const float* n2, const float* clst,
                             const float* tsqdist, const int32_t* tsign, const float* tclst, const double* noise,
                             uint64_t seed, double* loss, double* margin, float* normal, float* g_q, float* g_target,
-                            float* g_comp, cdx_stream_t stream) {
-  if (!chain || !p || chain->n_tips < 1 || chain->n_tips > CDX_MAX_TIPS || chain->n_dofs < 0 ||
-      chain->n_dofs > CDX_MAX_DOFS || chain->n_bodies < 1 || chain->n_bodies > CDX_MAX_BODIES || p->fe.n_tips != chain->n_tips)
+                            float* g_comp, float* g_tip, cdx_stream_t stream) {
+  if (!p || p->fe.n_tips < 1 || p->fe.n_tips > CDX_MAX_TIPS) return CDX_EINVAL;
+  if (chain && (chain->n_tips != p->fe.n_tips || chain->n_dofs < 0 || chain->n_dofs > CDX_MAX_DOFS ||
+                chain->n_bodies < 1 || chain->n_bodies > CDX_MAX_BODIES))
     return CDX_EINVAL;
   if (E < 0) return CDX_EINVAL;
   if (E == 0) return CDX_OK;
-  if (!q || !tip || !target || !comp || !sign1 || !n1 || !sqdist || !sign2 || !n2 || !clst || !tsqdist || !tsign ||
-      !tclst || !loss || !margin || !g_q || !g_target || !g_comp)
+  if (!tip || !target || !comp || !sign1 || !n1 || !sqdist || !sign2 || !n2 || !clst || !tsqdist || !tsign || !tclst ||
+      !loss || !margin || !g_target || !g_comp || (chain && (!q || !g_q)) || (!chain && !g_tip))
     return CDX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)((E + 63) / 64));
-  const bool shallow = cdx::chain_max_depth(*chain) <= 8;
-#define CDX_KIN_LAUNCH(NT, MAXD)                                                                                      \
-  hipLaunchKernelGGL((kin_cost_kernel<NT, MAXD>), grid, dim3(64), 0, s, *chain, *p, E, q, tip, target, comp, sign1, n1, \
+  const int T = p->fe.n_tips;
+  const cdx_chain c = chain ? *chain : cdx_chain{};
+  const bool shallow = !chain || cdx::chain_max_depth(*chain) <= 8;
+#define CDX_KIN_LAUNCH(NT, MAXD, FK)                                                                                  \
+  hipLaunchKernelGGL((kin_cost_kernel<NT, MAXD, FK>), grid, dim3(64), 0, s, c, *p, E, q, tip, target, comp, sign1, n1, \
                      sqdist, sign2, n2, clst, tsqdist, tsign, tclst, noise, seed, loss, margin, normal, g_q, g_target,    \
-                     g_comp)
-  if (chain->n_tips == 4 && shallow) CDX_KIN_LAUNCH(4, 8);
-  else if (chain->n_tips == 4) CDX_KIN_LAUNCH(4, CDX_MAX_DEPTH);
-  else if (shallow) CDX_KIN_LAUNCH(0, 8);
-  else CDX_KIN_LAUNCH(0, CDX_MAX_DEPTH);
+                     g_comp, g_tip, T)
+  if (!chain && T == 4) CDX_KIN_LAUNCH(4, 8, false);
+  else if (!chain) CDX_KIN_LAUNCH(0, 8, false);
+  else if (T == 4 && shallow) CDX_KIN_LAUNCH(4, 8, true);
+  else if (T == 4) CDX_KIN_LAUNCH(4, CDX_MAX_DEPTH, true);
+  else if (shallow) CDX_KIN_LAUNCH(0, 8, true);
+  else CDX_KIN_LAUNCH(0, CDX_MAX_DEPTH, true);
 #undef CDX_KIN_LAUNCH
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }

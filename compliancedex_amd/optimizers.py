@@ -217,7 +217,8 @@ class KinGraspOptimizer:
             N.check(lib.cdx_kin_cost(chain, prm, E, N.ptr(q), N.ptr(tips), N.ptr(tgt), N.ptr(comp), N.ptr(sign1),
                                      N.ptr(n1), N.ptr(dist), N.ptr(sign2), N.ptr(n2), N.ptr(clst), N.ptr(tdist),
                                      N.ptr(tsign), N.ptr(tclst), N.ptr(nz), next(_kin_seeds), N.ptr(loss), N.ptr(margin),
-                                     N.ptr(normal), N.ptr(g_q), N.ptr(g_target), N.ptr(g_comp), stream), "cdx_kin_cost")
+                                     N.ptr(normal), N.ptr(g_q), N.ptr(g_target), N.ptr(g_comp), None, stream),
+                    "cdx_kin_cost")
             joint_angles.grad = g_q.clone()
             compliance.grad = g_comp.clone()
             if self.optimize_target:
@@ -251,8 +252,10 @@ class SDFGraspOptimizer:
         self.mass, self.com, self.gravity = mass, list(com), gravity
 
     def optimize(self, tip_pose, target_pose, compliance, friction_mu, object_mesh, verbose=True, kabsch_noise=None,
-                 trace_rows=False):
-        """``trace_rows``: also keep every iteration's per-candidate loss in ``loss_rows`` (device)."""
+                 trace_rows=False, fused=True):
+        """``trace_rows``: also keep every iteration's per-candidate loss in ``loss_rows`` (device).
+        ``fused`` (default): per iteration the three TorchSDF queries on cached prepared meshes and ONE
+        cost-and-backward kernel (cdx_kin_cost without a chain); ``fused=False``: the autograd loop."""
         tip_pose = tip_pose.clone().requires_grad_(True)
         self.loss_history = []
         self.loss_rows = []
@@ -268,6 +271,9 @@ class SDFGraspOptimizer:
             optim = torch.optim.RMSprop([{"params": tip_pose, "lr": 1e-3}, {"params": compliance, "lr": 0.2}])
         E, T = tip_pose.shape[0], tip_pose.shape[1]
         best = _Best(torch.float32, E, T, self.device, tip=tip_pose, comp=compliance, target=target_pose)
+        if fused:
+            return self._optimize_fused(tip_pose, target_pose, compliance, friction_mu, faces, faces_deflate, optim,
+                                        best, verbose, kabsch_noise, trace_rows)
         for s in range(self.num_iters):
             optim.zero_grad()
             all_tip = tip_pose.view(-1, 3)
@@ -288,6 +294,54 @@ class SDFGraspOptimizer:
             if verbose:
                 print("Loss:", float(l.sum()), float(dist_cost.sum()), float(tar_dist_cost.sum()))
             best.update(l, margin, normal, tip=tip_pose, comp=compliance, target=target_pose)
+            optim.step()
+            with torch.no_grad():  # bounding-box constraints (:312-314)
+                tip_pose.clamp_(min=self.tip_bounding_box[0], max=self.tip_bounding_box[1])
+                target_pose.clamp_(min=self.tip_bounding_box[0], max=self.tip_bounding_box[1])
+        if verbose:
+            print(best.margin, best.normal)
+        self.best_loss = best.value
+        return best.params["tip"], best.params["comp"], best.params["target"], best.flag()
+
+    def _optimize_fused(self, tip_pose, target_pose, compliance, friction_mu, faces, faces_deflate, optim, best,
+                        verbose, kabsch_noise, trace_rows):
+        lib = N.load()
+        dev = self.device
+        E, T = tip_pose.shape[0], tip_pose.shape[1]
+        prm = N.CdxKinParams()
+        prm.fe = force_eq_descriptor(T, friction_mu, self.mass, 10.0 if self.gravity else None, 2.0, self.com)
+        f32 = dict(dtype=torch.float32, device=dev)
+        loss = torch.empty(E, dtype=torch.float64, device=dev)
+        margin = torch.empty(E, T, dtype=torch.float64, device=dev)
+        normal = torch.empty(E * T, 3, **f32)
+        g_tip, g_target, g_comp = torch.empty(E, T, 3, **f32), torch.empty(E, T, 3, **f32), torch.empty(E, T, **f32)
+        stream = N.stream_ptr(dev)
+        for s in range(self.num_iters):
+            tips = tip_pose.detach().reshape(-1, 3).contiguous()
+            tgt = target_pose.detach().reshape(-1, 3).contiguous()
+            if tips.dtype != torch.float32 or tgt.dtype != torch.float32:
+                raise ValueError("SDFGraspOptimizer: tip and target poses must be float32 (TorchSDF's path)")
+            _, sign1, n1, _, _ = _sdf_query(tips, faces_deflate, False)
+            dist, sign2, n2, clst, _ = _sdf_query(tips, faces, False)
+            tdist, tsign, _, tclst, _ = _sdf_query(tgt, faces, False)
+            nz = _noise(kabsch_noise, s)
+            nz = None if nz is None else nz.detach().to(device=dev, dtype=torch.float64).contiguous()
+            comp = compliance.detach().contiguous()
+            N.check(lib.cdx_kin_cost(None, prm, E, None, N.ptr(tips), N.ptr(tgt), N.ptr(comp), N.ptr(sign1), N.ptr(n1),
+                                     N.ptr(dist), N.ptr(sign2), N.ptr(n2), N.ptr(clst), N.ptr(tdist), N.ptr(tsign),
+                                     N.ptr(tclst), N.ptr(nz), next(_kin_seeds), N.ptr(loss), N.ptr(margin),
+                                     N.ptr(normal), None, N.ptr(g_target), N.ptr(g_comp), N.ptr(g_tip), stream),
+                    "cdx_kin_cost")
+            tip_pose.grad = g_tip.clone()
+            compliance.grad = g_comp.clone()
+            if self.optimize_target:
+                target_pose.grad = g_target.clone()
+            self.loss_history.append(loss.sum())  # device scalar, no sync
+            if trace_rows:
+                self.loss_rows.append(loss.clone())
+            if verbose:
+                print("Loss:", float(loss.sum()))
+            best.update(loss, margin, normal.clone(), tip=tip_pose, comp=compliance, target=target_pose)
             optim.step()
             with torch.no_grad():  # bounding-box constraints (:312-314)
                 tip_pose.clamp_(min=self.tip_bounding_box[0], max=self.tip_bounding_box[1])

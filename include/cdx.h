@@ -336,7 +336,9 @@ int cdx_force_eq_backward(const cdx_force_eq* p, int64_t B, const double* tip, c
  * the force-closure margins [E*T] (f64), the blended normals [E*T*3] (nullable) and the gradients of the
  * loss w.r.t. q [E*D], target [E*T*3] and compliance [E*T] (float32, the parameters' dtype) — through
  * force_eq_reward (noise [E*9] = its rand_like draw, or NULL: drawn on device from seed), the TorchSDF
- * backward and the FK chain (float32, like the reference's autograd). */
+ * backward and the FK chain (float32, like the reference's autograd).  g_tip [E*T*3] (nullable) receives
+ * the gradient w.r.t. the fingertips.  chain NULL: SDFGraspOptimizer's iteration (:229-320) — the tips are
+ * the parameters, no ref_cost, no FK backward (q, g_q unused; g_tip required). */
 typedef struct {
   cdx_force_eq fe;            /* force_eq_reward constants (mass, COM, gravity spring, friction) */
   float ref_q[CDX_MAX_DOFS];  /* ref_cost = 10·|q − ref_q| */
@@ -346,7 +348,7 @@ int cdx_kin_cost(const cdx_chain* chain, const cdx_kin_params* p, int64_t E, con
                  const float* sqdist, const int32_t* sign2, const float* n2, const float* clst,
                  const float* tsqdist, const int32_t* tsign, const float* tclst, const double* noise,
                  uint64_t seed, double* loss, double* margin, float* normal, float* g_q, float* g_target,
-                 float* g_comp, cdx_stream_t stream);
+                 float* g_comp, float* g_tip, cdx_stream_t stream);
 
 /* ------------------------------------------------------------ collision loss -------
  * Replaces ProbabilisticGraspOptimizer.compute_collision_loss (optimize_pregrasp.py:671-701):

@@ -630,10 +630,12 @@ def test_other_optimisers_vs_reference(name):
     assert bool(out[3]) == bool(d["flag"])
 
 
-def test_kin_optimiser_autograd_path_vs_reference():
-    """KinGraspOptimizer(fused=False): the reference-shaped loop through the autograd drop-ins (the fused
-    cdx_kin_cost loop is test_other_optimisers_vs_reference[mode_kin]) against the same reference run."""
-    name = [n for n in golden_names("mode_") if "kin" in n and "gpis" not in n]
+@pytest.mark.parametrize("mode", ["kin", "sdf"])
+def test_sdf_optimisers_autograd_path_vs_reference(mode):
+    """Kin/SDFGraspOptimizer(fused=False): the reference-shaped loop through the autograd drop-ins (the fused
+    cdx_kin_cost loop is test_other_optimisers_vs_reference[mode_kin / mode_sdf]) against the same reference
+    run."""
+    name = [n for n in golden_names("mode_") if n.startswith(f"mode_{mode}")]
     assert name
     d = golden(name[0])
     o, args = _mode_opt(d)
