@@ -635,9 +635,7 @@ def test_sdf_optimisers_autograd_path_vs_reference(mode):
     """Kin/SDFGraspOptimizer(fused=False): the reference-shaped loop through the autograd drop-ins (the fused
     cdx_kin_cost loop is test_other_optimisers_vs_reference[mode_kin / mode_sdf]) against the same reference
     run."""
-    name = [n for n in golden_names("mode_") if n.startswith(f"mode_{mode}")]
-    assert name
-    d = golden(name[0])
+    d = golden(f"mode_{mode}.npz")
     o, args = _mode_opt(d)
     noise = [torch.from_numpy(n).to(DEV) for n in d["noise"]]
     out = o.optimize(*args, verbose=False, kabsch_noise=noise, fused=False)
