@@ -197,16 +197,21 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # per-step stream times (the clock ramp): one event between steps on the closure's stream
-    # (CDX_BENCH_STEP_EVENTS=0 drops them for an A/B of their cost)
-    step_events = os.environ.get("CDX_BENCH_STEP_EVENTS", "1") != "0"
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if step_events else []
+    # per-step stream times of the first and last 5 timed steps (the clock ramp): events between those
+    # steps on the closure's stream — each record costs ≈ 8 µs of stream time (profiles/r04b_ab_*: 1.058
+    # vs 1.050 ms per step with one between every step), so only the 12 boundaries are marked
+    # (CDX_BENCH_STEP_EVENTS=0 drops them, =all marks every step)
+    mode = os.environ.get("CDX_BENCH_STEP_EVENTS", "1")
+    K = args.steps
+    marks = set() if mode == "0" else (set(range(K + 1)) if mode == "all" else
+                                        set(range(min(6, K + 1))) | set(range(max(0, K - 5), K + 1)))
+    evs = {i: torch.cuda.Event(enable_timing=True) for i in marks}
     t0 = time.perf_counter()
-    if evs:
+    if 0 in evs:
         evs[0].record()
     for i in range(args.steps):
         step()
-        if evs:
+        if i + 1 in evs:
             evs[i + 1].record()
     # the exchange is queued right behind the last step (no host sync in between, as an optimise loop
     # would run it); its time is the stream time from the last step's end to the exchange's end
@@ -252,7 +257,7 @@ def main():
         elapsed, gather_s = float(t[0]), float(t[1])
     nan_candidates = int((~torch.isfinite(opt.total_loss)).sum())
 
-    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)] if evs else []
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(K) if i in evs and i + 1 in evs]
     ms_per_step = 1e3 * elapsed / args.steps
     value = E * world / (elapsed / args.steps)
     stage_names = ["queries", "gpis_mean", "gpis_std_var", "cost_bwd", "gpis_std_grad", "gpis_screen"]
@@ -305,8 +310,9 @@ def main():
                                  "(informational)"},
             "step_ms": ({"min": min(step_ms), "median": statistics.median(step_ms), "max": max(step_ms),
                          "first5_mean": statistics.fmean(step_ms[:5]), "last5_mean": statistics.fmean(step_ms[-5:]),
-                         "note": "rank 0's stream time per timed step (HIP events between steps): the clock ramp "
-                                 "shows as first5_mean > last5_mean"} if step_ms else None),
+                         "steps_marked": len(step_ms),
+                         "note": "rank 0's stream time of the first and last 5 timed steps (HIP events between "
+                                 "them): the clock ramp shows as first5_mean > last5_mean"} if step_ms else None),
             "native": N.build_info(),
             "stage_ms": stage_ms,
             "stage_ms_note": "gpis_std_var (the refine kernel, the headline roofline): HIP events over "

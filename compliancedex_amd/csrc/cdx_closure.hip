@@ -729,7 +729,7 @@ bool side_stream(SideStream& out) {
     ss.gate = ev[2];
     ss.joinB = ev[3];
   }
-  if (mean_sched() == 2 && !ss.s2) {
+  if (mean_sched() >= 2 && !ss.s2) {
     // CDX_SIDEB_PRIO: the mean chunks' stream priority (0 normal, default: the merge's workgroups are
     // dispatched first and the mean fills the CUs around them; > 0 highest, < 0 lowest)
     const char* pe = getenv("CDX_SIDEB_PRIO");
@@ -1045,7 +1045,11 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     // for it).  Phase 2 right after the refine kernel (g2 recorded between it and the merge): B the
     // remaining all-tip / target rows, e2a, the pregrasp / palm rows; A waits e2a, runs the level kernel and
     // records join; B waits join and records jb, which the main stream waits for before the combine.
-    const bool sched2 = fork && kabsch_mode() == 1 && vlate && !mean_split() && mean_sched() == 2 && ss.s2;
+    const bool sched2 = fork && kabsch_mode() == 1 && vlate && !mean_split() && mean_sched() >= 2 && ss.s2;
+    // 3: the ∇std pass waits for both side streams (mean chunks, level kernel) instead of the combine, so
+    // that no mean / level workgroup holds a CU the pass needs
+    const bool wait_before_grad = sched2 && mean_sched() == 3;
+    bool joined_early = false;
     const int64_t M01 = (int64_t)(p->n_query_levels + 1) * E * T;  // all-tip + target rows (the level kernel's)
     const int64_t M1 = sched2 ? std::min<int64_t>(Mq, (int64_t)(mean_chunk1() * (double)Mq)) : 0;
     bool forked2 = false;
@@ -1127,6 +1131,10 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
         rc = cdx::repair_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.std_, w.var, w.sel, w.Xg, w.vrow, w.stats, s);
       if (rc) return joined(rc);
     }
+    if (wait_before_grad) {
+      if (hipStreamWaitEvent(s, ss.jb, 0) != hipSuccess) return joined(CDX_ELAUNCH);
+      joined_early = true;
+    }
     rc = cdx::gpis_grad_launch(p->gpis, w.Xg, Mg, w.sel, w.var, w.gstd, w.grad_ws, s, w.V, w.vrow,
                                grad_fold() ? &fold : nullptr);
     if (!rc && inject_fail(3)) rc = CDX_ELAUNCH;
@@ -1134,7 +1142,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     if (fork && !sched2 && (rc = launch_b())) return joined(rc);
     // mean A (and the Kabsch records of mode 1) before the level kernel; mean B is joined before the
     // combine kernel below (sched2: jb follows both side streams)
-    if (forked && hipStreamWaitEvent(s, sched2 ? ss.jb : ss.join, 0) != hipSuccess) {
+    if (forked && !joined_early && hipStreamWaitEvent(s, sched2 ? ss.jb : ss.join, 0) != hipSuccess) {
       forked = forked2 = false;
       return joined(CDX_ELAUNCH);
     }
