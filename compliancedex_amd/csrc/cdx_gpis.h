@@ -46,6 +46,21 @@ CDX_HD double sqrt_r2_gen(double x) {
 #endif
 }
 
+// sqrt(x) from an f32 reciprocal-root seed and one f64 Newton step (relative error ≈ 2⁻⁴⁵, 1e-14; against
+// ≤ 1 ulp for sqrt_r2_gen): the f32 transcendental and the two conversions replace v_rsq_f64 and the
+// Goldschmidt refinement — the GPIS mean's per-pair root (CDX_MEAN_RSQ32 builds).
+CDX_HD double sqrt_r2_f32seed(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float xf = fmaxf((float)x, 1e-30f);
+  const double y = (double)__builtin_amdgcn_rsqf(xf);
+  const double g = x * y, h = 0.5 * y;
+  const double d = fma(-g, g, x);
+  return fma(d, h, g);
+#else
+  return sqrt(x);
+#endif
+}
+
 template <int KT, bool GENSQRT = false>
 CDX_HD void gpis_k(double r2, double R, double inv_s2, double& k, double& kd) {
   if (KT == CDX_KERNEL_TPS) {

@@ -88,7 +88,9 @@ __device__ __forceinline__ void mean_tps_moments(const cdx_gpis& g, int64_t M, i
       const dbl4 p = sp[jj];
       const double dx = x0 - p.x, dy = x1 - p.y, dz = x2 - p.z;
       const double r2 = dx * dx + dy * dy + dz * dz;
-#ifndef CDX_MEAN_FULLSQRT  // the root without its final Newton correction (≤ 1 ulp), as the K* generation
+#if defined(CDX_MEAN_RSQ32)  // A/B: f32 seed + one f64 Newton step (≈ 1e-14 relative)
+      const double ar = p.w * cdx::sqrt_r2_f32seed(r2);
+#elif !defined(CDX_MEAN_FULLSQRT)  // the root without its final Newton correction (≤ 1 ulp), as the K* generation
       const double ar = p.w * cdx::sqrt_r2_gen(r2);
 #else
       const double ar = p.w * cdx::sqrt_r2(r2);
