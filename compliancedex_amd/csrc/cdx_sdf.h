@@ -119,10 +119,12 @@ CDX_HD float point_face_d(D3 p, D3 v1, D3 v2, D3 v3, D3& clst, D3& nrm, int& sgn
 // Per-face quantities of point_face, computed once per face with the SAME IEEE operations
 // (FP contraction off), so face_dist2 below returns bit-for-bit the squared distance
 // point_face returns.  40 floats: one s_load_dwordx8 ×5 per face on the device.
+// The padding words hold the face's own bounding sphere (centre bx..bz = the vertices' mean, radius br, |centre|
+// bn) for the culled kernel's per-face bound (the same bound as a chunk's sphere, face by face).
 struct FaceRec {
   F3 v1; int idx;  F3 v2; float den12;  F3 v3; float den23;  F3 e12; float den31;
-  F3 e23; float _p0;  F3 e31; float _p1;  F3 ne12; float _p2;  F3 ne23; float _p3;
-  F3 ne31; float _p4;  F3 un; float kappa;   // kappa = |e12||e31| / |n| (conditioning, 1/sinθ)
+  F3 e23; float bx;  F3 e31; float by;  F3 ne12; float bz;  F3 ne23; float br;
+  F3 ne31; float bn;  F3 un; float kappa;   // kappa = |e12||e31| / |n| (conditioning, 1/sinθ)
 };
 
 CDX_HD FaceRec face_rec(F3 v1, F3 v2, F3 v3, int idx) {
@@ -135,7 +137,14 @@ CDX_HD FaceRec face_rec(F3 v1, F3 v2, F3 v3, int idx) {
   const float nn = dotf(normal, normal);
   r.un = scl(normal, rsqrt_cr(nn));
   r.kappa = sqrtf(r.den12) * sqrtf(r.den31) / sqrtf(nn);
-  r._p0 = r._p1 = r._p2 = r._p3 = r._p4 = 0.f;
+  const float third = 1.f / 3.f;
+  r.bx = (v1.x + v2.x + v3.x) * third;
+  r.by = (v1.y + v2.y + v3.y) * third;
+  r.bz = (v1.z + v2.z + v3.z) * third;
+  const F3 c = f3(r.bx, r.by, r.bz);
+  r.br = fmaxf(fmaxf(sqrtf(dotf(sub(v1, c), sub(v1, c))), sqrtf(dotf(sub(v2, c), sub(v2, c)))),
+               sqrtf(dotf(sub(v3, c), sub(v3, c)))) * (1.f + 1e-5f);
+  r.bn = sqrtf(r.bx * r.bx + r.by * r.by + r.bz * r.bz);
   return r;
 }
 

@@ -37,8 +37,8 @@ constexpr float PT_LIM = 1e4f;      // |p| bound of the culled path (face_may_na
 
 struct Sphere { float cx, cy, cz, r, alpha, cnorm, _p0, _p1; };
 
-// Diagnostic counters (cdx_sdf_stats): [0] (point, face) pairs the culled kernel evaluated — faces of
-// every chunk a wave evaluates × its live lanes —, [1] pairs of the brute-force scans (exact path),
+// Diagnostic counters (cdx_sdf_stats): [0] (point, face) pairs the culled kernel evaluated — faces a wave
+// evaluates exactly (its chunk not ruled out, the face itself not ruled out for every lane) × its live lanes —, [1] pairs of the brute-force scans (exact path),
 // [2] points queried.  Counted only while enabled (one atomic per wave).
 __device__ unsigned long long g_sdf_stats[3];
 bool g_sdf_count = false;
@@ -264,9 +264,20 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled_kernel(
     if (!__any(need)) continue;
     const int f0 = c * CHUNK;
     const int nf = (int)min((int64_t)CHUNK, F - f0);
-    evaluated += nf;
     for (int k = 0; k < nf; ++k) {
       const cdx::FaceRec& r = rec[f0 + k];
+#if !defined(CDX_SDF_NO_FACEBOUND)
+      // The chunk test again, on the face's own sphere (FaceRec bx..bn, the chunk's conditioning margin
+      // alpha): a face every lane of the wave rules out is never evaluated — its computed distance is
+      // strictly above the lane's best, so it could neither win nor tie (the argument of the chunk bound).
+      {
+        const float fx = p.x - r.bx, fy = p.y - r.by, fz = p.z - r.bz;
+        const float fd = sqrtf(fx * fx + fy * fy + fz * fz);
+        const float Lf = fd * (1.f - s.alpha) - r.br * (1.f + s.alpha) - 1e-4f * (pnorm + r.bn + r.br);
+        if (!__any(!(Lf > 0.f && Lf * Lf > best))) continue;
+      }
+#endif
+      ++evaluated;
       const float d = cdx::face_dist2(p, r);
       if (d < best || (d == best && r.idx < bidx)) { best = d; bidx = r.idx; }
     }
