@@ -270,6 +270,41 @@ __device__ __forceinline__ void v_store(T* p, T v) {
   *p = v;
 #endif
 }
+// A wave's 64×64 sub-tile of V (acc[i][j][r] = D[row (l>>4) + 4r][col (l&15) + 16j] in block (i, j)) to
+// row-major dst (leading dimension ld, even column offset): with CDX_VSTORE_X4 the lane pairs (l, l^1)
+// trade one value per two rows (two xor-1 shuffles) so each stores two adjacent columns of two rows as
+// 16-byte stores — half the store instructions of the plain 8-byte-per-lane form, same bytes and values.
+template <class ACC>
+__device__ __forceinline__ void store_v_tile(double* dst, int64_t ld, const ACC& acc, int lane) {
+#if defined(CDX_VSTORE_X4)
+  const bool even = (lane & 1) == 0;
+  const int c0 = (lane & 15) & ~1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double a0 = acc[i][j][0], a1 = acc[i][j][1], a2 = acc[i][j][2], a3 = acc[i][j][3];
+      const double x0 = __shfl_xor(even ? a1 : a0, 1), x1 = __shfl_xor(even ? a3 : a2, 1);
+      // even lane: rows r = 0, 2 (own value, partner's); odd lane: rows r = 1, 3 (partner's, own value)
+      const int ra = even ? 0 : 1, rb = even ? 2 : 3;
+      const double2 va = even ? make_double2(a0, x0) : make_double2(x0, a1);
+      const double2 vb = even ? make_double2(a2, x1) : make_double2(x1, a3);
+      double* base = dst + (int64_t)(16 * i + (lane >> 4)) * ld + 16 * j + c0;
+      v_store(reinterpret_cast<double2*>(base + (int64_t)(4 * ra) * ld), va);
+      v_store(reinterpret_cast<double2*>(base + (int64_t)(4 * rb) * ld), vb);
+    }
+#else
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double* vr = dst + (int64_t)(16 * i + (lane >> 4) + 4 * r) * ld + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v_store(vr + 16 * j, acc[i][j][r]);
+    }
+#endif
+}
+
 template <class T>
 __device__ __forceinline__ T v_load(const T* p) {
 #if defined(CDX_NT_VLOAD)
@@ -764,14 +799,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
     double* red = smem;  // [ST_WN][ST_BM]
     if (LIST && !full) {  // a cut stripe: this segment's partial V tile to its slot
 #if !defined(CDX_DIAG_NOVSTORE)  // timing-only diagnostic build (outputs wrong): no V / partial-tile stores
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          double* vr = rl.slots + ((int64_t)pslot * ST_BM + wr + 16 * i + (lane >> 4) + 4 * r) * ST_BN + wc + (lane & 15);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v_store(vr + 16 * j, acc[i][j][r]);
-        }
+      store_v_tile(rl.slots + ((int64_t)pslot * ST_BM + wr) * ST_BN + wc, ST_BN, acc, lane);
 #endif
       return;
     }
@@ -792,14 +820,7 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
 #else
     if (vout) {
 #endif
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          double* vr = vout + (m0 + wr + 16 * i + (lane >> 4) + 4 * r) * (int64_t)Np + n0 + wc + (lane & 15);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v_store(vr + 16 * j, acc[i][j][r]);
-        }
+      store_v_tile(vout + (m0 + wr) * (int64_t)Np + n0 + wc, Np, acc, lane);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
