@@ -132,6 +132,7 @@ _SIGS = {
     "cdx_sdf_forward_f64": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "cdx_sdf_backward_f64": (C.c_int, [_P, _P, _P, _I64, _P, _P]),
     "cdx_sdf_stats": (C.c_int, [C.c_int32, C.POINTER(C.c_uint64), _P]),
+    "cdx_sdf_chunk_visits": (C.c_int, [C.POINTER(C.c_uint64), _P]),
     "cdx_kin_cost": (C.c_int, [C.POINTER(CdxChain), C.POINTER(CdxKinParams), _I64] + [_P] * 14 + [C.c_uint64] +
                      [_P] * 8),
     "cdx_sdf_mesh_bytes": (C.c_size_t, [_I64]),

@@ -40,7 +40,7 @@ def _deps():
 
 
 # Tuning switches compiled into the product library.
-DEFAULT_DEFINES = ("CDX_FAST_SQRT", "CDX_STD_SCHED")
+DEFAULT_DEFINES = ("CDX_FAST_SQRT", "CDX_STD_SCHED", "CDX_MEAN_RSQ32")
 
 
 def source_digest(defines=DEFAULT_DEFINES):

@@ -31,8 +31,11 @@ CDX_HD double sqrt_r2(double x) {
 
 // sqrt_r2 without its final Newton correction (≤ 1 ulp from the rounded root): the whitened
 // pass's on-chip K* generation (CDX_GEN_SQRT_FULL keeps the full sequence there).
+CDX_HD double sqrt_r2_f32seed(double x);
 CDX_HD double sqrt_r2_gen(double x) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(CDX_FAST_SQRT) && !defined(CDX_GEN_SQRT_FULL)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(CDX_GEN_RSQ32)  // A/B: the f32-seeded root (≈ 2⁻⁴⁵) in K* too
+  return sqrt_r2_f32seed(x);
+#elif defined(__HIP_DEVICE_COMPILE__) && defined(CDX_FAST_SQRT) && !defined(CDX_GEN_SQRT_FULL)
   x = fmax(x, 1e-200);
   const double y = __builtin_amdgcn_rsq(x);
   double g = x * y, h = 0.5 * y;

@@ -55,7 +55,12 @@ static_assert(MEAN_BLOCK == 256, "the mean kernel's moment reduction assumes 4 w
 // (p̃ = x_n − c, x̃ = x − c, c = the first inducing point, so both stay at the object's scale):
 //   Σ α r² = |x̃|² S0 − 2 x̃·S1 + S2,   Σ α (x − x_n) = x̃ S0 − S1.
 // Per pair only r, αr, Σ (αr) r² and Σ (αr) d remain: 17 f64 ops + v_rsq against 23 + v_rsq (r
-// without the root's final Newton correction, ≤ 1 ulp, as the whitened pass's K* generation).
+// without the root's final Newton correction, ≤ 1 ulp, as the whitened pass's K* generation).  The product
+// build (CDX_MEAN_RSQ32) seeds the root in f32 and takes one f64 Newton step (2⁻⁴⁵ relative, 3 DP ops fewer
+// per pair): the mean is DP-issue-bound beside the refine pass, and the closure runs ≈ 10 µs faster (4
+// interleaved A/Bs, profiles/r04cde_ab_*.jsonl, r04g_ab_roots.jsonl) while the mean moves by ≤ 6e-13 relative —
+// below its own distance from the reference's f64 autograd (1.3e-12 on the banana state, 2.3e-13 on the
+// synthetic one; tools/root_precision.py, profiles/r04g_root_precision.jsonl).
 // The moments are summed by the staging threads (one point each per block), then over the workgroup.
 __device__ __forceinline__ void mean_tps_moments(const cdx_gpis& g, int64_t M, int64_t m, double x0, double x1,
                                                  double x2, double* __restrict__ mean, double* __restrict__ gmean,
@@ -88,7 +93,7 @@ __device__ __forceinline__ void mean_tps_moments(const cdx_gpis& g, int64_t M, i
       const dbl4 p = sp[jj];
       const double dx = x0 - p.x, dy = x1 - p.y, dz = x2 - p.z;
       const double r2 = dx * dx + dy * dy + dz * dz;
-#if defined(CDX_MEAN_RSQ32)  // A/B: f32 seed + one f64 Newton step (≈ 1e-14 relative)
+#if defined(CDX_MEAN_RSQ32)  // (product build) f32 seed + one f64 Newton step (≈ 2⁻⁴⁵ relative), see below
       const double ar = p.w * cdx::sqrt_r2_f32seed(r2);
 #elif !defined(CDX_MEAN_FULLSQRT)  // the root without its final Newton correction (≤ 1 ulp), as the K* generation
       const double ar = p.w * cdx::sqrt_r2_gen(r2);

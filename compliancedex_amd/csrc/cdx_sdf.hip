@@ -40,7 +40,8 @@ struct Sphere { float cx, cy, cz, r, alpha, cnorm, _p0, _p1; };
 // Diagnostic counters (cdx_sdf_stats): [0] (point, face) pairs the culled kernel evaluated — faces a wave
 // evaluates exactly (its chunk not ruled out, the face itself not ruled out for every lane) × its live lanes —, [1] pairs of the brute-force scans (exact path),
 // [2] points queried.  Counted only while enabled (one atomic per wave).
-__device__ unsigned long long g_sdf_stats[3];
+// [3]: chunks the culled kernel visited (a wave fetched and bound-tested their faces), summed over waves.
+__device__ unsigned long long g_sdf_stats[4];
 bool g_sdf_count = false;
 
 __device__ inline unsigned fkey(float f) {
@@ -311,6 +312,251 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled_kernel(
   if (out_face) out_face[pi] = bidx;
 }
 
+// The culled kernel, staged through LDS (default; CDX_SDF_V1 builds sdf_culled_kernel above for the A/B).
+// Same bounds, same winner rule, same outputs — only where the data comes from and how the per-face tests
+// are ordered differ:
+//   * the chunk spheres of a block of SPH_BLK chunks sit in LDS (one cooperative load per block, instead
+//     of one dependent scalar load per chunk and pass);
+//   * a chunk some lane cannot rule out is fetched whole into the wave's LDS buffer with 5 vector loads per
+//     lane (one round trip instead of one scalar load per face), and the next such chunk's loads are
+//     issued before the current one is processed;
+//   * its 32 per-face bounds are tested first, branch-free, into a bit mask against the lanes' best at the
+//     chunk's start (sqrt-free: fd² against the squared threshold — the 1e-4 margins dwarf the few ulps
+//     the rearrangement moves), then only the faces of the mask are evaluated.
+// A skipped face is one whose bound lies above every lane's best at the time of the test, and a lane's
+// best only decreases: the chunk argument of sdf_culled_kernel, unchanged.
+constexpr int SPH_BLK = 512;                   // chunk spheres per LDS block (12 KB)
+constexpr int REC_WORDS = sizeof(cdx::FaceRec) / 4;  // 40
+static_assert(REC_WORDS * CHUNK % (64 * 4) == 0, "a chunk's records load as whole dwordx4 per lane");
+constexpr int REC_V4 = REC_WORDS * CHUNK / (64 * 4);   // dwordx4 loads per lane per chunk (5)
+
+#ifndef CDX_SDF_SPLIT
+#define CDX_SDF_SPLIT 4
+#endif
+constexpr int SDF_SPLIT = CDX_SDF_SPLIT;  // workgroups per 64-point group (chunk slices)
+
+// (distance, face) as one unsigned 64-bit word whose order is the winner rule's: a non-negative float's
+// bits order as unsigned integers, ties then go to the smaller index.
+__device__ inline unsigned long long pack_best(float d, int idx) {
+  return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)idx;
+}
+
+// Workgroup (g, k) of a split launch: the 64 Morton-sorted points of group g against chunk slice k (wave w
+// takes chunks c ≡ 4k + w mod 4·SPLIT), its per-point winner merged into best[pi] with a 64-bit atomic
+// minimum; sdf_culled_finalize_kernel then writes the outputs.  Splitting a point group over SPLIT
+// workgroups shortens its critical path — one group near no face (a point deep inside or far outside)
+// otherwise holds its CU while the others idle (PMC: mean wave life ≈ 1/3 of the kernel) — and gives the
+// dispatcher SPLIT× more, shorter workgroups to balance.  Each workgroup first takes the upper bound over
+// ALL chunks (pass 1) and the faces of the chunk nearest the group's middle point (the seed, shared over
+// its waves), so every slice starts with a best near the true distance; a face is still skipped only when
+// its bound lies above the lane's best (which only decreases), so the global lexicographic minimum over the
+// evaluated faces is the brute-force winner.
+__global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
+    const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
+    int64_t F, const cdx::FaceRec* __restrict__ rec, const Sphere* __restrict__ sph, int C,
+    const unsigned* __restrict__ ws, float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
+    float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face,
+    unsigned long long* __restrict__ best_out, int count) {
+  if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
+  __shared__ float4 s_sa[SPH_BLK];  // cx, cy, cz, r
+  __shared__ float2 s_sb[SPH_BLK];  // alpha, cnorm
+  __shared__ float4 s_rec[4][REC_WORDS * CHUNK / 4];  // per wave: one chunk's face records
+  __shared__ float s_val[4][64];
+  __shared__ int s_idx[4][64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = blockIdx.x / SDF_SPLIT, slice = blockIdx.x - grp * SDF_SPLIT;
+  const int64_t j = (int64_t)grp * 64 + lane;
+  const bool live = j < P;
+  const int64_t pi = porder[live ? j : P - 1];  // dead lanes shadow a live point
+  const cdx::F3 p = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
+  const bool ok = fabsf(p.x) <= PT_LIM && fabsf(p.y) <= PT_LIM && fabsf(p.z) <= PT_LIM;
+  if (!__all(ok)) {  // same points in every wave and slice: uniform over the workgroup
+    if (w == 0 && slice == 0) exact_point(p, faces, F, pi, out_dist, out_sign, out_nrm, out_clst, out_face, live);
+    if (count && w == 0 && slice == 0 && lane == 0)
+      atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(__ballot(live)));
+    return;
+  }
+  const float pnorm = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+  auto stage = [&](int cb) {  // spheres of chunks [cb, cb + SPH_BLK) into LDS (all waves)
+    __syncthreads();
+    const int nb = min(SPH_BLK, C - cb);
+    for (int i = threadIdx.x; i < nb; i += SDF_BLOCK) {
+      const Sphere sp = sph[cb + i];
+      s_sa[i] = make_float4(sp.cx, sp.cy, sp.cz, sp.r);
+      s_sb[i] = make_float2(sp.alpha, sp.cnorm);
+    }
+    __syncthreads();
+    return nb;
+  };
+
+  // pass 1 (all chunks): upper bound on the answer, and the chunk that gives it (the lane's nearest, roughly)
+  float ub = INFINITY;
+  int uc = 0;
+  for (int cb = 0; cb < C; cb += SPH_BLK) {
+    const int nb = stage(cb);
+    for (int c = w; c < nb; c += 4) {
+      const float4 a = s_sa[c];
+      const float2 b = s_sb[c];
+      const float dx = p.x - a.x, dy = p.y - a.y, dz = p.z - a.z;
+      const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
+      const float u = (dist + a.w) * (1.f + b.x) + 1e-4f * (pnorm + b.y + a.w);
+      if (u < ub) { ub = u; uc = cb + c; }
+    }
+  }
+  s_val[w][lane] = ub;
+  s_idx[w][lane] = uc;
+  __syncthreads();
+  int seed = s_idx[0][lane];
+  {
+    float m = s_val[0][lane];
+#pragma unroll
+    for (int v = 1; v < 4; ++v)
+      if (s_val[v][lane] < m) { m = s_val[v][lane]; seed = s_idx[v][lane]; }
+    ub = m;
+  }
+  const float T = ub * ub;
+  seed = __builtin_amdgcn_readlane(seed, 32);
+
+  // the seed chunk's faces, split over the waves (faces k ≡ w mod 4), merged in LDS: every wave of the
+  // workgroup starts with the same (best, face)
+  const float4* rec4 = reinterpret_cast<const float4*>(rec);
+  float4* buf = s_rec[w];
+  float best = INFINITY;
+  int bidx = 0x7fffffff;
+  unsigned evaluated = 0, visits = 0;  // faces evaluated / chunks visited by this wave (diagnostic counts)
+  {
+    const int nf = (int)min((int64_t)CHUNK, F - (int64_t)seed * CHUNK);
+    for (int k = w; k < nf; k += 4) {
+      const cdx::FaceRec r = rec[(int64_t)seed * CHUNK + k];
+      const float d = cdx::face_dist2(p, r);
+      if (d < best || (d == best && r.idx < bidx)) { best = d; bidx = r.idx; }
+      ++evaluated;
+    }
+    __syncthreads();  // pass 1's s_val / s_idx reads are done
+    s_val[w][lane] = best;
+    s_idx[w][lane] = bidx;
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float d = s_val[v][lane];
+      const int i = s_idx[v][lane];
+      if (d < best || (d == best && i < bidx)) { best = d; bidx = i; }
+    }
+    __syncthreads();  // s_val / s_idx are written again at the end
+  }
+
+  // pass 2 (this slice's chunks): exact distances over the chunks some lane cannot rule out
+  const int c0 = 4 * slice + w, cs = 4 * SDF_SPLIT;
+  for (int cb = 0; cb < C; cb += SPH_BLK) {
+    const int nb = C <= SPH_BLK ? C : stage(cb);  // (one block: still staged from pass 1)
+    // the wave's next chunk ≥ c (c ≡ c0 mod cs) some lane cannot rule out (uniform), or ≥ nb
+    auto next_needed = [&](int c) {
+      for (; c < nb; c += cs) {
+        const float4 a = s_sa[c];
+        const float2 b = s_sb[c];
+        const float dx = p.x - a.x, dy = p.y - a.y, dz = p.z - a.z;
+        const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
+        const float L = dist * (1.f - b.x) - a.w * (1.f + b.x) - 1e-4f * (pnorm + b.y + a.w);
+        if (__any(!(L > 0.f && L * L > fminf(T, best)))) break;
+      }
+      return c;
+    };
+    // first chunk of the slice in this block: c ≡ c0 (mod cs), c ≥ 0 relative to cb
+    const int cfirst = (int)(((int64_t)c0 - cb) % cs + cs) % cs;
+    int c = next_needed(cfirst);
+    float4 pre[REC_V4];
+    if (c < nb) {
+#pragma unroll
+      for (int i = 0; i < REC_V4; ++i) pre[i] = rec4[(int64_t)(cb + c) * (REC_WORDS * CHUNK / 4) + lane + 64 * i];
+    }
+    while (c < nb) {
+#pragma unroll
+      for (int i = 0; i < REC_V4; ++i) buf[lane + 64 * i] = pre[i];
+      const int cur = c;
+      const int64_t f0 = (int64_t)(cb + cur) * CHUNK;
+      const float alpha = s_sb[cur].x;
+      c = next_needed(cur + cs);
+      if (c < nb) {  // the next chunk's records in flight while this one is processed
+#pragma unroll
+        for (int i = 0; i < REC_V4; ++i) pre[i] = rec4[(int64_t)(cb + c) * (REC_WORDS * CHUNK / 4) + lane + 64 * i];
+      }
+      const cdx::FaceRec* rr = reinterpret_cast<const cdx::FaceRec*>(buf);
+      const int nf = (int)min((int64_t)CHUNK, F - f0);
+      ++visits;
+      // per-face bounds against the lane's best: bit k set = some lane cannot rule face k out
+      const float sb = sqrtf(best);  // (INF while the lane has no face yet)
+      const float a1 = 1.f - alpha, a2 = 1.f + alpha;
+      unsigned mask = 0;
+#pragma unroll 8
+      for (int k = 0; k < CHUNK; ++k) {
+        const cdx::FaceRec& r = rr[k];
+#if !defined(CDX_SDF_NO_FACEBOUND)
+        const float fx = p.x - r.bx, fy = p.y - r.by, fz = p.z - r.bz;
+        const float fd2 = fx * fx + fy * fy + fz * fz;
+        // skip ⇔ fd·a1 > br·a2 + β + sqrt(best)  (the chunk bound's Lf > 0 ∧ Lf² > best)
+        const float th = (r.br * a2 + 1e-4f * (pnorm + r.bn + r.br) + sb) / a1;
+        const bool need = !(fd2 > th * th);
+#else
+        const bool need = true;
+#endif
+        if (__any(need) && k < nf) mask |= 1u << k;
+      }
+      while (mask) {
+        const int k = __builtin_ctz(mask);
+        mask &= mask - 1;
+        const cdx::FaceRec& r = rr[k];
+        ++evaluated;
+        const float d = cdx::face_dist2(p, r);
+        if (d < best || (d == best && r.idx < bidx)) { best = d; bidx = r.idx; }
+      }
+    }
+  }
+  if (count) {
+    const unsigned long long nl = __popcll(__ballot(live));
+    if (lane == 0) {
+      atomicAdd(&g_sdf_stats[0], (unsigned long long)evaluated * nl);
+      atomicAdd(&g_sdf_stats[3], (unsigned long long)visits);
+      if (w == 0 && slice == 0) atomicAdd(&g_sdf_stats[2], nl);
+    }
+  }
+  s_val[w][lane] = best;
+  s_idx[w][lane] = bidx;
+  __syncthreads();
+  if (w != 0 || !live) return;
+#pragma unroll
+  for (int v = 1; v < 4; ++v) {
+    const float d = s_val[v][lane];
+    const int i = s_idx[v][lane];
+    if (d < best || (d == best && i < bidx)) { best = d; bidx = i; }
+  }
+  atomicMin(best_out + pi, pack_best(best, bidx));
+}
+
+// The outputs of the split launch's winners: point_face of each point's best face (the workgroups that ran
+// the brute-force rule or a NaN-capable mesh left best at ~0 and wrote their outputs themselves).
+__global__ __launch_bounds__(256) void sdf_culled_finalize_kernel(
+    const float* __restrict__ points, int64_t P, const float* __restrict__ faces,
+    const unsigned long long* __restrict__ best, float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
+    float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face) {
+  const int64_t pi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pi >= P) return;
+  const unsigned long long b = best[pi];
+  if (b == ~0ull) return;
+  const int bidx = (int)(unsigned)(b & 0xFFFFFFFFu);
+  const cdx::F3 p = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
+  const float* v = faces + 9 * (int64_t)bidx;
+  cdx::F3 cc, n;
+  int sg;
+  const float d = cdx::point_face(p, cdx::f3(v[0], v[1], v[2]), cdx::f3(v[3], v[4], v[5]),
+                                  cdx::f3(v[6], v[7], v[8]), cc, n, sg);
+  out_dist[pi] = d;
+  out_sign[pi] = sg;
+  out_nrm[3 * pi] = n.x; out_nrm[3 * pi + 1] = n.y; out_nrm[3 * pi + 2] = n.z;
+  out_clst[3 * pi] = cc.x; out_clst[3 * pi + 1] = cc.y; out_clst[3 * pi + 2] = cc.z;
+  if (out_face) out_face[pi] = bidx;
+}
+
 // Brute force with the reference's tile rule: one point per lane, faces streamed through LDS
 // in 512-face tiles.  Runs when ws (if given) flags a NaN-capable face.
 __global__ __launch_bounds__(SDF_BLOCK) void sdf_exact_kernel(const float* __restrict__ points, int64_t P,
@@ -490,6 +736,7 @@ int mesh_query(const char* mesh, const float* faces, int64_t F, const float* poi
   const size_t o_pk = off; off = align256(off + 2 * (size_t)m * sizeof(unsigned));
   const size_t o_pv = off; off = align256(off + 2 * (size_t)m * sizeof(int));
   const size_t o_tmp = off; off = align256(off + tp);
+  const size_t o_best = off; off = align256(off + (size_t)m * sizeof(unsigned long long));
   char* base = nullptr;
   if (hipMallocAsync(reinterpret_cast<void**>(&base), off, s) != hipSuccess) return CDX_ELAUNCH;
   const unsigned* ws = reinterpret_cast<const unsigned*>(mesh);
@@ -499,10 +746,21 @@ int mesh_query(const char* mesh, const float* faces, int64_t F, const float* poi
                      (const float*)nullptr, (int64_t)0, ws, (unsigned*)nullptr, (int*)nullptr, pk, pv);
   size_t t2 = tp;
   bool ok = hipcub::DeviceRadixSort::SortPairs(base + o_tmp, t2, pk, pk + m, pv, pv + m, m, 0, 30, s) == hipSuccess;
+#if defined(CDX_SDF_V1)
   hipLaunchKernelGGL(sdf_culled_kernel, dim3((unsigned)((P + 63) / 64)), dim3(SDF_BLOCK), 0, s, points, P,
                      (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
                      reinterpret_cast<const Sphere*>(mesh + mesh_sph_off(C)), C, ws, sqdist, sign, normals, clst,
                      face_idx, (int)g_sdf_count);
+#else
+  unsigned long long* best = reinterpret_cast<unsigned long long*>(base + o_best);
+  ok = ok && hipMemsetAsync(best, 0xFF, (size_t)m * sizeof(unsigned long long), s) == hipSuccess;
+  hipLaunchKernelGGL(sdf_culled2_kernel, dim3((unsigned)((P + 63) / 64 * SDF_SPLIT)), dim3(SDF_BLOCK), 0, s, points,
+                     P, (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
+                     reinterpret_cast<const Sphere*>(mesh + mesh_sph_off(C)), C, ws, sqdist, sign, normals, clst,
+                     face_idx, best, (int)g_sdf_count);
+  hipLaunchKernelGGL(sdf_culled_finalize_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P, faces,
+                     (const unsigned long long*)best, sqdist, sign, normals, clst, face_idx);
+#endif
   hipLaunchKernelGGL(sdf_exact_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0, s, points,
                      P, faces, F, ws, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
   ok = ok && hipGetLastError() == hipSuccess;
@@ -557,16 +815,26 @@ int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* 
   return mesh_query(static_cast<const char*>(mesh), faces, F, points, P, sqdist, sign, normals, clst, face_idx, s);
 }
 
+int cdx_sdf_chunk_visits(uint64_t* out, cdx_stream_t stream) {
+  if (!out) return CDX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_sdf_stats), sizeof(uint64_t), 3 * sizeof(uint64_t),
+                               hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return CDX_ELAUNCH;
+  return CDX_OK;
+}
+
 int cdx_sdf_stats(int32_t enable, uint64_t* out3, cdx_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (out3) {
-    if (hipMemcpyFromSymbolAsync(out3, HIP_SYMBOL(g_sdf_stats), sizeof(g_sdf_stats), 0, hipMemcpyDeviceToHost, s) !=
+    if (hipMemcpyFromSymbolAsync(out3, HIP_SYMBOL(g_sdf_stats), 3 * sizeof(uint64_t), 0, hipMemcpyDeviceToHost, s) !=
             hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
       return CDX_ELAUNCH;
   }
   if (enable >= 0) {
-    const unsigned long long z[3] = {0, 0, 0};
+    const unsigned long long z[4] = {0, 0, 0, 0};
     if (enable && hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sdf_stats), z, sizeof(z), 0, hipMemcpyHostToDevice, s) != hipSuccess)
       return CDX_ELAUNCH;
     if (enable && hipStreamSynchronize(s) != hipSuccess) return CDX_ELAUNCH;

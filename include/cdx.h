@@ -445,6 +445,9 @@ int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* 
  * enable 1: zero the counters and count from now on (one atomic per wave); 0: stop counting; −1: only
  * read.  Against P·F per call this is the culling's work saving. */
 int cdx_sdf_stats(int32_t enable, uint64_t* out3, cdx_stream_t stream);
+/* Diagnostic companion of cdx_sdf_stats: chunks (32 faces) the culled kernel's waves fetched and
+ * bound-tested face by face since counting was enabled, summed over waves. */
+int cdx_sdf_chunk_visits(uint64_t* out, cdx_stream_t stream);
 
 /* Library identification (gfx arch string compiled in). */
 const char* cdx_version(void);

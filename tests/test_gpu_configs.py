@@ -201,7 +201,8 @@ def test_config4_sdf_loop_at_size_vs_oracle():
     try:
         res = kin.optimize(torch.from_numpy(q).to(DEV), torch.from_numpy(target).to(DEV),
                            torch.from_numpy(comp).to(DEV), 1, TriangleMesh.from_npz(mesh_path), verbose=False,
-                           kabsch_noise=[torch.from_numpy(n).to(DEV) for n in noise], trace_rows=True)
+                           kabsch_noise=[torch.from_numpy(n).to(DEV) for n in noise], trace_rows=True,
+                           fused=False)  # the spied autograd loop (the fused one: test_kin_optimiser_fused_*)
     finally:
         opts.compute_sdf = real
     torch.cuda.synchronize()

@@ -172,6 +172,8 @@ def case_c4(dev):
         for i, f in enumerate((deflated, faces, faces)):
             compute_sdf(pts[i].detach(), f)
     N.check(lib.cdx_sdf_stats(0, st, N.stream_ptr(dev)), "cdx_sdf_stats")
+    visits = ctypes.c_uint64(0)
+    N.check(lib.cdx_sdf_chunk_visits(ctypes.byref(visits), N.stream_ptr(dev)), "cdx_sdf_chunk_visits")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     reps = 10
     with torch.no_grad():
@@ -191,9 +193,11 @@ def case_c4(dev):
                       "fk_evals_per_s": E / fk_s, "sdf_3calls_fwd_bwd_ms": sdf_s * 1e3,
                       "sdf_point_face_pairs_per_s": pairs / sdf_s, "faces": int(faces.shape[0]),
                       "sdf_evals_per_s": E / sdf_s,
-                      "roofline_sdf": {"bound": "valu", "kernel": "sdf_culled_kernel (+ Morton sorts, chunk build)",
+                      "roofline_sdf": {"bound": "valu", "kernel": "sdf_culled2_kernel (+ Morton sorts, chunk build)",
                                        "fwd_3calls_ms": fwd_ms, "points": n_pts, "brute_force_pairs": pairs,
                                        "pairs_evaluated": evaluated, "pairs_exact_path": brute_exact,
+                                       "chunk_visits_per_wave": int(visits.value) / max(1, 4 * ((n_pts + 63) // 64)),
+                                       "chunks": (int(faces.shape[0]) + 31) // 32,
                                        "evaluated_over_brute_force": (evaluated + brute_exact) / pairs,
                                        "flops_per_pair": flops_pair, "achieved": achieved, "peak": 157.3,
                                        "unit": "TFLOP/s (f32 vector)", "frac": achieved / 157.3,

@@ -26,16 +26,21 @@ def main(path, n=20):
     acc = {}
     for s in seqs:
         t0 = int(s[0]["Start_Timestamp"])
+        seen = {}
         for k, r in enumerate(s):
             if "closure_combine_kernel" in s[k - 1]["Kernel_Name"] and k > 0:
                 break
-            key = (k, short(r["Kernel_Name"]), r["Stream_Id"])
-            acc.setdefault(key, []).append((int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0))
-    print(f"{len(seqs)} closures; median us relative to the closure's first dispatch")
-    for key in sorted(acc):
+            # a kernel is identified by (name, stream, occurrence in the closure): the side streams'
+            # kernels interleave with the main stream's in a different order from closure to closure
+            nm = (short(r["Kernel_Name"]), r["Stream_Id"])
+            seen[nm] = seen.get(nm, 0) + 1
+            acc.setdefault(nm + (seen[nm],), []).append((int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0))
+    print(f"{len(seqs)} closures; median us relative to the closure's first dispatch (n: closures with the kernel)")
+    for key in sorted(acc, key=lambda kk: st.median(x[0] for x in acc[kk])):
         v = acc[key]
-        print(f"{key[0]:2d} {key[1]:40s} stream {key[2]}  start {st.median(x[0] for x in v) / 1e3:8.1f}"
-              f"  end {st.median(x[1] for x in v) / 1e3:8.1f}  dur {st.median(x[1] - x[0] for x in v) / 1e3:7.1f}")
+        print(f"{key[0]:40s} #{key[2]} stream {key[1]}  start {st.median(x[0] for x in v) / 1e3:8.1f}"
+              f"  end {st.median(x[1] for x in v) / 1e3:8.1f}  dur {st.median(x[1] - x[0] for x in v) / 1e3:7.1f}"
+              f"  n {len(v)}")
 
 
 if __name__ == "__main__":
