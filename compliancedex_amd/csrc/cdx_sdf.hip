@@ -331,9 +331,9 @@ static_assert(REC_WORDS * CHUNK % (64 * 4) == 0, "a chunk's records load as whol
 constexpr int REC_V4 = REC_WORDS * CHUNK / (64 * 4);   // dwordx4 loads per lane per chunk (5)
 
 #ifndef CDX_SDF_SPLIT
-#define CDX_SDF_SPLIT 4
+#define CDX_SDF_SPLIT 2
 #endif
-constexpr int SDF_SPLIT = CDX_SDF_SPLIT;  // workgroups per 64-point group (chunk slices)
+constexpr int SDF_SPLIT = CDX_SDF_SPLIT;  // workgroups per 64-point group (chunk slices; 2: profiles/r04i_*, r04j_*)
 
 // (distance, face) as one unsigned 64-bit word whose order is the winner rule's: a non-negative float's
 // bits order as unsigned integers, ties then go to the smaller index.
