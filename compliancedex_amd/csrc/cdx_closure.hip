@@ -1125,10 +1125,11 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
       // the repair pass, gated on this closure's checks (a no-op launch pair otherwise): every all-tip row
       // through the exact pass (identity list) and the unscreened selection — no screened result that
       // failed a check leaves the closure, whichever entry point called it
+      cdx::RepairSel rs;
+      rs.X = w.X; rs.G = Mg; rs.T = T; rs.std_ = w.std_; rs.var = w.var; rs.Xg = w.Xg; rs.sel = w.sel; rs.vrow = w.vrow;
+      rs.stats = w.stats;
       rc = cdx::gpis_refine_launch(p->gpis, w.X, nullptr, nullptr, (int)Ms, Ms, w.refine_ws, w.V, s, nullptr, nullptr,
-                                   w.stats, false);
-      if (!rc)
-        rc = cdx::repair_select_launch(p->gpis, w.X, Mg, T, rpart, rpad, w.std_, w.var, w.sel, w.Xg, w.vrow, w.stats, s);
+                                   w.stats, false, nullptr, &rs);
       if (rc) return joined(rc);
     }
     if (wait_before_grad) {

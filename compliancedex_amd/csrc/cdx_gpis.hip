@@ -332,6 +332,7 @@ struct RefineList {
   int n_uc;           // stripes with unit costs below (= N_pad/256), 0: equal K-step cuts
   int64_t uc[RC_MAX_NT];  // cost of one (stripe, query tile) unit per stripe (var_unit_cost, host)
   const int* gate;    // nullable: screen statistics; the launch has no rows unless cdx::screen_failed
+  cdx::RepairSel rs;  // rs.on: the closure's repair pass (whole units, then the selection, see below)
 };
 
 // Rows of a refine launch (device-side count; 0 when gated off).
@@ -921,6 +922,54 @@ __global__ __launch_bounds__(ST_THREADS, 2) void gpis_std_kernel(cdx_gpis g, con
   };  // tile
 
   if constexpr (LIST) {
+    if (rl.rs.on) {
+      // The repair pass (gated: only after a failed check, so its speed does not matter): whole units
+      // u = b, b + gridDim.x, … (no cut stripes, no merge), then the last workgroup to finish — an arrival
+      // counter in the workspace, released / acquired at agent scope — takes every group's exact
+      // selection (the unscreened closure's): std / var of all rows, the first maximum of log(100·std).
+      const int MtL = (int)((Mrows + ST_BM - 1) / ST_BM), Ntl = Np / ST_BN;
+      bool first_u = true;
+      for (int u = b; u < MtL * Ntl; u += gridDim.x) {
+        const int nt = u / MtL, mt = u - nt * MtL;
+        if (!first_u) __syncthreads();  // the previous unit's epilogue used the stage buffers
+        first_u = false;
+        tile(mt, nt, 0, min(g.N, nt * ST_BN + ST_BN - vsh), nt, true);
+      }
+      __shared__ int s_lastwg;
+      __threadfence();
+      __syncthreads();
+      if (tid == 0) {
+        s_lastwg = atomicAdd(rl.rs.done, 1) == (int)gridDim.x - 1;
+        if (s_lastwg) {
+          *rl.rs.done = 0;  // ready for the next launch
+          rl.rs.stats[cdx::SS_REPAIR] = 1;  // (not among the words screen_failed reads)
+          rl.rs.stats[cdx::SS_CUM + cdx::SS_REPAIR] += 1;
+        }
+      }
+      __syncthreads();
+      if (!s_lastwg) return;
+      __threadfence();
+      const double k0 = gpis_k0<KT>(g.R);
+      for (int64_t gi = tid; gi < rl.rs.G; gi += ST_THREADS) {
+        int fmax = 0;
+        double lmax = 0;
+        for (int f = 0; f < rl.rs.T; ++f) {
+          const int64_t q = gi * rl.rs.T + f;
+          double acc = 0;
+          for (int t = 0; t < Ntl; ++t) acc += partial[(int64_t)t * M_pad + q];
+          const double v = k0 - acc, sd = sqrt(fabs(v));
+          rl.rs.std_[q] = sd;
+          rl.rs.var[q] = v;
+          const double lv = log(100 * sd);
+          if (f == 0 || lv > lmax) { lmax = lv; fmax = f; }
+        }
+        const int64_t qi = gi * rl.rs.T + fmax;
+        rl.rs.sel[gi] = qi;
+        rl.rs.vrow[gi] = qi;
+        for (int i = 0; i < 3; ++i) rl.rs.Xg[3 * gi + i] = X[3 * qi + i];
+      }
+      return;
+    }
     // pieces of the concatenated K-sequence of all (stripe, query tile) units (refine_locate)
     const RefineCuts rc = refine_cuts(g, Mrows, gridDim.x);
     const int MtL = rc.MtL, pieces = rc.pieces;
@@ -1447,8 +1496,9 @@ static size_t refine_part_bytes(const cdx_gpis& g, int64_t Mcap) {
   return ((size_t)(g.N_pad / ST_BN) * (size_t)round_up(Mcap, ST_BM) * sizeof(double) + 255) / 256 * 256;
 }
 static size_t refine_slot_bytes() { return (size_t)REFINE_PIECES * 2 * ST_BM * ST_BN * sizeof(double); }
+// (+1: the repair pass's workgroup arrival counter, after the cut-unit counters)
 static size_t refine_cnt_bytes(const cdx_gpis& g, int64_t Mcap) {
-  return ((size_t)(g.N_pad / ST_BN) * (size_t)(round_up(Mcap, ST_BM) / ST_BM) * sizeof(int) + 255) / 256 * 256;
+  return ((size_t)(g.N_pad / ST_BN) * (size_t)(round_up(Mcap, ST_BM) / ST_BM) * sizeof(int) + sizeof(int) + 255) / 256 * 256;
 }
 
 static size_t refine_cuts_bytes() { return ((REFINE_PIECES + 1) * sizeof(int64_t) + 255) / 256 * 256; }
@@ -1471,20 +1521,27 @@ static void refine_launch_kt(const cdx_gpis& g, const double* X, int64_t Mcap, c
   if (prof) prof_mark(PROF_GPIS_STD, false, s);
   if (after) (void)hipEventRecord(after, s);
 #if !defined(CDX_MERGE_FUSED)
-  hipLaunchKernelGGL(gpis_var_merge, dim3(REFINE_PIECES), dim3(MERGE_THREADS), 0, s, g, rl, M_pad, partial, vout);
+  if (!rl.rs.on)  // (the repair pass runs whole units: nothing to merge)
+    hipLaunchKernelGGL(gpis_var_merge, dim3(REFINE_PIECES), dim3(MERGE_THREADS), 0, s, g, rl, M_pad, partial, vout);
 #endif
 }
 
 int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
                        void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out, const int* gate,
-                       bool prof, hipEvent_t after_refine) {
+                       bool prof, hipEvent_t after_refine, const RepairSel* repair) {
   if (Mcap <= 0 || G <= 0 || G > Mcap) return CDX_EINVAL;
+  if (repair && (!gate || rows || extra || repair->G * repair->T != G || repair->stats != gate)) return CDX_EINVAL;
   const int64_t M_pad = round_up(Mcap, ST_BM);
   double* partial = static_cast<double*>(ws);
   char* slots = static_cast<char*>(ws) + refine_part_bytes(g, Mcap);
   RefineList rl{rows, extra, G, reinterpret_cast<double*>(slots), reinterpret_cast<int*>(slots + refine_slot_bytes()),
                 (int)(M_pad / ST_BM),
-                reinterpret_cast<int64_t*>(slots + refine_slot_bytes() + refine_cnt_bytes(g, Mcap)), 0, {}, gate};
+                reinterpret_cast<int64_t*>(slots + refine_slot_bytes() + refine_cnt_bytes(g, Mcap)), 0, {}, gate, {}};
+  if (repair) {
+    rl.rs = *repair;
+    rl.rs.on = true;
+    rl.rs.done = rl.cnt + (size_t)(g.N_pad / ST_BN) * (size_t)(M_pad / ST_BM);
+  }
   const int Nt = g.N_pad / ST_BN;
   if (Nt <= RC_MAX_NT) {
     rl.n_uc = Nt;

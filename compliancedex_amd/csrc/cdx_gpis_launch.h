@@ -145,11 +145,26 @@ __device__ inline void grad_fold_gstd(const GradFold& f, int64_t m, double v, do
 // closure's screen statistics — the launch runs only when a check failed (cdx::screen_failed), else every
 // workgroup returns at once (the closure's repair pass).  prof: mark the launch for cdx_profile_read.
 // after_refine (nullable): recorded on s between the refine kernel and its merge.
+// repair (nullable; with gate = its stats, the identity list and G = repair->G·T rows): the closure's
+// repair pass — every all-tip row in whole units, then, by the last workgroup, the unscreened selection
+// (exact std / var of all rows, sel / vrow / Xg = each group's first maximum of log(100·std)); sets
+// SS_REPAIR and counts it.  One gated launch (no merge, no separate selection kernel).
+struct RepairSel {
+  bool on = false;
+  const double* X = nullptr;
+  int64_t G = 0;
+  int T = 0;
+  double *std_ = nullptr, *var = nullptr, *Xg = nullptr;
+  int64_t *sel = nullptr, *vrow = nullptr;
+  int* stats = nullptr;
+  int* done = nullptr;  // (set by the launcher: the workspace's arrival counter)
+};
 size_t gpis_refine_ws_bytes(const cdx_gpis& g, int64_t Mcap);
 // Zeroes the refine workspace's cut-unit arrival counters (once after allocation; every launch
 // leaves them zero).
 int gpis_refine_reset(const cdx_gpis& g, int64_t Mcap, void* ws, hipStream_t s);
 int gpis_refine_launch(const cdx_gpis& g, const double* X, const int* rows, const int* extra, int G, int64_t Mcap,
                        void* ws, double* vout, hipStream_t s, double** partial_out, int64_t* M_pad_out,
-                       const int* gate = nullptr, bool prof = true, hipEvent_t after_refine = nullptr);
+                       const int* gate = nullptr, bool prof = true, hipEvent_t after_refine = nullptr,
+                       const RepairSel* repair = nullptr);
 }  // namespace cdx

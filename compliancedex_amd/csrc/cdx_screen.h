@@ -130,10 +130,5 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
 int refine_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, const double* rpartial, int64_t M_pad,
                          const double* sv2, const int* vpos, const unsigned short* keep, double* std_, double* var,
                          int64_t* sel, double* Xg, int64_t* vrow, int* stats, hipStream_t s);
-// The repair (only when screen_failed(stats)): after a refine pass over EVERY all-tip row (identity list,
-// gated on the same stats), exact std/var of all rows and each group's first maximum of log(100·std) as
-// the ∇std row — the unscreened closure's selection; sets SS_REPAIR and counts it.  A no-op otherwise.
-int repair_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, const double* rpartial, int64_t M_pad,
-                         double* std_, double* var, int64_t* sel, double* Xg, int64_t* vrow, int* stats, hipStream_t s);
 
 }  // namespace cdx

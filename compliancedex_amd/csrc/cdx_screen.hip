@@ -806,43 +806,6 @@ __global__ __launch_bounds__(256) void refine_select_kernel(cdx_gpis g, const do
   }
 }
 
-// The repair's selection (gated: a no-op unless a check of this closure failed, cdx::screen_failed).  The
-// refine pass has just run every all-tip row at list position = row (identity list): exact std / var of
-// every row, the group's first maximum of log(100·std) — as gpis_var_finalize_select and level_fwd_bwd
-// take it — its query, point and V row.
-template <int KT>
-__global__ __launch_bounds__(256) void repair_select_kernel(cdx_gpis g, const double* __restrict__ rpartial,
-                                                            int64_t M_pad, int Nt, int64_t G, int T,
-                                                            const double* __restrict__ X, double* __restrict__ std_,
-                                                            double* __restrict__ var, int64_t* __restrict__ sel,
-                                                            double* __restrict__ Xg, int64_t* __restrict__ vrow,
-                                                            int* __restrict__ stats) {
-  if (!cdx::screen_failed(stats)) return;
-  const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi == 0) {  // (SS_REPAIR is not among the words screen_failed reads)
-    stats[cdx::SS_REPAIR] = 1;
-    stats[cdx::SS_CUM + cdx::SS_REPAIR] += 1;
-  }
-  if (gi >= G) return;
-  const double k0 = cdx::gpis_k0<KT>(g.R);
-  int fmax = 0;
-  double lmax = 0;
-  for (int f = 0; f < T; ++f) {
-    const int64_t q = gi * T + f;
-    double acc = 0;
-    for (int t = 0; t < Nt; ++t) acc += rpartial[(int64_t)t * M_pad + q];
-    const double v = k0 - acc, sd = sqrt(fabs(v));
-    std_[q] = sd;
-    var[q] = v;
-    const double lv = log(100 * sd);
-    if (f == 0 || lv > lmax) { lmax = lv; fmax = f; }
-  }
-  const int64_t qi = gi * T + fmax;
-  sel[gi] = qi;
-  vrow[gi] = qi;
-  for (int i = 0; i < 3; ++i) Xg[3 * gi + i] = X[3 * qi + i];
-}
-
 // ------------------------------------------------------------------ preparation (once per state)
 // Centre of the inducing points (mean of rows < N, one block, fixed-order tree reduction), the
 // centred fp32 copy X1f [N_pad] (padding rows = row 0), the A scale SA and rq² = (max(0, r_safe −
@@ -1051,24 +1014,6 @@ int refine_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, c
       break;
     default:
       hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
-      break;
-  }
-  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
-}
-
-int repair_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, const double* rpartial, int64_t M_pad,
-                         double* std_, double* var, int64_t* sel, double* Xg, int64_t* vrow, int* stats, hipStream_t s) {
-  const int Nt = g.N_pad / SC_BN;
-  const dim3 sgrid((unsigned)((G + SEL_BLOCK - 1) / SEL_BLOCK));
-  switch (g.kernel) {
-    case CDX_KERNEL_TPS:
-      hipLaunchKernelGGL(repair_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, X, std_, var, sel, Xg, vrow, stats);
-      break;
-    case CDX_KERNEL_RBF:
-      hipLaunchKernelGGL(repair_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, X, std_, var, sel, Xg, vrow, stats);
-      break;
-    default:
-      hipLaunchKernelGGL(repair_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, X, std_, var, sel, Xg, vrow, stats);
       break;
   }
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
