@@ -574,45 +574,54 @@ __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const do
 }
 
 // Deterministic compaction of the kept non-leader fingertips and the audited rows behind the G
-// leaders (group order, fingertip order): one workgroup; thread t owns the contiguous groups [t·C,
-// t·C + C), C = ceil(G/1024).  First the audit: an LDS histogram of the discarded rows' z bins and one
-// wave's scan of it give the cut (cdx_screen.h audit_bin: the lowest bins within the row budget A, plus
-// the bin that crosses A while the total stays ≤ 4A); the discarded rows below the cut are audited, i.e.
-// listed for the exact pass like the kept ones.  Then one scan of the per-thread counts (wave shuffles,
-// then the 16 wave totals through LDS).  Resets the per-closure statistics and counts the closure and its
-// audited rows in the cumulative block; records the smallest z left unaudited.
-__global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, unsigned short* __restrict__ keep,
-                                                              const unsigned* __restrict__ zkey,
-                                                              int* __restrict__ vpos, int* __restrict__ rows,
-                                                              int* __restrict__ stats, int A) {
-  __shared__ int hist[cdx::AUDIT_BINS], wsum[16], wsa[16], s_cut;
-  __shared__ unsigned wmin[16];
+// leaders (group order, fingertip order): one workgroup of 16 waves; wave w owns the contiguous groups
+// [w·64R, (w+1)·64R), R = ceil(G / 1024), read in R rounds of 64 consecutive groups (lane l: group
+// w·64R + 64r + l — coalesced; round 3 built per-thread chunks, whose strided loads made the kernel 20 µs).
+// First the audit: per-wave LDS histograms of the discarded rows' z bins, summed, and one wave's scan give
+// the cut (cdx_screen.h audit_bin: the lowest bins within the row budget A, plus the bin that crosses A
+// while the total stays ≤ 4A); the discarded rows below the cut are audited, i.e. listed for the exact
+// pass like the kept ones.  Then the listed rows are counted per wave, the 16 wave totals scanned through
+// LDS, and each round's positions taken from a wave prefix sum — the same positions as one sequential
+// pass in group order.  Resets the per-closure statistics and counts the closure and its audited rows in
+// the cumulative block; records the smallest z left unaudited.
+constexpr int COMPACT_WAVES = 16;
+__global__ __launch_bounds__(64 * COMPACT_WAVES) void screen_compact_kernel(int64_t G, int T,
+                                                                           unsigned short* __restrict__ keep,
+                                                                           const unsigned* __restrict__ zkey,
+                                                                           int* __restrict__ vpos, int* __restrict__ rows,
+                                                                           int* __restrict__ stats, int A) {
+  __shared__ int hist[COMPACT_WAVES][cdx::AUDIT_BINS];
+  __shared__ int wsum[COMPACT_WAVES], wsa[COMPACT_WAVES], wsd[COMPACT_WAVES], s_cut;
+  __shared__ unsigned wmin[COMPACT_WAVES];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int64_t C = (G + 1023) / 1024;
-  const int64_t g0 = (int64_t)t * C, g1 = g0 + C < G ? g0 + C : G;
-  if (t < cdx::AUDIT_BINS) hist[t] = 0;
+  const int64_t R = (G + 64 * COMPACT_WAVES - 1) / (64 * COMPACT_WAVES);
+  const int64_t gw = (int64_t)wave * 64 * R;  // this wave's first group
+  for (int i = t; i < COMPACT_WAVES * cdx::AUDIT_BINS; i += 64 * COMPACT_WAVES) (&hist[0][0])[i] = 0;
   if (t == 0) s_cut = A > 0 ? cdx::AUDIT_BINS : 0;
   __syncthreads();
-  int nd = 0;  // discarded rows of this thread
-  if (A > 0) {
-    for (int64_t gi = g0; gi < g1; ++gi)
-      for (int f = 0; f < T; ++f) {
-        const unsigned z = zkey[gi * T + f];
-        if (z != cdx::Z_NONE) {
-          atomicAdd(&hist[cdx::audit_bin(z)], 1);
-          ++nd;
-        }
-      }
-  } else {
-    for (int64_t gi = g0; gi < g1; ++gi)
-      for (int f = 0; f < T; ++f) nd += zkey[gi * T + f] != cdx::Z_NONE;
+  // pass 1: the discarded rows (histogram of their z bins when auditing)
+  int nd = 0;
+  for (int64_t r = 0; r < R; ++r) {
+    const int64_t gi = gw + 64 * r + lane;
+    if (gi >= G) break;
+    for (int f = 0; f < T; ++f) {
+      const unsigned z = zkey[gi * T + f];
+      if (z == cdx::Z_NONE) continue;
+      ++nd;
+      if (A > 0) atomicAdd(&hist[wave][cdx::audit_bin(z)], 1);
+    }
   }
   __syncthreads();
-  if (A > 0 && wave == 0) {  // the cut: lane l scans bins 4l .. 4l + 3
+  if (A > 0 && wave == 0) {  // the cut: lane l scans bins 4l .. 4l + 3 (summed over the waves' histograms)
     constexpr int PB = cdx::AUDIT_BINS / 64;
     int h[PB], s = 0;
 #pragma unroll
-    for (int i = 0; i < PB; ++i) s += (h[i] = hist[PB * lane + i]);
+    for (int i = 0; i < PB; ++i) {
+      int v = 0;
+#pragma unroll
+      for (int w = 0; w < COMPACT_WAVES; ++w) v += hist[w][PB * lane + i];
+      s += (h[i] = v);
+    }
     int inc = s;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -628,9 +637,9 @@ __global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, 
   }
   __syncthreads();
   const int cut = s_cut;
-  int n = 0, na = 0;
-  unsigned zmin = 0x7F800000u;  // +inf
-  for (int64_t gi = g0; gi < g1; ++gi) {
+  const unsigned tmask = (1u << T) - 1u;
+  // the group's kept | audited mask (low byte kept, high byte audited) and the smallest unaudited z
+  auto listed = [&](int64_t gi, unsigned& zmin) {
     unsigned m = keep[gi];
     for (int f = 0; f < T; ++f) {
       const unsigned z = zkey[gi * T + f];
@@ -638,56 +647,72 @@ __global__ __launch_bounds__(1024) void screen_compact_kernel(int64_t G, int T, 
       if (cdx::audit_bin(z) < cut) m |= 0x100u << f;
       else zmin = min(zmin, z);
     }
-    n += __popc(m);
+    return m;
+  };
+  // pass 2: listed rows per wave
+  int n = 0, na = 0;
+  unsigned zmin = 0x7F800000u;  // +inf
+  for (int64_t r = 0; r < R; ++r) {
+    const int64_t gi = gw + 64 * r + lane;
+    if (gi >= G) break;
+    const unsigned m = listed(gi, zmin);
+    n += __popc((m | (m >> 8)) & tmask);
     na += __popc(m >> 8);
   }
-  int inc = n;  // inclusive scan over the wave
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int v = __shfl_up(inc, d);
-    if (lane >= d) inc += v;
-  }
-  int wa = na, wd = nd;
+  int wn = n, wa = na, wd = nd;
   unsigned wz = zmin;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
+    wn += __shfl_xor(wn, d);
     wa += __shfl_xor(wa, d);
     wd += __shfl_xor(wd, d);
     wz = min(wz, (unsigned)__shfl_xor((int)wz, d));
   }
-  if (lane == 63) wsum[wave] = inc;
   if (lane == 0) {
+    wsum[wave] = wn;
     wsa[wave] = wa;
+    wsd[wave] = wd;
     wmin[wave] = wz;
-    hist[wave] = wd;  // (the histogram is no longer read)
   }
   __syncthreads();
   int before = 0, total = 0, total_a = 0, total_d = 0;
   unsigned zm = 0x7F800000u;
 #pragma unroll
-  for (int w = 0; w < 16; ++w) {
-    const int s = wsum[w];
-    before += w < wave ? s : 0;
-    total += s;
+  for (int w = 0; w < COMPACT_WAVES; ++w) {
+    const int sw = wsum[w];
+    before += w < wave ? sw : 0;
+    total += sw;
     total_a += wsa[w];
-    total_d += hist[w];
+    total_d += wsd[w];
     zm = min(zm, wmin[w]);
   }
-  int pos = (int)G + before + inc - n;
-  for (int64_t gi = g0; gi < g1; ++gi) {
-    unsigned m = keep[gi];
-    for (int f = 0; f < T; ++f) {
-      const unsigned z = zkey[gi * T + f];
-      if (z != cdx::Z_NONE && cdx::audit_bin(z) < cut) m |= 0x100u << f;
+  // pass 3: positions in group order — this wave's base, then per round a wave prefix sum
+  int base = (int)G + before;
+  for (int64_t r = 0; r < R; ++r) {
+    const int64_t gi = gw + 64 * r + lane;
+    const bool in = gi < G;
+    if (gw + 64 * r >= G) break;  // (uniform)
+    unsigned dummy = 0;
+    const unsigned m = in ? listed(gi, dummy) : 0u;
+    const int c = __popc((m | (m >> 8)) & tmask);
+    int inc = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(inc, d);
+      if (lane >= d) inc += v;
     }
-    keep[gi] = (unsigned short)m;
-    for (int f = 0; f < T; ++f)
-      if (((m >> f) | (m >> (8 + f))) & 1u) {
-        const int64_t q = gi * T + f;
-        vpos[q] = pos;
-        rows[pos] = (int)q;
-        ++pos;
-      }
+    int pos = base + inc - c;
+    if (in) {
+      keep[gi] = (unsigned short)m;
+      for (int f = 0; f < T; ++f)
+        if (((m >> f) | (m >> (8 + f))) & 1u) {
+          const int64_t q = gi * T + f;
+          vpos[q] = pos;
+          rows[pos] = (int)q;
+          ++pos;
+        }
+    }
+    base += __shfl(inc, 63);
   }
   if (t == 0) {
     stats[cdx::SS_EXTRA] = total;
@@ -995,7 +1020,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, zkey, X);
       break;
   }
-  hipLaunchKernelGGL(screen_compact_kernel, dim3(1), dim3(1024), 0, s, G, T, keep, (const unsigned*)zkey, vpos, rows, stats,
+  hipLaunchKernelGGL(screen_compact_kernel, dim3(1), dim3(64 * COMPACT_WAVES), 0, s, G, T, keep, (const unsigned*)zkey, vpos, rows, stats,
                      screen_audit_rows());
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
