@@ -736,69 +736,80 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void screen_compact_kernel(int6
 // query, Xg = its point, vrow = its V row (list position).  Checks every refined row's estimate
 // against its margin Δ_f.  A maximum on a row the exact pass did not run (only possible when a
 // margin failed) is a fault: the group falls back to its best refined row and its unrefined rows get
-// std 0, so the level kernel's argmax agrees and no V row outside the list is read.  One wave per
-// workgroup: counts and maxima are wave-reduced, then one atomic per statistic per wave.
+// std 0, so the level kernel's argmax agrees and no V row outside the list is read.
+// One thread per ROW (round 4; round 3 ran one thread per group, 4 dependent partial-load chains in
+// sequence on 64 waves): a workgroup of 64·T threads holds 64 whole groups, each row's exact value,
+// check and log(100·std) go through LDS to the group's first thread, which takes the maximum in
+// fingertip order.  Counts and maxima are wave-reduced, then one atomic per statistic per wave.
 template <int KT>
-__global__ __launch_bounds__(256) void refine_select_kernel(cdx_gpis g, const double* __restrict__ rpartial,
-                                                            int64_t M_pad, int Nt, int64_t G, int T,
-                                                            const double* __restrict__ sv2, const int* __restrict__ vpos,
-                                                            const unsigned short* __restrict__ keep,
-                                                            const double* __restrict__ X, double* __restrict__ std_,
-                                                            double* __restrict__ var, int64_t* __restrict__ sel,
-                                                            double* __restrict__ Xg, int64_t* __restrict__ vrow,
-                                                            int* __restrict__ stats) {
-  const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64 * CDX_MAX_TIPS) void refine_select_kernel(
+    cdx_gpis g, const double* __restrict__ rpartial, int64_t M_pad, int Nt, int64_t G, int T,
+    const double* __restrict__ sv2, const int* __restrict__ vpos, const unsigned short* __restrict__ keep,
+    const double* __restrict__ X, double* __restrict__ std_, double* __restrict__ var, int64_t* __restrict__ sel,
+    double* __restrict__ Xg, int64_t* __restrict__ vrow, int* __restrict__ stats) {
+  __shared__ double s_lv[64 * CDX_MAX_TIPS];
+  __shared__ int s_pos[64 * CDX_MAX_TIPS];
+  const int t = threadIdx.x;
+  const int64_t q = (int64_t)blockIdx.x * 64 * T + t;  // this thread's row
+  const int64_t gi = q / T;
+  const int f = (int)(q - gi * T);
+  const bool row = t < 64 * T && gi < G;
   int miss = 0, amiss = 0, aflip = 0, fault = 0;
   float rk = 0.f, ra = 0.f;
-  if (gi < G) {
-    const double k0 = cdx::gpis_k0<KT>(g.R), delta = g.screen_delta;
-    const double* ctr = cdx::screen_view(g).center;
-    const unsigned m = keep[gi];
+  if (row) {
+    const double k0 = cdx::gpis_k0<KT>(g.R);
+    const int pos = vpos[q];
+    double sd;
+    if (pos >= 0) {
+      double acc = 0;
+      for (int s2 = 0; s2 < Nt; ++s2) acc += rpartial[(int64_t)s2 * M_pad + pos];
+      const double v = k0 - acc;
+      sd = sqrt(fabs(v));
+      std_[q] = sd;
+      var[q] = v;
+      const double* ctr = cdx::screen_view(g).center;
+      const double e = fabs(sv2[q] - v),
+                   dd = screen_margin(g.screen_delta, ctr, cdx::screen_band(ctr, X[3 * q], X[3 * q + 1], X[3 * q + 2]),
+                                      k0, sv2[q]);
+      if (isfinite(v) && isfinite(sv2[q])) {
+        const float r = (float)(e / dd);
+        const bool bad = !(e <= dd);
+        if ((keep[gi] >> (8 + f)) & 1u) {
+          ra = r;
+          amiss = bad;
+        } else {
+          rk = r;
+          miss = bad;
+        }
+      }
+    } else {
+      sd = std_[q];
+    }
+    s_lv[t] = log(100 * sd);
+    s_pos[t] = pos;
+  }
+  __syncthreads();
+  if (row && f == 0) {  // the group's first thread: first maximum in fingertip order
+    const int t0 = t;
     int fmax = 0, fref = -1;
     double lmax = 0, lref = 0;
-    for (int f = 0; f < T; ++f) {
-      const int64_t q = gi * T + f;
-      const int pos = vpos[q];
-      double sd;
-      if (pos >= 0) {
-        double acc = 0;
-        for (int t = 0; t < Nt; ++t) acc += rpartial[(int64_t)t * M_pad + pos];
-        const double v = k0 - acc;
-        sd = sqrt(fabs(v));
-        std_[q] = sd;
-        var[q] = v;
-        const double e = fabs(sv2[q] - v),
-                     dd = screen_margin(delta, ctr, cdx::screen_band(ctr, X[3 * q], X[3 * q + 1], X[3 * q + 2]), k0,
-                                        sv2[q]);
-        if (isfinite(v) && isfinite(sv2[q])) {
-          const float r = (float)(e / dd);
-          const bool bad = !(e <= dd);
-          if ((m >> (8 + f)) & 1u) {
-            ra = fmaxf(ra, r);
-            amiss += bad;
-          } else {
-            rk = fmaxf(rk, r);
-            miss += bad;
-          }
-        }
-      } else {
-        sd = std_[q];
-      }
-      const double lv = log(100 * sd);
-      if (f == 0 || lv > lmax) { lmax = lv; fmax = f; }
-      if (pos >= 0 && (fref < 0 || lv > lref)) { lref = lv; fref = f; }
+    for (int ff = 0; ff < T; ++ff) {
+      const double lv = s_lv[t0 + ff];
+      const int pos = s_pos[t0 + ff];
+      if (ff == 0 || lv > lmax) { lmax = lv; fmax = ff; }
+      if (pos >= 0 && (fref < 0 || lv > lref)) { lref = lv; fref = ff; }
     }
-    if (vpos[gi * T + fmax] < 0) {
+    if (s_pos[t0 + fmax] < 0) {
       fault = 1;
       fmax = fref;  // the leader is always refined: fref ≥ 0
-      for (int f = 0; f < T; ++f)
-        if (vpos[gi * T + f] < 0) std_[gi * T + f] = 0.0;
-    } else if ((m >> (8 + fmax)) & 1u) {
+      for (int ff = 0; ff < T; ++ff)
+        if (s_pos[t0 + ff] < 0) std_[gi * T + ff] = 0.0;
+    } else if ((keep[gi] >> (8 + fmax)) & 1u) {
       aflip = 1;  // the exact maximum is an audited row: the screen had discarded it
     }
     const int64_t qi = gi * T + fmax;
     sel[gi] = qi;
-    vrow[gi] = vpos[qi];
+    vrow[gi] = s_pos[t0 + fmax];
     for (int i = 0; i < 3; ++i) Xg[3 * gi + i] = X[3 * qi + i];
   }
 #pragma unroll
@@ -810,7 +821,7 @@ __global__ __launch_bounds__(256) void refine_select_kernel(cdx_gpis g, const do
     rk = fmaxf(rk, __shfl_xor(rk, w));
     ra = fmaxf(ra, __shfl_xor(ra, w));
   }
-  if ((threadIdx.x & 63) == 0) {
+  if ((t & 63) == 0) {
     const int cnt[4] = {miss, amiss, aflip, fault};
     const int idx[4] = {cdx::SS_MISS, cdx::SS_AUDIT_MISS, cdx::SS_AUDIT_FLIP, cdx::SS_FAULT};
     for (int k = 0; k < 4; ++k)
@@ -1029,16 +1040,17 @@ int refine_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, c
                          const double* sv2, const int* vpos, const unsigned short* keep, double* std_, double* var,
                          int64_t* sel, double* Xg, int64_t* vrow, int* stats, hipStream_t s) {
   const int Nt = g.N_pad / SC_BN;
-  const dim3 sgrid((unsigned)((G + SEL_BLOCK - 1) / SEL_BLOCK));
+  if (T <= 0 || T > CDX_MAX_TIPS) return CDX_EINVAL;
+  const dim3 rgrid((unsigned)((G + 63) / 64));  // 64 groups (64·T rows) per workgroup
   switch (g.kernel) {
     case CDX_KERNEL_TPS:
-      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
+      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_TPS>, rgrid, dim3(64 * T), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
       break;
     case CDX_KERNEL_RBF:
-      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
+      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_RBF>, rgrid, dim3(64 * T), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
       break;
     default:
-      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
+      hipLaunchKernelGGL(refine_select_kernel<CDX_KERNEL_JOINT>, rgrid, dim3(64 * T), 0, s, g, rpartial, M_pad, Nt, G, T, sv2, vpos, keep, X, std_, var, sel, Xg, vrow, stats);
       break;
   }
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;

@@ -142,12 +142,16 @@ class KinGraspOptimizer:
         faces = _face_vertices(object_mesh, self.device)
         object_mesh.scale(0.9, center=[0, 0, 0])
         faces_deflate = _face_vertices(object_mesh, self.device)
+        # the fused loop also takes torch's single-kernel Adam (same update rule; one launch per step instead
+        # of the foreach path's ≈ 21 — profiles/r04d_config4_kin_iteration_split.json)
+        afused = dict(fused=True) if fused and self.device.type == "cuda" else {}
         if self.optimize_target:
             target_pose = target_pose.clone().requires_grad_(True)
             optim = torch.optim.Adam([{"params": joint_angles, "lr": 2e-3}, {"params": target_pose, "lr": 1e-5},
-                                      {"params": compliance, "lr": 0.2}])
+                                      {"params": compliance, "lr": 0.2}], **afused)
         else:
-            optim = torch.optim.Adam([{"params": joint_angles, "lr": 1e-2}, {"params": compliance, "lr": 0.2}])
+            optim = torch.optim.Adam([{"params": joint_angles, "lr": 1e-2}, {"params": compliance, "lr": 0.2}],
+                                     **afused)
         E, T = target_pose.shape[0], target_pose.shape[1]
         best = _Best(torch.float32, E, T, self.device, q=joint_angles, comp=compliance, target=target_pose)
         if fused:
