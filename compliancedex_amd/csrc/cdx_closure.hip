@@ -635,6 +635,14 @@ int mean_sched() {
   }();
   return m;
 }
+// CDX_MEAN_FIRST=1: the side stream runs mean A before the Kabsch records (A/B; default records first)
+bool mean_first() {
+  static const bool on = [] {
+    const char* e = getenv("CDX_MEAN_FIRST");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
 double mean_chunk1() {
   static const double f = [] {
     const char* e = getenv("CDX_MEAN_CHUNK1");
@@ -1013,12 +1021,13 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     auto launch_fork = [&]() -> int {
       forked = true;
       if (hipEventRecord(ss.fork, s) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess) return CDX_ELAUNCH;
-      if (kmode == 1) {
+      if (kmode == 1 && !mean_first()) {
         const int r = launch_records(ss.s);
         if (r) return r;
       }
       int r = cdx_gpis_mean(&p->gpis, w.X, MqA, w.mean, w.gmean, w.normal, side);
       if (r) return r;
+      if (kmode == 1 && mean_first() && (r = launch_records(ss.s))) return r;
       if (vlate) {  // the level kernel reads the mean A rows, the Kabsch records and no std
         GpisView gv0;
         gv0.mean = w.mean; gv0.gmean = w.gmean; gv0.normal = w.normal; gv0.std_ = w.std_; gv0.gstd = w.gstd;

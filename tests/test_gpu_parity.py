@@ -437,6 +437,38 @@ def test_sdf_culled_near_surface_bitwise():
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+def test_sdf_split_ties_and_far_points_bitwise():
+    """The round-4 culled kernel merges a point group's two chunk slices with a 64-bit atomic minimum on
+    (distance bits, face index): exact ties between a face and its duplicate (appended, so a higher
+    index) must resolve to the first index as the reference's scan does, whichever slice holds each copy;
+    points far outside the mesh (every chunk bound weak, the seeded pass carries the pruning) and a point
+    count that leaves dead lanes must match the brute-force C oracle bit for bit."""
+    from compliancedex_amd import compute_sdf_with_faces
+    from tests import _sdf_oracle
+    base = np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))
+    rng = np.random.default_rng(23)
+    dup = rng.choice(len(base), 300, replace=False)
+    faces = np.concatenate([base, base[dup]]).astype(np.float32)
+    lo, hi = base.reshape(-1, 3).min(0), base.reshape(-1, 3).max(0)
+    ext = hi - lo
+    cen = faces[dup].mean(1)
+    nrm = np.cross(faces[dup, 1] - faces[dup, 0], faces[dup, 2] - faces[dup, 0])
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    pts = np.concatenate([
+        cen + 1e-3 * nrm,                                                     # nearest: a duplicated face
+        faces[dup, 0],                                                        # on a duplicated vertex
+        lo - 5 * ext + 11 * ext * rng.random((700, 3)),                       # far outside
+        lo - 0.1 * ext + 1.2 * ext * rng.random((1037, 3)),                   # around the mesh
+    ]).astype(np.float32)
+    dist, sign, nrmo, clst, face = [t.cpu().numpy() for t in compute_sdf_with_faces(
+        torch.from_numpy(pts).to(DEV), torch.from_numpy(faces).to(DEV))]
+    o = _sdf_oracle.forward(pts, faces)
+    assert np.array_equal(face, o[4]) and np.array_equal(sign, o[1])
+    for a, b in zip((dist, nrmo, clst), (o[0], o[2], o[3])):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert (face[:300] < len(base)).all()  # the duplicate never wins its tie
+
+
 def test_sdf_prepared_mesh_equals_one_shot():
     """compute_sdf queries a cached prepared mesh (cdx_sdf_mesh_prepare once, cdx_sdf_query per call,
     the face frame only) and the _C shim the one-shot cdx_sdf_forward (the points ∪ faces frame): the
