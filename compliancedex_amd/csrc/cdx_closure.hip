@@ -635,11 +635,16 @@ int mean_sched() {
   }();
   return m;
 }
-// CDX_MEAN_FIRST=1: the side stream runs mean A before the Kabsch records (A/B; default records first)
+// The side stream runs mean A before the Kabsch records (round 4 default; CDX_MEAN_FIRST=0: records
+// first): the mean starts right after the screen, in the window of the latency-bound selection and
+// compaction, instead of 25 µs later, and the refine pass then shares the chip with less of it.  With the
+// side stream at normal priority (below): 1.013 vs 1.036 ms per closure over 4 interleaved rounds
+// (profiles/r04q_ab_mean_first_side_prio.jsonl; at the highest priority the mean's workgroups also take
+// the CUs the one-workgroup compaction needs: −4 µs only, r04p).
 bool mean_first() {
   static const bool on = [] {
     const char* e = getenv("CDX_MEAN_FIRST");
-    return e && atoi(e) != 0;
+    return !e || atoi(e) != 0;
   }();
   return on;
 }
@@ -705,13 +710,14 @@ bool side_stream(SideStream& out) {
   SideStream& ss = per_dev[dev];
   if (!ss.s) {
     hipStream_t st;
-    // CDX_SIDE_PRIO: < 0 creates the side stream at the device's lowest priority, > 0 (default, round 3)
-    // at its highest (the CP prefers a higher-priority queue's dispatches: the mean and the level kernel,
-    // which gate the ∇std pass, over the merge; 1.009–1.013 vs 1.012–1.016 ms per closure over 3
-    // interleaved rounds, profiles/r03zi_side_prio_ab.jsonl; as the default 1.017–1.023 vs 1.017–1.030,
-    // r03zj_side_prio_default_ab.jsonl), 0 normal.
+    // CDX_SIDE_PRIO: < 0 creates the side stream at the device's lowest priority, > 0 at its highest (the
+    // CP prefers a higher-priority queue's dispatches; round 3's default, −3…−4 µs then with the records
+    // first, profiles/r03zi_side_prio_ab.jsonl, r03zj_side_prio_default_ab.jsonl), 0 normal (round 4
+    // default, with the mean first: the highest priority lets the mean's workgroups starve the main
+    // stream's compaction; 1.013 vs 1.016 (lowest) vs 1.036 ms (highest, records first),
+    // r04q_ab_mean_first_side_prio.jsonl).
     const char* pe = getenv("CDX_SIDE_PRIO");
-    const int want = pe ? atoi(pe) : 1;
+    const int want = pe ? atoi(pe) : 0;
     int least = 0, greatest = 0;
     hipError_t ce;
     if (want != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
