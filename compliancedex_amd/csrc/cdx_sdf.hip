@@ -486,16 +486,19 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
       ++visits;
       // per-face bounds against the lane's best: bit k set = some lane cannot rule face k out
       const float sb = sqrtf(best);  // (INF while the lane has no face yet)
-      const float a1 = 1.f - alpha, a2 = 1.f + alpha;
+      // skip ⇔ fd·(1 − α) > br·(1 + α) + β + sqrt(best), β = 1e-4·(|p| + bn + br) (the chunk bound's Lf > 0
+      // ∧ Lf² > best), as th = (br·(1 + α + 1e-4) + 1e-4·bn + (1e-4·|p| + sqrt(best))) / (1 − α) with the
+      // chunk's and the lane's terms hoisted and explicit FMAs: the rearrangement moves the threshold by
+      // a few ulps, nothing against the 1e-4 margins (α = 1: 1/(1 − α) = ∞, never skipped)
+      const float ia1 = 1.f / (1.f - alpha), k1 = (1.f + alpha) + 1e-4f, k0 = fmaf(1e-4f, pnorm, sb);
       unsigned mask = 0;
 #pragma unroll 8
       for (int k = 0; k < CHUNK; ++k) {
         const cdx::FaceRec& r = rr[k];
 #if !defined(CDX_SDF_NO_FACEBOUND)
         const float fx = p.x - r.bx, fy = p.y - r.by, fz = p.z - r.bz;
-        const float fd2 = fx * fx + fy * fy + fz * fz;
-        // skip ⇔ fd·a1 > br·a2 + β + sqrt(best)  (the chunk bound's Lf > 0 ∧ Lf² > best)
-        const float th = (r.br * a2 + 1e-4f * (pnorm + r.bn + r.br) + sb) / a1;
+        const float fd2 = fmaf(fx, fx, fmaf(fy, fy, fz * fz));
+        const float th = fmaf(r.br, k1, fmaf(1e-4f, r.bn, k0)) * ia1;
         const bool need = !(fd2 > th * th);
 #else
         const bool need = true;
