@@ -128,9 +128,13 @@ __global__ __launch_bounds__(256) void sdf_keys_kernel(const float* __restrict__
 }
 
 // One thread per sorted face slot; a 32-lane half-wave builds one chunk's sphere.
+// fsph[j] (the culled2 kernel's per-face test in one 16-byte read): the face's sphere centre and
+// br·(1 + α + 1e-4) + 1e-4·bn, α its chunk's conditioning margin — the face-dependent part of the bound's
+// threshold (sdf_culled2_kernel).
 __global__ __launch_bounds__(256) void sdf_chunk_kernel(const float* __restrict__ faces, int64_t F,
                                                         const int* __restrict__ order, cdx::FaceRec* __restrict__ rec,
-                                                        Sphere* __restrict__ sph, unsigned* ws) {
+                                                        Sphere* __restrict__ sph, float4* __restrict__ fsph,
+                                                        unsigned* ws) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = j < F;
   cdx::FaceRec r;
@@ -170,6 +174,12 @@ __global__ __launch_bounds__(256) void sdf_chunk_kernel(const float* __restrict_
   for (int o = 16; o >= 1; o >>= 1) {
     rad = fmaxf(rad, __shfl_xor(rad, o));
     kappa = fmaxf(kappa, __shfl_xor(kappa, o));
+  }
+  {
+    const float a = 1e-4f + 1e-5f * kappa;  // (the chunk's alpha, as below)
+    const float alpha = a < 1.f ? a : 1.f;
+    if (live) fsph[j] = make_float4(r.bx, r.by, r.bz, r.br * ((1.f + alpha) + 1e-4f) + 1e-4f * r.bn);
+    else if (j < (F + CHUNK - 1) / CHUNK * CHUNK) fsph[j] = make_float4(0.f, 0.f, 0.f, 0.f);  // (never tested: nf)
   }
   if ((j & (CHUNK - 1)) == 0 && live) {
     Sphere s;
@@ -356,11 +366,12 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
     int64_t F, const cdx::FaceRec* __restrict__ rec, const Sphere* __restrict__ sph, int C,
     const unsigned* __restrict__ ws, float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
     float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face,
-    unsigned long long* __restrict__ best_out, int count) {
+    unsigned long long* __restrict__ best_out, const float4* __restrict__ fsph, int count) {
   if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
   __shared__ float4 s_sa[SPH_BLK];  // cx, cy, cz, r
   __shared__ float2 s_sb[SPH_BLK];  // alpha, cnorm
   __shared__ float4 s_rec[4][REC_WORDS * CHUNK / 4];  // per wave: one chunk's face records
+  __shared__ float4 s_fs[4][CHUNK];                   // … and its per-face bounds (sdf_chunk_kernel fsph)
   __shared__ float s_val[4][64];
   __shared__ int s_idx[4][64];
   const int lane = threadIdx.x & 63;
@@ -465,14 +476,16 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
     // first chunk of the slice in this block: c ≡ c0 (mod cs), c ≥ 0 relative to cb
     const int cfirst = (int)(((int64_t)c0 - cb) % cs + cs) % cs;
     int c = next_needed(cfirst);
-    float4 pre[REC_V4];
+    float4 pre[REC_V4], pref = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c < nb) {
 #pragma unroll
       for (int i = 0; i < REC_V4; ++i) pre[i] = rec4[(int64_t)(cb + c) * (REC_WORDS * CHUNK / 4) + lane + 64 * i];
+      if (lane < CHUNK) pref = fsph[(int64_t)(cb + c) * CHUNK + lane];
     }
     while (c < nb) {
 #pragma unroll
       for (int i = 0; i < REC_V4; ++i) buf[lane + 64 * i] = pre[i];
+      if (lane < CHUNK) s_fs[w][lane] = pref;
       const int cur = c;
       const int64_t f0 = (int64_t)(cb + cur) * CHUNK;
       const float alpha = s_sb[cur].x;
@@ -480,6 +493,7 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
       if (c < nb) {  // the next chunk's records in flight while this one is processed
 #pragma unroll
         for (int i = 0; i < REC_V4; ++i) pre[i] = rec4[(int64_t)(cb + c) * (REC_WORDS * CHUNK / 4) + lane + 64 * i];
+        if (lane < CHUNK) pref = fsph[(int64_t)(cb + c) * CHUNK + lane];
       }
       const cdx::FaceRec* rr = reinterpret_cast<const cdx::FaceRec*>(buf);
       const int nf = (int)min((int64_t)CHUNK, F - f0);
@@ -490,15 +504,16 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
       // ∧ Lf² > best), as th = (br·(1 + α + 1e-4) + 1e-4·bn + (1e-4·|p| + sqrt(best))) / (1 − α) with the
       // chunk's and the lane's terms hoisted and explicit FMAs: the rearrangement moves the threshold by
       // a few ulps, nothing against the 1e-4 margins (α = 1: 1/(1 − α) = ∞, never skipped)
-      const float ia1 = 1.f / (1.f - alpha), k1 = (1.f + alpha) + 1e-4f, k0 = fmaf(1e-4f, pnorm, sb);
+      // (the face's part br·(1 + α + 1e-4) + 1e-4·bn comes precomputed with its centre, fsph)
+      const float ia1 = 1.f / (1.f - alpha), k0 = fmaf(1e-4f, pnorm, sb);
       unsigned mask = 0;
 #pragma unroll 8
       for (int k = 0; k < CHUNK; ++k) {
-        const cdx::FaceRec& r = rr[k];
 #if !defined(CDX_SDF_NO_FACEBOUND)
-        const float fx = p.x - r.bx, fy = p.y - r.by, fz = p.z - r.bz;
+        const float4 fs = s_fs[w][k];
+        const float fx = p.x - fs.x, fy = p.y - fs.y, fz = p.z - fs.z;
         const float fd2 = fmaf(fx, fx, fmaf(fy, fy, fz * fz));
-        const float th = fmaf(r.br, k1, fmaf(1e-4f, r.bn, k0)) * ia1;
+        const float th = (fs.w + k0) * ia1;
         const bool need = !(fd2 > th * th);
 #else
         const bool need = true;
@@ -683,11 +698,13 @@ int sdf_mode() {  // CDX_SDF_MODE=exact forces the brute-force kernel (benchmark
 }
 
 // Prepared mesh: [ws words: bbox min keys ×3, max keys ×3, may-NaN flag, 0][records: C·CHUNK FaceRec][spheres]
+// [face bounds: C·CHUNK float4]
 size_t mesh_rec_off() { return align256(8 * sizeof(unsigned)); }
 size_t mesh_sph_off(int64_t C) { return mesh_rec_off() + align256((size_t)C * CHUNK * sizeof(cdx::FaceRec)); }
+size_t mesh_fsph_off(int64_t C) { return mesh_sph_off(C) + align256((size_t)C * sizeof(Sphere)); }
 size_t mesh_bytes(int64_t F) {
   const int64_t C = (F + CHUNK - 1) / CHUNK;
-  return mesh_sph_off(C) + align256((size_t)C * sizeof(Sphere));
+  return mesh_fsph_off(C) + align256((size_t)C * CHUNK * sizeof(float4));
 }
 
 // Face records and chunk spheres in Morton order of the bounding box of the faces (and of the points,
@@ -719,7 +736,8 @@ int mesh_build(const float* faces, int64_t F, const float* points, int64_t P, ch
   bool ok = hipcub::DeviceRadixSort::SortPairs(base + o_tmp, t1, fk, fk + n, fv, fv + n, n, 0, 30, s) == hipSuccess;
   hipLaunchKernelGGL(sdf_chunk_kernel, dim3((unsigned)((C * CHUNK + 255) / 256)), dim3(256), 0, s, faces, F,
                      (const int*)(fv + n), reinterpret_cast<cdx::FaceRec*>(mesh + mesh_rec_off()),
-                     reinterpret_cast<Sphere*>(mesh + mesh_sph_off(C)), ws);
+                     reinterpret_cast<Sphere*>(mesh + mesh_sph_off(C)), reinterpret_cast<float4*>(mesh + mesh_fsph_off(C)),
+                     ws);
   ok = ok && hipGetLastError() == hipSuccess;
   ok = (hipFreeAsync(base, s) == hipSuccess) && ok;
   return ok ? CDX_OK : CDX_ELAUNCH;
@@ -760,7 +778,7 @@ int mesh_query(const char* mesh, const float* faces, int64_t F, const float* poi
   hipLaunchKernelGGL(sdf_culled2_kernel, dim3((unsigned)((P + 63) / 64 * SDF_SPLIT)), dim3(SDF_BLOCK), 0, s, points,
                      P, (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
                      reinterpret_cast<const Sphere*>(mesh + mesh_sph_off(C)), C, ws, sqdist, sign, normals, clst,
-                     face_idx, best, (int)g_sdf_count);
+                     face_idx, best, reinterpret_cast<const float4*>(mesh + mesh_fsph_off(C)), (int)g_sdf_count);
   hipLaunchKernelGGL(sdf_culled_finalize_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P, faces,
                      (const unsigned long long*)best, sqdist, sign, normals, clst, face_idx);
 #endif
