@@ -131,10 +131,13 @@ __global__ __launch_bounds__(256) void sdf_keys_kernel(const float* __restrict__
 // fsph[j] (the culled2 kernel's per-face test in one 16-byte read): the face's sphere centre and
 // br·(1 + α + 1e-4) + 1e-4·bn, α its chunk's conditioning margin — the face-dependent part of the bound's
 // threshold (sdf_culled2_kernel).
+// ssph[j / SUB] the same for each SUB-face run of a chunk (its bounding sphere: centre, radius·(1 + α +
+// 1e-4) + 1e-4·|centre|), tested before its faces.
+constexpr int SUB = 8;
 __global__ __launch_bounds__(256) void sdf_chunk_kernel(const float* __restrict__ faces, int64_t F,
                                                         const int* __restrict__ order, cdx::FaceRec* __restrict__ rec,
                                                         Sphere* __restrict__ sph, float4* __restrict__ fsph,
-                                                        unsigned* ws) {
+                                                        float4* __restrict__ ssph, unsigned* ws) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = j < F;
   cdx::FaceRec r;
@@ -155,10 +158,28 @@ __global__ __launch_bounds__(256) void sdf_chunk_kernel(const float* __restrict_
     }
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(ws + 6, 1u);
+  // the SUB-face run's box first (lanes j & ~(SUB − 1) … ), then the chunk's
 #pragma unroll
   for (int c = 0; c < 3; ++c)
 #pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) {
+    for (int o = 1; o < SUB; o <<= 1) {
+      lo[c] = fminf(lo[c], __shfl_xor(lo[c], o));
+      hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o));
+    }
+  const float sx = 0.5f * (lo[0] + hi[0]), sy = 0.5f * (lo[1] + hi[1]), sz = 0.5f * (lo[2] + hi[2]);
+  float srad = 0.f;
+  if (live) {
+    const cdx::F3 c = cdx::f3(sx, sy, sz);
+    srad = fmaxf(fmaxf(sqrtf(cdx::dotf(cdx::sub(r.v1, c), cdx::sub(r.v1, c))),
+                       sqrtf(cdx::dotf(cdx::sub(r.v2, c), cdx::sub(r.v2, c)))),
+                 sqrtf(cdx::dotf(cdx::sub(r.v3, c), cdx::sub(r.v3, c))));
+  }
+#pragma unroll
+  for (int o = 1; o < SUB; o <<= 1) srad = fmaxf(srad, __shfl_xor(srad, o));
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int o = SUB; o < CHUNK; o <<= 1) {
       lo[c] = fminf(lo[c], __shfl_xor(lo[c], o));
       hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o));
     }
@@ -180,6 +201,10 @@ __global__ __launch_bounds__(256) void sdf_chunk_kernel(const float* __restrict_
     const float alpha = a < 1.f ? a : 1.f;
     if (live) fsph[j] = make_float4(r.bx, r.by, r.bz, r.br * ((1.f + alpha) + 1e-4f) + 1e-4f * r.bn);
     else if (j < (F + CHUNK - 1) / CHUNK * CHUNK) fsph[j] = make_float4(0.f, 0.f, 0.f, 0.f);  // (never tested: nf)
+    // (a run without live faces gets a NaN centre: its test then always says "needed", and nf masks its faces)
+    if ((j & (SUB - 1)) == 0 && j < (F + CHUNK - 1) / CHUNK * CHUNK)
+      ssph[j / SUB] = make_float4(sx, sy, sz, srad * (1.f + 1e-5f) * ((1.f + alpha) + 1e-4f) +
+                                               1e-4f * sqrtf(sx * sx + sy * sy + sz * sz));
   }
   if ((j & (CHUNK - 1)) == 0 && live) {
     Sphere s;
@@ -366,12 +391,14 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
     int64_t F, const cdx::FaceRec* __restrict__ rec, const Sphere* __restrict__ sph, int C,
     const unsigned* __restrict__ ws, float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
     float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face,
-    unsigned long long* __restrict__ best_out, const float4* __restrict__ fsph, int count) {
+    unsigned long long* __restrict__ best_out, const float4* __restrict__ fsph, const float4* __restrict__ ssph,
+    int count) {
   if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
   __shared__ float4 s_sa[SPH_BLK];  // cx, cy, cz, r
   __shared__ float2 s_sb[SPH_BLK];  // alpha, cnorm
   __shared__ float4 s_rec[4][REC_WORDS * CHUNK / 4];  // per wave: one chunk's face records
   __shared__ float4 s_fs[4][CHUNK];                   // … and its per-face bounds (sdf_chunk_kernel fsph)
+  __shared__ float4 s_ss[4][CHUNK / SUB];             // … and its SUB-face runs' bounds (ssph)
   __shared__ float s_val[4][64];
   __shared__ int s_idx[4][64];
   const int lane = threadIdx.x & 63;
@@ -481,11 +508,13 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
 #pragma unroll
       for (int i = 0; i < REC_V4; ++i) pre[i] = rec4[(int64_t)(cb + c) * (REC_WORDS * CHUNK / 4) + lane + 64 * i];
       if (lane < CHUNK) pref = fsph[(int64_t)(cb + c) * CHUNK + lane];
+      else if (lane < CHUNK + CHUNK / SUB) pref = ssph[(int64_t)(cb + c) * (CHUNK / SUB) + lane - CHUNK];
     }
     while (c < nb) {
 #pragma unroll
       for (int i = 0; i < REC_V4; ++i) buf[lane + 64 * i] = pre[i];
       if (lane < CHUNK) s_fs[w][lane] = pref;
+      else if (lane < CHUNK + CHUNK / SUB) s_ss[w][lane - CHUNK] = pref;
       const int cur = c;
       const int64_t f0 = (int64_t)(cb + cur) * CHUNK;
       const float alpha = s_sb[cur].x;
@@ -494,6 +523,7 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
 #pragma unroll
         for (int i = 0; i < REC_V4; ++i) pre[i] = rec4[(int64_t)(cb + c) * (REC_WORDS * CHUNK / 4) + lane + 64 * i];
         if (lane < CHUNK) pref = fsph[(int64_t)(cb + c) * CHUNK + lane];
+        else if (lane < CHUNK + CHUNK / SUB) pref = ssph[(int64_t)(cb + c) * (CHUNK / SUB) + lane - CHUNK];
       }
       const cdx::FaceRec* rr = reinterpret_cast<const cdx::FaceRec*>(buf);
       const int nf = (int)min((int64_t)CHUNK, F - f0);
@@ -507,18 +537,30 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
       // (the face's part br·(1 + α + 1e-4) + 1e-4·bn comes precomputed with its centre, fsph)
       const float ia1 = 1.f / (1.f - alpha), k0 = fmaf(1e-4f, pnorm, sb);
       unsigned mask = 0;
-#pragma unroll 8
-      for (int k = 0; k < CHUNK; ++k) {
+      for (int sr = 0; sr < CHUNK / SUB; ++sr) {
 #if !defined(CDX_SDF_NO_FACEBOUND)
-        const float4 fs = s_fs[w][k];
-        const float fx = p.x - fs.x, fy = p.y - fs.y, fz = p.z - fs.z;
-        const float fd2 = fmaf(fx, fx, fmaf(fy, fy, fz * fz));
-        const float th = (fs.w + k0) * ia1;
-        const bool need = !(fd2 > th * th);
-#else
-        const bool need = true;
+        {  // the run's sphere first: a run every lane rules out skips its SUB face tests
+          const float4 ss = s_ss[w][sr];
+          const float ux = p.x - ss.x, uy = p.y - ss.y, uz = p.z - ss.z;
+          const float ud2 = fmaf(ux, ux, fmaf(uy, uy, uz * uz));
+          const float uth = (ss.w + k0) * ia1;
+          if (!__any(!(ud2 > uth * uth))) continue;
+        }
 #endif
-        if (__any(need) && k < nf) mask |= 1u << k;
+#pragma unroll
+        for (int kk = 0; kk < SUB; ++kk) {
+          const int k = SUB * sr + kk;
+#if !defined(CDX_SDF_NO_FACEBOUND)
+          const float4 fs = s_fs[w][k];
+          const float fx = p.x - fs.x, fy = p.y - fs.y, fz = p.z - fs.z;
+          const float fd2 = fmaf(fx, fx, fmaf(fy, fy, fz * fz));
+          const float th = (fs.w + k0) * ia1;
+          const bool need = !(fd2 > th * th);
+#else
+          const bool need = true;
+#endif
+          if (__any(need) && k < nf) mask |= 1u << k;
+        }
       }
       while (mask) {
         const int k = __builtin_ctz(mask);
@@ -698,13 +740,14 @@ int sdf_mode() {  // CDX_SDF_MODE=exact forces the brute-force kernel (benchmark
 }
 
 // Prepared mesh: [ws words: bbox min keys ×3, max keys ×3, may-NaN flag, 0][records: C·CHUNK FaceRec][spheres]
-// [face bounds: C·CHUNK float4]
+// [face bounds: C·CHUNK float4][run bounds: C·CHUNK/SUB float4]
 size_t mesh_rec_off() { return align256(8 * sizeof(unsigned)); }
 size_t mesh_sph_off(int64_t C) { return mesh_rec_off() + align256((size_t)C * CHUNK * sizeof(cdx::FaceRec)); }
 size_t mesh_fsph_off(int64_t C) { return mesh_sph_off(C) + align256((size_t)C * sizeof(Sphere)); }
+size_t mesh_ssph_off(int64_t C) { return mesh_fsph_off(C) + align256((size_t)C * CHUNK * sizeof(float4)); }
 size_t mesh_bytes(int64_t F) {
   const int64_t C = (F + CHUNK - 1) / CHUNK;
-  return mesh_fsph_off(C) + align256((size_t)C * CHUNK * sizeof(float4));
+  return mesh_ssph_off(C) + align256((size_t)C * (CHUNK / SUB) * sizeof(float4));
 }
 
 // Face records and chunk spheres in Morton order of the bounding box of the faces (and of the points,
@@ -737,7 +780,7 @@ int mesh_build(const float* faces, int64_t F, const float* points, int64_t P, ch
   hipLaunchKernelGGL(sdf_chunk_kernel, dim3((unsigned)((C * CHUNK + 255) / 256)), dim3(256), 0, s, faces, F,
                      (const int*)(fv + n), reinterpret_cast<cdx::FaceRec*>(mesh + mesh_rec_off()),
                      reinterpret_cast<Sphere*>(mesh + mesh_sph_off(C)), reinterpret_cast<float4*>(mesh + mesh_fsph_off(C)),
-                     ws);
+                     reinterpret_cast<float4*>(mesh + mesh_ssph_off(C)), ws);
   ok = ok && hipGetLastError() == hipSuccess;
   ok = (hipFreeAsync(base, s) == hipSuccess) && ok;
   return ok ? CDX_OK : CDX_ELAUNCH;
@@ -778,7 +821,8 @@ int mesh_query(const char* mesh, const float* faces, int64_t F, const float* poi
   hipLaunchKernelGGL(sdf_culled2_kernel, dim3((unsigned)((P + 63) / 64 * SDF_SPLIT)), dim3(SDF_BLOCK), 0, s, points,
                      P, (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
                      reinterpret_cast<const Sphere*>(mesh + mesh_sph_off(C)), C, ws, sqdist, sign, normals, clst,
-                     face_idx, best, reinterpret_cast<const float4*>(mesh + mesh_fsph_off(C)), (int)g_sdf_count);
+                     face_idx, best, reinterpret_cast<const float4*>(mesh + mesh_fsph_off(C)),
+                     reinterpret_cast<const float4*>(mesh + mesh_ssph_off(C)), (int)g_sdf_count);
   hipLaunchKernelGGL(sdf_culled_finalize_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P, faces,
                      (const unsigned long long*)best, sqdist, sign, normals, clst, face_idx);
 #endif
