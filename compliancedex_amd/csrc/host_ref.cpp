@@ -179,4 +179,18 @@ void cdxh_sdf_forward(const float* points, int64_t P, const float* faces, int64_
   }
 }
 
+// Test-only: face_dist2 (the culled kernels' evaluation from a face record) and point_face's squared
+// distance for n (point, face) pairs — tests/test_sdf_cpu.py checks them bit-identical.
+void cdxh_face_dist2(const float* points, const float* faces, int64_t n, float* d_rec, float* d_ref) {
+  for (int64_t i = 0; i < n; ++i) {
+    const cdx::F3 p = cdx::f3(points[3 * i], points[3 * i + 1], points[3 * i + 2]);
+    const float* v = faces + 9 * i;
+    const cdx::F3 v1 = cdx::f3(v[0], v[1], v[2]), v2 = cdx::f3(v[3], v[4], v[5]), v3 = cdx::f3(v[6], v[7], v[8]);
+    d_rec[i] = cdx::face_dist2(p, cdx::face_rec(v1, v2, v3, (int)i));
+    cdx::F3 c, nrm;
+    int sg;
+    d_ref[i] = cdx::point_face(p, v1, v2, v3, c, nrm, sg);
+  }
+}
+
 }  // extern "C"
