@@ -428,12 +428,21 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
     return nb;
   };
 
-  // pass 1 (all chunks): upper bound on the answer, and the chunk that gives it (the lane's nearest, roughly)
+  // pass 1 (this slice's chunks — any subset bounds the answer from above, and the slices interleave over
+  // the whole Morton order): upper bound on the answer, and the chunk that gives it (the lane's nearest,
+  // roughly)
   float ub = INFINITY;
   int uc = 0;
+#if defined(CDX_SDF_PASS1_ALL)
+  constexpr int p1s = 4;
+  const int p1c = w;
+#else
+  constexpr int p1s = 4 * SDF_SPLIT;
+  const int p1c = 4 * slice + w;
+#endif
   for (int cb = 0; cb < C; cb += SPH_BLK) {
     const int nb = stage(cb);
-    for (int c = w; c < nb; c += 4) {
+    for (int c = (int)(((int64_t)p1c - cb) % p1s + p1s) % p1s; c < nb; c += p1s) {
       const float4 a = s_sa[c];
       const float2 b = s_sb[c];
       const float dx = p.x - a.x, dy = p.y - a.y, dz = p.z - a.z;
