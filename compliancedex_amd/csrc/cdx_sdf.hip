@@ -366,9 +366,9 @@ static_assert(REC_WORDS * CHUNK % (64 * 4) == 0, "a chunk's records load as whol
 constexpr int REC_V4 = REC_WORDS * CHUNK / (64 * 4);   // dwordx4 loads per lane per chunk (5)
 
 #ifndef CDX_SDF_SPLIT
-#define CDX_SDF_SPLIT 2
+#define CDX_SDF_SPLIT 4
 #endif
-constexpr int SDF_SPLIT = CDX_SDF_SPLIT;  // workgroups per 64-point group (chunk slices; 2: profiles/r04i_*, r04j_*)
+constexpr int SDF_SPLIT = CDX_SDF_SPLIT;  // workgroups per 64-point group (chunk slices; 4 since the per-slice bound pass: profiles/r04y4_*)
 
 // (distance, face) as one unsigned 64-bit word whose order is the winner rule's: a non-negative float's
 // bits order as unsigned integers, ties then go to the smaller index.
@@ -382,8 +382,9 @@ __device__ inline unsigned long long pack_best(float d, int idx) {
 // workgroups shortens its critical path — one group near no face (a point deep inside or far outside)
 // otherwise holds its CU while the others idle (PMC: mean wave life ≈ 1/3 of the kernel) — and gives the
 // dispatcher SPLIT× more, shorter workgroups to balance.  Each workgroup first takes the upper bound over
-// ALL chunks (pass 1) and the faces of the chunk nearest the group's middle point (the seed, shared over
-// its waves), so every slice starts with a best near the true distance; a face is still skipped only when
+// its own slice's chunks (pass 1; the slices interleave over the whole Morton order, so the bound stays
+// close to the one over all chunks) and the faces of the slice's chunk nearest the group's middle point
+// (the seed, shared over its waves), so every slice starts with a best near the true distance; a face is still skipped only when
 // its bound lies above the lane's best (which only decreases), so the global lexicographic minimum over the
 // evaluated faces is the brute-force winner.
 __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
