@@ -255,6 +255,10 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled_kernel(
     const unsigned* __restrict__ ws, float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
     float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face, int count) {
   if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
+#if SDF_COMPACT
+  __shared__ unsigned long long s_best[4][64];  // per wave: each lane's packed (distance, face) best
+  __shared__ unsigned short s_pair[4][128];     // … and its pending (lane << 5 | face) pairs
+#endif
   __shared__ float s_val[4][64];
   __shared__ int s_idx[4][64];
   const int lane = threadIdx.x & 63;
@@ -365,6 +369,11 @@ constexpr int REC_WORDS = sizeof(cdx::FaceRec) / 4;  // 40
 static_assert(REC_WORDS * CHUNK % (64 * 4) == 0, "a chunk's records load as whole dwordx4 per lane");
 constexpr int REC_V4 = REC_WORDS * CHUNK / (64 * 4);   // dwordx4 loads per lane per chunk (5)
 
+#if defined(CDX_SDF_NO_COMPACT)
+#define SDF_COMPACT 0
+#else
+#define SDF_COMPACT 1  // pass 2 evaluates compacted (lane, face) pairs (sdf_culled2_kernel)
+#endif
 #ifndef CDX_SDF_SPLIT
 #define CDX_SDF_SPLIT 4
 #endif
@@ -400,6 +409,10 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
   __shared__ float4 s_rec[4][REC_WORDS * CHUNK / 4];  // per wave: one chunk's face records
   __shared__ float4 s_fs[4][CHUNK];                   // … and its per-face bounds (sdf_chunk_kernel fsph)
   __shared__ float4 s_ss[4][CHUNK / SUB];             // … and its SUB-face runs' bounds (ssph)
+#if SDF_COMPACT
+  __shared__ unsigned long long s_best[4][64];  // per wave: each lane's packed (distance, face) best
+  __shared__ unsigned short s_pair[4][128];     // … and its pending (lane << 5 | face) pairs
+#endif
   __shared__ float s_val[4][64];
   __shared__ int s_idx[4][64];
   const int lane = threadIdx.x & 63;
@@ -472,7 +485,7 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
   float4* buf = s_rec[w];
   float best = INFINITY;
   int bidx = 0x7fffffff;
-  unsigned evaluated = 0, visits = 0;  // faces evaluated / chunks visited by this wave (diagnostic counts)
+  unsigned evaluated = 0, visits = 0, pairs = 0;  // faces evaluated / chunks visited by this wave (diagnostic counts)
   {
     const int nf = (int)min((int64_t)CHUNK, F - (int64_t)seed * CHUNK);
     for (int k = w; k < nf; k += 4) {
@@ -493,6 +506,9 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
     }
     __syncthreads();  // s_val / s_idx are written again at the end
   }
+#if SDF_COMPACT
+  s_best[w][lane] = pack_best(best, bidx);
+#endif
 
   // pass 2 (this slice's chunks): exact distances over the chunks some lane cannot rule out
   const int c0 = 4 * slice + w, cs = 4 * SDF_SPLIT;
@@ -547,6 +563,9 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
       // (the face's part br·(1 + α + 1e-4) + 1e-4·bn comes precomputed with its centre, fsph)
       const float ia1 = 1.f / (1.f - alpha), k0 = fmaf(1e-4f, pnorm, sb);
       unsigned mask = 0;
+#if SDF_COMPACT
+      unsigned lmask = 0;  // this lane's faces
+#endif
       for (int sr = 0; sr < CHUNK / SUB; ++sr) {
 #if !defined(CDX_SDF_NO_FACEBOUND)
         {  // the run's sphere first: a run every lane rules out skips its SUB face tests
@@ -569,9 +588,55 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
 #else
           const bool need = true;
 #endif
+#if SDF_COMPACT
+          if (need && k < nf && live) lmask |= 1u << k;
+          if (__any(need && live) && k < nf) mask |= 1u << k;
+#else
           if (__any(need) && k < nf) mask |= 1u << k;
+#endif
         }
       }
+#if SDF_COMPACT
+      // the (lane, face) pairs some lane needs, packed 64 to a round: lane i of a round evaluates pair i
+      // (its point read from the owning lane) and folds the result into the owner's packed best in LDS
+      // with a 64-bit minimum (the same lexicographic (distance, index) order); the owners read their
+      // best back after the chunk.  A face only some lanes need no longer costs the whole wave.
+      auto eval_round = [&](int n) {
+        const unsigned e = s_pair[w][lane];
+        const int l = lane < n ? (int)(e >> 5) : lane;
+        const float qx = __shfl(p.x, l), qy = __shfl(p.y, l), qz = __shfl(p.z, l);
+        if (lane < n) {
+          const cdx::FaceRec& r = rr[e & 31u];
+          const float d = cdx::face_dist2(cdx::f3(qx, qy, qz), r);
+          atomicMin(&s_best[w][l], pack_best(d, r.idx));
+        }
+        pairs += (unsigned)n;
+      };
+      int cnt = 0;
+      while (mask) {
+        const int k = __builtin_ctz(mask);
+        mask &= mask - 1;
+        const bool mine = (lmask >> k) & 1u;
+        const unsigned long long b = __ballot(mine);
+        if (mine)
+          s_pair[w][cnt + __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u))] =
+              (unsigned short)((lane << 5) | k);
+        cnt += __popcll(b);
+        if (cnt >= 64) {
+          eval_round(64);
+          cnt -= 64;
+          const unsigned short tail = s_pair[w][64 + lane];  // (read before any lane overwrites its slot)
+          __builtin_amdgcn_wave_barrier();
+          if (lane < cnt) s_pair[w][lane] = tail;
+        }
+      }
+      if (cnt > 0) eval_round(cnt);
+      {
+        const unsigned long long bb = s_best[w][lane];
+        best = __uint_as_float((unsigned)(bb >> 32));
+        bidx = (int)(unsigned)bb;
+      }
+#else
       while (mask) {
         const int k = __builtin_ctz(mask);
         mask &= mask - 1;
@@ -580,12 +645,13 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
         const float d = cdx::face_dist2(p, r);
         if (d < best || (d == best && r.idx < bidx)) { best = d; bidx = r.idx; }
       }
+#endif
     }
   }
   if (count) {
     const unsigned long long nl = __popcll(__ballot(live));
     if (lane == 0) {
-      atomicAdd(&g_sdf_stats[0], (unsigned long long)evaluated * nl);
+      atomicAdd(&g_sdf_stats[0], (unsigned long long)evaluated * nl + pairs);
       atomicAdd(&g_sdf_stats[3], (unsigned long long)visits);
       if (w == 0 && slice == 0) atomicAdd(&g_sdf_stats[2], nl);
     }

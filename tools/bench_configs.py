@@ -273,8 +273,25 @@ def case_c4kin(dev):
     def loop():
         kin.optimize(qf, tg, cp, 1, TriangleMesh(mesh.vertices, mesh.triangles), verbose=False)
     sec = timed(loop, 3, warm=1)
+    # the culled forward's work counters over one more loop (after the timing): pairs evaluated per call
+    import ctypes
+    from compliancedex_amd import _native as N
+    lib = N.load()
+    st = (ctypes.c_uint64 * 3)()
+    visits = ctypes.c_uint64(0)
+    N.check(lib.cdx_sdf_stats(1, None, N.stream_ptr(dev)), "cdx_sdf_stats")
+    N.check(lib.cdx_sdf_chunk_visits(ctypes.byref(visits), N.stream_ptr(dev)), "cdx_sdf_chunk_visits")
+    loop()
+    N.check(lib.cdx_sdf_stats(0, st, N.stream_ptr(dev)), "cdx_sdf_stats")
+    N.check(lib.cdx_sdf_chunk_visits(ctypes.byref(visits), N.stream_ptr(dev)), "cdx_sdf_chunk_visits")
+    calls = max(1, int(st[2]) // (4 * E))
     print(json.dumps({"case": "config4_kin_sdf_loop", "E": E, "iterations": iters, "faces": int(len(mesh.triangles)),
-                      "ms_per_iteration": sec / iters * 1e3, "evals_per_s": E * iters / sec}), flush=True)
+                      "ms_per_iteration": sec / iters * 1e3, "evals_per_s": E * iters / sec,
+                      "sdf_calls": calls, "pairs_evaluated_per_call": int(st[0]) / calls,
+                      "pairs_exact_path_per_call": int(st[1]) / calls,
+                      "brute_force_pairs_per_call": 4 * E * len(mesh.triangles),
+                      "chunk_visits_per_point_group_wave": int(visits.value) / max(1, 4 * (int(st[2]) // 64))}),
+          flush=True)
 
 
 def case_c5(dev):
