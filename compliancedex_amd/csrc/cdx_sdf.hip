@@ -133,7 +133,10 @@ __global__ __launch_bounds__(256) void sdf_keys_kernel(const float* __restrict__
 // threshold (sdf_culled2_kernel).
 // ssph[j / SUB] the same for each SUB-face run of a chunk (its bounding sphere: centre, radius·(1 + α +
 // 1e-4) + 1e-4·|centre|), tested before its faces.
-constexpr int SUB = 8;
+#ifndef CDX_SDF_SUB
+#define CDX_SDF_SUB 8
+#endif
+constexpr int SUB = CDX_SDF_SUB;
 __global__ __launch_bounds__(256) void sdf_chunk_kernel(const float* __restrict__ faces, int64_t F,
                                                         const int* __restrict__ order, cdx::FaceRec* __restrict__ rec,
                                                         Sphere* __restrict__ sph, float4* __restrict__ fsph,
@@ -395,7 +398,10 @@ __device__ inline unsigned long long pack_best(float d, int idx) {
 // close to the one over all chunks) and the faces of the slice's chunk nearest the group's middle point
 // (the seed, shared over its waves), so every slice starts with a best near the true distance; a face is still skipped only when
 // its bound lies above the lane's best (which only decreases), so the global lexicographic minimum over the
-// evaluated faces is the brute-force winner.
+// evaluated faces is the brute-force winner.  Pass 2 evaluates (lane, face) pairs, not faces: each lane keeps
+// the mask of the chunk's faces its own bounds cannot rule out, and the wave packs those pairs 64 to a round
+// (SDF_COMPACT; a wave of far points otherwise evaluated every face any lane needed — 3× the pairs).
+// (The order of evaluation is free: the result is a minimum.)
 __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
     const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
     int64_t F, const cdx::FaceRec* __restrict__ rec, const Sphere* __restrict__ sph, int C,
@@ -562,6 +568,9 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
       // a few ulps, nothing against the 1e-4 margins (α = 1: 1/(1 − α) = ∞, never skipped)
       // (the face's part br·(1 + α + 1e-4) + 1e-4·bn comes precomputed with its centre, fsph)
       const float ia1 = 1.f / (1.f - alpha), k0 = fmaf(1e-4f, pnorm, sb);
+#if defined(CDX_SDF_TH_FMA)
+      const float k1 = k0 * ia1;
+#endif
       unsigned mask = 0;
 #if SDF_COMPACT
       unsigned lmask = 0;  // this lane's faces
@@ -572,7 +581,11 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
           const float4 ss = s_ss[w][sr];
           const float ux = p.x - ss.x, uy = p.y - ss.y, uz = p.z - ss.z;
           const float ud2 = fmaf(ux, ux, fmaf(uy, uy, uz * uz));
+#if defined(CDX_SDF_TH_FMA)
+          const float uth = fmaf(ss.w, ia1, k1);
+#else
           const float uth = (ss.w + k0) * ia1;
+#endif
           if (!__any(!(ud2 > uth * uth))) continue;
         }
 #endif
@@ -583,7 +596,11 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
           const float4 fs = s_fs[w][k];
           const float fx = p.x - fs.x, fy = p.y - fs.y, fz = p.z - fs.z;
           const float fd2 = fmaf(fx, fx, fmaf(fy, fy, fz * fz));
+#if defined(CDX_SDF_TH_FMA)
+          const float th = fmaf(fs.w, ia1, k1);
+#else
           const float th = (fs.w + k0) * ia1;
+#endif
           const bool need = !(fd2 > th * th);
 #else
           const bool need = true;
