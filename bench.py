@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-E", type=int, default=256)
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal on one GPU)")
+    ap.add_argument("--no-config4", action="store_true", help="skip the config-4 SDF/Kin block (N = 1)")
+    ap.add_argument("--config4-iters", type=int, default=20)
     return ap.parse_args()
 
 
@@ -117,6 +119,91 @@ def traffic_block(E, n, key, algorithmic):
 
 
 CONFIG3 = ["banana", "mug", "mug2", "hammer", "lego", "coffeebottle", "box", "realsense"]
+F32_VALU_PEAK_TFLOPS = 157.3  # gfx950 f32 vector (MI355X_MICROARCH.md)
+SDF_FLOPS_PER_PAIR = 46       # face_dist2's usual branch, 3 IEEE divisions counted as 1 flop each (cdx_sdf.h)
+
+
+def config4_kin(args, dev):
+    """Config 4's SDF leg (BASELINE configs[3]: iiwa7_allegro arm + hand, TorchSDF on): the fused KinGraspOptimizer
+    loop (optimize_pregrasp.py:183-223) at E = 16 384 candidates on the 16 384-face banana — per iteration three
+    TorchSDF queries on prepared meshes (3 × 65 536 points), cdx_kin_cost, cdx_kin_step — timed over
+    ``--config4-iters`` iterations after a warm-up call (HIP events on the loop's stream), then the three queries
+    of one iteration alone (the TorchSDF forward) and the culled kernel's work counters."""
+    import copy
+    import ctypes
+
+    import torch
+
+    from compliancedex_amd import KinGraspOptimizer
+    from compliancedex_amd import _native as N
+    from compliancedex_amd.workloads import banana_mesh, config4_kin_inputs
+
+    lib = N.load()
+    E, iters = 16384, args.config4_iters
+    links, offs, palm, q, target, comp = config4_kin_inputs(E, device=dev)
+    kin = KinGraspOptimizer("iiwa7_allegro", links, offs, palm_offset=palm.tolist(), num_iters=iters,
+                            optimize_target=True, ref_q=[0.0] * 23, device=dev)
+    x = [torch.from_numpy(a).to(dev) for a in (q, target, comp)]
+    mesh = banana_mesh()
+    kin.optimize(*x, 1, copy.deepcopy(mesh), verbose=False)  # warm-up: prepares, allocator, clocks
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    # the timed region: the iterations (the two meshes are prepared once per optimize call, before it)
+    kin.loop_events = ev[:2]
+    res = kin.optimize(*x, 1, copy.deepcopy(mesh), verbose=False)
+    kin.loop_events = None
+    torch.cuda.synchronize()
+    ms_iter = ev[0].elapsed_time(ev[1]) / iters
+    # the TorchSDF forward of one iteration alone (the loop's three queries on its final fingertips / targets)
+    from compliancedex_amd import PreparedMesh
+    from compliancedex_amd.optimizers import _face_vertices
+    m = copy.deepcopy(mesh)
+    faces = _face_vertices(m, dev)
+    m.scale(0.9, center=[0, 0, 0])
+    meshes = (PreparedMesh(_face_vertices(m, dev)), PreparedMesh(faces), PreparedMesh(faces))
+    from compliancedex_amd import DifferentiableRobotModel
+    tips = (DifferentiableRobotModel("iiwa7_allegro", device=dev).compute_forward_kinematics(
+        res[0].detach(), links, offsets=offs)[0].view(-1, 3) + torch.from_numpy(palm).to(dev)).contiguous()
+    pts = (tips, tips, res[2].detach().reshape(-1, 3).contiguous())
+    for mh, pt in zip(meshes, pts):
+        mh.query(pt)
+    st = (ctypes.c_uint64 * 3)()
+    visits = ctypes.c_uint64(0)
+    N.check(lib.cdx_sdf_stats(1, None, N.stream_ptr(dev)), "cdx_sdf_stats")
+    for mh, pt in zip(meshes, pts):
+        mh.query(pt)
+    N.check(lib.cdx_sdf_stats(0, st, N.stream_ptr(dev)), "cdx_sdf_stats")
+    N.check(lib.cdx_sdf_chunk_visits(ctypes.byref(visits), N.stream_ptr(dev)), "cdx_sdf_chunk_visits")
+    reps = 10
+    ev[2].record()
+    for _ in range(reps):
+        for mh, pt in zip(meshes, pts):
+            mh.query(pt)
+    ev[3].record()
+    torch.cuda.synchronize()
+    fwd_ms = ev[2].elapsed_time(ev[3]) / reps
+    n_pts, F = int(st[2]), int(faces.shape[0])
+    brute = n_pts * F
+    evaluated = int(st[0]) + int(st[1])
+    achieved = evaluated * SDF_FLOPS_PER_PAIR / (fwd_ms * 1e-3) / 1e12
+    brute_eq = brute * SDF_FLOPS_PER_PAIR / (fwd_ms * 1e-3) / 1e12
+    return {"workload": "config 4: KinGraspOptimizer (fused) on iiwa7_allegro (23 DOF, chain depth 13), "
+                        f"E={E} candidates, 16 384-face banana mesh, optimize_target, 3 TorchSDF queries per iteration",
+            "iterations": iters, "ms_per_iteration": ms_iter, "evals_per_s": E / (ms_iter * 1e-3),
+            "launches_per_iteration": "3 TorchSDF queries (init/bbox, Morton keys, radix sort, sdf_tree_kernel, "
+                                      "exact-path gate each) + cdx_kin_cost + cdx_kin_step + the loss sum",
+            "roofline_sdf": {"bound": "valu", "kernel": "sdf_tree_kernel (+ per-query bbox, Morton keys, radix sort)",
+                             "fwd_3calls_ms": fwd_ms, "points": n_pts, "faces": F, "brute_force_pairs": brute,
+                             "pairs_evaluated": int(st[0]), "pairs_exact_path": int(st[1]),
+                             "pairs_per_point": int(st[0]) / max(1, n_pts),
+                             "chunk_visits_per_wave": int(visits.value) / max(1, (n_pts + 63) // 64),
+                             "evaluated_over_brute_force": evaluated / brute,
+                             "flops_per_pair": SDF_FLOPS_PER_PAIR, "achieved": achieved, "peak": F32_VALU_PEAK_TFLOPS,
+                             "unit": "TFLOP/s (f32 vector)", "frac": achieved / F32_VALU_PEAK_TFLOPS,
+                             "brute_force_equivalent": brute_eq,
+                             "note": "achieved counts only the evaluated pairs' face_dist2 flops over the three "
+                                     "queries' whole forward (sorts and culling tests included), so it falls as the "
+                                     "culling improves; brute_force_equivalent = the reference's brute-force pair "
+                                     "flops (P·F·46) over the same time"}}
 
 
 def main():
@@ -375,6 +462,8 @@ def main():
         cands = [k for k in stage_of if k in out and out[k]["achieved"] and live[stage_of[k]]]
         dom = max(cands, key=lambda k: out[k]["flops_per_launch"] / out[k]["achieved"]) if cands else "roofline_refine"
         out["roofline"] = dict(out[dom], which=dom)
+        if world == 1 and not args.no_config4:
+            out["config4_kin"] = config4_kin(args, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, ref_q, cfg)
         print(json.dumps(out), flush=True)

@@ -18,6 +18,6 @@ from .force_eq import force_eq_reward  # noqa: F401
 from .optimizers import (GPISGraspOptimizer, KinGPISGraspOptimizer, KinGraspOptimizer,  # noqa: F401
                          SDFGraspOptimizer, TriangleMesh)
 from .robot_model import DifferentiableRobotModel  # noqa: F401
-from .torchsdf import compute_sdf, compute_sdf_with_faces, index_vertices_by_faces  # noqa: F401
+from .torchsdf import PreparedMesh, compute_sdf, compute_sdf_with_faces, index_vertices_by_faces  # noqa: F401
 
 __version__ = "0.1.0"

@@ -65,6 +65,22 @@ class CdxKinParams(C.Structure):
     _fields_ = [("fe", CdxForceEq), ("ref_q", C.c_float * MAX_DOFS)]
 
 
+class CdxKinOpt(C.Structure):
+    _fields_ = [("rule", C.c_int32), ("clamp_box", C.c_int32), ("lr", C.c_double * 3), ("beta1", C.c_double),
+                ("beta2", C.c_double), ("eps", C.c_double), ("alpha", C.c_double), ("palm_offset", C.c_float * 3),
+                ("box_lb", C.c_float * (MAX_TIPS * 3)), ("box_ub", C.c_float * (MAX_TIPS * 3)), ("_pad", C.c_int32)]
+
+
+KIN_OPT_FIELDS = ["pose", "target", "comp", "g_pose", "g_target", "g_comp", "m_pose", "v_pose", "m_target", "v_target",
+                  "m_comp", "v_comp", "loss"]
+
+
+class CdxKinOptBuffers(C.Structure):
+    _fields_ = ([(n, C.c_void_p) for n in KIN_OPT_FIELDS] + [("margin", C.c_void_p * 2), ("normal", C.c_void_p * 2)] +
+                [(n, C.c_void_p) for n in ("opt_value", "opt_margin", "opt_normal", "opt_pose", "opt_target",
+                                            "opt_comp", "any", "tips")])
+
+
 class CdxAdam(C.Structure):
     _fields_ = [("lr", C.c_double * 5), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double),
                 ("comp_min", C.c_double), ("target_lb", C.c_double * (MAX_TIPS * 3)),
@@ -137,7 +153,8 @@ _SIGS = {
                      [_P] * 8),
     "cdx_sdf_mesh_bytes": (C.c_size_t, [_I64]),
     "cdx_sdf_mesh_prepare": (C.c_int, [_P, _I64, _P, _P]),
-    "cdx_sdf_query": (C.c_int, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
+    "cdx_sdf_query_workspace": (C.c_size_t, [_I64]),
+    "cdx_sdf_query": (C.c_int, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, C.c_size_t, _P]),
     "cdx_version": (C.c_char_p, []),
     "cdx_abi_sizes": (None, [C.POINTER(C.c_size_t)]),
     "cdx_selftest_mfma_f64": (C.c_int, [_P, _P, _P, _P]),
@@ -145,6 +162,8 @@ _SIGS = {
     "cdx_optimizer_step": (C.c_int, [C.POINTER(CdxAdam), C.POINTER(CdxOptBuffers), _I64, C.c_int32, C.c_int32,
                                      C.c_int32, _P]),
     "cdx_profile_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    "cdx_kin_step": (C.c_int, [C.POINTER(CdxChain), C.POINTER(CdxKinOpt), C.POINTER(CdxKinOptBuffers), _I64, C.c_int32,
+                               C.c_int32, C.c_int32, _P]),
 }
 
 _lib = None
@@ -170,11 +189,11 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        sizes = (C.c_size_t * 9)()
+        sizes = (C.c_size_t * 12)()
         lib.cdx_abi_sizes(sizes)
         mine = [C.sizeof(CdxGpis), C.sizeof(CdxBody), C.sizeof(CdxChain), C.sizeof(CdxProblem),
                 C.sizeof(CdxCollision), C.sizeof(CdxAdam), C.sizeof(CdxOptBuffers), C.sizeof(CdxForceEq),
-                C.sizeof(CdxScreenReport)]
+                C.sizeof(CdxScreenReport), C.sizeof(CdxKinParams), C.sizeof(CdxKinOpt), C.sizeof(CdxKinOptBuffers)]
         if list(sizes) != mine:
             raise ImportError(f"ABI struct size mismatch: library {list(sizes)} vs binding {mine}")
         info = build_info()

@@ -1347,4 +1347,7 @@ extern "C" void cdx_abi_sizes(size_t* out) {
   out[6] = sizeof(cdx_opt_buffers);
   out[7] = sizeof(cdx_force_eq);
   out[8] = sizeof(cdx_screen_report);
+  out[9] = sizeof(cdx_kin_params);
+  out[10] = sizeof(cdx_kin_opt);
+  out[11] = sizeof(cdx_kin_opt_buffers);
 }

@@ -188,3 +188,153 @@ extern "C" int cdx_kin_cost(const cdx_chain* chain, const cdx_kin_params* p, int
 #undef CDX_KIN_LAUNCH
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
+
+// ------------------------------------------------------------------ Kin / SDF optimiser step
+// One launch per iteration after cdx_kin_cost (optimize_pregrasp.py:212-223 Kin, :299-314 SDF): threads
+// (candidate e, tip f), T to a candidate, 64 / T candidates to a 64-thread workgroup.
+namespace {
+
+// Joint-angle reader over the workgroup's LDS copy of the candidate's updated row.
+struct QRowLds {
+  const float* p;
+  __device__ __forceinline__ float operator[](int i) const { return p[i]; }
+};
+
+__device__ __forceinline__ float adam_f32(float p, float g, float& m, float& v, float w1, float b2, float w2, float bc2s,
+                                          float eps, float step) {
+  // torch.optim.Adam's single-tensor / foreach update in float32 opmath: m.lerp_(g, 1 − β1);
+  // v.mul_(β2).addcmul_(g, g, 1 − β2); p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, −lr/bc1)
+  m = m + w1 * (g - m);
+  v = v * b2 + (w2 * g) * g;
+  const float denom = sqrtf(v) / bc2s + eps;
+  return p + step * (m / denom);
+}
+
+__device__ __forceinline__ float rmsprop_f32(float p, float g, float& v, float a, float w2, float eps, float lr) {
+  // torch.optim.RMSprop (no momentum, not centred): v.mul_(α).addcmul_(g, g, 1 − α); p.addcdiv_(g, sqrt(v) + eps, −lr)
+  v = v * a + (w2 * g) * g;
+  const float avg = sqrtf(v) + eps;
+  return p + lr * (g / avg);
+}
+
+__global__ __launch_bounds__(64) void kin_step_kernel(cdx_chain chain, cdx_kin_opt cfg, cdx_kin_opt_buffers b, int64_t E,
+                                                      int T, int D, int s, int finalize) {
+  __shared__ float s_q[64 * CDX_MAX_DOFS];  // updated joint rows of the workgroup's candidates (G·D ≤ 64·32)
+  const int G = 64 / T;
+  const int t = threadIdx.x;
+  const int gl = t / T, f = t - gl * T;
+  const int64_t e = (int64_t)blockIdx.x * G + gl;
+  const bool on = gl < G && e < E;
+  const int64_t r = e * T + f;
+  // commit the previous iteration's margin / normal if some candidate improved in it (its flags are final:
+  // that step kernel has finished)
+  if (s > 0 && b.any[(s - 1) % 3] && on) {
+    const int ps = (s - 1) & 1;
+    b.opt_margin[r] = b.margin[ps][r];
+    for (int i = 0; i < 3; ++i) b.opt_normal[3 * r + i] = b.normal[ps][3 * r + i];
+  }
+  if (finalize) return;
+  if (blockIdx.x == 0 && t == 0) b.any[(s + 1) % 3] = 0u;  // (written at s − 2, read at s − 1: free now)
+  const bool kin = cfg.rule == 0;
+  const int npose = kin ? D : 3;               // pose entries this thread owns: q[i], i ≡ f (mod T) / tip f's xyz
+  // best iterate (before the step, with the parameters the loss was computed on)
+  bool flag = false;
+  if (on) {
+    const double l = b.loss[e];
+    flag = l < (double)b.opt_value[e];
+    if (flag) {
+      if (f == 0) b.opt_value[e] = (float)l;
+      if (kin) {
+        for (int i = f; i < D; i += T) b.opt_pose[e * D + i] = b.pose[e * D + i];
+      } else {
+        for (int i = 0; i < 3; ++i) b.opt_pose[3 * r + i] = b.pose[3 * r + i];
+      }
+      for (int i = 0; i < 3; ++i) b.opt_target[3 * r + i] = b.target[3 * r + i];
+      b.opt_comp[r] = b.comp[r];
+    }
+  }
+  if (__any(flag) && (t & 63) == 0) atomicOr(b.any + s % 3, 1u);
+  if (!on) return;
+  const double step = (double)(s + 1);
+  float w1 = 0.f, b2 = 0.f, w2 = 0.f, bc2s = 1.f, eps = (float)cfg.eps, sz[3] = {0.f, 0.f, 0.f};
+  if (kin) {
+    const double bc1 = 1.0 - pow(cfg.beta1, step), bc2 = 1.0 - pow(cfg.beta2, step);
+    w1 = (float)(1.0 - cfg.beta1);
+    b2 = (float)cfg.beta2;
+    w2 = (float)(1.0 - cfg.beta2);
+    bc2s = (float)sqrt(bc2);
+    for (int g = 0; g < 3; ++g) sz[g] = (float)(-(cfg.lr[g] / bc1));
+  } else {
+    b2 = (float)cfg.alpha;
+    w2 = (float)(1.0 - cfg.alpha);
+    for (int g = 0; g < 3; ++g) sz[g] = (float)(-cfg.lr[g]);
+  }
+  auto upd = [&](float* p, const float* g, float* m, float* v, int64_t k, int grp) {
+    if (cfg.lr[grp] == 0.0) return;
+    p[k] = kin ? adam_f32(p[k], g[k], m[k], v[k], w1, b2, w2, bc2s, eps, sz[grp])
+               : rmsprop_f32(p[k], g[k], v[k], b2, w2, eps, sz[grp]);
+  };
+  // pose: Kin — the joint angles this thread owns, and the whole updated row into LDS for the FK; SDF — tip f
+  if (kin) {
+    float* qs = s_q + gl * D;
+    for (int i = 0; i < D; ++i) {
+      const int64_t k = e * D + i;
+      float qn = b.pose[k];
+      if (cfg.lr[0] != 0.0) {
+        float m = b.m_pose[k], v = b.v_pose[k];
+        qn = adam_f32(qn, b.g_pose[k], m, v, w1, b2, w2, bc2s, eps, sz[0]);
+        if (i % T == f) { b.m_pose[k] = m; b.v_pose[k] = v; }
+      }
+      if (i % T == f) b.pose[k] = qn;
+      if (f == 0) qs[i] = qn;
+    }
+  } else {
+    for (int i = 0; i < 3; ++i) upd(b.pose, b.g_pose, b.m_pose, b.v_pose, 3 * r + i, 0);
+  }
+  for (int i = 0; i < 3; ++i) upd(b.target, b.g_target, b.m_target, b.v_target, 3 * r + i, 1);
+  upd(b.comp, b.g_comp, b.m_comp, b.v_comp, r, 2);
+  if (cfg.clamp_box)  // (:312-314) torch.clamp: NaN stays NaN
+    for (int i = 0; i < 3; ++i) {
+      const float lo = cfg.box_lb[3 * f + i], hi = cfg.box_ub[3 * f + i];
+      float x = b.target[3 * r + i];
+      x = x < lo ? lo : x;
+      b.target[3 * r + i] = x > hi ? hi : x;
+      if (!kin) {
+        float y = b.pose[3 * r + i];
+        y = y < lo ? lo : y;
+        b.pose[3 * r + i] = y > hi ? hi : y;
+      }
+    }
+  (void)npose;
+  if (!kin || !b.tips) return;
+  // the next iteration's fingertip f: FK(q) + palm offset (:148)
+  __syncthreads();
+  float pos[3];
+  cdx::fk_tip(chain, f, QRowLds{s_q + gl * D}, pos, nullptr);
+  for (int i = 0; i < 3; ++i) b.tips[3 * r + i] = pos[i] + cfg.palm_offset[i];
+}
+
+}  // namespace
+
+extern "C" int cdx_kin_step(const cdx_chain* chain, const cdx_kin_opt* cfg, const cdx_kin_opt_buffers* buf, int64_t E,
+                            int32_t n_tips, int32_t iteration, int32_t finalize, cdx_stream_t stream) {
+  if (!cfg || !buf || E < 0 || n_tips < 1 || n_tips > CDX_MAX_TIPS || iteration < 0 || (cfg->rule != 0 && cfg->rule != 1))
+    return CDX_EINVAL;
+  const bool kin = cfg->rule == 0;
+  if (kin && (!chain || chain->n_tips != n_tips || chain->n_dofs < 1 || chain->n_dofs > CDX_MAX_DOFS ||
+              chain->n_bodies < 1 || chain->n_bodies > CDX_MAX_BODIES))
+    return CDX_EINVAL;
+  if (E == 0) return CDX_OK;
+  const cdx_kin_opt_buffers& b = *buf;
+  if (!b.margin[0] || !b.margin[1] || !b.normal[0] || !b.normal[1] || !b.opt_margin || !b.opt_normal || !b.any)
+    return CDX_EINVAL;
+  if (!finalize && (!b.pose || !b.target || !b.comp || !b.g_pose || !b.g_target || !b.g_comp || !b.v_pose ||
+                    !b.v_target || !b.v_comp || (kin && (!b.m_pose || !b.m_target || !b.m_comp)) || !b.loss ||
+                    !b.opt_value || !b.opt_pose || !b.opt_target || !b.opt_comp))
+    return CDX_EINVAL;
+  const int G = 64 / n_tips;
+  const cdx_chain c = chain ? *chain : cdx_chain{};
+  hipLaunchKernelGGL(kin_step_kernel, dim3((unsigned)((E + G - 1) / G)), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     c, *cfg, b, E, (int)n_tips, kin ? (int)chain->n_dofs : 0, (int)iteration, (int)finalize);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}

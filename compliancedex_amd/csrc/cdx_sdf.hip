@@ -2,27 +2,40 @@
 // normal and closest point, plus the argmin face index — bit-identical to the reference's
 // brute-force scan (unbatched_triangle_distance_cuda.cu:186-246) and to oracle/sdf_oracle.c.
 //
-// Culled path (meshes without NaN-capable faces, the normal case):
-//   1. bbox of points ∪ vertices; 30-bit Morton keys of face centroids and of points;
-//      hipCUB radix sort of both (faces once per call, points so a wave is spatially coherent).
-//   2. Face records (FaceRec: every per-face quantity of point_face, computed once) in Morton
-//      order, in 32-face chunks with a bounding sphere (centre, radius) and a conditioning
-//      margin alpha derived from the worst face's 1/sinθ.
-//   3. A workgroup = 64 sorted points × 4 waves; wave w owns chunks c ≡ w (mod 4).  Pass 1
-//      takes each lane's upper bound U over chunks (every face of a chunk is at most
-//      (|p−c|+r)(1+α)+β away, so the answer is ≤ U²); pass 2 evaluates a chunk only when some
-//      lane's lower bound L = |p−c|(1−α) − r(1+α) − β has L ≤ 0 or L² ≤ min(U², best).  β =
-//      1e-4·(|p|+|c|+r) and α ≥ 1e-4 exceed every rounding error of point_face by orders of
-//      magnitude, so a skipped face's computed distance is strictly greater
-//      than the winner's: it can neither win nor tie.  Faces are compared lexicographically on
-//      (distance, index), which, with no NaN distances, is exactly the reference's first-
-//      minimum tile rule.  The four waves' winners merge in LDS; the winner's closest point,
-//      normal and sign are recomputed with point_face (deterministic, so bit-identical).
-// Exact path: a mesh with a face that can produce NaN (face_may_nan) runs the brute-force
-// tile-rule kernel (512-face LDS tiles); a workgroup holding a non-finite or |p| > 1e4 point
-// runs the tile rule on its own wave.  The choice is made on the device (no host sync).
+// Culled path (meshes without NaN-capable faces, the normal case), round 5:
+//   * a mesh is a two-level hierarchy over its faces in a spatially compact order: 32-face chunks
+//     (leaves), 16 chunks to a top node.  Prepared meshes (cdx_sdf_mesh_prepare, queried every
+//     iteration by the SDF/Kin optimisers) take the order of a median-split k-d tree on the face
+//     centroids, built on the host once (chunk radius 5.3 mm median on the 16 384-face banana, against
+//     10.5 mm for the round-4 Morton chunks — tools/sdf_cull_sim.py); the one-shot cdx_sdf_forward
+//     sorts the centroids by Morton code in a cubic frame on the device (no host round trip).
+//   * every node carries a bounding cylinder (axis = the area-weighted mean normal, centre, half-
+//     thickness, radius) intersected with a bounding ball; every face a disk slab (centroid, unit
+//     normal, in-plane radius, half-thickness).  Their distances are lower bounds on the distance to
+//     every face inside; the slab bound leaves 10× fewer (point, face) pairs than a per-face ball
+//     (tools/sdf_bound_study.py).  Node and slab data are computed in double from the f32 vertices and
+//     rounded outward.
+//   * one wave per 64 points (Morton-sorted in the points' own cubic frame): each lane first descends
+//     greedily (nearest top node → nearest chunk → face of smallest slab bound) and evaluates that one
+//     face, which gives it a near-final best; then the wave walks the top nodes and chunks some lane
+//     cannot rule out, tests the chunk's 32 slab bounds per lane, and evaluates only the (lane, face)
+//     pairs a lane needs, packed 64 to a round (ballot/mbcnt into LDS, an LDS 64-bit minimum on
+//     (distance bits, face index) into the owner's best).
+// A skip needs bound·(1 − α) − β > sqrt(best): α = 1e-4 + 1e-5·κ (κ = the worst face's 1/sinθ in the
+// node; α ≥ 1 or a NaN κ never skips) and β = 1e-4·(|p| + |c| + 3R) exceed every rounding error of
+// point_face and of the bound by orders of magnitude, so a skipped face's computed
+// distance is strictly greater than the winner's: it can neither win nor tie.  Faces are compared
+// lexicographically on (distance, index) — with no NaN distances, exactly the reference's first-minimum
+// tile rule — and the winner's outputs are recomputed with point_face (bit-identical).
+// Exact path: a mesh with a face that can produce NaN (face_may_nan) runs the brute-force tile-rule
+// kernel (512-face LDS tiles); a wave holding a non-finite or |p| > 1e4 point runs the tile rule itself.
+// The choice is made on the device (no host sync).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
 
 #include "cdx_sdf.h"
 
@@ -32,15 +45,20 @@ namespace {
 
 constexpr int SDF_BLOCK = 256;
 constexpr int SDF_TILE = CDX_SDF_REF_TILE;
-constexpr int CHUNK = 32;           // faces per culling chunk
+constexpr int CHUNK = 32;           // faces per chunk (leaf node)
+constexpr int TOPB = 16;            // chunks per top node
 constexpr float PT_LIM = 1e4f;      // |p| bound of the culled path (face_may_nan's premise)
 
-struct Sphere { float cx, cy, cz, r, alpha, cnorm, _p0, _p1; };
+// Bounding volume of a node: a = (centre xyz, ball radius R), b = (cylinder axis xyz, half-thickness t),
+// m = (cylinder radius rc, 1/(1 − α), w = 1e-4·(|centre| + 3R)/(1 − α), 0).
+struct Node { float4 a, b, m; };
+// Disk slab of a face: a = (centroid xyz, in-plane radius r), b = (unit normal xyz, half-thickness t).
+struct Slab { float4 a, b; };
 
-// Diagnostic counters (cdx_sdf_stats): [0] (point, face) pairs the culled kernel evaluated — faces a wave
-// evaluates exactly (its chunk not ruled out, the face itself not ruled out for every lane) × its live lanes —, [1] pairs of the brute-force scans (exact path),
-// [2] points queried.  Counted only while enabled (one atomic per wave).
-// [3]: chunks the culled kernel visited (a wave fetched and bound-tested their faces), summed over waves.
+// Diagnostic counters (cdx_sdf_stats): [0] (point, face) pairs the culled kernel evaluated (the greedy seed
+// face of every lane plus the compacted pairs), [1] pairs of the brute-force scans (exact path), [2] points
+// queried, [3] chunks the culled kernel's waves visited (tested face by face).  Counted only while enabled
+// (one atomic per wave).
 __device__ unsigned long long g_sdf_stats[4];
 bool g_sdf_count = false;
 
@@ -60,11 +78,11 @@ __device__ inline unsigned spread10(unsigned v) {  // 10 bits → every third bi
   return v;
 }
 
-// ws layout (unsigned words): [0..2] bbox min keys, [3..5] bbox max keys, [6] may-NaN flag
+// frame words: [0..2] bbox min keys, [3..5] bbox max keys (mesh header: [6] may-NaN flag, [7] unused)
 __global__ void sdf_init_kernel(unsigned* ws) {
   const int t = threadIdx.x;
   if (t < 3) ws[t] = 0xFFFFFFFFu;
-  else if (t < 7) ws[t] = 0u;
+  else if (t < 8) ws[t] = 0u;
 }
 
 __device__ inline void bb_acc(float x, float y, float z, unsigned (&lo)[3], unsigned (&hi)[3]) {
@@ -74,14 +92,11 @@ __device__ inline void bb_acc(float x, float y, float z, unsigned (&lo)[3], unsi
   for (int c = 0; c < 3; ++c) { lo[c] = min(lo[c], k[c]); hi[c] = max(hi[c], k[c]); }
 }
 
-__global__ __launch_bounds__(256) void sdf_bbox_kernel(const float* __restrict__ points, int64_t P,
-                                                       const float* __restrict__ faces, int64_t F, unsigned* ws) {
+// Bounding box of n points (3 floats each) into frame words 0..5.
+__global__ __launch_bounds__(256) void sdf_bbox_kernel(const float* __restrict__ v, int64_t n, unsigned* ws) {
   unsigned lo[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, hi[3] = {0u, 0u, 0u};
-  const int64_t n = P + 3 * F;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float* v = i < P ? points + 3 * i : faces + 3 * (i - P);
-    bb_acc(v[0], v[1], v[2], lo, hi);
-  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    bb_acc(v[3 * i], v[3 * i + 1], v[3 * i + 2], lo, hi);
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
 #pragma unroll
@@ -96,131 +111,194 @@ __global__ __launch_bounds__(256) void sdf_bbox_kernel(const float* __restrict__
   }
 }
 
+// 30-bit Morton code in the frame's CUBIC box (the largest extent on every axis: cells are cubes, so a run
+// of codes is compact in space whatever the box's aspect)
 __device__ inline unsigned morton(float x, float y, float z, const unsigned* ws) {
+  const float lo[3] = {fkey_inv(ws[0]), fkey_inv(ws[1]), fkey_inv(ws[2])};
+  const float ext = fmaxf(fmaxf(fkey_inv(ws[3]) - lo[0], fkey_inv(ws[4]) - lo[1]), fkey_inv(ws[5]) - lo[2]);
   const float v[3] = {x, y, z};
   unsigned m = 0;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    const float lo = fkey_inv(ws[c]), hi = fkey_inv(ws[3 + c]);
-    const float ext = hi - lo;
-    float t = ext > 0.f ? (v[c] - lo) / ext : 0.f;
+    float t = ext > 0.f ? (v[c] - lo[c]) / ext : 0.f;
     t = fminf(fmaxf(t, 0.f), 1.f);  // NaN → 0
     m |= spread10((unsigned)(t * 1023.f)) << c;
   }
   return m;
 }
 
-__global__ __launch_bounds__(256) void sdf_keys_kernel(const float* __restrict__ points, int64_t P,
-                                                       const float* __restrict__ faces, int64_t F,
-                                                       const unsigned* __restrict__ ws, unsigned* fkeys, int* fvals,
-                                                       unsigned* pkeys, int* pvals) {
+// Morton keys of points (centroid = false) or of face centroids (centroid = true, 9 floats a face).
+__global__ __launch_bounds__(256) void sdf_keys_kernel(const float* __restrict__ v, int64_t n, int centroid,
+                                                       const unsigned* __restrict__ ws, unsigned* keys, int* vals) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < F) {
-    const float* v = faces + 9 * i;
+  if (i >= n) return;
+  float x, y, z;
+  if (centroid) {
+    const float* f = v + 9 * i;
     const float third = 1.f / 3.f;
-    fkeys[i] = morton((v[0] + v[3] + v[6]) * third, (v[1] + v[4] + v[7]) * third, (v[2] + v[5] + v[8]) * third, ws);
-    fvals[i] = (int)i;
-  } else if (i < F + P) {
-    const int64_t j = i - F;
-    pkeys[j] = morton(points[3 * j], points[3 * j + 1], points[3 * j + 2], ws);
-    pvals[j] = (int)j;
+    x = (f[0] + f[3] + f[6]) * third; y = (f[1] + f[4] + f[7]) * third; z = (f[2] + f[5] + f[8]) * third;
+  } else {
+    x = v[3 * i]; y = v[3 * i + 1]; z = v[3 * i + 2];
   }
+  keys[i] = morton(x, y, z, ws);
+  vals[i] = (int)i;
 }
 
-// One thread per sorted face slot; a 32-lane half-wave builds one chunk's sphere.
-// fsph[j] (the culled2 kernel's per-face test in one 16-byte read): the face's sphere centre and
-// br·(1 + α + 1e-4) + 1e-4·bn, α its chunk's conditioning margin — the face-dependent part of the bound's
-// threshold (sdf_culled2_kernel).
-// ssph[j / SUB] the same for each SUB-face run of a chunk (its bounding sphere: centre, radius·(1 + α +
-// 1e-4) + 1e-4·|centre|), tested before its faces.
-#ifndef CDX_SDF_SUB
-#define CDX_SDF_SUB 8
-#endif
-constexpr int SUB = CDX_SDF_SUB;
-__global__ __launch_bounds__(256) void sdf_chunk_kernel(const float* __restrict__ faces, int64_t F,
-                                                        const int* __restrict__ order, cdx::FaceRec* __restrict__ rec,
-                                                        Sphere* __restrict__ sph, float4* __restrict__ fsph,
-                                                        float4* __restrict__ ssph, unsigned* ws) {
+// One thread per slot j of the face order (C·CHUNK slots, the tail past F zeroed): the face record of
+// point_face (FaceRec) and its disk slab, in double from the f32 vertices: centroid c (→ f32), unit normal
+// n (→ f32), then relative to those rounded values the half-thickness t = max |n̂·(v − c)| and the in-plane
+// radius r = max |(v − c) − (n̂·(v − c))·n̂| (n̂ = the f32 normal renormalised in double), rounded up.
+// A face without a finite normal gets a NaN slab (never skipped; its mesh takes the exact path anyway).
+__global__ __launch_bounds__(256) void sdf_face_kernel(const float* __restrict__ faces, int64_t F, int64_t slots,
+                                                       const int* __restrict__ order, cdx::FaceRec* __restrict__ rec,
+                                                       Slab* __restrict__ slab, unsigned* ws) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = j < F;
-  cdx::FaceRec r;
-  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-  float kappa = 0.f;
+  if (j >= slots) return;
   bool bad = false;
-  if (live) {
+  if (j < F) {
     const int f = order[j];
     const float* v = faces + 9 * (int64_t)f;
-    r = cdx::face_rec(cdx::f3(v[0], v[1], v[2]), cdx::f3(v[3], v[4], v[5]), cdx::f3(v[6], v[7], v[8]), f);
+    const cdx::FaceRec r = cdx::face_rec(cdx::f3(v[0], v[1], v[2]), cdx::f3(v[3], v[4], v[5]), cdx::f3(v[6], v[7], v[8]), f);
     rec[j] = r;
     bad = cdx::face_may_nan(r);
-    kappa = r.kappa;
-#pragma unroll
+    double p[3][3];
+    for (int k = 0; k < 3; ++k)
+      for (int c = 0; c < 3; ++c) p[k][c] = (double)v[3 * k + c];
+    double cen[3], e1[3], e2[3];
     for (int c = 0; c < 3; ++c) {
-      lo[c] = fminf(fminf(v[c], v[3 + c]), v[6 + c]);
-      hi[c] = fmaxf(fmaxf(v[c], v[3 + c]), v[6 + c]);
+      cen[c] = (p[0][c] + p[1][c] + p[2][c]) / 3.0;
+      e1[c] = p[1][c] - p[0][c];
+      e2[c] = p[2][c] - p[0][c];
     }
+    const double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+    const double nl = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    Slab s;
+    if (nl > 0.0 && nl < INFINITY) {
+      const float c32[3] = {(float)cen[0], (float)cen[1], (float)cen[2]};
+      const float n32[3] = {(float)(n[0] / nl), (float)(n[1] / nl), (float)(n[2] / nl)};
+      const double m = sqrt((double)n32[0] * n32[0] + (double)n32[1] * n32[1] + (double)n32[2] * n32[2]);
+      const double nh[3] = {n32[0] / m, n32[1] / m, n32[2] / m};
+      double t = 0.0, r2 = 0.0;
+      for (int k = 0; k < 3; ++k) {
+        const double d[3] = {p[k][0] - c32[0], p[k][1] - c32[1], p[k][2] - c32[2]};
+        const double h = d[0] * nh[0] + d[1] * nh[1] + d[2] * nh[2];
+        const double e[3] = {d[0] - h * nh[0], d[1] - h * nh[1], d[2] - h * nh[2]};
+        t = fmax(t, fabs(h));
+        r2 = fmax(r2, e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+      }
+      s.a = make_float4(c32[0], c32[1], c32[2], (float)(sqrt(r2) * (1.0 + 1e-6)));
+      s.b = make_float4(n32[0], n32[1], n32[2], (float)(t * (1.0 + 1e-6)));
+    } else {
+      s.a = make_float4(NAN, NAN, NAN, NAN);
+      s.b = make_float4(NAN, NAN, NAN, NAN);
+    }
+    slab[j] = s;
+  } else {
+    cdx::FaceRec r = {};
+    r.idx = 0x7fffffff;
+    rec[j] = r;
+    Slab s;
+    s.a = make_float4(0.f, 0.f, 0.f, 0.f);
+    s.b = make_float4(0.f, 0.f, 0.f, 0.f);
+    slab[j] = s;
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(ws + 6, 1u);
-  // the SUB-face run's box first (lanes j & ~(SUB − 1) … ), then the chunk's
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int o = 1; o < SUB; o <<= 1) {
-      lo[c] = fminf(lo[c], __shfl_xor(lo[c], o));
-      hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o));
+}
+
+__device__ inline double wave_min(double v) {
+  for (int o = 32; o >= 1; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ inline double wave_max(double v) {
+  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ inline double wave_sum(double v) {
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// One wave per node of S consecutive face slots: the node's bounding ball and cylinder, in double from the
+// f32 vertices of its face records and relative to the f32-rounded centre and axis the kernel will use:
+//   pass 1  box centre c, area-weighted normal sum → axis a (z if it vanishes), the faces' worst κ;
+//   pass 2  extent along a → the cylinder's mid-plane, moved into the centre c;
+//   pass 3  half-thickness t, cylinder radius rc, ball radius R (all rounded up by 1e-6).
+// Margins: α = 1e-4 + 1e-5·κ (1 for a NaN κ: never skipped), ia1 = 1/(1 − α), w = 1e-4·(|c| + 3R)·ia1.
+__global__ __launch_bounds__(64) void sdf_node_kernel(const cdx::FaceRec* __restrict__ rec, int64_t F, int S,
+                                                      Node* __restrict__ out) {
+  const int64_t f0 = (int64_t)blockIdx.x * S, f1 = min(F, f0 + S);
+  const int lane = threadIdx.x;
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY}, ns[3] = {0, 0, 0};
+  double kmax = 0.0;
+  for (int64_t f = f0 + lane; f < f1; f += 64) {
+    const cdx::FaceRec& r = rec[f];
+    const double v[3][3] = {{r.v1.x, r.v1.y, r.v1.z}, {r.v2.x, r.v2.y, r.v2.z}, {r.v3.x, r.v3.y, r.v3.z}};
+    for (int k = 0; k < 3; ++k)
+      for (int c = 0; c < 3; ++c) { lo[c] = fmin(lo[c], v[k][c]); hi[c] = fmax(hi[c], v[k][c]); }
+    const double e1[3] = {v[1][0] - v[0][0], v[1][1] - v[0][1], v[1][2] - v[0][2]};
+    const double e2[3] = {v[2][0] - v[0][0], v[2][1] - v[0][1], v[2][2] - v[0][2]};
+    ns[0] += e1[1] * e2[2] - e1[2] * e2[1];
+    ns[1] += e1[2] * e2[0] - e1[0] * e2[2];
+    ns[2] += e1[0] * e2[1] - e1[1] * e2[0];
+    kmax = (r.kappa <= 1e30f) ? fmax(kmax, (double)r.kappa) : INFINITY;  // NaN / inf κ: never skip
+  }
+  double c[3], a[3];
+  for (int k = 0; k < 3; ++k) {
+    lo[k] = wave_min(lo[k]);
+    hi[k] = wave_max(hi[k]);
+    ns[k] = wave_sum(ns[k]);
+    c[k] = (double)(float)(0.5 * (lo[k] + hi[k]));
+  }
+  kmax = wave_max(kmax);
+  const double nl = sqrt(ns[0] * ns[0] + ns[1] * ns[1] + ns[2] * ns[2]);
+  float a32[3] = {0.f, 0.f, 1.f};
+  if (nl > 0.0 && nl < INFINITY)
+    for (int k = 0; k < 3; ++k) a32[k] = (float)(ns[k] / nl);
+  const double am = sqrt((double)a32[0] * a32[0] + (double)a32[1] * a32[1] + (double)a32[2] * a32[2]);
+  for (int k = 0; k < 3; ++k) a[k] = a32[k] / am;
+  // pass 2: the extent along the axis
+  double hlo = INFINITY, hhi = -INFINITY;
+  for (int64_t f = f0 + lane; f < f1; f += 64) {
+    const cdx::FaceRec& r = rec[f];
+    const cdx::F3 vv[3] = {r.v1, r.v2, r.v3};
+    for (int k = 0; k < 3; ++k) {
+      const double h = (vv[k].x - c[0]) * a[0] + (vv[k].y - c[1]) * a[1] + (vv[k].z - c[2]) * a[2];
+      hlo = fmin(hlo, h);
+      hhi = fmax(hhi, h);
     }
-  const float sx = 0.5f * (lo[0] + hi[0]), sy = 0.5f * (lo[1] + hi[1]), sz = 0.5f * (lo[2] + hi[2]);
-  float srad = 0.f;
-  if (live) {
-    const cdx::F3 c = cdx::f3(sx, sy, sz);
-    srad = fmaxf(fmaxf(sqrtf(cdx::dotf(cdx::sub(r.v1, c), cdx::sub(r.v1, c))),
-                       sqrtf(cdx::dotf(cdx::sub(r.v2, c), cdx::sub(r.v2, c)))),
-                 sqrtf(cdx::dotf(cdx::sub(r.v3, c), cdx::sub(r.v3, c))));
   }
-#pragma unroll
-  for (int o = 1; o < SUB; o <<= 1) srad = fmaxf(srad, __shfl_xor(srad, o));
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int o = SUB; o < CHUNK; o <<= 1) {
-      lo[c] = fminf(lo[c], __shfl_xor(lo[c], o));
-      hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o));
+  hlo = wave_min(hlo);
+  hhi = wave_max(hhi);
+  const double mid = f1 > f0 ? 0.5 * (hlo + hhi) : 0.0;
+  for (int k = 0; k < 3; ++k) c[k] = (double)(float)(c[k] + mid * a[k]);
+  // pass 3: half-thickness, cylinder radius, ball radius about the final centre
+  double t = 0.0, rc2 = 0.0, R2 = 0.0;
+  for (int64_t f = f0 + lane; f < f1; f += 64) {
+    const cdx::FaceRec& r = rec[f];
+    const cdx::F3 vv[3] = {r.v1, r.v2, r.v3};
+    for (int k = 0; k < 3; ++k) {
+      const double d[3] = {vv[k].x - c[0], vv[k].y - c[1], vv[k].z - c[2]};
+      const double h = d[0] * a[0] + d[1] * a[1] + d[2] * a[2];
+      const double e[3] = {d[0] - h * a[0], d[1] - h * a[1], d[2] - h * a[2]};
+      t = fmax(t, fabs(h));
+      rc2 = fmax(rc2, e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+      R2 = fmax(R2, d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
     }
-  const float cx = 0.5f * (lo[0] + hi[0]), cy = 0.5f * (lo[1] + hi[1]), cz = 0.5f * (lo[2] + hi[2]);
-  float rad = 0.f;
-  if (live) {
-    const cdx::F3 c = cdx::f3(cx, cy, cz);
-    rad = fmaxf(fmaxf(sqrtf(cdx::dotf(cdx::sub(r.v1, c), cdx::sub(r.v1, c))),
-                      sqrtf(cdx::dotf(cdx::sub(r.v2, c), cdx::sub(r.v2, c)))),
-                sqrtf(cdx::dotf(cdx::sub(r.v3, c), cdx::sub(r.v3, c))));
   }
-#pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) {
-    rad = fmaxf(rad, __shfl_xor(rad, o));
-    kappa = fmaxf(kappa, __shfl_xor(kappa, o));
-  }
-  {
-    const float a = 1e-4f + 1e-5f * kappa;  // (the chunk's alpha, as below)
-    const float alpha = a < 1.f ? a : 1.f;
-    if (live) fsph[j] = make_float4(r.bx, r.by, r.bz, r.br * ((1.f + alpha) + 1e-4f) + 1e-4f * r.bn);
-    else if (j < (F + CHUNK - 1) / CHUNK * CHUNK) fsph[j] = make_float4(0.f, 0.f, 0.f, 0.f);  // (never tested: nf)
-    // (a run without live faces gets a NaN centre: its test then always says "needed", and nf masks its faces)
-    if ((j & (SUB - 1)) == 0 && j < (F + CHUNK - 1) / CHUNK * CHUNK)
-      ssph[j / SUB] = make_float4(sx, sy, sz, srad * (1.f + 1e-5f) * ((1.f + alpha) + 1e-4f) +
-                                               1e-4f * sqrtf(sx * sx + sy * sy + sz * sz));
-  }
-  if ((j & (CHUNK - 1)) == 0 && live) {
-    Sphere s;
-    s.cx = cx; s.cy = cy; s.cz = cz;
-    s.r = rad * (1.f + 1e-5f);
-    // normal-direction error of point_face's plane projection ≲ 10ε·κ; 1e-5·κ ≈ 170ε·κ.
-    // alpha ≥ 1 (or a NaN kappa) makes every lower bound ≤ 0: the chunk is always evaluated.
-    const float a = 1e-4f + 1e-5f * kappa;
-    s.alpha = a < 1.f ? a : 1.f;
-    s.cnorm = sqrtf(cx * cx + cy * cy + cz * cz);
-    s._p0 = s._p1 = 0.f;
-    sph[j / CHUNK] = s;
-  }
+  t = wave_max(t);
+  rc2 = wave_max(rc2);
+  R2 = wave_max(R2);
+  if (lane != 0) return;
+  const double R = sqrt(R2) * (1.0 + 1e-6);
+  const double al = 1e-4 + 1e-5 * kmax;  // (inf for a NaN κ)
+  const double ia1 = al < 1.0 ? 1.0 / (1.0 - al) : INFINITY;
+  const double cn = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+  Node nd;
+  nd.a = make_float4((float)c[0], (float)c[1], (float)c[2], (float)R);
+  nd.b = make_float4(a32[0], a32[1], a32[2], (float)(t * (1.0 + 1e-6)));
+  nd.m = make_float4((float)(sqrt(rc2) * (1.0 + 1e-6)), (float)(ia1 * (1.0 + 1e-6)),
+                     (float)(1e-4 * (cn + 3.0 * R) * ia1 * (1.0 + 1e-6)), 0.f);
+  out[blockIdx.x] = nd;
 }
 
 // Reference tile rule for one point over all faces (uniform face loads); writes outputs.
@@ -252,135 +330,51 @@ __device__ void exact_point(cdx::F3 p, const float* __restrict__ faces, int64_t 
   if (out_face) out_face[pi] = bface;
 }
 
-__global__ __launch_bounds__(SDF_BLOCK) void sdf_culled_kernel(
-    const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
-    int64_t F, const cdx::FaceRec* __restrict__ rec, const Sphere* __restrict__ sph, int C,
-    const unsigned* __restrict__ ws, float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
-    float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face, int count) {
-  if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
-#if SDF_COMPACT
-  __shared__ unsigned long long s_best[4][64];  // per wave: each lane's packed (distance, face) best
-  __shared__ unsigned short s_pair[4][128];     // … and its pending (lane << 5 | face) pairs
-#endif
-  __shared__ float s_val[4][64];
-  __shared__ int s_idx[4][64];
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t j = (int64_t)blockIdx.x * 64 + lane;
-  const bool live = j < P;
-  const int64_t pi = porder[live ? j : P - 1];  // dead lanes shadow a live point
-  const cdx::F3 p = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
-  const bool ok = fabsf(p.x) <= PT_LIM && fabsf(p.y) <= PT_LIM && fabsf(p.z) <= PT_LIM;
-  if (!__all(ok)) {  // same points in every wave: uniform over the workgroup
-    if (w == 0) exact_point(p, faces, F, pi, out_dist, out_sign, out_nrm, out_clst, out_face, live);
-    if (count && w == 0 && lane == 0)
-      atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(__ballot(live)));
-    return;
-  }
-  const float pnorm = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
 
-  // pass 1: upper bound on the answer
-  float ub = INFINITY;
-  for (int c = w; c < C; c += 4) {
-    const Sphere s = sph[c];
-    const float dx = p.x - s.cx, dy = p.y - s.cy, dz = p.z - s.cz;
-    const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
-    const float u = (dist + s.r) * (1.f + s.alpha) + 1e-4f * (pnorm + s.cnorm + s.r);
-    ub = fminf(ub, u);
-  }
-  s_val[w][lane] = ub;
-  __syncthreads();
-  ub = fminf(fminf(s_val[0][lane], s_val[1][lane]), fminf(s_val[2][lane], s_val[3][lane]));
-  const float T = ub * ub;
-  __syncthreads();
-
-  // pass 2: exact distances over the chunks some lane cannot rule out
-  float best = INFINITY;
-  int bidx = 0x7fffffff;
-  unsigned evaluated = 0;  // faces of the chunks this wave evaluated (diagnostic count)
-  for (int c = w; c < C; c += 4) {
-    const Sphere s = sph[c];
-    const float dx = p.x - s.cx, dy = p.y - s.cy, dz = p.z - s.cz;
-    const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
-    const float L = dist * (1.f - s.alpha) - s.r * (1.f + s.alpha) - 1e-4f * (pnorm + s.cnorm + s.r);
-    const bool need = !(L > 0.f && L * L > fminf(T, best));
-    if (!__any(need)) continue;
-    const int f0 = c * CHUNK;
-    const int nf = (int)min((int64_t)CHUNK, F - f0);
-    for (int k = 0; k < nf; ++k) {
-      const cdx::FaceRec& r = rec[f0 + k];
-#if !defined(CDX_SDF_NO_FACEBOUND)
-      // The chunk test again, on the face's own sphere (FaceRec bx..bn, the chunk's conditioning margin
-      // alpha): a face every lane of the wave rules out is never evaluated — its computed distance is
-      // strictly above the lane's best, so it could neither win nor tie (the argument of the chunk bound).
-      {
-        const float fx = p.x - r.bx, fy = p.y - r.by, fz = p.z - r.bz;
-        const float fd = sqrtf(fx * fx + fy * fy + fz * fz);
-        const float Lf = fd * (1.f - s.alpha) - r.br * (1.f + s.alpha) - 1e-4f * (pnorm + r.bn + r.br);
-        if (!__any(!(Lf > 0.f && Lf * Lf > best))) continue;
-      }
-#endif
-      ++evaluated;
-      const float d = cdx::face_dist2(p, r);
-      if (d < best || (d == best && r.idx < bidx)) { best = d; bidx = r.idx; }
-    }
-  }
-  if (count) {
-    const unsigned long long nl = __popcll(__ballot(live));
-    if (lane == 0) {
-      atomicAdd(&g_sdf_stats[0], (unsigned long long)evaluated * nl);
-      if (w == 0) atomicAdd(&g_sdf_stats[2], nl);
-    }
-  }
-  s_val[w][lane] = best;
-  s_idx[w][lane] = bidx;
-  __syncthreads();
-  if (w != 0 || !live) return;
-#pragma unroll
-  for (int v = 1; v < 4; ++v) {
-    const float d = s_val[v][lane];
-    const int i = s_idx[v][lane];
-    if (d < best || (d == best && i < bidx)) { best = d; bidx = i; }
-  }
-  const float* v = faces + 9 * (int64_t)bidx;
-  cdx::F3 c, n;
-  int sg;
-  const float d = cdx::point_face(p, cdx::f3(v[0], v[1], v[2]), cdx::f3(v[3], v[4], v[5]),
-                                  cdx::f3(v[6], v[7], v[8]), c, n, sg);
-  out_dist[pi] = d;
-  out_sign[pi] = sg;
-  out_nrm[3 * pi] = n.x; out_nrm[3 * pi + 1] = n.y; out_nrm[3 * pi + 2] = n.z;
-  out_clst[3 * pi] = c.x; out_clst[3 * pi + 1] = c.y; out_clst[3 * pi + 2] = c.z;
-  if (out_face) out_face[pi] = bidx;
+// Squared distance from p to a node's cylinder (its ball: *d2 = |p − c|² for the caller's ball test).
+__device__ __forceinline__ float cyl_lb2(cdx::F3 p, float4 a, float4 b, float rc, float* d2) {
+  const float dx = p.x - a.x, dy = p.y - a.y, dz = p.z - a.z;
+  const float h = b.x * dx + b.y * dy + b.z * dz;
+  const float ex = dx - h * b.x, ey = dy - h * b.y, ez = dz - h * b.z;
+  const float rho = sqrtf(ex * ex + ey * ey + ez * ez);
+  const float dh = fmaxf(fabsf(h) - b.w, 0.f), dr = fmaxf(rho - rc, 0.f);  // (fmaxf: NaN → 0, a bound of 0)
+  *d2 = dx * dx + dy * dy + dz * dz;
+  return dh * dh + dr * dr;
 }
 
-// The culled kernel, staged through LDS (default; CDX_SDF_V1 builds sdf_culled_kernel above for the A/B).
-// Same bounds, same winner rule, same outputs — only where the data comes from and how the per-face tests
-// are ordered differ:
-//   * the chunk spheres of a block of SPH_BLK chunks sit in LDS (one cooperative load per block, instead
-//     of one dependent scalar load per chunk and pass);
-//   * a chunk some lane cannot rule out is fetched whole into the wave's LDS buffer with 5 vector loads per
-//     lane (one round trip instead of one scalar load per face), and the next such chunk's loads are
-//     issued before the current one is processed;
-//   * its 32 per-face bounds are tested first, branch-free, into a bit mask against the lanes' best at the
-//     chunk's start (sqrt-free: fd² against the squared threshold — the 1e-4 margins dwarf the few ulps
-//     the rearrangement moves), then only the faces of the mask are evaluated.
-// A skipped face is one whose bound lies above every lane's best at the time of the test, and a lane's
-// best only decreases: the chunk argument of sdf_culled_kernel, unchanged.
-constexpr int SPH_BLK = 512;                   // chunk spheres per LDS block (12 KB)
+// A lane cannot rule the node out: its distance bound is not above th = (sqrt(best) + 1e-4·|p|)/(1 − α) + w
+// (k0 = sqrt(best) + 1e-4·|p|).  Written so that any NaN (bounds, an infinite ia1 times k0 = 0) keeps it.
+__device__ __forceinline__ bool node_needed(cdx::F3 p, const Node& n, float k0) {
+  float d2;
+  const float l2 = cyl_lb2(p, n.a, n.b, n.m.x, &d2);
+  const float th = k0 * n.m.y + n.m.z;
+  const float ts = th + n.a.w;
+  return !(l2 > th * th || d2 > ts * ts);
+}
+
+// Distance bound of a node for the greedy descent (larger of the cylinder's and the ball's).
+__device__ __forceinline__ float node_lb(cdx::F3 p, const Node& n) {
+  float d2;
+  const float l2 = cyl_lb2(p, n.a, n.b, n.m.x, &d2);
+  return fmaxf(sqrtf(l2), sqrtf(d2) - n.a.w);
+}
+
+__device__ __forceinline__ Node load_node(const Node* __restrict__ p, int i) {
+  const float4* q = reinterpret_cast<const float4*>(p + i);
+  Node n;
+  n.a = q[0]; n.b = q[1]; n.m = q[2];
+  return n;
+}
+__device__ __forceinline__ Slab load_slab(const Slab* __restrict__ p, int64_t i) {
+  const float4* q = reinterpret_cast<const float4*>(p + i);
+  Slab s;
+  s.a = q[0]; s.b = q[1];
+  return s;
+}
+
 constexpr int REC_WORDS = sizeof(cdx::FaceRec) / 4;  // 40
 static_assert(REC_WORDS * CHUNK % (64 * 4) == 0, "a chunk's records load as whole dwordx4 per lane");
 constexpr int REC_V4 = REC_WORDS * CHUNK / (64 * 4);   // dwordx4 loads per lane per chunk (5)
-
-#if defined(CDX_SDF_NO_COMPACT)
-#define SDF_COMPACT 0
-#else
-#define SDF_COMPACT 1  // pass 2 evaluates compacted (lane, face) pairs (sdf_culled2_kernel)
-#endif
-#ifndef CDX_SDF_SPLIT
-#define CDX_SDF_SPLIT 4
-#endif
-constexpr int SDF_SPLIT = CDX_SDF_SPLIT;  // workgroups per 64-point group (chunk slices; 4 since the per-slice bound pass: profiles/r04y4_*)
 
 // (distance, face) as one unsigned 64-bit word whose order is the winner rule's: a non-negative float's
 // bits order as unsigned integers, ties then go to the smaller index.
@@ -388,236 +382,113 @@ __device__ inline unsigned long long pack_best(float d, int idx) {
   return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)idx;
 }
 
-// Workgroup (g, k) of a split launch: the 64 Morton-sorted points of group g against chunk slice k (wave w
-// takes chunks c ≡ 4k + w mod 4·SPLIT), its per-point winner merged into best[pi] with a 64-bit atomic
-// minimum; sdf_culled_finalize_kernel then writes the outputs.  Splitting a point group over SPLIT
-// workgroups shortens its critical path — one group near no face (a point deep inside or far outside)
-// otherwise holds its CU while the others idle (PMC: mean wave life ≈ 1/3 of the kernel) — and gives the
-// dispatcher SPLIT× more, shorter workgroups to balance.  Each workgroup first takes the upper bound over
-// its own slice's chunks (pass 1; the slices interleave over the whole Morton order, so the bound stays
-// close to the one over all chunks) and the faces of the slice's chunk nearest the group's middle point
-// (the seed, shared over its waves), so every slice starts with a best near the true distance; a face is still skipped only when
-// its bound lies above the lane's best (which only decreases), so the global lexicographic minimum over the
-// evaluated faces is the brute-force winner.  Pass 2 evaluates (lane, face) pairs, not faces: each lane keeps
-// the mask of the chunk's faces its own bounds cannot rule out, and the wave packs those pairs 64 to a round
-// (SDF_COMPACT; a wave of far points otherwise evaluated every face any lane needed — 3× the pairs).
-// (The order of evaluation is free: the result is a minimum.)
-__global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
+// One wave per 64 Morton-sorted points, waves independent (four to a workgroup, no barrier).
+__global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
     const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
-    int64_t F, const cdx::FaceRec* __restrict__ rec, const Sphere* __restrict__ sph, int C,
-    const unsigned* __restrict__ ws, float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
-    float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face,
-    unsigned long long* __restrict__ best_out, const float4* __restrict__ fsph, const float4* __restrict__ ssph,
-    int count) {
+    int64_t F, const cdx::FaceRec* __restrict__ rec, const Slab* __restrict__ slab, const Node* __restrict__ chunk,
+    const Node* __restrict__ top, int C, int T, const unsigned* __restrict__ ws, float* __restrict__ out_dist,
+    int32_t* __restrict__ out_sign, float* __restrict__ out_nrm, float* __restrict__ out_clst,
+    int32_t* __restrict__ out_face, int count) {
   if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
-  __shared__ float4 s_sa[SPH_BLK];  // cx, cy, cz, r
-  __shared__ float2 s_sb[SPH_BLK];  // alpha, cnorm
-  __shared__ float4 s_rec[4][REC_WORDS * CHUNK / 4];  // per wave: one chunk's face records
-  __shared__ float4 s_fs[4][CHUNK];                   // … and its per-face bounds (sdf_chunk_kernel fsph)
-  __shared__ float4 s_ss[4][CHUNK / SUB];             // … and its SUB-face runs' bounds (ssph)
-#if SDF_COMPACT
-  __shared__ unsigned long long s_best[4][64];  // per wave: each lane's packed (distance, face) best
-  __shared__ unsigned short s_pair[4][128];     // … and its pending (lane << 5 | face) pairs
-#endif
-  __shared__ float s_val[4][64];
-  __shared__ int s_idx[4][64];
+  __shared__ float4 s_rec[4][REC_WORDS * CHUNK / 4];  // per wave: the visited chunk's face records
+  __shared__ unsigned long long s_best[4][64];        // … each lane's packed (distance, face) best
+  __shared__ unsigned short s_pair[4][128];           // … and its pending (lane << 5 | face) pairs
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int grp = blockIdx.x / SDF_SPLIT, slice = blockIdx.x - grp * SDF_SPLIT;
-  const int64_t j = (int64_t)grp * 64 + lane;
+  const int64_t j0 = ((int64_t)blockIdx.x * 4 + w) * 64;
+  if (j0 >= P) return;
+  const int64_t j = j0 + lane;
   const bool live = j < P;
   const int64_t pi = porder[live ? j : P - 1];  // dead lanes shadow a live point
   const cdx::F3 p = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
   const bool ok = fabsf(p.x) <= PT_LIM && fabsf(p.y) <= PT_LIM && fabsf(p.z) <= PT_LIM;
-  if (!__all(ok)) {  // same points in every wave and slice: uniform over the workgroup
-    if (w == 0 && slice == 0) exact_point(p, faces, F, pi, out_dist, out_sign, out_nrm, out_clst, out_face, live);
-    if (count && w == 0 && slice == 0 && lane == 0)
-      atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(__ballot(live)));
+  if (!__all(ok)) {
+    exact_point(p, faces, F, pi, out_dist, out_sign, out_nrm, out_clst, out_face, live);
+    if (count && lane == 0) atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(__ballot(live)));
     return;
   }
   const float pnorm = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
-  auto stage = [&](int cb) {  // spheres of chunks [cb, cb + SPH_BLK) into LDS (all waves)
-    __syncthreads();
-    const int nb = min(SPH_BLK, C - cb);
-    for (int i = threadIdx.x; i < nb; i += SDF_BLOCK) {
-      const Sphere sp = sph[cb + i];
-      s_sa[i] = make_float4(sp.cx, sp.cy, sp.cz, sp.r);
-      s_sb[i] = make_float2(sp.alpha, sp.cnorm);
-    }
-    __syncthreads();
-    return nb;
-  };
 
-  // pass 1 (this slice's chunks — any subset bounds the answer from above, and the slices interleave over
-  // the whole Morton order): upper bound on the answer, and the chunk that gives it (the lane's nearest,
-  // roughly)
-  float ub = INFINITY;
-  int uc = 0;
-#if defined(CDX_SDF_PASS1_ALL)
-  constexpr int p1s = 4;
-  const int p1c = w;
-#else
-  constexpr int p1s = 4 * SDF_SPLIT;
-  const int p1c = 4 * slice + w;
-#endif
-  for (int cb = 0; cb < C; cb += SPH_BLK) {
-    const int nb = stage(cb);
-    for (int c = (int)(((int64_t)p1c - cb) % p1s + p1s) % p1s; c < nb; c += p1s) {
-      const float4 a = s_sa[c];
-      const float2 b = s_sb[c];
-      const float dx = p.x - a.x, dy = p.y - a.y, dz = p.z - a.z;
-      const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
-      const float u = (dist + a.w) * (1.f + b.x) + 1e-4f * (pnorm + b.y + a.w);
-      if (u < ub) { ub = u; uc = cb + c; }
-    }
-  }
-  s_val[w][lane] = ub;
-  s_idx[w][lane] = uc;
-  __syncthreads();
-  int seed = s_idx[0][lane];
+  // greedy seed: nearest top node, nearest chunk in it, the face of smallest slab bound in that chunk —
+  // evaluated exactly, so the lane starts with a real (distance, face) near its answer
+  int tsel = 0;
   {
-    float m = s_val[0][lane];
-#pragma unroll
-    for (int v = 1; v < 4; ++v)
-      if (s_val[v][lane] < m) { m = s_val[v][lane]; seed = s_idx[v][lane]; }
-    ub = m;
+    float tl = INFINITY;
+    for (int t = 0; t < T; ++t) {
+      const float lb = node_lb(p, load_node(top, t));
+      if (lb < tl) { tl = lb; tsel = t; }
+    }
   }
-  const float T = ub * ub;
-  seed = __builtin_amdgcn_readlane(seed, 32);
+  int csel = tsel * TOPB;
+  {
+    float cl = INFINITY;
+    const int ce = min(C, tsel * TOPB + TOPB);
+    for (int c = tsel * TOPB; c < ce; ++c) {
+      const float lb = node_lb(p, load_node(chunk, c));
+      if (lb < cl) { cl = lb; csel = c; }
+    }
+  }
+  int64_t fsel = (int64_t)csel * CHUNK;
+  {
+    float fl = INFINITY;
+    const int64_t fe = min(F, (int64_t)csel * CHUNK + CHUNK);
+    for (int64_t f = (int64_t)csel * CHUNK; f < fe; ++f) {
+      const Slab s = load_slab(slab, f);
+      float d2;
+      const float l2 = cyl_lb2(p, s.a, s.b, s.a.w, &d2);
+      if (l2 < fl) { fl = l2; fsel = f; }
+    }
+  }
+  float best;
+  int bidx;
+  {
+    const cdx::FaceRec r = rec[fsel];
+    best = cdx::face_dist2(p, r);
+    bidx = r.idx;
+  }
+  s_best[w][lane] = pack_best(best, bidx);
+  unsigned visits = 0, pairs = 64;
 
-  // the seed chunk's faces, split over the waves (faces k ≡ w mod 4), merged in LDS: every wave of the
-  // workgroup starts with the same (best, face)
   const float4* rec4 = reinterpret_cast<const float4*>(rec);
   float4* buf = s_rec[w];
-  float best = INFINITY;
-  int bidx = 0x7fffffff;
-  unsigned evaluated = 0, visits = 0, pairs = 0;  // faces evaluated / chunks visited by this wave (diagnostic counts)
-  {
-    const int nf = (int)min((int64_t)CHUNK, F - (int64_t)seed * CHUNK);
-    for (int k = w; k < nf; k += 4) {
-      const cdx::FaceRec r = rec[(int64_t)seed * CHUNK + k];
-      const float d = cdx::face_dist2(p, r);
-      if (d < best || (d == best && r.idx < bidx)) { best = d; bidx = r.idx; }
-      ++evaluated;
-    }
-    __syncthreads();  // pass 1's s_val / s_idx reads are done
-    s_val[w][lane] = best;
-    s_idx[w][lane] = bidx;
-    __syncthreads();
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const float d = s_val[v][lane];
-      const int i = s_idx[v][lane];
-      if (d < best || (d == best && i < bidx)) { best = d; bidx = i; }
-    }
-    __syncthreads();  // s_val / s_idx are written again at the end
-  }
-#if SDF_COMPACT
-  s_best[w][lane] = pack_best(best, bidx);
-#endif
-
-  // pass 2 (this slice's chunks): exact distances over the chunks some lane cannot rule out
-  const int c0 = 4 * slice + w, cs = 4 * SDF_SPLIT;
-  for (int cb = 0; cb < C; cb += SPH_BLK) {
-    const int nb = C <= SPH_BLK ? C : stage(cb);  // (one block: still staged from pass 1)
-    // the wave's next chunk ≥ c (c ≡ c0 mod cs) some lane cannot rule out (uniform), or ≥ nb
-    auto next_needed = [&](int c) {
-      for (; c < nb; c += cs) {
-        const float4 a = s_sa[c];
-        const float2 b = s_sb[c];
-        const float dx = p.x - a.x, dy = p.y - a.y, dz = p.z - a.z;
-        const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
-        const float L = dist * (1.f - b.x) - a.w * (1.f + b.x) - 1e-4f * (pnorm + b.y + a.w);
-        if (__any(!(L > 0.f && L * L > fminf(T, best)))) break;
+  const cdx::FaceRec* rr = reinterpret_cast<const cdx::FaceRec*>(buf);
+  for (int t = 0; t < T; ++t) {
+    if (!__any(node_needed(p, load_node(top, t), fmaf(1e-4f, pnorm, sqrtf(best))))) continue;
+    const int ce = min(C, t * TOPB + TOPB);
+    for (int c = t * TOPB; c < ce; ++c) {
+      const Node cn = load_node(chunk, c);
+      const float k0 = fmaf(1e-4f, pnorm, sqrtf(best));
+      if (!__any(node_needed(p, cn, k0))) continue;
+      // the chunk's faces a lane cannot rule out: slab bound against th = k0/(1 − α) + w (the chunk's margins)
+      const float th = k0 * cn.m.y + cn.m.z;
+      const float th2 = th * th;
+      const int nf = (int)min((int64_t)CHUNK, F - (int64_t)c * CHUNK);
+      unsigned lmask = 0;
+#pragma unroll 8
+      for (int k = 0; k < CHUNK; ++k) {
+        const Slab s = load_slab(slab, (int64_t)c * CHUNK + k);
+        float d2;
+        const float l2 = cyl_lb2(p, s.a, s.b, s.a.w, &d2);
+        if (!(l2 > th2) && k < nf && live) lmask |= 1u << k;
       }
-      return c;
-    };
-    // first chunk of the slice in this block: c ≡ c0 (mod cs), c ≥ 0 relative to cb
-    const int cfirst = (int)(((int64_t)c0 - cb) % cs + cs) % cs;
-    int c = next_needed(cfirst);
-    float4 pre[REC_V4], pref = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c < nb) {
+      unsigned mask = lmask;
 #pragma unroll
-      for (int i = 0; i < REC_V4; ++i) pre[i] = rec4[(int64_t)(cb + c) * (REC_WORDS * CHUNK / 4) + lane + 64 * i];
-      if (lane < CHUNK) pref = fsph[(int64_t)(cb + c) * CHUNK + lane];
-      else if (lane < CHUNK + CHUNK / SUB) pref = ssph[(int64_t)(cb + c) * (CHUNK / SUB) + lane - CHUNK];
-    }
-    while (c < nb) {
-#pragma unroll
-      for (int i = 0; i < REC_V4; ++i) buf[lane + 64 * i] = pre[i];
-      if (lane < CHUNK) s_fs[w][lane] = pref;
-      else if (lane < CHUNK + CHUNK / SUB) s_ss[w][lane - CHUNK] = pref;
-      const int cur = c;
-      const int64_t f0 = (int64_t)(cb + cur) * CHUNK;
-      const float alpha = s_sb[cur].x;
-      c = next_needed(cur + cs);
-      if (c < nb) {  // the next chunk's records in flight while this one is processed
-#pragma unroll
-        for (int i = 0; i < REC_V4; ++i) pre[i] = rec4[(int64_t)(cb + c) * (REC_WORDS * CHUNK / 4) + lane + 64 * i];
-        if (lane < CHUNK) pref = fsph[(int64_t)(cb + c) * CHUNK + lane];
-        else if (lane < CHUNK + CHUNK / SUB) pref = ssph[(int64_t)(cb + c) * (CHUNK / SUB) + lane - CHUNK];
-      }
-      const cdx::FaceRec* rr = reinterpret_cast<const cdx::FaceRec*>(buf);
-      const int nf = (int)min((int64_t)CHUNK, F - f0);
+      for (int o = 32; o >= 1; o >>= 1) mask |= (unsigned)__shfl_xor((int)mask, o);
+      mask = __builtin_amdgcn_readfirstlane(mask);
+      if (!mask) continue;
       ++visits;
-      // per-face bounds against the lane's best: bit k set = some lane cannot rule face k out
-      const float sb = sqrtf(best);  // (INF while the lane has no face yet)
-      // skip ⇔ fd·(1 − α) > br·(1 + α) + β + sqrt(best), β = 1e-4·(|p| + bn + br) (the chunk bound's Lf > 0
-      // ∧ Lf² > best), as th = (br·(1 + α + 1e-4) + 1e-4·bn + (1e-4·|p| + sqrt(best))) / (1 − α) with the
-      // chunk's and the lane's terms hoisted and explicit FMAs: the rearrangement moves the threshold by
-      // a few ulps, nothing against the 1e-4 margins (α = 1: 1/(1 − α) = ∞, never skipped)
-      // (the face's part br·(1 + α + 1e-4) + 1e-4·bn comes precomputed with its centre, fsph)
-      const float ia1 = 1.f / (1.f - alpha), k0 = fmaf(1e-4f, pnorm, sb);
-#if defined(CDX_SDF_TH_FMA)
-      const float k1 = k0 * ia1;
-#endif
-      unsigned mask = 0;
-#if SDF_COMPACT
-      unsigned lmask = 0;  // this lane's faces
-#endif
-      for (int sr = 0; sr < CHUNK / SUB; ++sr) {
-#if !defined(CDX_SDF_NO_FACEBOUND)
-        {  // the run's sphere first: a run every lane rules out skips its SUB face tests
-          const float4 ss = s_ss[w][sr];
-          const float ux = p.x - ss.x, uy = p.y - ss.y, uz = p.z - ss.z;
-          const float ud2 = fmaf(ux, ux, fmaf(uy, uy, uz * uz));
-#if defined(CDX_SDF_TH_FMA)
-          const float uth = fmaf(ss.w, ia1, k1);
-#else
-          const float uth = (ss.w + k0) * ia1;
-#endif
-          if (!__any(!(ud2 > uth * uth))) continue;
-        }
-#endif
+      // the chunk's 32 face records into the wave's LDS buffer (5 dwordx4 per lane)
+      {
+        float4 v[REC_V4];
 #pragma unroll
-        for (int kk = 0; kk < SUB; ++kk) {
-          const int k = SUB * sr + kk;
-#if !defined(CDX_SDF_NO_FACEBOUND)
-          const float4 fs = s_fs[w][k];
-          const float fx = p.x - fs.x, fy = p.y - fs.y, fz = p.z - fs.z;
-          const float fd2 = fmaf(fx, fx, fmaf(fy, fy, fz * fz));
-#if defined(CDX_SDF_TH_FMA)
-          const float th = fmaf(fs.w, ia1, k1);
-#else
-          const float th = (fs.w + k0) * ia1;
-#endif
-          const bool need = !(fd2 > th * th);
-#else
-          const bool need = true;
-#endif
-#if SDF_COMPACT
-          if (need && k < nf && live) lmask |= 1u << k;
-          if (__any(need && live) && k < nf) mask |= 1u << k;
-#else
-          if (__any(need) && k < nf) mask |= 1u << k;
-#endif
-        }
+        for (int i = 0; i < REC_V4; ++i) v[i] = rec4[(int64_t)c * (REC_WORDS * CHUNK / 4) + lane + 64 * i];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < REC_V4; ++i) buf[lane + 64 * i] = v[i];
+        __builtin_amdgcn_wave_barrier();
       }
-#if SDF_COMPACT
-      // the (lane, face) pairs some lane needs, packed 64 to a round: lane i of a round evaluates pair i
-      // (its point read from the owning lane) and folds the result into the owner's packed best in LDS
-      // with a 64-bit minimum (the same lexicographic (distance, index) order); the owners read their
-      // best back after the chunk.  A face only some lanes need no longer costs the whole wave.
+      // the (lane, face) pairs, packed 64 to a round: lane i of a round evaluates pair i (its point read from
+      // the owner) and folds it into the owner's packed best with an LDS 64-bit minimum (the winner order)
       auto eval_round = [&](int n) {
         const unsigned e = s_pair[w][lane];
         const int l = lane < n ? (int)(e >> 5) : lane;
@@ -640,6 +511,7 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
               (unsigned short)((lane << 5) | k);
         cnt += __popcll(b);
         if (cnt >= 64) {
+          __builtin_amdgcn_wave_barrier();
           eval_round(64);
           cnt -= 64;
           const unsigned short tail = s_pair[w][64 + lane];  // (read before any lane overwrites its slot)
@@ -647,57 +519,25 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_culled2_kernel(
           if (lane < cnt) s_pair[w][lane] = tail;
         }
       }
+      __builtin_amdgcn_wave_barrier();
       if (cnt > 0) eval_round(cnt);
+      __builtin_amdgcn_wave_barrier();
       {
         const unsigned long long bb = s_best[w][lane];
         best = __uint_as_float((unsigned)(bb >> 32));
         bidx = (int)(unsigned)bb;
       }
-#else
-      while (mask) {
-        const int k = __builtin_ctz(mask);
-        mask &= mask - 1;
-        const cdx::FaceRec& r = rr[k];
-        ++evaluated;
-        const float d = cdx::face_dist2(p, r);
-        if (d < best || (d == best && r.idx < bidx)) { best = d; bidx = r.idx; }
-      }
-#endif
     }
   }
   if (count) {
     const unsigned long long nl = __popcll(__ballot(live));
     if (lane == 0) {
-      atomicAdd(&g_sdf_stats[0], (unsigned long long)evaluated * nl + pairs);
+      atomicAdd(&g_sdf_stats[0], (unsigned long long)pairs - 64 + nl);
+      atomicAdd(&g_sdf_stats[2], nl);
       atomicAdd(&g_sdf_stats[3], (unsigned long long)visits);
-      if (w == 0 && slice == 0) atomicAdd(&g_sdf_stats[2], nl);
     }
   }
-  s_val[w][lane] = best;
-  s_idx[w][lane] = bidx;
-  __syncthreads();
-  if (w != 0 || !live) return;
-#pragma unroll
-  for (int v = 1; v < 4; ++v) {
-    const float d = s_val[v][lane];
-    const int i = s_idx[v][lane];
-    if (d < best || (d == best && i < bidx)) { best = d; bidx = i; }
-  }
-  atomicMin(best_out + pi, pack_best(best, bidx));
-}
-
-// The outputs of the split launch's winners: point_face of each point's best face (the workgroups that ran
-// the brute-force rule or a NaN-capable mesh left best at ~0 and wrote their outputs themselves).
-__global__ __launch_bounds__(256) void sdf_culled_finalize_kernel(
-    const float* __restrict__ points, int64_t P, const float* __restrict__ faces,
-    const unsigned long long* __restrict__ best, float* __restrict__ out_dist, int32_t* __restrict__ out_sign,
-    float* __restrict__ out_nrm, float* __restrict__ out_clst, int32_t* __restrict__ out_face) {
-  const int64_t pi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (pi >= P) return;
-  const unsigned long long b = best[pi];
-  if (b == ~0ull) return;
-  const int bidx = (int)(unsigned)(b & 0xFFFFFFFFu);
-  const cdx::F3 p = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
+  if (!live) return;
   const float* v = faces + 9 * (int64_t)bidx;
   cdx::F3 cc, n;
   int sg;
@@ -832,23 +672,36 @@ int sdf_mode() {  // CDX_SDF_MODE=exact forces the brute-force kernel (benchmark
   return m;
 }
 
-// Prepared mesh: [ws words: bbox min keys ×3, max keys ×3, may-NaN flag, 0][records: C·CHUNK FaceRec][spheres]
-// [face bounds: C·CHUNK float4][run bounds: C·CHUNK/SUB float4]
+
+// Mesh: [header words: frame keys ×6, may-NaN flag, 0][face records: C·CHUNK FaceRec][slabs: C·CHUNK Slab]
+// [chunk nodes: C Node][top nodes: T Node], C = ⌈F/32⌉, T = ⌈C/16⌉, faces in the build's order.
+int64_t n_chunks(int64_t F) { return (F + CHUNK - 1) / CHUNK; }
+int64_t n_tops(int64_t F) { return (n_chunks(F) + TOPB - 1) / TOPB; }
 size_t mesh_rec_off() { return align256(8 * sizeof(unsigned)); }
-size_t mesh_sph_off(int64_t C) { return mesh_rec_off() + align256((size_t)C * CHUNK * sizeof(cdx::FaceRec)); }
-size_t mesh_fsph_off(int64_t C) { return mesh_sph_off(C) + align256((size_t)C * sizeof(Sphere)); }
-size_t mesh_ssph_off(int64_t C) { return mesh_fsph_off(C) + align256((size_t)C * CHUNK * sizeof(float4)); }
+size_t mesh_slab_off(int64_t C) { return mesh_rec_off() + align256((size_t)C * CHUNK * sizeof(cdx::FaceRec)); }
+size_t mesh_chunk_off(int64_t C) { return mesh_slab_off(C) + align256((size_t)C * CHUNK * sizeof(Slab)); }
+size_t mesh_top_off(int64_t C) { return mesh_chunk_off(C) + align256((size_t)C * sizeof(Node)); }
 size_t mesh_bytes(int64_t F) {
-  const int64_t C = (F + CHUNK - 1) / CHUNK;
-  return mesh_ssph_off(C) + align256((size_t)C * (CHUNK / SUB) * sizeof(float4));
+  const int64_t C = n_chunks(F);
+  return mesh_top_off(C) + align256((size_t)n_tops(F) * sizeof(Node));
 }
 
-// Face records and chunk spheres in Morton order of the bounding box of the faces (and of the points,
-// when given: the one-shot cdx_sdf_forward keeps its point-inclusive frame).  The order only steers the
-// culling (ties resolve by face index), so any frame gives identical outputs.
-int mesh_build(const float* faces, int64_t F, const float* points, int64_t P, char* mesh, hipStream_t s) {
+// Records, slabs and nodes of the faces in `order` (device int[F]).
+void mesh_fill(const float* faces, int64_t F, const int* order, char* mesh, hipStream_t s) {
+  const int64_t C = n_chunks(F), T = n_tops(F);
+  unsigned* ws = reinterpret_cast<unsigned*>(mesh);
+  auto* rec = reinterpret_cast<cdx::FaceRec*>(mesh + mesh_rec_off());
+  hipLaunchKernelGGL(sdf_face_kernel, dim3((unsigned)((C * CHUNK + 255) / 256)), dim3(256), 0, s, faces, F,
+                     (int64_t)(C * CHUNK), order, rec, reinterpret_cast<Slab*>(mesh + mesh_slab_off(C)), ws);
+  hipLaunchKernelGGL(sdf_node_kernel, dim3((unsigned)C), dim3(64), 0, s, (const cdx::FaceRec*)rec, F, CHUNK,
+                     reinterpret_cast<Node*>(mesh + mesh_chunk_off(C)));
+  hipLaunchKernelGGL(sdf_node_kernel, dim3((unsigned)T), dim3(64), 0, s, (const cdx::FaceRec*)rec, F, CHUNK * TOPB,
+                     reinterpret_cast<Node*>(mesh + mesh_top_off(C)));
+}
+
+// One-shot build on the device: face centroids in Morton order of the faces' cubic frame.
+int mesh_build_morton(const float* faces, int64_t F, char* mesh, hipStream_t s) {
   const int n = (int)F;
-  const int C = (n + CHUNK - 1) / CHUNK;
   size_t tf = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, tf, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
                                          (int*)nullptr, n, 0, 30, s) != hipSuccess)
@@ -863,67 +716,142 @@ int mesh_build(const float* faces, int64_t F, const float* points, int64_t P, ch
   unsigned* fk = reinterpret_cast<unsigned*>(base + o_fk);
   int* fv = reinterpret_cast<int*>(base + o_fv);
   hipLaunchKernelGGL(sdf_init_kernel, dim3(1), dim3(64), 0, s, ws);
-  const int64_t nbb = P + 3 * F;
-  const unsigned bbb = (unsigned)std::min<int64_t>((nbb + 255) / 256, 1024);
-  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(bbb), dim3(256), 0, s, points, P, faces, F, ws);
-  hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((F + 255) / 256)), dim3(256), 0, s, (const float*)nullptr,
-                     (int64_t)0, faces, F, (const unsigned*)ws, fk, fv, (unsigned*)nullptr, (int*)nullptr);
+  const unsigned bbb = (unsigned)std::min<int64_t>((3 * F + 255) / 256, 1024);
+  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(bbb), dim3(256), 0, s, faces, 3 * F, ws);
+  hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((F + 255) / 256)), dim3(256), 0, s, faces, F, 1,
+                     (const unsigned*)ws, fk, fv);
   size_t t1 = tf;
   bool ok = hipcub::DeviceRadixSort::SortPairs(base + o_tmp, t1, fk, fk + n, fv, fv + n, n, 0, 30, s) == hipSuccess;
-  hipLaunchKernelGGL(sdf_chunk_kernel, dim3((unsigned)((C * CHUNK + 255) / 256)), dim3(256), 0, s, faces, F,
-                     (const int*)(fv + n), reinterpret_cast<cdx::FaceRec*>(mesh + mesh_rec_off()),
-                     reinterpret_cast<Sphere*>(mesh + mesh_sph_off(C)), reinterpret_cast<float4*>(mesh + mesh_fsph_off(C)),
-                     reinterpret_cast<float4*>(mesh + mesh_ssph_off(C)), ws);
+  mesh_fill(faces, F, fv + n, mesh, s);
   ok = ok && hipGetLastError() == hipSuccess;
   ok = (hipFreeAsync(base, s) == hipSuccess) && ok;
   return ok ? CDX_OK : CDX_ELAUNCH;
 }
 
-// Points in Morton order of the mesh's frame (a wave then holds nearby points), the culled kernel, and
+// Face order of a median-split k-d tree on the centroids: split the longest extent of the
+// node's centroids at a left size that is a multiple of a top node (512 faces) while the node is larger than
+// one, else of a chunk (32), so every chunk and every top node is one subtree (a compact cluster).
+void kd_order(const std::vector<float>& cen, std::vector<int>& idx) {
+  struct Range { int lo, hi; };
+  std::vector<Range> stack{{0, (int)idx.size()}};
+  while (!stack.empty()) {
+    const Range r = stack.back();
+    stack.pop_back();
+    const int n = r.hi - r.lo;
+    if (n <= CHUNK) continue;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = r.lo; i < r.hi; ++i)
+      for (int c = 0; c < 3; ++c) {
+        const float v = cen[3 * (size_t)idx[i] + c];
+        if (v < lo[c]) lo[c] = v;
+        if (v > hi[c]) hi[c] = v;
+      }
+    int ax = 0;
+    for (int c = 1; c < 3; ++c)
+      if (hi[c] - lo[c] > hi[ax] - lo[ax]) ax = c;
+    const int unit = n > CHUNK * TOPB ? CHUNK * TOPB : CHUNK;
+    const int half = std::min(((n + 1) / 2 + unit - 1) / unit * unit, n - 1);
+    std::nth_element(idx.begin() + r.lo, idx.begin() + r.lo + half, idx.begin() + r.hi, [&](int a, int b) {
+      const float ka = cen[3 * (size_t)a + ax], kb = cen[3 * (size_t)b + ax];
+      return ka < kb || (ka == kb && a < b);  // (NaN centroids: any consistent side is fine for the order)
+    });
+    stack.push_back({r.lo, r.lo + half});
+    stack.push_back({r.lo + half, r.hi});
+  }
+}
+
+// Prepared build: the k-d order on the host (one device→host copy of the faces and a wait on the stream),
+// then the records and nodes on the device.
+int mesh_build_kd(const float* faces, int64_t F, char* mesh, hipStream_t s) {
+  std::vector<float> fh((size_t)F * 9);
+  if (hipMemcpyAsync(fh.data(), faces, fh.size() * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return CDX_ELAUNCH;
+  std::vector<float> cen((size_t)F * 3);
+  for (int64_t f = 0; f < F; ++f)
+    for (int c = 0; c < 3; ++c) {
+      const float* v = &fh[9 * (size_t)f];
+      cen[3 * (size_t)f + c] = (v[c] + v[3 + c] + v[6 + c]) / 3.f;
+    }
+  std::vector<int> idx((size_t)F);
+  for (int64_t f = 0; f < F; ++f) idx[(size_t)f] = (int)f;
+  kd_order(cen, idx);
+  int* order = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&order), (size_t)F * sizeof(int), s) != hipSuccess) return CDX_ELAUNCH;
+  bool ok = hipMemcpyAsync(order, idx.data(), (size_t)F * sizeof(int), hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess;  // (idx is freed on return)
+  unsigned* ws = reinterpret_cast<unsigned*>(mesh);
+  hipLaunchKernelGGL(sdf_init_kernel, dim3(1), dim3(64), 0, s, ws);
+  const unsigned bbb = (unsigned)std::min<int64_t>((3 * F + 255) / 256, 1024);
+  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(bbb), dim3(256), 0, s, faces, 3 * F, ws);
+  mesh_fill(faces, F, order, mesh, s);
+  ok = ok && hipGetLastError() == hipSuccess;
+  ok = (hipFreeAsync(order, s) == hipSuccess) && ok;
+  return ok ? CDX_OK : CDX_ELAUNCH;
+}
+
+// Query workspace: [point frame words ×8][keys 2P][values 2P][radix-sort scratch].
+struct QueryWs { size_t o_pk, o_pv, o_tmp, bytes, tp; };
+bool query_ws(int64_t P, hipStream_t s, QueryWs& q) {
+  const int m = (int)P;
+  q.tp = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, q.tp, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
+                                         (int*)nullptr, m, 0, 30, s) != hipSuccess)
+    return false;
+  size_t off = align256(8 * sizeof(unsigned));
+  q.o_pk = off; off = align256(off + 2 * (size_t)m * sizeof(unsigned));
+  q.o_pv = off; off = align256(off + 2 * (size_t)m * sizeof(int));
+  q.o_tmp = off; off = align256(off + q.tp);
+  q.bytes = off;
+  return true;
+}
+
+// Points in Morton order of their own cubic frame (a wave then holds nearby points), the tree kernel, and
 // the brute-force tile rule when the mesh may produce NaN distances (decided on the device).
 int mesh_query(const char* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
-               int32_t* sign, float* normals, float* clst, int32_t* face_idx, hipStream_t s) {
+               int32_t* sign, float* normals, float* clst, int32_t* face_idx, char* base, const QueryWs& q,
+               hipStream_t s) {
   const int m = (int)P;
-  const int C = (int)((F + CHUNK - 1) / CHUNK);
-  size_t tp = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tp, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
-                                         (int*)nullptr, m, 0, 30, s) != hipSuccess)
-    return CDX_ELAUNCH;
-  size_t off = 0;
-  const size_t o_pk = off; off = align256(off + 2 * (size_t)m * sizeof(unsigned));
-  const size_t o_pv = off; off = align256(off + 2 * (size_t)m * sizeof(int));
-  const size_t o_tmp = off; off = align256(off + tp);
-  const size_t o_best = off; off = align256(off + (size_t)m * sizeof(unsigned long long));
-  char* base = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void**>(&base), off, s) != hipSuccess) return CDX_ELAUNCH;
-  const unsigned* ws = reinterpret_cast<const unsigned*>(mesh);
-  unsigned* pk = reinterpret_cast<unsigned*>(base + o_pk);
-  int* pv = reinterpret_cast<int*>(base + o_pv);
-  hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P,
-                     (const float*)nullptr, (int64_t)0, ws, (unsigned*)nullptr, (int*)nullptr, pk, pv);
-  size_t t2 = tp;
-  bool ok = hipcub::DeviceRadixSort::SortPairs(base + o_tmp, t2, pk, pk + m, pv, pv + m, m, 0, 30, s) == hipSuccess;
-#if defined(CDX_SDF_V1)
-  hipLaunchKernelGGL(sdf_culled_kernel, dim3((unsigned)((P + 63) / 64)), dim3(SDF_BLOCK), 0, s, points, P,
-                     (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
-                     reinterpret_cast<const Sphere*>(mesh + mesh_sph_off(C)), C, ws, sqdist, sign, normals, clst,
-                     face_idx, (int)g_sdf_count);
-#else
-  unsigned long long* best = reinterpret_cast<unsigned long long*>(base + o_best);
-  ok = ok && hipMemsetAsync(best, 0xFF, (size_t)m * sizeof(unsigned long long), s) == hipSuccess;
-  hipLaunchKernelGGL(sdf_culled2_kernel, dim3((unsigned)((P + 63) / 64 * SDF_SPLIT)), dim3(SDF_BLOCK), 0, s, points,
+  const int64_t C = n_chunks(F), T = n_tops(F);
+  const unsigned* mws = reinterpret_cast<const unsigned*>(mesh);
+  unsigned* pws = reinterpret_cast<unsigned*>(base);
+  unsigned* pk = reinterpret_cast<unsigned*>(base + q.o_pk);
+  int* pv = reinterpret_cast<int*>(base + q.o_pv);
+  hipLaunchKernelGGL(sdf_init_kernel, dim3(1), dim3(64), 0, s, pws);
+  const unsigned bbb = (unsigned)std::min<int64_t>((P + 255) / 256, 1024);
+  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(bbb), dim3(256), 0, s, points, P, pws);
+  hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P, 0,
+                     (const unsigned*)pws, pk, pv);
+  size_t t2 = q.tp;
+  bool ok = hipcub::DeviceRadixSort::SortPairs(base + q.o_tmp, t2, pk, pk + m, pv, pv + m, m, 0, 30, s) == hipSuccess;
+  hipLaunchKernelGGL(sdf_tree_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0, s, points,
                      P, (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
-                     reinterpret_cast<const Sphere*>(mesh + mesh_sph_off(C)), C, ws, sqdist, sign, normals, clst,
-                     face_idx, best, reinterpret_cast<const float4*>(mesh + mesh_fsph_off(C)),
-                     reinterpret_cast<const float4*>(mesh + mesh_ssph_off(C)), (int)g_sdf_count);
-  hipLaunchKernelGGL(sdf_culled_finalize_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P, faces,
-                     (const unsigned long long*)best, sqdist, sign, normals, clst, face_idx);
-#endif
+                     reinterpret_cast<const Slab*>(mesh + mesh_slab_off(C)),
+                     reinterpret_cast<const Node*>(mesh + mesh_chunk_off(C)),
+                     reinterpret_cast<const Node*>(mesh + mesh_top_off(C)), (int)C, (int)T, mws, sqdist, sign, normals,
+                     clst, face_idx, (int)g_sdf_count);
   hipLaunchKernelGGL(sdf_exact_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0, s, points,
-                     P, faces, F, ws, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
+                     P, faces, F, mws, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
   ok = ok && hipGetLastError() == hipSuccess;
-  ok = (hipFreeAsync(base, s) == hipSuccess) && ok;
   return ok ? CDX_OK : CDX_ELAUNCH;
+}
+
+// mesh_query with workspace `ws` (ws_bytes ≥ cdx_sdf_query_workspace(P)), or stream-ordered scratch when ws is
+// NULL.
+int mesh_query_ws(const char* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
+                  int32_t* sign, float* normals, float* clst, int32_t* face_idx, void* ws, size_t ws_bytes,
+                  hipStream_t s) {
+  QueryWs q;
+  if (!query_ws(P, s, q)) return CDX_ELAUNCH;
+  if (ws) {
+    if (ws_bytes < q.bytes) return CDX_EINVAL;
+    return mesh_query(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, static_cast<char*>(ws), q, s);
+  }
+  char* base = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&base), q.bytes, s) != hipSuccess) return CDX_ELAUNCH;
+  int rc = mesh_query(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, base, q, s);
+  if (hipFreeAsync(base, s) != hipSuccess && !rc) rc = CDX_ELAUNCH;
+  return rc;
 }
 
 bool sdf_args_ok(int64_t P, const float* points, const float* faces, int64_t F, const float* sqdist,
@@ -950,27 +878,35 @@ int cdx_sdf_forward(const float* points, int64_t P, const float* faces, int64_t 
   }
   char* mesh = nullptr;
   if (hipMallocAsync(reinterpret_cast<void**>(&mesh), mesh_bytes(F), s) != hipSuccess) return CDX_ELAUNCH;
-  int rc = mesh_build(faces, F, points, P, mesh, s);
-  if (!rc) rc = mesh_query(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, s);
+  int rc = mesh_build_morton(faces, F, mesh, s);
+  if (!rc) rc = mesh_query_ws(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, nullptr, 0, s);
   if (hipFreeAsync(mesh, s) != hipSuccess && !rc) rc = CDX_ELAUNCH;
   return rc;
 }
 
-size_t cdx_sdf_mesh_bytes(int64_t F) { return F > 0 ? mesh_bytes(F) : 0; }
+size_t cdx_sdf_mesh_bytes(int64_t F) { return F > 0 && F <= INT32_MAX / 9 ? mesh_bytes(F) : 0; }
 
 int cdx_sdf_mesh_prepare(const float* faces, int64_t F, void* mesh, cdx_stream_t stream) {
   if (F <= 0 || F > INT32_MAX / 9 || !faces || !mesh) return CDX_EINVAL;
-  return mesh_build(faces, F, nullptr, 0, static_cast<char*>(mesh), reinterpret_cast<hipStream_t>(stream));
+  return mesh_build_kd(faces, F, static_cast<char*>(mesh), reinterpret_cast<hipStream_t>(stream));
+}
+
+size_t cdx_sdf_query_workspace(int64_t P) {
+  if (P <= 0 || P > INT32_MAX) return 0;
+  QueryWs q;
+  return query_ws(P, nullptr, q) ? q.bytes : 0;
 }
 
 int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
-                  int32_t* sign, float* normals, float* clst, int32_t* face_idx, cdx_stream_t stream) {
+                  int32_t* sign, float* normals, float* clst, int32_t* face_idx, void* workspace,
+                  size_t workspace_bytes, cdx_stream_t stream) {
   if (P < 0 || F < 0 || !mesh) return CDX_EINVAL;
   if (P == 0) return CDX_OK;
   if (!sdf_args_ok(P, points, faces, F, sqdist, sign, normals, clst)) return CDX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (sdf_mode() == 1) return cdx_sdf_forward(points, P, faces, F, sqdist, sign, normals, clst, face_idx, stream);
-  return mesh_query(static_cast<const char*>(mesh), faces, F, points, P, sqdist, sign, normals, clst, face_idx, s);
+  return mesh_query_ws(static_cast<const char*>(mesh), faces, F, points, P, sqdist, sign, normals, clst, face_idx,
+                       workspace, workspace_bytes, s);
 }
 
 int cdx_sdf_chunk_visits(uint64_t* out, cdx_stream_t stream) {

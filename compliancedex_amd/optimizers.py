@@ -24,8 +24,7 @@ from . import _native as N
 from .force_eq import force_eq_descriptor, force_eq_reward
 from .optimizer import EE_OFFSETS, FINGERTIP_LB, FINGERTIP_UB, WRIST_OFFSET
 from .robot_model import DifferentiableRobotModel
-from .torchsdf import _forward as _sdf_query
-from .torchsdf import compute_sdf
+from .torchsdf import PreparedMesh, compute_sdf
 
 
 class TriangleMesh:
@@ -105,13 +104,61 @@ def _noise(tape, s):
     return None if tape is None else tape[s]
 
 
+class _FusedLoop:
+    """Device state of a fused Kin / SDF loop: the two prepared meshes, cdx_kin_cost's outputs (margin / normal
+    in two alternating slots), the optimiser moments, the best iterate and the cdx_kin_step buffers.  Per
+    iteration the loop is three TorchSDF queries, cdx_kin_cost and cdx_kin_step (optimiser, best iterate,
+    clamps and — Kin — the next fingertips' FK): no autograd graph, no host sync."""
+
+    def __init__(self, E, T, pose, target, comp, faces, faces_deflate, dev):
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.mesh, self.mesh_def = PreparedMesh(faces), PreparedMesh(faces_deflate)
+        self.pose, self.target, self.comp = pose, target, comp
+        self.loss = torch.empty(E, dtype=torch.float64, device=dev)
+        self.margin = [torch.zeros(E, T, dtype=torch.float64, device=dev) for _ in range(2)]
+        self.normal = [torch.zeros(E * T, 3, **f32) for _ in range(2)]
+        self.g = [torch.empty_like(pose), torch.empty_like(target), torch.empty_like(comp)]
+        self.m = [torch.zeros_like(pose), torch.zeros_like(target), torch.zeros_like(comp)]
+        self.v = [torch.zeros_like(pose), torch.zeros_like(target), torch.zeros_like(comp)]
+        self.opt_value = torch.full((E,), float("inf"), **f32)
+        self.opt_margin = torch.zeros(E, T, dtype=torch.float64, device=dev)
+        self.opt_normal = torch.zeros(E * T, 3, **f32)
+        self.opt = [pose.clone(), target.clone(), comp.clone()]
+        self.any = torch.zeros(3, dtype=torch.int32, device=dev)
+        self.tips = torch.empty(E * T, 3, **f32)
+        b = N.CdxKinOptBuffers()
+        for name, t in (("pose", pose), ("target", target), ("comp", comp), ("g_pose", self.g[0]),
+                        ("g_target", self.g[1]), ("g_comp", self.g[2]), ("m_pose", self.m[0]), ("v_pose", self.v[0]),
+                        ("m_target", self.m[1]), ("v_target", self.v[1]), ("m_comp", self.m[2]), ("v_comp", self.v[2]),
+                        ("loss", self.loss), ("opt_value", self.opt_value), ("opt_margin", self.opt_margin),
+                        ("opt_normal", self.opt_normal), ("opt_pose", self.opt[0]), ("opt_target", self.opt[1]),
+                        ("opt_comp", self.opt[2]), ("any", self.any)):
+            setattr(b, name, N.ptr(t))
+        for i in range(2):
+            b.margin[i], b.normal[i] = N.ptr(self.margin[i]), N.ptr(self.normal[i])
+        self.buffers = b
+
+    def queries(self, tips, target):
+        _, sign1, n1, _, _ = self.mesh_def.query(tips)
+        dist, sign2, n2, clst, _ = self.mesh.query(tips)
+        tdist, tsign, _, tclst, _ = self.mesh.query(target.view(-1, 3))
+        return sign1, n1, dist, sign2, n2, clst, tdist, tsign, tclst
+
+    def best(self):
+        return self.opt[0], self.opt[2], self.opt[1], (self.opt_margin > 0.0).all()
+
+
 class KinGraspOptimizer:
     """Joint-space optimiser on the TorchSDF mesh distance (optimize_pregrasp.py:121-227)."""
 
     def __init__(self, robot_urdf, ee_link_names, ee_link_offsets=EE_OFFSETS, palm_offset=(-0.01, 0.015, 0.12),
                  num_iters=1000, optimize_target=False, ref_q=None, mass=0.1, com=(0.0, 0.0, 0.0), gravity=True,
-                 uncertainty=0.0, device="cuda"):
+                 uncertainty=0.0, device="cuda", seed=0):
+        """``seed``: key of the fused loop's on-device Kabsch noise (used when no ``kabsch_noise`` tape is given);
+        iteration k of this optimiser's n-th fused call draws with key seed + (iterations before it) + k + 1."""
         self.device = torch.device(device)
+        self._seed = int(seed)
+        self.loop_events = None  # optional (start, end) CUDA events around a fused loop's iterations
         self.ref_q = torch.tensor(list(ref_q)).to(self.device)
         self.robot_model = DifferentiableRobotModel(robot_urdf, device=device)
         self.num_iters = num_iters
@@ -130,33 +177,31 @@ class KinGraspOptimizer:
     def optimize(self, joint_angles, target_pose, compliance, friction_mu, object_mesh, verbose=True,
                  kabsch_noise=None, trace_rows=False, fused=True):
         """``trace_rows``: also keep every iteration's per-candidate loss in ``loss_rows`` (device).
-        ``fused`` (default): per iteration one FK launch, the three TorchSDF queries on cached prepared
-        meshes and ONE cost-and-backward kernel (cdx_kin_cost: force_eq_reward, the six cost terms and the
-        backward through them, TorchSDF and the FK chain) writing the parameters' gradients — no autograd
-        graph; ``fused=False``: the same loop through the autograd drop-ins (compute_sdf, force_eq_reward,
-        the FK module) and torch tensor ops, as the reference writes it."""
+        ``fused`` (default): per iteration the three TorchSDF queries on prepared meshes, ONE cost-and-backward
+        kernel (cdx_kin_cost: force_eq_reward, the six cost terms and the backward through them, TorchSDF and
+        the FK chain) and ONE step kernel (cdx_kin_step: Adam, the best iterate, the next fingertips' FK) — no
+        autograd graph, no host sync; ``fused=False``: the same loop through the autograd drop-ins
+        (compute_sdf, force_eq_reward, the FK module), torch tensor ops and torch.optim.Adam, as the reference
+        writes it."""
         self.loss_history = []
         self.loss_rows = []
-        joint_angles = joint_angles.clone().requires_grad_(True)
-        compliance = compliance.clone().requires_grad_(True)
         faces = _face_vertices(object_mesh, self.device)
         object_mesh.scale(0.9, center=[0, 0, 0])
         faces_deflate = _face_vertices(object_mesh, self.device)
-        # the fused loop also takes torch's single-kernel Adam (same update rule; one launch per step instead
-        # of the foreach path's ≈ 21 — profiles/r04d_config4_kin_iteration_split.json)
-        afused = dict(fused=True) if fused and self.device.type == "cuda" else {}
+        E, T = target_pose.shape[0], target_pose.shape[1]
+        lrs = (2e-3, 1e-5, 0.2) if self.optimize_target else (1e-2, 0.0, 0.2)  # q, target, compliance (:168-176)
+        if fused:
+            return self._optimize_fused(joint_angles, target_pose, compliance, friction_mu, faces, faces_deflate, lrs,
+                                        verbose, kabsch_noise, trace_rows)
+        joint_angles = joint_angles.clone().requires_grad_(True)
+        compliance = compliance.clone().requires_grad_(True)
         if self.optimize_target:
             target_pose = target_pose.clone().requires_grad_(True)
-            optim = torch.optim.Adam([{"params": joint_angles, "lr": 2e-3}, {"params": target_pose, "lr": 1e-5},
-                                      {"params": compliance, "lr": 0.2}], **afused)
+            optim = torch.optim.Adam([{"params": joint_angles, "lr": lrs[0]}, {"params": target_pose, "lr": lrs[1]},
+                                      {"params": compliance, "lr": lrs[2]}])
         else:
-            optim = torch.optim.Adam([{"params": joint_angles, "lr": 1e-2}, {"params": compliance, "lr": 0.2}],
-                                     **afused)
-        E, T = target_pose.shape[0], target_pose.shape[1]
+            optim = torch.optim.Adam([{"params": joint_angles, "lr": lrs[0]}, {"params": compliance, "lr": lrs[2]}])
         best = _Best(torch.float32, E, T, self.device, q=joint_angles, comp=compliance, target=target_pose)
-        if fused:
-            return self._optimize_fused(joint_angles, target_pose, compliance, friction_mu, faces, faces_deflate,
-                                        optim, best, verbose, kabsch_noise, trace_rows)
         for s in range(self.num_iters):
             optim.zero_grad()
             all_tip = self.forward_kinematics(joint_angles)
@@ -186,69 +231,66 @@ class KinGraspOptimizer:
         self.best_loss = best.value
         return best.params["q"], best.params["comp"], best.params["target"], best.flag()
 
-    def _optimize_fused(self, joint_angles, target_pose, compliance, friction_mu, faces, faces_deflate, optim, best,
-                        verbose, kabsch_noise, trace_rows):
+    def _optimize_fused(self, joint_angles, target_pose, compliance, friction_mu, faces, faces_deflate, lrs, verbose,
+                        kabsch_noise, trace_rows):
         lib = N.load()
         dev = self.device
         E, T = target_pose.shape[0], target_pose.shape[1]
+        q, tgt, comp = (x.detach().clone().contiguous() for x in (joint_angles, target_pose, compliance))
+        if any(x.dtype != torch.float32 for x in (q, tgt, comp)):
+            raise ValueError("KinGraspOptimizer: joint angles, targets and compliances must be float32 (the "
+                             "reference's dtype on this path)")
         chain = self.robot_model._descriptor(self.ee_link_names, self.ee_link_offsets)
-        D = chain.n_dofs
         prm = N.CdxKinParams()
         prm.fe = force_eq_descriptor(T, friction_mu, self.mass, 10.0 if self.gravity else None, 2.0, self.com)
         for i, v in enumerate(self.ref_q.float().tolist()):
             prm.ref_q[i] = v
-        f32 = dict(dtype=torch.float32, device=dev)
-        tips = torch.empty(E * T, 3, **f32)
-        loss = torch.empty(E, dtype=torch.float64, device=dev)
-        margin = torch.empty(E, T, dtype=torch.float64, device=dev)
-        normal = torch.empty(E * T, 3, **f32)
-        g_q, g_target, g_comp = torch.empty(E, D, **f32), torch.empty(E, T, 3, **f32), torch.empty(E, T, **f32)
-        offset = self.palm_offset.float()
+        cfg = N.CdxKinOpt()
+        cfg.rule, cfg.clamp_box = 0, 0
+        cfg.lr[0], cfg.lr[1], cfg.lr[2] = lrs
+        cfg.beta1, cfg.beta2, cfg.eps = 0.9, 0.999, 1e-8  # torch.optim.Adam defaults (:171)
+        off = self.palm_offset.float().cpu().tolist()
+        for i in range(3):
+            cfg.palm_offset[i] = off[i]
+        st = _FusedLoop(E, T, q, tgt, comp, faces, faces_deflate, dev)
+        st.buffers.tips = N.ptr(st.tips)
         stream = N.stream_ptr(dev)
+        N.check(lib.cdx_fk_forward(chain, N.ptr(q), E, N.ptr(st.tips), None, stream), "cdx_fk_forward")
+        st.tips.add_(self.palm_offset.float())  # FK + palm offset (:148); later iterations: cdx_kin_step
+        if self.loop_events:
+            self.loop_events[0].record()
         for s in range(self.num_iters):
-            q = joint_angles.detach()
-            if not q.is_contiguous() or q.dtype != torch.float32:
-                raise ValueError("KinGraspOptimizer: joint angles must be a contiguous float32 tensor")
-            N.check(lib.cdx_fk_forward(chain, N.ptr(q), E, N.ptr(tips), None, stream), "cdx_fk_forward")
-            tips.add_(offset)  # FK + palm offset (:148)
-            tgt = target_pose.detach().reshape(-1, 3).contiguous()
-            _, sign1, n1, _, _ = _sdf_query(tips, faces_deflate, False)
-            dist, sign2, n2, clst, _ = _sdf_query(tips, faces, False)
-            tdist, tsign, _, tclst, _ = _sdf_query(tgt, faces, False)
             nz = _noise(kabsch_noise, s)
             nz = None if nz is None else nz.detach().to(device=dev, dtype=torch.float64).contiguous()
-            comp = compliance.detach().contiguous()
-            N.check(lib.cdx_kin_cost(chain, prm, E, N.ptr(q), N.ptr(tips), N.ptr(tgt), N.ptr(comp), N.ptr(sign1),
-                                     N.ptr(n1), N.ptr(dist), N.ptr(sign2), N.ptr(n2), N.ptr(clst), N.ptr(tdist),
-                                     N.ptr(tsign), N.ptr(tclst), N.ptr(nz), next(_kin_seeds), N.ptr(loss), N.ptr(margin),
-                                     N.ptr(normal), N.ptr(g_q), N.ptr(g_target), N.ptr(g_comp), None, stream),
-                    "cdx_kin_cost")
-            joint_angles.grad = g_q.clone()
-            compliance.grad = g_comp.clone()
-            if self.optimize_target:
-                target_pose.grad = g_target.clone()
-            self.loss_history.append(loss.sum())  # device scalar, no sync
+            self._seed += 1
+            N.check(lib.cdx_kin_cost(chain, prm, E, N.ptr(q), N.ptr(st.tips), N.ptr(tgt), N.ptr(comp),
+                                     *(N.ptr(t) for t in st.queries(st.tips, tgt)), N.ptr(nz), self._seed,
+                                     N.ptr(st.loss), N.ptr(st.margin[s & 1]), N.ptr(st.normal[s & 1]), N.ptr(st.g[0]),
+                                     N.ptr(st.g[1]), N.ptr(st.g[2]), None, stream), "cdx_kin_cost")
+            self.loss_history.append(st.loss.sum())  # device scalar, no sync
             if trace_rows:
-                self.loss_rows.append(loss.clone())
+                self.loss_rows.append(st.loss.clone())
             if verbose:
-                print("Loss:", float(loss.sum()), compliance)
-            best.update(loss, margin, normal.clone(), q=joint_angles, comp=compliance, target=target_pose)
-            optim.step()
+                print("Loss:", float(st.loss.sum()), comp)
+            N.check(lib.cdx_kin_step(chain, cfg, st.buffers, E, T, s, 0, stream), "cdx_kin_step")
+        N.check(lib.cdx_kin_step(chain, cfg, st.buffers, E, T, self.num_iters, 1, stream), "cdx_kin_step")
+        if self.loop_events:
+            self.loop_events[1].record()
         if verbose:
-            print(best.margin, best.normal)
-        self.best_loss = best.value
-        return best.params["q"], best.params["comp"], best.params["target"], best.flag()
-
-
-_kin_seeds = __import__("itertools").count(0x6B1)
+            print(st.opt_margin, st.opt_normal)
+        self.best_loss = st.opt_value
+        return st.best()
 
 
 class SDFGraspOptimizer:
     """Fingertip-space optimiser on the TorchSDF mesh distance (optimize_pregrasp.py:229-320)."""
 
     def __init__(self, tip_bounding_box, num_iters=2000, optimize_target=False, mass=0.1, com=(0.0, 0.0, 0.0),
-                 gravity=True, uncertainty=0.0, device="cuda"):
+                 gravity=True, uncertainty=0.0, device="cuda", seed=0):
+        """``seed``: key of the fused loop's on-device Kabsch noise (as KinGraspOptimizer's)."""
         self.device = torch.device(device)
+        self._seed = int(seed)
+        self.loop_events = None  # optional (start, end) CUDA events around a fused loop's iterations
         self.tip_bounding_box = [torch.tensor(tip_bounding_box[0]).to(self.device).view(-1, 3),
                                  torch.tensor(tip_bounding_box[1]).to(self.device).view(-1, 3)]
         self.num_iters = num_iters
@@ -258,26 +300,28 @@ class SDFGraspOptimizer:
     def optimize(self, tip_pose, target_pose, compliance, friction_mu, object_mesh, verbose=True, kabsch_noise=None,
                  trace_rows=False, fused=True):
         """``trace_rows``: also keep every iteration's per-candidate loss in ``loss_rows`` (device).
-        ``fused`` (default): per iteration the three TorchSDF queries on cached prepared meshes and ONE
-        cost-and-backward kernel (cdx_kin_cost without a chain); ``fused=False``: the autograd loop."""
-        tip_pose = tip_pose.clone().requires_grad_(True)
+        ``fused`` (default): per iteration the three TorchSDF queries on prepared meshes, ONE cost-and-backward
+        kernel (cdx_kin_cost without a chain) and ONE step kernel (cdx_kin_step: RMSprop, the best iterate, the
+        box clamps); ``fused=False``: the autograd loop with torch.optim.RMSprop."""
         self.loss_history = []
         self.loss_rows = []
-        compliance = compliance.clone().requires_grad_(True)
         faces = _face_vertices(object_mesh, self.device)
         object_mesh.scale(0.9, center=[0, 0, 0])
         faces_deflate = _face_vertices(object_mesh, self.device)
+        E, T = tip_pose.shape[0], tip_pose.shape[1]
+        lrs = (1e-3, 1e-3 if self.optimize_target else 0.0, 0.2)  # tips, target, compliance (:250-259)
+        if fused:
+            return self._optimize_fused(tip_pose, target_pose, compliance, friction_mu, faces, faces_deflate, lrs,
+                                        verbose, kabsch_noise, trace_rows)
+        tip_pose = tip_pose.clone().requires_grad_(True)
+        compliance = compliance.clone().requires_grad_(True)
         if self.optimize_target:
             target_pose = target_pose.clone().requires_grad_(True)
-            optim = torch.optim.RMSprop([{"params": tip_pose, "lr": 1e-3}, {"params": target_pose, "lr": 1e-3},
-                                         {"params": compliance, "lr": 0.2}])
+            optim = torch.optim.RMSprop([{"params": tip_pose, "lr": lrs[0]}, {"params": target_pose, "lr": lrs[1]},
+                                         {"params": compliance, "lr": lrs[2]}])
         else:
-            optim = torch.optim.RMSprop([{"params": tip_pose, "lr": 1e-3}, {"params": compliance, "lr": 0.2}])
-        E, T = tip_pose.shape[0], tip_pose.shape[1]
+            optim = torch.optim.RMSprop([{"params": tip_pose, "lr": lrs[0]}, {"params": compliance, "lr": lrs[2]}])
         best = _Best(torch.float32, E, T, self.device, tip=tip_pose, comp=compliance, target=target_pose)
-        if fused:
-            return self._optimize_fused(tip_pose, target_pose, compliance, friction_mu, faces, faces_deflate, optim,
-                                        best, verbose, kabsch_noise, trace_rows)
         for s in range(self.num_iters):
             optim.zero_grad()
             all_tip = tip_pose.view(-1, 3)
@@ -307,53 +351,50 @@ class SDFGraspOptimizer:
         self.best_loss = best.value
         return best.params["tip"], best.params["comp"], best.params["target"], best.flag()
 
-    def _optimize_fused(self, tip_pose, target_pose, compliance, friction_mu, faces, faces_deflate, optim, best,
-                        verbose, kabsch_noise, trace_rows):
+    def _optimize_fused(self, tip_pose, target_pose, compliance, friction_mu, faces, faces_deflate, lrs, verbose,
+                        kabsch_noise, trace_rows):
         lib = N.load()
         dev = self.device
         E, T = tip_pose.shape[0], tip_pose.shape[1]
+        tips, tgt, comp = (x.detach().clone().contiguous() for x in (tip_pose, target_pose, compliance))
+        if any(x.dtype != torch.float32 for x in (tips, tgt, comp)):
+            raise ValueError("SDFGraspOptimizer: tip poses, targets and compliances must be float32 (TorchSDF's path)")
         prm = N.CdxKinParams()
         prm.fe = force_eq_descriptor(T, friction_mu, self.mass, 10.0 if self.gravity else None, 2.0, self.com)
-        f32 = dict(dtype=torch.float32, device=dev)
-        loss = torch.empty(E, dtype=torch.float64, device=dev)
-        margin = torch.empty(E, T, dtype=torch.float64, device=dev)
-        normal = torch.empty(E * T, 3, **f32)
-        g_tip, g_target, g_comp = torch.empty(E, T, 3, **f32), torch.empty(E, T, 3, **f32), torch.empty(E, T, **f32)
+        cfg = N.CdxKinOpt()
+        cfg.rule, cfg.clamp_box = 1, 1
+        cfg.lr[0], cfg.lr[1], cfg.lr[2] = lrs
+        cfg.alpha, cfg.eps = 0.99, 1e-8  # torch.optim.RMSprop defaults (:253)
+        lb = self.tip_bounding_box[0].float().expand(T, 3).reshape(-1).cpu().tolist()
+        ub = self.tip_bounding_box[1].float().expand(T, 3).reshape(-1).cpu().tolist()
+        for i in range(3 * T):
+            cfg.box_lb[i], cfg.box_ub[i] = lb[i], ub[i]
+        st = _FusedLoop(E, T, tips, tgt, comp, faces, faces_deflate, dev)
         stream = N.stream_ptr(dev)
+        if self.loop_events:
+            self.loop_events[0].record()
         for s in range(self.num_iters):
-            tips = tip_pose.detach().reshape(-1, 3).contiguous()
-            tgt = target_pose.detach().reshape(-1, 3).contiguous()
-            if tips.dtype != torch.float32 or tgt.dtype != torch.float32:
-                raise ValueError("SDFGraspOptimizer: tip and target poses must be float32 (TorchSDF's path)")
-            _, sign1, n1, _, _ = _sdf_query(tips, faces_deflate, False)
-            dist, sign2, n2, clst, _ = _sdf_query(tips, faces, False)
-            tdist, tsign, _, tclst, _ = _sdf_query(tgt, faces, False)
             nz = _noise(kabsch_noise, s)
             nz = None if nz is None else nz.detach().to(device=dev, dtype=torch.float64).contiguous()
-            comp = compliance.detach().contiguous()
-            N.check(lib.cdx_kin_cost(None, prm, E, None, N.ptr(tips), N.ptr(tgt), N.ptr(comp), N.ptr(sign1), N.ptr(n1),
-                                     N.ptr(dist), N.ptr(sign2), N.ptr(n2), N.ptr(clst), N.ptr(tdist), N.ptr(tsign),
-                                     N.ptr(tclst), N.ptr(nz), next(_kin_seeds), N.ptr(loss), N.ptr(margin),
-                                     N.ptr(normal), None, N.ptr(g_target), N.ptr(g_comp), N.ptr(g_tip), stream),
-                    "cdx_kin_cost")
-            tip_pose.grad = g_tip.clone()
-            compliance.grad = g_comp.clone()
-            if self.optimize_target:
-                target_pose.grad = g_target.clone()
-            self.loss_history.append(loss.sum())  # device scalar, no sync
+            self._seed += 1
+            pts = tips.view(-1, 3)
+            N.check(lib.cdx_kin_cost(None, prm, E, None, N.ptr(pts), N.ptr(tgt), N.ptr(comp),
+                                     *(N.ptr(t) for t in st.queries(pts, tgt)), N.ptr(nz), self._seed, N.ptr(st.loss),
+                                     N.ptr(st.margin[s & 1]), N.ptr(st.normal[s & 1]), None, N.ptr(st.g[1]),
+                                     N.ptr(st.g[2]), N.ptr(st.g[0]), stream), "cdx_kin_cost")
+            self.loss_history.append(st.loss.sum())  # device scalar, no sync
             if trace_rows:
-                self.loss_rows.append(loss.clone())
+                self.loss_rows.append(st.loss.clone())
             if verbose:
-                print("Loss:", float(loss.sum()))
-            best.update(loss, margin, normal.clone(), tip=tip_pose, comp=compliance, target=target_pose)
-            optim.step()
-            with torch.no_grad():  # bounding-box constraints (:312-314)
-                tip_pose.clamp_(min=self.tip_bounding_box[0], max=self.tip_bounding_box[1])
-                target_pose.clamp_(min=self.tip_bounding_box[0], max=self.tip_bounding_box[1])
+                print("Loss:", float(st.loss.sum()))
+            N.check(lib.cdx_kin_step(None, cfg, st.buffers, E, T, s, 0, stream), "cdx_kin_step")
+        N.check(lib.cdx_kin_step(None, cfg, st.buffers, E, T, self.num_iters, 1, stream), "cdx_kin_step")
+        if self.loop_events:
+            self.loop_events[1].record()
         if verbose:
-            print(best.margin, best.normal)
-        self.best_loss = best.value
-        return best.params["tip"], best.params["comp"], best.params["target"], best.flag()
+            print(st.opt_margin, st.opt_normal)
+        self.best_loss = st.opt_value
+        return st.best()
 
 
 class GPISGraspOptimizer:

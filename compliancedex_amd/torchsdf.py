@@ -2,8 +2,8 @@
 
 ``compute_sdf(points, face_vertices) -> (sqdist, sign, normals, clst_points)``: squared
 distance (autograd w.r.t. points), int32 sign, unit (p − c) normal and closest point
-(sdf.py:34-64), computed by cdx_sdf_query on a cached prepared mesh / cdx_sdf_backward (float32, the
-culled path) or
+(sdf.py:34-64), computed by cdx_sdf_forward (one shot) or cdx_sdf_query on a PreparedMesh /
+cdx_sdf_backward (float32, the culled path) or
 cdx_sdf_forward_f64 / cdx_sdf_backward_f64 (float64, the reference's double instantiation,
 unbatched_triangle_distance_cuda.cu:282).  ``compute_sdf_with_faces`` additionally returns the
 argmin face index.
@@ -34,34 +34,60 @@ def _check(points, faces):
         raise RuntimeError(f"face_vertices must have shape [F, 3, 3], got {tuple(faces.shape)}")
 
 
-class _MeshCache:
-    """Prepared float32 meshes (cdx_sdf_mesh_prepare) of the face tensors queried last: the optimisers
-    query the same two meshes every iteration, so the face records / chunk spheres are built once.
-    Keyed by the face tensor's storage, shape, device and version counter (an in-place change bumps
-    it); an entry holds its face tensor, so the storage cannot be reused while cached."""
+class PreparedMesh:
+    """A float32 triangle mesh prepared once for repeated queries (cdx_sdf_mesh_prepare: face records in the
+    order of a k-d tree on the centroids, their disk slabs, the 32-face chunks' and 512-face top nodes'
+    bounding cylinders) — the SDF / Kin optimisers query the same two meshes every iteration.
 
-    def __init__(self, size=8):
-        self.size, self.entries = size, {}
+    The handle owns a private copy of the faces: later writes to the caller's tensor (in place, through
+    ``.data``, DLPack, raw device pointers or a graph replay) never reach it, so a query always answers for
+    the mesh the handle was built from; build a new handle for a changed mesh.  Its query scratch (the points'
+    Morton sort) is kept and regrown when a larger batch comes, so a loop at a fixed point count allocates
+    nothing per query.  Preparing copies the faces to the host once (a wait on the current stream)."""
 
-    def get(self, faces):
-        key = (faces.data_ptr(), tuple(faces.shape), faces.device.index, faces._version)
-        hit = self.entries.pop(key, None)
-        if hit is None:
-            lib = N.load()
-            buf = torch.empty(lib.cdx_sdf_mesh_bytes(faces.shape[0]), dtype=torch.uint8, device=faces.device)
-            N.check(lib.cdx_sdf_mesh_prepare(N.ptr(faces), faces.shape[0], N.ptr(buf), N.stream_ptr(faces.device)),
-                    "cdx_sdf_mesh_prepare")
-            hit = (faces, buf)
-            if len(self.entries) >= self.size:
-                self.entries.pop(next(iter(self.entries)))
-        self.entries[key] = hit  # most recent last
-        return hit[1]
+    def __init__(self, face_vertices):
+        _check(face_vertices.new_zeros(0, 3), face_vertices)
+        if face_vertices.dtype != torch.float32 or face_vertices.shape[0] == 0:
+            raise RuntimeError("PreparedMesh takes a non-empty float32 [F, 3, 3] face tensor")
+        lib = N.load()
+        self.faces = face_vertices.detach().contiguous().clone()
+        F = self.faces.shape[0]
+        self.buf = torch.empty(lib.cdx_sdf_mesh_bytes(F), dtype=torch.uint8, device=self.faces.device)
+        N.check(lib.cdx_sdf_mesh_prepare(N.ptr(self.faces), F, N.ptr(self.buf), N.stream_ptr(self.faces.device)),
+                "cdx_sdf_mesh_prepare")
+        self._ws = torch.empty(0, dtype=torch.uint8, device=self.faces.device)
 
+    @property
+    def num_faces(self):
+        return self.faces.shape[0]
 
-_meshes = _MeshCache()
+    def query(self, points, want_face=False):
+        """(sqdist, sign, normals, clst, face | None) of float32 points [P, 3] (cdx_sdf_query)."""
+        _check(points, self.faces)
+        lib = N.load()
+        points = points.detach().contiguous()
+        P, dev = points.shape[0], points.device
+        dist = torch.empty(P, dtype=torch.float32, device=dev)
+        sign = torch.empty(P, dtype=torch.int32, device=dev)
+        normals = torch.empty(P, 3, dtype=torch.float32, device=dev)
+        clst = torch.empty(P, 3, dtype=torch.float32, device=dev)
+        face = torch.empty(P, dtype=torch.int32, device=dev) if want_face else None
+        if P == 0:
+            return dist, sign, normals, clst, face
+        need = lib.cdx_sdf_query_workspace(P)
+        if self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        N.check(lib.cdx_sdf_query(N.ptr(self.buf), N.ptr(self.faces), self.faces.shape[0], N.ptr(points), P,
+                                  N.ptr(dist), N.ptr(sign), N.ptr(normals), N.ptr(clst), N.ptr(face),
+                                  N.ptr(self._ws), self._ws.numel(), N.stream_ptr(dev)), "cdx_sdf_query")
+        return dist, sign, normals, clst, face
 
 
 def _forward(points, faces, want_face):
+    """One-shot query (cdx_sdf_forward: the mesh's records and bounds are built for this call on the device —
+    faces in Morton order of their cubic frame — or the double instantiation's brute-force scan)."""
+    if isinstance(faces, PreparedMesh):
+        return faces.query(points, want_face)
     _check(points, faces)
     lib = N.load()
     points = points.contiguous()
@@ -72,11 +98,6 @@ def _forward(points, faces, want_face):
     normals = torch.zeros(P, 3, dtype=points.dtype, device=points.device)
     clst = torch.zeros(P, 3, dtype=points.dtype, device=points.device)
     face = torch.zeros(P, dtype=torch.int32, device=points.device) if want_face else None
-    if points.dtype == torch.float32 and P > 0 and faces.shape[0] > 0:
-        N.check(lib.cdx_sdf_query(N.ptr(_meshes.get(faces)), N.ptr(faces), faces.shape[0], N.ptr(points), P, N.ptr(dist),
-                                  N.ptr(sign), N.ptr(normals), N.ptr(clst), N.ptr(face), N.stream_ptr(points.device)),
-                "cdx_sdf_query")
-        return dist, sign, normals, clst, face
     fwd = lib.cdx_sdf_forward if points.dtype == torch.float32 else lib.cdx_sdf_forward_f64
     N.check(fwd(N.ptr(points), P, N.ptr(faces), faces.shape[0], N.ptr(dist), N.ptr(sign), N.ptr(normals), N.ptr(clst),
                 N.ptr(face), N.stream_ptr(points.device)), "cdx_sdf_forward")
@@ -85,8 +106,9 @@ def _forward(points, faces, want_face):
 
 class _UnbatchedTriangleDistance(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, points, face_vertices):
-        dist, sign, normals, clst, _ = _forward(points.detach(), face_vertices.detach(), False)
+    def forward(ctx, points, face_vertices, mesh):
+        dist, sign, normals, clst, _ = _forward(points.detach(), mesh if mesh is not None else face_vertices.detach(),
+                                                False)
         ctx.save_for_backward(points.detach().contiguous(), clst)
         ctx.mark_non_differentiable(sign, normals, clst)
         return dist, sign, normals, clst
@@ -100,14 +122,18 @@ class _UnbatchedTriangleDistance(torch.autograd.Function):
         bwd = lib.cdx_sdf_backward if points.dtype == torch.float32 else lib.cdx_sdf_backward_f64
         N.check(bwd(N.ptr(grad_dist), N.ptr(points), N.ptr(clst), points.shape[0], N.ptr(grad_points),
                     N.stream_ptr(points.device)), "cdx_sdf_backward")
-        return grad_points, None
+        return grad_points, None, None
 
 
 def compute_sdf(pointclouds, face_vertices):
-    return _UnbatchedTriangleDistance.apply(pointclouds, face_vertices)
+    """sdf.py:34-64.  ``face_vertices``: a [F, 3, 3] tensor (one-shot query) or a PreparedMesh."""
+    if isinstance(face_vertices, PreparedMesh):
+        return _UnbatchedTriangleDistance.apply(pointclouds, face_vertices.faces, face_vertices)
+    return _UnbatchedTriangleDistance.apply(pointclouds, face_vertices, None)
 
 
 def compute_sdf_with_faces(points, face_vertices):
-    """Forward only; also returns the argmin face (first minimum, reference tile rule)."""
+    """Forward only; also returns the argmin face (first minimum, reference tile rule).  ``face_vertices``: a
+    tensor or a PreparedMesh."""
     with torch.no_grad():
         return _forward(points, face_vertices, True)

@@ -181,3 +181,32 @@ def surface_center(gpis):
 def config3_inputs(gpis, ref_q, E, seed):
     """Config 3's per-object candidates: ``prob_inputs`` around the object's surface centre."""
     return prob_inputs(ref_q, E, seed=seed, spread=True, center=surface_center(gpis))
+
+
+# Config 4's SDF / Kin leg: the KinGraspOptimizer iteration on iiwa7_allegro (23 DOF, the arm + Allegro chain,
+# depth 13) against the 16 384-face banana mesh, E = 16 384 candidates.  The arm base ("palm offset") is
+# placed so the fingertips at q = 0 surround the banana; q = 0.05·N(0, 1) per joint; targets at the banana's
+# centre + 1 cm noise; compliance [10, 10, 10, 20].  Three TorchSDF calls per iteration (:186-188):
+# 4E fingertips vs the deflated and the true mesh, 4E targets vs the true mesh.
+CONFIG4_OFFSETS = [[0.0, -0.04, 0.015]] * 3 + [[0.0, -0.05, -0.015]]
+
+
+def config4_kin_inputs(E=16384, seed=44, device="cuda", q_scale=0.05):
+    """(links, offsets, palm_offset [3] f32, q [E, 23], target [E, 4, 3], comp [E, 4]) — float32 numpy."""
+    from .robot_model import DifferentiableRobotModel
+    from .urdf import load_robot
+    D = 23
+    links = load_robot("iiwa7_allegro")["config"]["ee_link_name"]
+    center = np.load(os.path.join(DATA, "banana_center.npy"))
+    tips0 = DifferentiableRobotModel("iiwa7_allegro", device=device).compute_forward_kinematics(
+        torch.zeros(1, D, device=device), links, offsets=CONFIG4_OFFSETS)[0].view(4, 3).double().mean(0).cpu().numpy()
+    rng = np.random.default_rng(seed)
+    q = (q_scale * rng.standard_normal((E, D))).astype(np.float32)
+    target = (np.tile(center, (E, 4, 1)) + 0.01 * rng.standard_normal((E, 4, 3))).astype(np.float32)
+    comp = np.tile(np.array([10.0, 10.0, 10.0, 20.0], np.float32), (E, 1))
+    return links, CONFIG4_OFFSETS, (center - tips0).astype(np.float32), q, target, comp
+
+
+def banana_mesh():
+    from .optimizers import TriangleMesh
+    return TriangleMesh.from_npz(os.path.join(DATA, "meshes", "banana_mesh.npz"))

@@ -350,6 +350,52 @@ int cdx_kin_cost(const cdx_chain* chain, const cdx_kin_params* p, int64_t E, con
                  uint64_t seed, double* loss, double* margin, float* normal, float* g_q, float* g_target,
                  float* g_comp, float* g_tip, cdx_stream_t stream);
 
+/* ------------------------------------------------------- Kin / SDF optimiser step ------
+ * One launch per iteration of KinGraspOptimizer / SDFGraspOptimizer after cdx_kin_cost (float32 like the
+ * reference's parameters):
+ *   1. the best-iterate update (optimize_pregrasp.py:212-222 / :299-309): per candidate, loss < opt_value
+ *      (compared in double, stored as float) copies the pose, target and compliance the loss was computed on;
+ *      opt_margin / opt_normal are the WHOLE batch's margin / normal of the last iteration in which ANY
+ *      candidate improved (:215-217) — committed one launch late from the alternating kin_cost output slots
+ *      margin[s & 1] / normal[s & 1] through the device flags any[3] (zero them before iteration 0), and by a
+ *      `finalize` call after the last iteration (iteration = the iteration count; only commits);
+ *   2. the optimiser step (torch's single-tensor update order in float32): rule 0 Adam (Kin, :171-176; step
+ *      count iteration + 1), rule 1 RMSprop (SDF, :253-259; alpha, eps); lr 0 freezes a group;
+ *   3. clamp_box: target (and, for rule 1, the tips) into [box_lb, box_ub] per fingertip (:312-314);
+ *   4. rule 0 with `tips` set: the next iteration's fingertips FK(q) + palm_offset (:148), so the loop needs
+ *      no separate FK launch.
+ * pose is q [E*n_dofs] (rule 0) or the tips [E*n_tips*3] (rule 1); m_* are unused by RMSprop (v_* hold its
+ * square averages).  chain is required for rule 0 and ignored for rule 1. */
+typedef struct {
+  int32_t rule;                           /* 0 Adam (Kin), 1 RMSprop (SDF) */
+  int32_t clamp_box;
+  double lr[3];                           /* pose, target, compliance */
+  double beta1, beta2, eps;               /* Adam (eps also RMSprop's) */
+  double alpha;                           /* RMSprop */
+  float palm_offset[3];                   /* rule 0: tips = FK(q) + palm_offset */
+  float box_lb[CDX_MAX_TIPS * 3];
+  float box_ub[CDX_MAX_TIPS * 3];
+  int32_t _pad;
+} cdx_kin_opt;
+
+typedef struct {                          /* device pointers, candidate-major */
+  float *pose, *target, *comp;            /* parameters, in place */
+  const float *g_pose, *g_target, *g_comp;
+  float *m_pose, *v_pose, *m_target, *v_target, *m_comp, *v_comp;
+  const double* loss;                     /* [E] this iteration's cdx_kin_cost loss */
+  double* margin[2];                      /* [E*n_tips] cdx_kin_cost margin slots (iteration s wrote s & 1) */
+  float* normal[2];                       /* [E*n_tips*3] cdx_kin_cost normal slots */
+  float* opt_value;                       /* [E], +inf before iteration 0 */
+  double* opt_margin;                     /* [E*n_tips] */
+  float* opt_normal;                      /* [E*n_tips*3] */
+  float *opt_pose, *opt_target, *opt_comp;
+  uint32_t* any;                          /* [3] */
+  float* tips;                            /* rule 0: next fingertips [E*n_tips*3] (nullable) */
+} cdx_kin_opt_buffers;
+
+int cdx_kin_step(const cdx_chain* chain, const cdx_kin_opt* cfg, const cdx_kin_opt_buffers* buf, int64_t E,
+                 int32_t n_tips, int32_t iteration, int32_t finalize, cdx_stream_t stream);
+
 /* ------------------------------------------------------------ collision loss -------
  * Replaces ProbabilisticGraspOptimizer.compute_collision_loss (optimize_pregrasp.py:671-701):
  * anchor links by f32 FK (:674-676), palm transform R(euler XYZ)·a + palm_pos (:677-678), then
@@ -429,24 +475,30 @@ int cdx_sdf_forward_f64(const double* points, int64_t P, const double* faces, in
 int cdx_sdf_backward_f64(const double* grad_dist, const double* points, const double* clst, int64_t P,
                          double* grad_points, cdx_stream_t stream);
 
-/* A prepared mesh for repeated float32 queries (the SDF optimisers query the same meshes every
- * iteration): the face records in Morton order, their 32-face chunks' bounding spheres and the
- * may-NaN flag of cdx_sdf_forward's culled path, built once.  cdx_sdf_query is cdx_sdf_forward on it —
- * identical outputs (the face order only steers the culling; ties resolve by face index).  faces must
- * stay the ones prepared (the exact path of a NaN-capable mesh scans them).  mesh: cdx_sdf_mesh_bytes(F)
- * caller-owned device bytes. */
+/* A prepared mesh for repeated float32 queries (the SDF optimisers query the same two meshes every
+ * iteration): the face records in the order of a median-split k-d tree on the face centroids (built on
+ * the host: cdx_sdf_mesh_prepare copies the faces to the host and WAITS on `stream`), their disk slabs,
+ * the 32-face chunks' and 512-face top nodes' bounding cylinders and balls, and the may-NaN flag of the
+ * culled path.  cdx_sdf_query is cdx_sdf_forward on it — identical outputs (the face order only steers the
+ * culling; ties resolve by face index).  faces must stay the ones prepared (the exact path of a NaN-capable
+ * mesh scans them, and every output is recomputed from them).  mesh: cdx_sdf_mesh_bytes(F) caller-owned
+ * device bytes.  cdx_sdf_query's scratch (the points' Morton sort) is `workspace` (device, at least
+ * cdx_sdf_query_workspace(P) bytes — no allocation in the call), or stream-ordered scratch allocated by the
+ * call when workspace is NULL. */
 size_t cdx_sdf_mesh_bytes(int64_t F);
 int cdx_sdf_mesh_prepare(const float* faces, int64_t F, void* mesh, cdx_stream_t stream);
+size_t cdx_sdf_query_workspace(int64_t P);
 int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
-                  int32_t* sign, float* normals, float* clst, int32_t* face_idx, cdx_stream_t stream);
-/* Diagnostic work counters of cdx_sdf_forward (float path): out3 (nullable, host) = [(point, face) pairs
- * the culled kernel evaluated — every face of each chunk a wave could not rule out, times its live
- * lanes —, pairs of brute-force scans (the exact path), points queried]; read before `enable` applies.
+                  int32_t* sign, float* normals, float* clst, int32_t* face_idx, void* workspace,
+                  size_t workspace_bytes, cdx_stream_t stream);
+/* Diagnostic work counters of cdx_sdf_forward / cdx_sdf_query (float path): out3 (nullable, host) =
+ * [(point, face) pairs the culled kernel evaluated exactly — each lane's greedy seed face plus the pairs
+ * its slab bounds could not rule out —, pairs of brute-force scans (the exact path), points queried]; read before `enable` applies.
  * enable 1: zero the counters and count from now on (one atomic per wave); 0: stop counting; −1: only
  * read.  Against P·F per call this is the culling's work saving. */
 int cdx_sdf_stats(int32_t enable, uint64_t* out3, cdx_stream_t stream);
-/* Diagnostic companion of cdx_sdf_stats: chunks (32 faces) the culled kernel's waves fetched and
- * bound-tested face by face since counting was enabled, summed over waves. */
+/* Diagnostic companion of cdx_sdf_stats: chunks (32 faces) the culled kernel's waves evaluated pairs in
+ * since counting was enabled, summed over waves. */
 int cdx_sdf_chunk_visits(uint64_t* out, cdx_stream_t stream);
 
 /* Library identification (gfx arch string compiled in). */
@@ -465,9 +517,9 @@ int cdx_profile_read(double* ms6, int64_t* count6);
 
 /* sizeof(cdx_gpis), sizeof(cdx_body), sizeof(cdx_chain), sizeof(cdx_problem),
  * sizeof(cdx_collision), sizeof(cdx_adam), sizeof(cdx_opt_buffers), sizeof(cdx_force_eq),
- * sizeof(cdx_screen_report) — lets
- * a binding verify its struct layouts before the first call. */
-void cdx_abi_sizes(size_t* out9);
+ * sizeof(cdx_screen_report), sizeof(cdx_kin_params), sizeof(cdx_kin_opt), sizeof(cdx_kin_opt_buffers)
+ * — lets a binding verify its struct layouts before the first call. */
+void cdx_abi_sizes(size_t* out12);
 
 /* Test hook: D[16×16] = A[16×4]·B[4×16] through one v_mfma_f64_16x16x4_f64 (checks the
  * fragment layout the GPIS std kernel relies on). */

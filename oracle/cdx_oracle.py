@@ -480,3 +480,58 @@ def kin_sdf_loop(chain, ee_links, ee_offsets, palm_offset, ref_q, q0, target0, c
                 opt_comp[flag] = comp[flag]
         optim.step()
     return torch.stack(trace), opt_q, opt_comp, opt_target, bool((opt_margin > 0.0).all())
+
+
+# ----------------------------------------------------------------------------- SDF mode
+def sdf_mode_loop(tips0, target0, comp0, mu, faces, faces_deflate, sdf, noise_tape, iters, box_lb, box_ub,
+                  mass=0.1, com=(0.0, 0.0, 0.0), gravity=True):
+    """SDFGraspOptimizer.optimize with optimize_target=True (optimize_pregrasp.py:240-320), in the reference's
+    float32: the three TorchSDF calls per iteration (:273-275) through ``sdf(points, faces)`` (the C oracle of
+    the kernel), blended signed normals (:277-278), force_eq_reward with the replayed Kabsch noise (:279-287),
+    the five cost terms (:288-296), backward, best-iterate tracking (:301-309), RMSprop (:250-253, :310) and the
+    bounding-box clamps of tips and targets (:312-314).  ``tar_sign`` is read as [E, T] (the reference's [E·T]
+    broadcast at :296 runs only for E = 1).  Returns (loss [iters, E], opt_tips, opt_comp, opt_target, flag)."""
+    tips = torch.as_tensor(tips0, dtype=F32).clone().requires_grad_(True)
+    comp = torch.as_tensor(comp0, dtype=F32).clone().requires_grad_(True)
+    target = torch.as_tensor(target0, dtype=F32).clone().requires_grad_(True)
+    lb = torch.as_tensor(box_lb, dtype=F32).view(-1, 3)
+    ub = torch.as_tensor(box_ub, dtype=F32).view(-1, 3)
+    optim = torch.optim.RMSprop([{"params": tips, "lr": 1e-3}, {"params": target, "lr": 1e-3},
+                                 {"params": comp, "lr": 0.2}])
+    E, T = tips.shape[0], tips.shape[1]
+    opt_tips, opt_comp, opt_target = tips.detach().clone(), comp.detach().clone(), target.detach().clone()
+    opt_value = torch.full((E,), float("inf"))
+    opt_margin = None
+    trace = []
+    for s in range(iters):
+        optim.zero_grad()
+        all_tip = tips.view(-1, 3)
+        _, sign1, n1, _ = sdf(all_tip, faces_deflate)
+        dist, sign2, n2, _ = sdf(all_tip, faces)
+        tar_dist, tar_sign, _, _ = sdf(target.reshape(-1, 3), faces)
+        normal = 0.5 * sign1.unsqueeze(1) * n1 + 0.5 * sign2.unsqueeze(1) * n2
+        normal = normal / normal.norm(dim=1).unsqueeze(1)
+        noise = torch.as_tensor(noise_tape[s]).to(F32)
+        reward, margin, fnorm, _ = force_eq_reward(tips, target, comp, mu, normal.view(E, T, 3).detach(), noise,
+                                                   mass=mass, gravity=10.0 if gravity else None, COM=com)
+        c = -reward * 5.0
+        center_cost = (tips.mean(dim=1) - target.mean(dim=1)).norm(dim=1) * 10.0
+        force_cost = -(fnorm * torch.nn.functional.softmin(fnorm, dim=1)).clamp(max=1.0).sum(dim=1)
+        dist_cost = 1000 * torch.sqrt(dist).view(E, T).sum(dim=1)
+        tar_dist_cost = 10 * (torch.sqrt(tar_dist).view(E, T) * tar_sign.view(E, T)).sum(dim=1)
+        l = c + dist_cost + tar_dist_cost + center_cost + force_cost
+        l.sum().backward()
+        trace.append(l.detach().clone())
+        with torch.no_grad():
+            flag = l < opt_value
+            if flag.any():
+                opt_margin = margin.detach().clone()
+                opt_value[flag] = l[flag]
+                opt_tips[flag] = tips[flag]
+                opt_target[flag] = target[flag]
+                opt_comp[flag] = comp[flag]
+        optim.step()
+        with torch.no_grad():
+            tips.clamp_(min=lb, max=ub)
+            target.clamp_(min=lb, max=ub)
+    return torch.stack(trace), opt_tips, opt_comp, opt_target, bool((opt_margin > 0.0).all())

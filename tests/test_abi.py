@@ -40,6 +40,16 @@ def test_bad_arguments_are_rejected_without_launch():
     c = N.CdxChain()
     assert lib.cdx_fk_forward(c, None, 1, None, None, None) == -3
     assert lib.cdx_sdf_forward(None, 5, None, 0, None, None, None, None, None, None) == -1
+    assert lib.cdx_sdf_query(None, None, 0, None, 5, None, None, None, None, None, None, 0, None) == -1
+    assert lib.cdx_sdf_query_workspace(0) == 0 and lib.cdx_sdf_mesh_bytes(0) == 0
+    assert lib.cdx_sdf_mesh_prepare(None, 10, None, None) == -1
+    cfg, buf = N.CdxKinOpt(), N.CdxKinOptBuffers()
+    cfg.rule = 2
+    assert lib.cdx_kin_step(None, cfg, buf, 4, 4, 0, 0, None) == -1  # unknown rule
+    cfg.rule = 0
+    assert lib.cdx_kin_step(None, cfg, buf, 4, 4, 0, 0, None) == -1  # Adam (Kin) without a chain
+    cfg.rule = 1
+    assert lib.cdx_kin_step(None, cfg, buf, 4, 4, 0, 0, None) == -1  # null buffers
     p = N.CdxProblem()
     assert lib.cdx_closure_workspace(p, 10) == 0
     assert lib.cdx_closure(p, 10, *([None] * 6), ctypes.c_uint64(0), *([None] * 11)) == -1

@@ -234,6 +234,147 @@ def test_config4_sdf_loop_at_size_vs_oracle():
         assert rel_err(x.detach().cpu().double().numpy()[sl], y.double().numpy()) < 1e-4
 
 
+def _chain_depth(robot, links):
+    """Deepest root→tip path of the fingertip chain (the fused Kin kernel's MAXD instantiation: ≤ 8 or 16)."""
+    from compliancedex_amd.urdf import load_robot
+    bodies = load_robot(robot)["bodies"]
+    names = [b["name"] for b in bodies]
+    depth = 0
+    for link in links:
+        i, n = names.index(link), 0
+        while bodies[i]["parent"] is not None and bodies[i]["parent"] >= 0:
+            i, n = bodies[i]["parent"], n + 1
+        depth = max(depth, n)
+    return depth
+
+
+def _spy_prepared_queries(monkeypatch):
+    """Records every PreparedMesh.query of a fused loop: (points, faces, outputs)."""
+    from compliancedex_amd import torchsdf
+    calls = []
+    real = torchsdf.PreparedMesh.query
+
+    def spy(self, points, want_face=False):
+        out = real(self, points, want_face)
+        calls.append((points.detach().clone(), self.faces, [t.detach().clone() for t in out[:4]]))
+        return out
+    monkeypatch.setattr(torchsdf.PreparedMesh, "query", spy)
+    return calls
+
+
+def _check_queries_bitwise(calls, rng, n_rows=1500):
+    """Each recorded TorchSDF query on row slices against the C oracle, bit for bit, and its argmin face."""
+    from compliancedex_amd import compute_sdf_with_faces
+    from tests import _sdf_oracle
+    for pts, faces, (d, sg, nr, cl) in calls:
+        P = pts.shape[0]
+        rows = np.unique(np.concatenate([rng.choice(P, n_rows, replace=False), np.arange(8), np.arange(P - 8, P)]))
+        o = _sdf_oracle.forward(pts[rows].cpu().numpy(), faces.cpu().numpy())
+        face = compute_sdf_with_faces(pts[rows].contiguous(), faces)[4].cpu().numpy()
+        assert np.array_equal(sg[rows].cpu().numpy(), o[1]) and np.array_equal(face, o[4])
+        for a, b in zip((d[rows], nr[rows], cl[rows]), (o[0], o[2], o[3])):
+            assert np.array_equal(a.cpu().numpy().view(np.uint32), b.view(np.uint32))
+
+
+def test_config4_kin_fused_at_size_vs_oracle(monkeypatch):
+    """Config 4's TIMED path: the fused Kin loop (three TorchSDF queries on prepared k-d meshes, cdx_kin_cost,
+    cdx_kin_step) on iiwa7_allegro — chain depth 13, so cdx_kin_cost runs kin_cost_kernel<4, 16, true> — with
+    E = 16 384 candidates against the 16 384-face banana for 3 iterations.
+    (a) every TorchSDF query of the loop (3 × 65 536 points per iteration) bitwise against the C oracle on row
+        slices, argmin face included;
+    (b) candidate slices against the oracle's Kin loop (oracle.kin_sdf_loop, pinned to the reference's own run
+        by test_oracle_golden) with the same Kabsch noise: per-iteration per-candidate losses and the best-
+        iterate joint angles / compliances / targets within 1e-4 (north_star's bar; the reference computes this
+        mode in float32, cdx_kin_cost takes the force-equilibrium reward in f64)."""
+    import os
+    import compliancedex_amd.optimizers as opts
+    from compliancedex_amd import DifferentiableRobotModel, KinGraspOptimizer, TriangleMesh
+    from compliancedex_amd.urdf import load_robot
+    from oracle.cdx_oracle import kin_sdf_loop
+    from tests import _sdf_oracle
+    from tests.conftest import REPO
+    E, D, iters = 16384, 23, 3
+    links = load_robot("iiwa7_allegro")["config"]["ee_link_name"]
+    assert _chain_depth("iiwa7_allegro", links) > 8  # the deep-chain instantiation
+    offs = [[0.0, -0.04, 0.015]] * 3 + [[0.0, -0.05, -0.015]]
+    center = np.load(os.path.join(REPO, "compliancedex_amd", "data", "banana_center.npy"))
+    tips0 = DifferentiableRobotModel("iiwa7_allegro", device=DEV).compute_forward_kinematics(
+        torch.zeros(1, D, device=DEV), links, offsets=offs)[0].view(4, 3).double().mean(0).cpu().numpy()
+    palm_off = (center - tips0).astype(np.float32)
+    rng = np.random.default_rng(45)
+    q = (0.05 * rng.standard_normal((E, D))).astype(np.float32)
+    target = (np.tile(center, (E, 4, 1)) + 0.01 * rng.standard_normal((E, 4, 3))).astype(np.float32)
+    comp = np.tile(np.array([10.0, 10.0, 10.0, 20.0], np.float32), (E, 1))
+    noise = rng.random((iters, E, 3, 3)).astype(np.float32)
+    mesh_path = os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_mesh.npz")
+    calls = _spy_prepared_queries(monkeypatch)
+    kin = KinGraspOptimizer("iiwa7_allegro", links, offs, palm_offset=palm_off.tolist(), num_iters=iters,
+                            optimize_target=True, ref_q=[0.0] * D)
+    res = kin.optimize(torch.from_numpy(q).to(DEV), torch.from_numpy(target).to(DEV), torch.from_numpy(comp).to(DEV),
+                       1, TriangleMesh.from_npz(mesh_path), verbose=False,
+                       kabsch_noise=[torch.from_numpy(n).to(DEV) for n in noise], trace_rows=True, fused=True)
+    torch.cuda.synchronize()
+    assert len(calls) == 3 * iters and all(c[0].shape == (4 * E, 3) for c in calls)
+    _check_queries_bitwise(calls, rng)
+    sl = np.unique(np.concatenate([np.arange(8), rng.choice(E, 16, replace=False), np.arange(E - 8, E)]))
+    chain, _ = oracle_chain("iiwa7_allegro")
+    mesh = TriangleMesh.from_npz(mesh_path)
+    faces = opts._face_vertices(mesh, "cpu")
+    faces_def = opts._face_vertices(mesh.scale(0.9, center=[0, 0, 0]), "cpu")
+    loss, oq, oc, ot, _ = kin_sdf_loop(chain, links, offs, palm_off, [0.0] * D, q[sl], target[sl], comp[sl], 1, faces,
+                                       faces_def, _sdf_oracle.oracle_sdf, noise[:, sl], iters)
+    got = torch.stack(kin.loss_rows).cpu().numpy()[:, sl]
+    assert np.isfinite(got).all()
+    assert rel_err(got, loss.double().numpy()) < 1e-4, (got, loss)
+    for x, y in zip(res[:3], (oq, oc, ot)):
+        assert rel_err(x.detach().cpu().double().numpy()[sl], y.double().numpy()) < 1e-4
+
+
+def test_config4_sdf_mode_fused_at_size_vs_oracle(monkeypatch):
+    """The fused SDF-mode loop (SDFGraspOptimizer: three TorchSDF queries on prepared meshes, cdx_kin_cost
+    without a chain, cdx_kin_step's RMSprop and box clamps) at config 4's batch, E = 16 384 candidates (fingertips
+    1–5 cm around the banana, targets near its centre), 3 iterations: every query bitwise against the C oracle
+    on row slices; candidate slices against oracle.sdf_mode_loop (pinned to the reference's SDFGraspOptimizer run
+    by test_oracle_golden) with the same Kabsch noise — per-iteration losses and the best-iterate tips /
+    compliances / targets within 1e-4."""
+    import os
+    import compliancedex_amd.optimizers as opts
+    from compliancedex_amd import SDFGraspOptimizer, TriangleMesh
+    from compliancedex_amd.optimizer import FINGERTIP_LB, FINGERTIP_UB
+    from oracle.cdx_oracle import sdf_mode_loop
+    from tests import _sdf_oracle
+    from tests.conftest import REPO
+    E, iters = 16384, 3
+    center = np.load(os.path.join(REPO, "compliancedex_amd", "data", "banana_center.npy"))
+    rng = np.random.default_rng(46)
+    dirs = rng.standard_normal((E, 4, 3))
+    dirs /= np.linalg.norm(dirs, axis=-1, keepdims=True)
+    tips = (center + dirs * rng.uniform(0.01, 0.05, (E, 4, 1)) * np.array([1.0, 2.5, 1.0])).astype(np.float32)
+    target = (np.tile(center, (E, 4, 1)) + 0.01 * rng.standard_normal((E, 4, 3))).astype(np.float32)
+    comp = np.tile(np.array([10.0, 10.0, 10.0, 20.0], np.float32), (E, 1))
+    noise = rng.random((iters, E, 3, 3)).astype(np.float32)
+    mesh_path = os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_mesh.npz")
+    calls = _spy_prepared_queries(monkeypatch)
+    opt = SDFGraspOptimizer([FINGERTIP_LB, FINGERTIP_UB], num_iters=iters, optimize_target=True)
+    res = opt.optimize(torch.from_numpy(tips).to(DEV), torch.from_numpy(target).to(DEV), torch.from_numpy(comp).to(DEV),
+                       1, TriangleMesh.from_npz(mesh_path), verbose=False,
+                       kabsch_noise=[torch.from_numpy(n).to(DEV) for n in noise], trace_rows=True, fused=True)
+    torch.cuda.synchronize()
+    assert len(calls) == 3 * iters
+    _check_queries_bitwise(calls, rng)
+    sl = np.unique(np.concatenate([np.arange(8), rng.choice(E, 16, replace=False), np.arange(E - 8, E)]))
+    mesh = TriangleMesh.from_npz(mesh_path)
+    faces = opts._face_vertices(mesh, "cpu")
+    faces_def = opts._face_vertices(mesh.scale(0.9, center=[0, 0, 0]), "cpu")
+    loss, ot, oc, og, _ = sdf_mode_loop(tips[sl], target[sl], comp[sl], 1, faces, faces_def, _sdf_oracle.oracle_sdf,
+                                        noise[:, sl], iters, FINGERTIP_LB, FINGERTIP_UB)
+    got = torch.stack(opt.loss_rows).cpu().numpy()[:, sl]
+    assert np.isfinite(got).all()
+    assert rel_err(got, loss.double().numpy()) < 1e-4, (got, loss)
+    for x, y in zip(res[:3], (ot, oc, og)):
+        assert rel_err(x.detach().cpu().double().numpy()[sl], y.double().numpy()) < 1e-4
+
+
 # ------------------------------------------------------------------------------ config 3
 CONFIG3 = ["banana", "mug", "mug2", "hammer", "lego", "coffeebottle", "box", "dummy"]
 

@@ -393,9 +393,20 @@ def _bitwise_equal_nan_aware(a, b):
     return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
 
 
+def _sdf_run(pts, faces, path):
+    """compute_sdf_with_faces on numpy inputs through the one-shot call or a PreparedMesh (k-d order)."""
+    from compliancedex_amd import PreparedMesh, compute_sdf_with_faces
+    f = torch.from_numpy(np.ascontiguousarray(faces)).to(DEV)
+    return [t.cpu().numpy() for t in compute_sdf_with_faces(torch.from_numpy(np.ascontiguousarray(pts)).to(DEV),
+                                                            PreparedMesh(f) if path == "prepared" else f)]
+
+
+SDF_PATHS = ["one_shot", "prepared"]
+
+
+@pytest.mark.parametrize("path", SDF_PATHS)
 @pytest.mark.parametrize("mesh", ["cube", "sphere42", "banana"])
-def test_sdf_vs_oracle_bitwise(mesh):
-    from compliancedex_amd import compute_sdf_with_faces
+def test_sdf_vs_oracle_bitwise(mesh, path):
     from tests import _sdf_oracle
     faces = np.load(os.path.join(DATA, "meshes", f"{mesh}_faces.npy"))
     rng = np.random.default_rng(7)
@@ -403,19 +414,18 @@ def test_sdf_vs_oracle_bitwise(mesh):
     n = 3000 if mesh == "banana" else 20000
     pts = (lo - 0.2 * (hi - lo) + 1.4 * (hi - lo) * rng.random((n, 3))).astype(np.float32)
     pts[:min(50, len(faces))] = faces[:50, 0]
-    dist, sign, nrm, clst, face = [t.cpu().numpy() for t in compute_sdf_with_faces(
-        torch.from_numpy(pts).to(DEV), torch.from_numpy(faces).to(DEV))]
+    dist, sign, nrm, clst, face = _sdf_run(pts, faces, path)
     o = _sdf_oracle.forward(pts, faces)
     assert np.array_equal(sign, o[1]) and np.array_equal(face, o[4])
     for a, b in zip((dist, nrm, clst), (o[0], o[2], o[3])):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
-def test_sdf_culled_near_surface_bitwise():
-    """The culled path (Morton-sorted chunks with sphere bounds) against the brute-force C
-    oracle where culling margins matter most: points within 1e-6..1e-3 of the surface, on
-    vertices and on edges, where many faces tie or nearly tie."""
-    from compliancedex_amd import compute_sdf_with_faces
+@pytest.mark.parametrize("path", SDF_PATHS)
+def test_sdf_culled_near_surface_bitwise(path):
+    """The culled path (chunk cylinders, face slabs) against the brute-force C oracle where culling margins
+    matter most: points within 1e-6..1e-3 of the surface, on vertices and on edges, where many faces tie or
+    nearly tie."""
     from tests import _sdf_oracle
     faces = np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))
     rng = np.random.default_rng(11)
@@ -429,21 +439,20 @@ def test_sdf_culled_near_surface_bitwise():
     pts = (on + off[:, None] * nrm).astype(np.float32)
     pts[:500] = faces[f[:500], rng.integers(0, 3, 500)]                        # on vertices
     pts[500:1000] = 0.5 * (faces[f[500:1000], 0] + faces[f[500:1000], 1])     # on edges
-    dist, sign, nrmo, clst, face = [t.cpu().numpy() for t in compute_sdf_with_faces(
-        torch.from_numpy(pts).to(DEV), torch.from_numpy(faces).to(DEV))]
+    dist, sign, nrmo, clst, face = _sdf_run(pts, faces, path)
     o = _sdf_oracle.forward(pts, faces)
     assert np.array_equal(face, o[4]) and np.array_equal(sign, o[1])
     for a, b in zip((dist, nrmo, clst), (o[0], o[2], o[3])):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
-def test_sdf_split_ties_and_far_points_bitwise():
-    """The round-4 culled kernel merges a point group's two chunk slices with a 64-bit atomic minimum on
-    (distance bits, face index): exact ties between a face and its duplicate (appended, so a higher
-    index) must resolve to the first index as the reference's scan does, whichever slice holds each copy;
-    points far outside the mesh (every chunk bound weak, the seeded pass carries the pruning) and a point
-    count that leaves dead lanes must match the brute-force C oracle bit for bit."""
-    from compliancedex_amd import compute_sdf_with_faces
+@pytest.mark.parametrize("path", SDF_PATHS)
+def test_sdf_split_ties_and_far_points_bitwise(path):
+    """The culled kernel merges a lane's pairs with a 64-bit LDS minimum on (distance bits, face index): exact
+    ties between a face and its duplicate (appended, so a higher index) must resolve to the first index as the
+    reference's scan does, wherever the k-d / Morton order puts each copy; points far outside the mesh (every
+    bound weak, the greedy seed carries the pruning) and a point count that leaves dead lanes must match the
+    brute-force C oracle bit for bit."""
     from tests import _sdf_oracle
     base = np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))
     rng = np.random.default_rng(23)
@@ -460,8 +469,7 @@ def test_sdf_split_ties_and_far_points_bitwise():
         lo - 5 * ext + 11 * ext * rng.random((700, 3)),                       # far outside
         lo - 0.1 * ext + 1.2 * ext * rng.random((1037, 3)),                   # around the mesh
     ]).astype(np.float32)
-    dist, sign, nrmo, clst, face = [t.cpu().numpy() for t in compute_sdf_with_faces(
-        torch.from_numpy(pts).to(DEV), torch.from_numpy(faces).to(DEV))]
+    dist, sign, nrmo, clst, face = _sdf_run(pts, faces, path)
     o = _sdf_oracle.forward(pts, faces)
     assert np.array_equal(face, o[4]) and np.array_equal(sign, o[1])
     for a, b in zip((dist, nrmo, clst), (o[0], o[2], o[3])):
@@ -469,38 +477,42 @@ def test_sdf_split_ties_and_far_points_bitwise():
     assert (face[:300] < len(base)).all()  # the duplicate never wins its tie
 
 
-def test_sdf_prepared_mesh_equals_one_shot():
-    """compute_sdf queries a cached prepared mesh (cdx_sdf_mesh_prepare once, cdx_sdf_query per call,
-    the face frame only) and the _C shim the one-shot cdx_sdf_forward (the points ∪ faces frame): the
-    Morton frame only steers the culling, so the outputs are bit-identical; an in-place change of the
-    face tensor invalidates the cached mesh (its version counter)."""
-    from compliancedex_amd import _native as N
-    from compliancedex_amd import compute_sdf_with_faces
-    lib = N.load()
+def test_sdf_prepared_mesh_equals_one_shot_and_owns_its_faces():
+    """A PreparedMesh (k-d order, built on the host) and the one-shot cdx_sdf_forward (Morton order on the device)
+    give bit-identical outputs — the order only steers the culling.  compute_sdf keeps no implicit cache: a
+    write to the face tensor that leaves its version counter unchanged (through ``.data``) shows in the next
+    one-shot call; a PreparedMesh owns a copy of its faces, so the same write never reaches it."""
+    from compliancedex_amd import PreparedMesh, compute_sdf, compute_sdf_with_faces
     faces = torch.from_numpy(np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))).to(DEV)
     rng = np.random.default_rng(17)
     lo, hi = faces.reshape(-1, 3).min(0)[0], faces.reshape(-1, 3).max(0)[0]
     pts = (lo - 0.3 + (hi - lo + 0.6) * torch.from_numpy(rng.random((5000, 3))).to(DEV).float()).contiguous()
+    mesh = PreparedMesh(faces)
+    before = [t.cpu().numpy() for t in compute_sdf_with_faces(pts, faces)]
+    prepared = [t.cpu().numpy() for t in compute_sdf_with_faces(pts, mesh)]
+    for a, b in zip(before, prepared):
+        assert _bitwise_equal_nan_aware(a, b)
+    v = faces._version
+    faces.data.mul_(1.1)  # not seen by autograd's version counter
+    assert faces._version == v
+    after = [t.cpu().numpy() for t in compute_sdf_with_faces(pts, faces)]
+    assert not np.array_equal(after[0], before[0])
+    scaled = [t.cpu().numpy() for t in compute_sdf_with_faces(pts, PreparedMesh(faces))]
+    for a, b in zip(after, scaled):
+        assert _bitwise_equal_nan_aware(a, b)
+    again = [t.cpu().numpy() for t in compute_sdf_with_faces(pts, mesh)]  # the handle kept its own copy
+    for a, b in zip(prepared, again):
+        assert _bitwise_equal_nan_aware(a, b)
+    # autograd through a PreparedMesh: the TorchSDF backward 2·g·(p − clst)
+    x = pts.clone().requires_grad_(True)
+    d, _, _, c = compute_sdf(x, mesh)
+    g, = torch.autograd.grad(d.sum(), x)
+    assert torch.equal(g, 2 * (pts - c))
 
-    def one_shot(f):
-        P = pts.shape[0]
-        o = [torch.zeros(P, device=DEV), torch.zeros(P, dtype=torch.int32, device=DEV), torch.zeros(P, 3, device=DEV),
-             torch.zeros(P, 3, device=DEV), torch.zeros(P, dtype=torch.int32, device=DEV)]
-        N.check(lib.cdx_sdf_forward(N.ptr(pts), P, N.ptr(f), f.shape[0], *(N.ptr(t) for t in o), N.stream_ptr(DEV)), "fwd")
-        return [t.cpu().numpy() for t in o]
 
-    for step in range(2):
-        got = [t.cpu().numpy() for t in compute_sdf_with_faces(pts, faces)]
-        again = [t.cpu().numpy() for t in compute_sdf_with_faces(pts, faces)]  # cache hit
-        want = one_shot(faces)
-        for a, b, c in zip(got, again, want):
-            assert _bitwise_equal_nan_aware(a, c) and _bitwise_equal_nan_aware(b, c), step
-        faces.mul_(1.1)  # in place: the next query must re-prepare
-
-
-def test_sdf_nonfinite_points_take_exact_path():
-    """A workgroup holding a NaN / inf / |p| > 1e4 point runs the reference tile rule."""
-    from compliancedex_amd import compute_sdf_with_faces
+@pytest.mark.parametrize("path", SDF_PATHS)
+def test_sdf_nonfinite_points_take_exact_path(path):
+    """A wave holding a NaN / inf / |p| > 1e4 point runs the reference tile rule."""
     from tests import _sdf_oracle
     faces = np.load(os.path.join(DATA, "meshes", "sphere42_faces.npy"))
     rng = np.random.default_rng(3)
@@ -508,15 +520,15 @@ def test_sdf_nonfinite_points_take_exact_path():
     pts[5] = np.nan
     pts[300] = [np.inf, 0, 0]
     pts[700] = [2e4, 1, 1]
-    got = [t.cpu().numpy() for t in compute_sdf_with_faces(torch.from_numpy(pts).to(DEV),
-                                                           torch.from_numpy(faces).to(DEV))]
+    got = _sdf_run(pts, faces, path)
     o = _sdf_oracle.forward(pts, faces)
     for a, b in zip(got, o):
         assert _bitwise_equal_nan_aware(a, b)
 
 
-def test_sdf_degenerate_and_autograd():
-    from compliancedex_amd import compute_sdf, compute_sdf_with_faces
+@pytest.mark.parametrize("path", SDF_PATHS)
+def test_sdf_degenerate_and_autograd(path):
+    from compliancedex_amd import compute_sdf
     from tests import _sdf_oracle
     rng = np.random.default_rng(1)
     faces = rng.random((1100, 3, 3)).astype(np.float32)
@@ -524,7 +536,7 @@ def test_sdf_degenerate_and_autograd():
     faces[512, 1] = faces[512, 0]
     faces[700] = faces[3]
     pts = rng.random((777, 3)).astype(np.float32)
-    got = [t.cpu().numpy() for t in compute_sdf_with_faces(torch.from_numpy(pts).to(DEV), torch.from_numpy(faces).to(DEV))]
+    got = _sdf_run(pts, faces, path)
     o = _sdf_oracle.forward(pts, faces)
     for a, b in zip(got, o):
         assert _bitwise_equal_nan_aware(a, b)

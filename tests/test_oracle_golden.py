@@ -142,3 +142,27 @@ def test_kin_sdf_loop_oracle_vs_reference_run():
     for i, x in enumerate((oq, oc, ot)):
         assert rel_err(x.double(), d[f"out{i}"]) < 1e-4, i
     assert flag == bool(d["flag"])
+
+
+def test_sdf_mode_loop_oracle_vs_reference_run():
+    """The oracle's SDF-mode loop (oracle.sdf_mode_loop: 3 TorchSDF calls through the C oracle → force_eq_reward
+    → costs → RMSprop → box clamps, float32) against the reference's own SDFGraspOptimizer run (golden mode_sdf:
+    12 iterations, E = 1, replayed Kabsch noise, its TorchSDF the same C oracle).  This pins the oracle the
+    fused SDF-mode GPU test at E = 16 384 compares with."""
+    import os
+    from compliancedex_amd.optimizer import FINGERTIP_LB, FINGERTIP_UB
+    from compliancedex_amd.optimizers import TriangleMesh, _face_vertices
+    from oracle.cdx_oracle import sdf_mode_loop
+    from tests._sdf_oracle import oracle_sdf
+    from tests.conftest import REPO
+    d = golden("mode_sdf.npz")
+    mesh = TriangleMesh.from_npz(os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_mesh.npz"))
+    faces = _face_vertices(mesh, "cpu")
+    faces_def = _face_vertices(mesh.scale(0.9, center=[0, 0, 0]), "cpu")
+    loss, ot, oc, og, flag = sdf_mode_loop(d["tips"], d["target"], d["comp"], 1, faces, faces_def, oracle_sdf,
+                                           d["noise"], int(d["iters"]), FINGERTIP_LB, FINGERTIP_UB)
+    trace = loss.sum(dim=1).double().numpy()
+    assert np.abs(trace - d["loss_trace"]).max() <= 1e-5 * np.abs(d["loss_trace"]).max(), (trace, d["loss_trace"])
+    for i, x in enumerate((ot, oc, og)):
+        assert rel_err(x.double(), d[f"out{i}"]) < 1e-5, i
+    assert flag == bool(d["flag"])

@@ -11,6 +11,8 @@
 #   mfma             SQ_VALU_MFMA_BUSY_CYCLES & co. over a short bench (pmc_mfma_TAG/)
 #   timeline         per-closure kernel timeline from the trace step's output
 #   configs          tools/bench_configs.py (configs 1-5)
+#   c4kin            tools/c4_kin.py: the fused config-4 Kin loop, ms per iteration + TorchSDF counters
+#   c4trace          rocprofv3 --kernel-trace --stats over tools/c4_kin.py (prof_c4_TAG/)
 #   ab=SPEC,SPEC,..  interleaved bench A/B (R rounds, env R=3): SPEC = lib name ("base" = libcdx.so) with
 #                    optional +VAR=VAL settings, e.g. ab=base,base+CDX_SCREEN_REPAIR=0
 set -u
@@ -59,6 +61,13 @@ for STEP in "$@"; do
     timeline)
       python3 tools/closure_timeline.py "$OUT/prof_$TAG/run_kernel_trace.csv" > "$OUT/closure_timeline_$TAG.txt" 2>&1
       echo "timeline rc=$?"; tail -25 "$OUT/closure_timeline_$TAG.txt" ;;
+    c4kin)
+      timeout -k 10 300 python -u tools/c4_kin.py 20 3 > "$OUT/c4kin_$TAG.jsonl" 2> "$OUT/c4kin_$TAG.log"
+      rc=$?; echo "c4kin rc=$rc"; cat "$OUT/c4kin_$TAG.jsonl"; tail -3 "$OUT/c4kin_$TAG.log"; stop_if_fault $rc ;;
+    c4trace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4_$TAG" -o run -- \
+        python3 "$ROOT/tools/c4_kin.py" 10 2 > "$OUT/rocprof_c4_$TAG.log" 2>&1
+      rc=$?; echo "rocprof c4 rc=$rc"; tail -2 "$OUT/rocprof_c4_$TAG.log"; stop_if_fault $rc ;;
     configs)
       timeout -k 10 600 python -u tools/bench_configs.py > "$OUT/configs_$TAG.jsonl" 2> "$OUT/configs_$TAG.log"
       rc=$?; echo "configs rc=$rc"; tail -c 3000 "$OUT/configs_$TAG.jsonl"; stop_if_fault $rc ;;
