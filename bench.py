@@ -251,7 +251,7 @@ def main():
     def exchange(check_shape=True):
         """Surviving grasps of this rank's object → one all_gather of fixed-capacity records
         (capacity E on every rank; the header keeps the true count).  The buffer shapes are checked
-        equal across ranks (one all_reduce) on the warm-up exchange; the timed one reuses that shape."""
+        equal across ranks first (one all_reduce and its host read), as every library caller does."""
         buf = D.pack_survivors(E, rank, rank, 0, opt.total_loss, opt.total_margin, qt.detach(), ct.detach(),
                                tt.detach(), torch.cat([pp, po], 1).detach())
         if world > 1:
@@ -305,7 +305,7 @@ def main():
     # (pack + all_gather + the header read), from events on the step's stream
     eg0, eg1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     eg0.record()
-    buf, records, bufs = exchange(check_shape=False)
+    buf, records, bufs = exchange()
     n_records = int(records.shape[0])
     eg1.record()
     torch.cuda.synchronize()
@@ -390,7 +390,8 @@ def main():
                          "overflow": D.overflow(bufs),
                          "ms_repeat_median": (1e3 * sorted(reps)[len(reps) // 2]) if reps else None,
                          "note": "pack (cdx_pack_survivors: per-tile counts + rows, two launches, device "
-                                 "compaction, header counts on device) + all_gather + unpack (the one host read of "
+                                 "compaction, header counts on device) + the shape check (one all_reduce, N > 1) "
+                                 "+ all_gather + unpack (the one host read of "
                                  "the headers), inside the timed region, queued behind the last step (ms: HIP events on the step stream "
                                  "from the last step's end to the exchange's end); ms_repeat_median: the same "
                                  "exchange repeated after the timed region, host wall time with a sync before each "

@@ -593,7 +593,7 @@ ClosureWs closure_ws_layout(const cdx_problem* p, int64_t E, char* base) {
   w.vpos = scr ? (int*)take(Ms * sizeof(int)) : nullptr;
   w.rows = scr ? (int*)take(Ms * sizeof(int)) : nullptr;
   w.stats = scr ? (int*)take(cdx::SS_WORDS * sizeof(int)) : nullptr;
-  w.zkey = scr ? (unsigned*)take(Ms * sizeof(unsigned)) : nullptr;
+  w.zkey = scr ? (unsigned*)take((Ms + cdx::screen_compact_words(Mg)) * sizeof(unsigned)) : nullptr;
   w.keep = scr ? (unsigned short*)take(Mg * sizeof(unsigned short)) : nullptr;
   w.vrow = scr ? (int64_t*)take(Mg * sizeof(int64_t)) : nullptr;
   w.screen_ws = scr ? take(cdx::screen_ws_bytes(p->gpis, Ms)) : nullptr;

@@ -113,12 +113,18 @@ __device__ __host__ inline unsigned audit_bin_floor(int b) {  // float bits of t
   return b >= AUDIT_BINS ? 0x7F800000u : 0x3F800000u + ((unsigned)b << 20);
 }
 
+// Words of compaction scratch the caller allocates right behind zkey's M words (select blocks' z histograms,
+// compaction block counts).
+inline int64_t screen_compact_words(int64_t G) {
+  return (G + 63) / 64 * AUDIT_BINS + 4 * ((G + 255) / 256) + 1;
+}
+
 // Closure screening of the all-tip rows (G groups of T, M = G·T): screen partials in ws
 // (screen_ws_bytes(g, M)), per-row estimate sv2, rows kept for the exact pass listed in rows[0 .. G +
 // stats[SS_EXTRA]) (the G group leaders first, at position = group, then the other kept rows and the
 // audited rows in group order), vpos[q] = list position or −1 (then std_[q] = the estimate), keep [G]
-// masks (low byte kept, high byte audited), zkey [M] the discarded rows' z (float bits; Z_NONE
-// otherwise) from which the compaction picks the audited rows.
+// masks (low byte kept, high byte audited), zkey [M + screen_compact_words(G)] the discarded rows' z (float bits;
+// Z_NONE otherwise) from which the compaction picks the audited rows, then the compaction's scratch.
 // after_screen(ctx), when given, runs on the host between the screen kernel's launch and the
 // selection's (the closure forks its side stream there); its nonzero return is returned.
 int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, void* ws, double* sv2, double* std_,

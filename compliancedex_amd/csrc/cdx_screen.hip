@@ -528,14 +528,11 @@ using cdx::screen_margin;
 // function of the inputs only: the same inputs give the same exact-pass list, hence bit-identical results
 // (the refine pass's K-split depends on the list length).
 template <int KT>
-__global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const double* __restrict__ partial,
-                                                            int64_t M_pad, int Nt, int64_t G, int T,
-                                                            double* __restrict__ sv2, double* __restrict__ std_,
-                                                            int* __restrict__ vpos, int* __restrict__ rows,
-                                                            unsigned short* __restrict__ keep,
-                                                            unsigned* __restrict__ zkey, const double* __restrict__ X) {
-  const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi >= G) return;
+__device__ __forceinline__ void select_group(const cdx_gpis& g, const double* __restrict__ partial, int64_t M_pad, int Nt,
+                                             int64_t gi, int T, double* __restrict__ sv2, double* __restrict__ std_,
+                                             int* __restrict__ vpos, int* __restrict__ rows,
+                                             unsigned short* __restrict__ keep, unsigned* __restrict__ zkey,
+                                             const double* __restrict__ X, int* s_hist) {
   const double k0 = cdx::gpis_k0<KT>(g.R), delta = g.screen_delta;
   const double* ctr = cdx::screen_view(g).center;
   double a[CDX_MAX_TIPS], d[CDX_MAX_TIPS];
@@ -562,73 +559,93 @@ __global__ __launch_bounds__(256) void screen_select_kernel(cdx_gpis g, const do
       vpos[q] = (int)gi;
       rows[gi] = (int)q;
     } else if (!finite || a[f] + d[f] >= lo) {
-      mask |= 1u << f;  // kept: position assigned by screen_compact_kernel
+      mask |= 1u << f;  // kept: position assigned by screen_place_kernel
     } else {
       vpos[q] = -1;  // discarded (the compaction may still list it as audited)
       std_[q] = sqrt(a[f]);
       z = __float_as_uint((float)((lo - a[f]) / d[f]));
+      atomicAdd(&s_hist[cdx::audit_bin(z)], 1);
     }
     zkey[q] = z;
   }
   keep[gi] = (unsigned short)mask;
 }
 
-// Deterministic compaction of the kept non-leader fingertips and the audited rows behind the G
-// leaders (group order, fingertip order): one workgroup of 16 waves; wave w owns the contiguous groups
-// [w·64R, (w+1)·64R), R = ceil(G / 1024), read in R rounds of 64 consecutive groups (lane l: group
-// w·64R + 64r + l — coalesced; round 3 built per-thread chunks, whose strided loads made the kernel 20 µs).
-// First the audit: per-wave LDS histograms of the discarded rows' z bins, summed, and one wave's scan give
-// the cut (cdx_screen.h audit_bin: the lowest bins within the row budget A, plus the bin that crosses A
-// while the total stays ≤ 4A); the discarded rows below the cut are audited, i.e. listed for the exact
-// pass like the kept ones.  Then the listed rows are counted per wave, the 16 wave totals scanned through
-// LDS, and each round's positions taken from a wave prefix sum — the same positions as one sequential
-// pass in group order.  Resets the per-closure statistics and counts the closure and its audited rows in
-// the cumulative block; records the smallest z left unaudited.
-constexpr int COMPACT_WAVES = 16;
-__global__ __launch_bounds__(64 * COMPACT_WAVES) void screen_compact_kernel(int64_t G, int T,
-                                                                           unsigned short* __restrict__ keep,
-                                                                           const unsigned* __restrict__ zkey,
-                                                                           int* __restrict__ vpos, int* __restrict__ rows,
-                                                                           int* __restrict__ stats, int A) {
-  __shared__ int hist[COMPACT_WAVES][cdx::AUDIT_BINS];
-  __shared__ int wsum[COMPACT_WAVES], wsa[COMPACT_WAVES], wsd[COMPACT_WAVES], s_cut;
-  __shared__ unsigned wmin[COMPACT_WAVES];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int64_t R = (G + 64 * COMPACT_WAVES - 1) / (64 * COMPACT_WAVES);
-  const int64_t gw = (int64_t)wave * 64 * R;  // this wave's first group
-  for (int i = t; i < COMPACT_WAVES * cdx::AUDIT_BINS; i += 64 * COMPACT_WAVES) (&hist[0][0])[i] = 0;
+// The select kernel also writes its block's histogram of the discarded rows' z bins (one row of AUDIT_BINS ints
+// per block, fully overwritten: no zeroing between closures) for the compaction's audit cut.
+template <int KT>
+__global__ __launch_bounds__(SEL_BLOCK) void screen_select_kernel(cdx_gpis g, const double* __restrict__ partial,
+                                                                  int64_t M_pad, int Nt, int64_t G, int T,
+                                                                  double* __restrict__ sv2, double* __restrict__ std_,
+                                                                  int* __restrict__ vpos, int* __restrict__ rows,
+                                                                  unsigned short* __restrict__ keep,
+                                                                  unsigned* __restrict__ zkey, const double* __restrict__ X,
+                                                                  int* __restrict__ hist) {
+  __shared__ int s_hist[cdx::AUDIT_BINS];
+  for (int i = threadIdx.x; i < cdx::AUDIT_BINS; i += SEL_BLOCK) s_hist[i] = 0;
+  __syncthreads();
+  const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi < G) select_group<KT>(g, partial, M_pad, Nt, gi, T, sv2, std_, vpos, rows, keep, zkey, X, s_hist);
+  __syncthreads();
+  for (int i = threadIdx.x; i < cdx::AUDIT_BINS; i += SEL_BLOCK) hist[(int64_t)blockIdx.x * cdx::AUDIT_BINS + i] = s_hist[i];
+}
+
+// Deterministic compaction of the kept non-leader fingertips and the audited rows behind the G leaders (group
+// order, fingertip order), over the whole chip — two kernels of CB_GROUPS groups per workgroup (round 4 ran
+// one workgroup, which a co-running kernel could starve: 77 µs in the closure against 17 µs alone):
+//   screen_count_kernel  sums the select blocks' z-bin histograms, takes the audit cut (cdx_screen.h
+//                        audit_bin: the lowest bins within the row budget A, plus the bin that crosses A while
+//                        the total stays ≤ 4A — every workgroup computes the same cut), marks each group's
+//                        listed rows (kept | audited, keep mask: low byte kept, high byte audited) and writes its
+//                        block's counts (listed, audited, discarded) and smallest unaudited z;
+//   screen_place_kernel  positions in group order: the listed rows of the earlier blocks (a sum over the
+//                        block counts), then a workgroup prefix sum — the same positions as one sequential pass;
+//                        block 0 writes the per-closure statistics and the cumulative block.
+// Audited beyond the cut: an input-keyed sample of ~1/SAMPLE of the other discarded rows (hash of the row and its
+// z), so the audit's checks also reach rows far below the keep threshold.
+constexpr int CB_GROUPS = 256;
+constexpr unsigned AUDIT_SAMPLE_SHIFT = 9;  // 1 in 512
+__device__ __forceinline__ bool audit_sampled(int64_t q, unsigned z) {
+  unsigned h = (unsigned)q * 0x9E3779B1u ^ z;
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return (h >> (32 - AUDIT_SAMPLE_SHIFT)) == 0u;
+}
+
+__device__ __forceinline__ int block_sum(int v, int* red) {  // 256 threads, `red` 4 ints of LDS
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(CB_GROUPS) void screen_count_kernel(int64_t G, int T, int nsel, const int* __restrict__ hist,
+                                                                 unsigned short* __restrict__ keep,
+                                                                 const unsigned* __restrict__ zkey, int* __restrict__ bcount,
+                                                                 int A) {
+  __shared__ int s_hist[cdx::AUDIT_BINS];
+  __shared__ int red[4], s_cut;
+  __shared__ unsigned s_zmin[4];
+  const int t = threadIdx.x, lane = t & 63;
+  if (A > 0) {
+    int v = 0;
+    for (int b = 0; b < nsel; ++b) v += hist[(int64_t)b * cdx::AUDIT_BINS + t];
+    s_hist[t] = v;
+  }
   if (t == 0) s_cut = A > 0 ? cdx::AUDIT_BINS : 0;
   __syncthreads();
-  // pass 1: the discarded rows (histogram of their z bins when auditing)
-  int nd = 0;
-  for (int64_t r = 0; r < R; ++r) {
-    const int64_t gi = gw + 64 * r + lane;
-    if (gi >= G) break;
-    for (int f = 0; f < T; ++f) {
-      const unsigned z = zkey[gi * T + f];
-      if (z == cdx::Z_NONE) continue;
-      ++nd;
-      if (A > 0) atomicAdd(&hist[wave][cdx::audit_bin(z)], 1);
-    }
-  }
-  __syncthreads();
-  if (A > 0 && wave == 0) {  // the cut: lane l scans bins 4l .. 4l + 3 (summed over the waves' histograms)
+  if (A > 0 && t < 64) {  // the cut: lane l scans bins 4l .. 4l + 3
     constexpr int PB = cdx::AUDIT_BINS / 64;
-    int h[PB], s = 0;
+    int h[PB], sm = 0;
 #pragma unroll
-    for (int i = 0; i < PB; ++i) {
-      int v = 0;
-#pragma unroll
-      for (int w = 0; w < COMPACT_WAVES; ++w) v += hist[w][PB * lane + i];
-      s += (h[i] = v);
-    }
-    int inc = s;
+    for (int i = 0; i < PB; ++i) sm += (h[i] = s_hist[PB * lane + i]);
+    int inc = sm;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const int v = __shfl_up(inc, d);
       if (lane >= d) inc += v;
     }
-    int c = inc - s;  // rows in the bins below this lane's
+    int c = inc - sm;  // rows in the bins below this lane's
     if (c < A && inc >= A) {  // the lane holding the first bin whose cumulative count reaches A
       int b = 0;
       while (c + h[b] < A) c += h[b++];
@@ -638,87 +655,94 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void screen_compact_kernel(int6
   __syncthreads();
   const int cut = s_cut;
   const unsigned tmask = (1u << T) - 1u;
-  // the group's kept | audited mask (low byte kept, high byte audited) and the smallest unaudited z
-  auto listed = [&](int64_t gi, unsigned& zmin) {
+  const int64_t gi = (int64_t)blockIdx.x * CB_GROUPS + t;
+  int n = 0, na = 0, nd = 0;
+  unsigned zmin = 0x7F800000u;  // +inf
+  if (gi < G) {
     unsigned m = keep[gi];
     for (int f = 0; f < T; ++f) {
-      const unsigned z = zkey[gi * T + f];
+      const int64_t q = gi * T + f;
+      const unsigned z = zkey[q];
       if (z == cdx::Z_NONE) continue;
-      if (cdx::audit_bin(z) < cut) m |= 0x100u << f;
+      ++nd;
+      if (A > 0 && (cdx::audit_bin(z) < cut || audit_sampled(q, z))) m |= 0x100u << f;
       else zmin = min(zmin, z);
     }
-    return m;
-  };
-  // pass 2: listed rows per wave
-  int n = 0, na = 0;
-  unsigned zmin = 0x7F800000u;  // +inf
-  for (int64_t r = 0; r < R; ++r) {
-    const int64_t gi = gw + 64 * r + lane;
-    if (gi >= G) break;
-    const unsigned m = listed(gi, zmin);
-    n += __popc((m | (m >> 8)) & tmask);
-    na += __popc(m >> 8);
+    keep[gi] = (unsigned short)m;
+    n = __popc((m | (m >> 8)) & tmask);
+    na = __popc(m >> 8);
   }
-  int wn = n, wa = na, wd = nd;
-  unsigned wz = zmin;
+  n = block_sum(n, red);
+  na = block_sum(na, red);
+  nd = block_sum(nd, red);
+  for (int d = 32; d >= 1; d >>= 1) zmin = min(zmin, (unsigned)__shfl_xor((int)zmin, d));
+  if (lane == 0) s_zmin[t >> 6] = zmin;
+  __syncthreads();
+  if (t == 0) {
+    int* o = bcount + 4 * (int64_t)blockIdx.x;
+    o[0] = n;
+    o[1] = na;
+    o[2] = nd;
+    o[3] = (int)min(min(s_zmin[0], s_zmin[1]), min(s_zmin[2], s_zmin[3]));
+    if (blockIdx.x == 0) bcount[4 * (int64_t)gridDim.x] = cut;
+  }
+}
+
+__global__ __launch_bounds__(CB_GROUPS) void screen_place_kernel(int64_t G, int T, const unsigned short* __restrict__ keep,
+                                                                 const int* __restrict__ bcount, int* __restrict__ vpos,
+                                                                 int* __restrict__ rows, int* __restrict__ stats) {
+  __shared__ int red[4], wsum[4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+  // listed rows of the earlier blocks (and, for block 0's statistics, the totals)
+  int before = 0;
+  for (int i = t; i < b; i += CB_GROUPS) before += bcount[4 * (int64_t)i];
+  before = block_sum(before, red);
+  const unsigned tmask = (1u << T) - 1u;
+  const int64_t gi = (int64_t)b * CB_GROUPS + t;
+  const unsigned m = gi < G ? keep[gi] : 0u;
+  const int c = __popc((m | (m >> 8)) & tmask);
+  int inc = c;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    wn += __shfl_xor(wn, d);
-    wa += __shfl_xor(wa, d);
-    wd += __shfl_xor(wd, d);
-    wz = min(wz, (unsigned)__shfl_xor((int)wz, d));
+    const int v = __shfl_up(inc, d);
+    if (lane >= d) inc += v;
   }
-  if (lane == 0) {
-    wsum[wave] = wn;
-    wsa[wave] = wa;
-    wsd[wave] = wd;
-    wmin[wave] = wz;
-  }
+  if (lane == 63) wsum[wave] = inc;
   __syncthreads();
-  int before = 0, total = 0, total_a = 0, total_d = 0;
+  int pos = (int)G + before + inc - c;
+  for (int w = 0; w < wave; ++w) pos += wsum[w];
+  if (gi < G)
+    for (int f = 0; f < T; ++f)
+      if (((m >> f) | (m >> (8 + f))) & 1u) {
+        const int64_t q = gi * T + f;
+        vpos[q] = pos;
+        rows[pos] = (int)q;
+        ++pos;
+      }
+  if (b != 0) return;
+  int total = 0, total_a = 0, total_d = 0;
   unsigned zm = 0x7F800000u;
-#pragma unroll
-  for (int w = 0; w < COMPACT_WAVES; ++w) {
-    const int sw = wsum[w];
-    before += w < wave ? sw : 0;
-    total += sw;
-    total_a += wsa[w];
-    total_d += wsd[w];
-    zm = min(zm, wmin[w]);
+  for (int i = t; i < nb; i += CB_GROUPS) {
+    const int* o = bcount + 4 * (int64_t)i;
+    total += o[0];
+    total_a += o[1];
+    total_d += o[2];
+    zm = min(zm, (unsigned)o[3]);
   }
-  // pass 3: positions in group order — this wave's base, then per round a wave prefix sum
-  int base = (int)G + before;
-  for (int64_t r = 0; r < R; ++r) {
-    const int64_t gi = gw + 64 * r + lane;
-    const bool in = gi < G;
-    if (gw + 64 * r >= G) break;  // (uniform)
-    unsigned dummy = 0;
-    const unsigned m = in ? listed(gi, dummy) : 0u;
-    const int c = __popc((m | (m >> 8)) & tmask);
-    int inc = c;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int v = __shfl_up(inc, d);
-      if (lane >= d) inc += v;
-    }
-    int pos = base + inc - c;
-    if (in) {
-      keep[gi] = (unsigned short)m;
-      for (int f = 0; f < T; ++f)
-        if (((m >> f) | (m >> (8 + f))) & 1u) {
-          const int64_t q = gi * T + f;
-          vpos[q] = pos;
-          rows[pos] = (int)q;
-          ++pos;
-        }
-    }
-    base += __shfl(inc, 63);
-  }
+  total = block_sum(total, red);
+  total_a = block_sum(total_a, red);
+  total_d = block_sum(total_d, red);
+  for (int d = 32; d >= 1; d >>= 1) zm = min(zm, (unsigned)__shfl_xor((int)zm, d));
+  __syncthreads();
+  if (lane == 0) wsum[wave] = (int)zm;
+  __syncthreads();
   if (t == 0) {
+    zm = min(min((unsigned)wsum[0], (unsigned)wsum[1]), min((unsigned)wsum[2], (unsigned)wsum[3]));
     stats[cdx::SS_EXTRA] = total;
     stats[cdx::SS_AUDIT] = total_a;
     stats[cdx::SS_GAP] = (int)zm;
-    stats[cdx::SS_AUDIT_CUT] = (int)cdx::audit_bin_floor(cut);
+    stats[cdx::SS_AUDIT_CUT] = (int)cdx::audit_bin_floor(bcount[4 * (int64_t)nb]);
     stats[cdx::SS_DISCARD] = total_d;
     for (int k : {cdx::SS_MISS, cdx::SS_AUDIT_MISS, cdx::SS_AUDIT_FLIP, cdx::SS_FAULT, cdx::SS_RATIO,
                   cdx::SS_RATIO_AUDIT, cdx::SS_REPAIR})
@@ -1002,6 +1026,9 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
   const int Mt = (int)(M_pad / SC_BM);
   double* partial = static_cast<double*>(ws);
   const dim3 grid((unsigned)(Mt * Nt)), sgrid((unsigned)((G + SEL_BLOCK - 1) / SEL_BLOCK));
+  const int nsel = (int)sgrid.x, ncb = (int)((G + CB_GROUPS - 1) / CB_GROUPS);
+  int* hist = reinterpret_cast<int*>(zkey + G * T);  // screen_compact_words(G) words behind zkey
+  int* bcount = hist + (int64_t)nsel * cdx::AUDIT_BINS;
   switch (g.kernel) {
     case CDX_KERNEL_TPS:
       prof_mark(PROF_SCREEN, true, s);
@@ -1010,7 +1037,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, zkey, X);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_TPS>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, zkey, X, hist);
       break;
     case CDX_KERNEL_RBF:
       prof_mark(PROF_SCREEN, true, s);
@@ -1019,7 +1046,7 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, zkey, X);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_RBF>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, zkey, X, hist);
       break;
     default:
       prof_mark(PROF_SCREEN, true, s);
@@ -1028,11 +1055,13 @@ int screen_select_launch(const cdx_gpis& g, const double* X, int64_t G, int T, v
       if (after_screen) {
         if (const int r = after_screen(ctx)) return r;
       }
-      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, zkey, X);
+      hipLaunchKernelGGL(screen_select_kernel<CDX_KERNEL_JOINT>, sgrid, dim3(SEL_BLOCK), 0, s, g, partial, M_pad, Nt, G, T, sv2, std_, vpos, rows, keep, zkey, X, hist);
       break;
   }
-  hipLaunchKernelGGL(screen_compact_kernel, dim3(1), dim3(64 * COMPACT_WAVES), 0, s, G, T, keep, (const unsigned*)zkey, vpos, rows, stats,
-                     screen_audit_rows());
+  hipLaunchKernelGGL(screen_count_kernel, dim3((unsigned)ncb), dim3(CB_GROUPS), 0, s, G, T, nsel, (const int*)hist, keep,
+                     (const unsigned*)zkey, bcount, screen_audit_rows());
+  hipLaunchKernelGGL(screen_place_kernel, dim3((unsigned)ncb), dim3(CB_GROUPS), 0, s, G, T, (const unsigned short*)keep,
+                     (const int*)bcount, vpos, rows, stats);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
