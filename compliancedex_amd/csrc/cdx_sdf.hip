@@ -22,8 +22,8 @@
 //     pairs a lane needs, packed 64 to a round (ballot/mbcnt into LDS, an LDS 64-bit minimum on
 //     (distance bits, face index) into the owner's best).
 // A skip needs bound·(1 − α) − β > sqrt(best): α = 1e-4 + 1e-5·κ (κ = the worst face's 1/sinθ in the
-// node; α ≥ 1 or a NaN κ never skips) and β = 1e-4·(|p| + |c| + 3R) exceed every rounding error of
-// point_face and of the bound by orders of magnitude, so a skipped face's computed
+// node; α ≥ 1 or a NaN κ never skips) and β = (1e-4 + 1e-8·κ)·(|p| + |c| + 3R) exceed every rounding error
+// of point_face and of the bound (tests/test_sdf_bounds_cpu.py), so a skipped face's computed
 // distance is strictly greater than the winner's: it can neither win nor tie.  Faces are compared
 // lexicographically on (distance, index) — with no NaN distances, exactly the reference's first-minimum
 // tile rule — and the winner's outputs are recomputed with point_face (bit-identical).
@@ -50,7 +50,7 @@ constexpr int TOPB = 16;            // chunks per top node
 constexpr float PT_LIM = 1e4f;      // |p| bound of the culled path (face_may_nan's premise)
 
 // Bounding volume of a node: a = (centre xyz, ball radius R), b = (cylinder axis xyz, half-thickness t),
-// m = (cylinder radius rc, 1/(1 − α), w = 1e-4·(|centre| + 3R)/(1 − α), 0).
+// m = (cylinder radius rc, 1/(1 − α), w = γ·(|centre| + 3R)/(1 − α), γ) with γ = 1e-4 + 1e-8·κ.
 struct Node { float4 a, b, m; };
 // Disk slab of a face: a = (centroid xyz, in-plane radius r), b = (unit normal xyz, half-thickness t).
 struct Slab { float4 a, b; };
@@ -223,7 +223,9 @@ __device__ inline double wave_sum(double v) {
 //   pass 1  box centre c, area-weighted normal sum → axis a (z if it vanishes), the faces' worst κ;
 //   pass 2  extent along a → the cylinder's mid-plane, moved into the centre c;
 //   pass 3  half-thickness t, cylinder radius rc, ball radius R (all rounded up by 1e-6).
-// Margins: α = 1e-4 + 1e-5·κ (1 for a NaN κ: never skipped), ia1 = 1/(1 − α), w = 1e-4·(|c| + 3R)·ia1.
+// Margins: α = 1e-4 + 1e-5·κ (1 for a NaN κ: never skipped), ia1 = 1/(1 − α), γ = 1e-4 + 1e-8·κ,
+// w = γ·(|c| + 3R)·ia1 (tests/test_sdf_bounds_cpu.py: point_face's absolute error stays below 1e-9·κ·(|p| + |c| + r)
+// on slivers up to κ ~ 1e6, 1.4e-6·(|p| + |c| + r) on ordinary faces).
 __global__ __launch_bounds__(64) void sdf_node_kernel(const cdx::FaceRec* __restrict__ rec, int64_t F, int S,
                                                       Node* __restrict__ out) {
   const int64_t f0 = (int64_t)blockIdx.x * S, f1 = min(F, f0 + S);
@@ -292,12 +294,13 @@ __global__ __launch_bounds__(64) void sdf_node_kernel(const cdx::FaceRec* __rest
   const double R = sqrt(R2) * (1.0 + 1e-6);
   const double al = 1e-4 + 1e-5 * kmax;  // (inf for a NaN κ)
   const double ia1 = al < 1.0 ? 1.0 / (1.0 - al) : INFINITY;
+  const double gam = 1e-4 + 1e-8 * kmax;
   const double cn = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
   Node nd;
   nd.a = make_float4((float)c[0], (float)c[1], (float)c[2], (float)R);
   nd.b = make_float4(a32[0], a32[1], a32[2], (float)(t * (1.0 + 1e-6)));
   nd.m = make_float4((float)(sqrt(rc2) * (1.0 + 1e-6)), (float)(ia1 * (1.0 + 1e-6)),
-                     (float)(1e-4 * (cn + 3.0 * R) * ia1 * (1.0 + 1e-6)), 0.f);
+                     (float)(gam * (cn + 3.0 * R) * ia1 * (1.0 + 1e-6)), (float)(gam * (1.0 + 1e-6)));
   out[blockIdx.x] = nd;
 }
 
@@ -342,12 +345,17 @@ __device__ __forceinline__ float cyl_lb2(cdx::F3 p, float4 a, float4 b, float rc
   return dh * dh + dr * dr;
 }
 
-// A lane cannot rule the node out: its distance bound is not above th = (sqrt(best) + 1e-4·|p|)/(1 − α) + w
-// (k0 = sqrt(best) + 1e-4·|p|).  Written so that any NaN (bounds, an infinite ia1 times k0 = 0) keeps it.
-__device__ __forceinline__ bool node_needed(cdx::F3 p, const Node& n, float k0) {
+// The node's skip threshold th = (sqrt(best) + γ·|p|)/(1 − α) + w, sb = sqrt(best).
+__device__ __forceinline__ float node_th(const Node& n, float sb, float pnorm) {
+  return fmaf(n.m.w, pnorm, sb) * n.m.y + n.m.z;
+}
+
+// A lane cannot rule the node out: its distance bound is not above th.  Written so that any NaN (bounds, an
+// infinite ia1 times a zero k0) keeps it.
+__device__ __forceinline__ bool node_needed(cdx::F3 p, const Node& n, float sb, float pnorm) {
   float d2;
   const float l2 = cyl_lb2(p, n.a, n.b, n.m.x, &d2);
-  const float th = k0 * n.m.y + n.m.z;
+  const float th = node_th(n, sb, pnorm);
   const float ts = th + n.a.w;
   return !(l2 > th * th || d2 > ts * ts);
 }
@@ -453,14 +461,14 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
   float4* buf = s_rec[w];
   const cdx::FaceRec* rr = reinterpret_cast<const cdx::FaceRec*>(buf);
   for (int t = 0; t < T; ++t) {
-    if (!__any(node_needed(p, load_node(top, t), fmaf(1e-4f, pnorm, sqrtf(best))))) continue;
+    if (!__any(node_needed(p, load_node(top, t), sqrtf(best), pnorm))) continue;
     const int ce = min(C, t * TOPB + TOPB);
     for (int c = t * TOPB; c < ce; ++c) {
       const Node cn = load_node(chunk, c);
-      const float k0 = fmaf(1e-4f, pnorm, sqrtf(best));
-      if (!__any(node_needed(p, cn, k0))) continue;
-      // the chunk's faces a lane cannot rule out: slab bound against th = k0/(1 − α) + w (the chunk's margins)
-      const float th = k0 * cn.m.y + cn.m.z;
+      const float sb = sqrtf(best);
+      if (!__any(node_needed(p, cn, sb, pnorm))) continue;
+      // the chunk's faces a lane cannot rule out: slab bound against the chunk's threshold (its margins)
+      const float th = node_th(cn, sb, pnorm);
       const float th2 = th * th;
       const int nf = (int)min((int64_t)CHUNK, F - (int64_t)c * CHUNK);
       unsigned lmask = 0;

@@ -1,0 +1,166 @@
+"""The culled TorchSDF kernel (cdx_sdf.hip sdf_tree_kernel) skips a face only when its distance bound says the
+face's COMPUTED distance exceeds the lane's best.  The premise, per face f with true distance D_f:
+
+    sqrt(point_face(p, f))  ≥  LB_f·(1 − α_f) − β_f      for every bound LB_f the kernel computes,
+
+α_f = 1e-4 + 1e-5·κ_f (κ_f = the face's conditioning |e12||e31|/|n|), β_f = γ_f·(|p| + |c_f| + r_f) with
+γ_f = 1e-4 + 1e-8·κ_f — the node
+bounds use the largest α and a β ≥ every face's (cdx_sdf.hip sdf_node_kernel).  Checked here on the host with
+the kernel's own arithmetic: point_face is the host build of cdx_sdf.h (FP contraction off, as on the device),
+the face slab and the node cylinders are built in double and rounded to float32 as sdf_face_kernel /
+sdf_node_kernel do, and the bound itself (cyl_lb2) is evaluated in float32 operation by operation (numpy
+float32 rounds each operation like the device without contraction).  Cases: random faces of four scales, slivers
+(κ up to ~1e4), points on / near / far from the surface and on the region boundaries, far points up to the
+culled path's |p| ≤ 1e4.  CPU only."""
+import ctypes as C
+
+import numpy as np
+
+from tests._host import host, p
+
+F32 = np.float32
+
+
+def _point_face(pts, faces):
+    pts = np.ascontiguousarray(pts, F32)
+    faces = np.ascontiguousarray(faces, F32)
+    n = len(pts)
+    d_rec, d_ref = np.zeros(n, F32), np.zeros(n, F32)
+    host().cdxh_face_dist2(p(pts), p(faces), C.c_int64(n), p(d_rec), p(d_ref))
+    return d_ref
+
+
+def _slab(faces):
+    """sdf_face_kernel's disk slab: centroid and unit normal in double → f32, then half-thickness and in-plane
+    radius about those rounded values (renormalised normal), rounded up by 1e-6."""
+    v = faces.astype(np.float64)
+    cen = v.mean(1)
+    n = np.cross(v[:, 1] - v[:, 0], v[:, 2] - v[:, 0])
+    nl = np.linalg.norm(n, axis=1, keepdims=True)
+    c32 = cen.astype(F32)
+    n32 = (n / nl).astype(F32)
+    nh = n32.astype(np.float64) / np.linalg.norm(n32.astype(np.float64), axis=1, keepdims=True)
+    d = v - c32.astype(np.float64)[:, None]
+    h = (d * nh[:, None]).sum(-1)
+    e = d - h[..., None] * nh[:, None]
+    t = np.abs(h).max(1)
+    r = np.sqrt((e ** 2).sum(-1).max(1))
+    return c32, (r * (1 + 1e-6)).astype(F32), n32, (t * (1 + 1e-6)).astype(F32)
+
+
+def _cyl_lb2(pts, c, axis, t, rc):
+    """cyl_lb2 in float32, operation by operation (returns lb², |p − c|²)."""
+    pts = pts.astype(F32)
+    dx, dy, dz = (pts[:, i] - c[:, i] for i in range(3))
+    h = (axis[:, 0] * dx + axis[:, 1] * dy) + axis[:, 2] * dz
+    ex, ey, ez = dx - h * axis[:, 0], dy - h * axis[:, 1], dz - h * axis[:, 2]
+    rho = np.sqrt((ex * ex + ey * ey) + ez * ez)
+    dh = np.maximum(np.abs(h) - t, F32(0))
+    dr = np.maximum(rho - rc, F32(0))
+    return dh * dh + dr * dr, (dx * dx + dy * dy) + dz * dz
+
+
+def _kappa(faces):
+    v = faces.astype(np.float64)
+    e12, e31 = v[:, 1] - v[:, 0], v[:, 0] - v[:, 2]
+    n = np.cross(v[:, 0] - v[:, 1], e31)
+    return np.linalg.norm(e12, axis=1) * np.linalg.norm(e31, axis=1) / np.linalg.norm(n, axis=1)
+
+
+def _check_faces(pts, faces):
+    d32 = _point_face(pts, faces).astype(np.float64)
+    c, r, n, t = _slab(faces)
+    lb2, _ = _cyl_lb2(pts, c, n, t, r)
+    lb = np.sqrt(lb2.astype(np.float64))
+    kap = _kappa(faces)
+    alpha = 1e-4 + 1e-5 * kap
+    beta = (1e-4 + 1e-8 * kap) * (np.linalg.norm(pts.astype(np.float64), axis=1) +
+                                  np.linalg.norm(c.astype(np.float64), axis=1) + r)
+    bound = lb * (1 - alpha) - beta
+    bad = (alpha < 1) & (np.sqrt(d32) < bound)
+    assert not bad.any(), (int(bad.sum()), pts[bad][:3], faces[bad][:3], np.sqrt(d32[bad][:3]), bound[bad][:3])
+    return float(np.max(np.where(alpha < 1, (bound - np.sqrt(d32)) / np.maximum(lb, 1e-30), -np.inf)))
+
+
+def _faces(rng, n, scale, sliver=0.0):
+    v = rng.standard_normal((n, 3, 3)) * scale
+    if sliver:  # third vertex pushed onto the first edge's line: small angles, κ up to ~1/sliver
+        a = rng.random((n, 1))
+        v[:, 2] = v[:, 0] + a * (v[:, 1] - v[:, 0]) + sliver * scale * rng.standard_normal((n, 3))
+    e1, e2 = v[:, 1] - v[:, 0], v[:, 2] - v[:, 0]
+    keep = np.linalg.norm(np.cross(e1, e2), axis=1) > 1e-12 * scale * scale
+    return v[keep].astype(F32)
+
+
+def test_face_slab_bound_premise_random_and_slivers():
+    rng = np.random.default_rng(5)
+    for scale in (1e-3, 0.05, 1.0, 300.0):
+        for sliver in (0.0, 1e-2, 1e-3, 1e-4):
+            f = _faces(rng, 100_000, scale, sliver)
+            cen = f.mean(1)
+            far = rng.choice([1e-4, 0.01, 0.3, 1.0, 5.0, 100.0], (len(f), 1))
+            pts = cen + rng.standard_normal((len(f), 3)) * scale * far
+            pts = pts[np.abs(pts).max(1) <= 1e4]
+            _check_faces(pts.astype(F32), f[:len(pts)])
+
+
+def test_face_slab_bound_premise_on_the_surface():
+    """Points on the face, on its edges and vertices, and 1e-7..1e-3 off its plane — the region-boundary
+    cases where point_face's branch choice and the slab's in-plane test both meet rounding."""
+    rng = np.random.default_rng(6)
+    for scale in (1e-3, 0.05, 1.0):
+        for sliver in (0.0, 1e-3):
+            f = _faces(rng, 100_000, scale, sliver)
+            m = len(f)
+            bary = rng.dirichlet([1, 1, 1], m)
+            on = np.einsum("nk,nkc->nc", bary, f.astype(np.float64))
+            nrm = np.cross(f[:, 1] - f[:, 0], f[:, 2] - f[:, 0]).astype(np.float64)
+            nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+            off = scale * 10.0 ** rng.uniform(-7, -3, m) * rng.choice([-1, 1], m)
+            pts = on + off[:, None] * nrm
+            k = m // 4
+            pts[:k] = f[:k, rng.integers(0, 3)]                                        # vertices
+            pts[k:2 * k] = 0.5 * (f[k:2 * k, 0] + f[k:2 * k, 1]) + off[k:2 * k, None] * nrm[k:2 * k]  # edges
+            _check_faces(pts.astype(F32), f)
+
+
+def _node(faces):
+    """sdf_node_kernel's cylinder ∩ ball of a face group (double, rounded as the kernel rounds)."""
+    v = faces.astype(np.float64).reshape(-1, 3)
+    c = (0.5 * (v.min(0) + v.max(0))).astype(F32).astype(np.float64)
+    ns = np.cross(faces[:, 1].astype(np.float64) - faces[:, 0], faces[:, 2].astype(np.float64) - faces[:, 0]).sum(0)
+    a32 = (ns / np.linalg.norm(ns)).astype(F32) if np.linalg.norm(ns) > 0 else np.array([0, 0, 1], F32)
+    a = a32.astype(np.float64) / np.linalg.norm(a32.astype(np.float64))
+    h = (v - c) @ a
+    c = (c + 0.5 * (h.min() + h.max()) * a).astype(F32).astype(np.float64)
+    d = v - c
+    h = d @ a
+    e = d - h[:, None] * a
+    t, rc, R = np.abs(h).max(), np.sqrt((e ** 2).sum(1).max()), np.sqrt((d ** 2).sum(1).max())
+    return c.astype(F32), a32, F32(t * (1 + 1e-6)), F32(rc * (1 + 1e-6)), R * (1 + 1e-6)
+
+
+def test_node_cylinder_bound_premise():
+    """Every face of a node against the node's cylinder ∩ ball bound with the node's margins (the largest α of
+    its faces, β = 1e-4·(|p| + |c| + 3R)): groups of 32 and 512 faces of the banana mesh in k-d order, points
+    around and far from the mesh."""
+    import os
+    from compliancedex_amd.workloads import DATA
+    faces = np.load(os.path.join(DATA, "meshes", "banana_faces.npy")).astype(F32)
+    rng = np.random.default_rng(7)
+    order = np.argsort(faces.mean(1)[:, 1], kind="stable")  # slabs along the banana's long axis
+    lo, hi = faces.reshape(-1, 3).min(0), faces.reshape(-1, 3).max(0)
+    pts = (lo - 2.0 * (hi - lo) + 5.0 * (hi - lo) * rng.random((4000, 3))).astype(F32)
+    for size in (32, 512):
+        for k in range(0, 8 * size, size):
+            grp = faces[order[k * 3:k * 3 + size]]
+            c, a, t, rc, R = _node(grp)
+            n = len(pts)
+            lb2, d2 = _cyl_lb2(pts, np.tile(c, (n, 1)), np.tile(a, (n, 1)), np.full(n, t, F32), np.full(n, rc, F32))
+            lb = np.maximum(np.sqrt(lb2.astype(np.float64)), np.sqrt(d2.astype(np.float64)) - R)
+            alpha = 1e-4 + 1e-5 * _kappa(grp).max()
+            beta = (1e-4 + 1e-8 * _kappa(grp).max()) * (np.linalg.norm(pts.astype(np.float64), axis=1) + np.linalg.norm(c.astype(np.float64)) + 3 * R)
+            bound = lb * (1 - alpha) - beta
+            for f in grp:
+                d = np.sqrt(_point_face(pts, np.repeat(f[None], n, 0)).astype(np.float64))
+                assert (d >= bound).all(), (size, k, float((bound - d).max()))

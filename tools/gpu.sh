@@ -13,6 +13,7 @@
 #   configs          tools/bench_configs.py (configs 1-5)
 #   c4kin            tools/c4_kin.py: the fused config-4 Kin loop, ms per iteration + TorchSDF counters
 #   c4trace          rocprofv3 --kernel-trace --stats over tools/c4_kin.py (prof_c4_TAG/)
+#   sdfpmc           tools/pmc_sdf.sh: PMC passes over tools/sdf_child.py (the config-4 queries), sdf_tree_kernel
 #   ab=SPEC,SPEC,..  interleaved bench A/B (R rounds, env R=3): SPEC = lib name ("base" = libcdx.so) with
 #                    optional +VAR=VAL settings, e.g. ab=base,base+CDX_SCREEN_REPAIR=0
 set -u
@@ -68,6 +69,9 @@ for STEP in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4_$TAG" -o run -- \
         python3 "$ROOT/tools/c4_kin.py" 10 2 > "$OUT/rocprof_c4_$TAG.log" 2>&1
       rc=$?; echo "rocprof c4 rc=$rc"; tail -2 "$OUT/rocprof_c4_$TAG.log"; stop_if_fault $rc ;;
+    sdfpmc)
+      bash tools/pmc_sdf.sh "$TAG" > "$OUT/pmc_sdf_$TAG.txt" 2>&1
+      rc=$?; echo "sdf pmc rc=$rc"; tail -40 "$OUT/pmc_sdf_$TAG.txt"; stop_if_fault $rc ;;
     configs)
       timeout -k 10 600 python -u tools/bench_configs.py > "$OUT/configs_$TAG.jsonl" 2> "$OUT/configs_$TAG.log"
       rc=$?; echo "configs rc=$rc"; tail -c 3000 "$OUT/configs_$TAG.jsonl"; stop_if_fault $rc ;;

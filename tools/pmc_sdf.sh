@@ -2,7 +2,7 @@
 # PMC passes (one counter group per run) over tools/sdf_child.py: the config-4 TorchSDF forward.
 #   bash tools/pmc_sdf.sh <tag>      (on the GPU box; CDX_LIB selects the library)
 set -u
-TAG=${1:-r04}
+TAG=${1:-r05}
 OUT=gpurun_out/pmc_sdf_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -15,5 +15,5 @@ for G in "SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_ACTI
     > "$OUT/p$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
-python3 tools/pmc_kernel_summary.py "$OUT" sdf_culled > "$OUT/summary.txt" 2>&1; cat "$OUT/summary.txt"
+python3 tools/pmc_kernel_summary.py "$OUT" sdf_tree > "$OUT/summary.txt" 2>&1; cat "$OUT/summary.txt"
 exit 0

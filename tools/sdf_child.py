@@ -1,31 +1,35 @@
-"""Config-4 TorchSDF forward as a profiling child: 3 × 65 536 random points around the 16 384-face banana
-(the c4 case's points), the three cdx_sdf_forward calls of one SDF/Kin iteration, repeated REPS times.
+"""Config-4 TorchSDF forward as a profiling child: the three queries of one SDF/Kin iteration (4E fingertips vs
+the deflated and the true 16 384-face banana, 4E targets vs the true mesh; E = 16 384, workloads.config4_kin_inputs)
+on prepared meshes, repeated REPS times.
 
   python tools/sdf_child.py [REPS]        (under rocprofv3 --pmc / --kernel-trace; tools/pmc_sdf.sh)
 """
 import os
 import sys
 
-import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from compliancedex_amd.torchsdf import compute_sdf  # noqa: E402
-
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def main(reps):
+    from compliancedex_amd import DifferentiableRobotModel, PreparedMesh
+    from compliancedex_amd.optimizers import _face_vertices
+    from compliancedex_amd.workloads import banana_mesh, config4_kin_inputs
     dev = "cuda"
-    torch.manual_seed(0)
-    faces = torch.from_numpy(np.load(os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_faces.npy"))).to(dev)
-    lo, hi = faces.reshape(-1, 3).min(0)[0], faces.reshape(-1, 3).max(0)[0]
-    pts = [lo - 0.02 + (hi - lo + 0.04) * torch.rand(65536, 3, device=dev) for _ in range(3)]
-    deflated = faces * 0.9
+    links, offs, palm, q, target, comp = config4_kin_inputs(16384, device=dev)
+    tips = (DifferentiableRobotModel("iiwa7_allegro", device=dev).compute_forward_kinematics(
+        torch.from_numpy(q).to(dev), links, offsets=offs)[0].view(-1, 3) + torch.from_numpy(palm).to(dev)).contiguous()
+    tg = torch.from_numpy(target).to(dev).view(-1, 3).contiguous()
+    m = banana_mesh()
+    faces = _face_vertices(m, dev)
+    m.scale(0.9, center=[0, 0, 0])
+    full, deflated = PreparedMesh(faces), PreparedMesh(_face_vertices(m, dev))
     with torch.no_grad():
         for _ in range(reps):
-            for i, f in enumerate((deflated, faces, faces)):
-                compute_sdf(pts[i], f)
+            deflated.query(tips)
+            full.query(tips)
+            full.query(tg)
     torch.cuda.synchronize()
 
 
