@@ -17,6 +17,7 @@ KERNELS = {"tps": 0, "rbf": 1, "joint": 2}
 NPAD_ALIGN = 256  # CDX_NPAD_ALIGN
 SCREEN_BANDS = 24  # CDX_SCREEN_BANDS
 PROF_STAGES = 6   # cdx_profile_read array length
+SDF_REUSE_ORDER, SDF_MESH_CULLED, SDF_MESH_EXACT = 1, 2, 4  # cdx_sdf_query flags
 ERRORS = {-1: "invalid argument", -2: "unsupported GPIS kernel", -3: "chain exceeds descriptor capacity",
           -10: "HIP launch failed"}
 
@@ -154,7 +155,8 @@ _SIGS = {
     "cdx_sdf_mesh_bytes": (C.c_size_t, [_I64]),
     "cdx_sdf_mesh_prepare": (C.c_int, [_P, _I64, _P, _P]),
     "cdx_sdf_query_workspace": (C.c_size_t, [_I64]),
-    "cdx_sdf_query": (C.c_int, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, C.c_size_t, _P]),
+    "cdx_sdf_query": (C.c_int, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, C.c_size_t, C.c_int32, _P]),
+    "cdx_sdf_mesh_flags": (C.c_int, [_P, C.POINTER(C.c_int32), _P]),
     "cdx_version": (C.c_char_p, []),
     "cdx_abi_sizes": (None, [C.POINTER(C.c_size_t)]),
     "cdx_selftest_mfma_f64": (C.c_int, [_P, _P, _P, _P]),

@@ -92,8 +92,13 @@ __device__ inline void bb_acc(float x, float y, float z, unsigned (&lo)[3], unsi
   for (int c = 0; c < 3; ++c) { lo[c] = min(lo[c], k[c]); hi[c] = max(hi[c], k[c]); }
 }
 
-// Bounding box of n points (3 floats each) into frame words 0..5.
-__global__ __launch_bounds__(256) void sdf_bbox_kernel(const float* __restrict__ v, int64_t n, unsigned* ws) {
+// Bounding box of n points (3 floats each): block b writes its partial (min keys ×3, max keys ×3) to part[6b ..]
+// (no atomics: ≤ BBOX_BLOCKS partials, reduced by the keys kernel).  Block 0 also clears the mesh header's
+// may-NaN flag when `flag` is given (a build's face kernel ORs into it afterwards).
+constexpr int BBOX_BLOCKS = 32;
+__global__ __launch_bounds__(256) void sdf_bbox_kernel(const float* __restrict__ v, int64_t n, unsigned* __restrict__ part,
+                                                       unsigned* flag) {
+  __shared__ unsigned s_lo[4][3], s_hi[4][3];
   unsigned lo[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, hi[3] = {0u, 0u, 0u};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     bb_acc(v[3 * i], v[3 * i + 1], v[3 * i + 2], lo, hi);
@@ -105,17 +110,23 @@ __global__ __launch_bounds__(256) void sdf_bbox_kernel(const float* __restrict__
       hi[c] = max(hi[c], (unsigned)__shfl_xor((int)hi[c], o));
     }
   }
-  if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int c = 0; c < 3; ++c) { atomicMin(ws + c, lo[c]); atomicMax(ws + 3 + c, hi[c]); }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int c = 0; c < 3; ++c) { s_lo[w][c] = lo[c]; s_hi[w][c] = hi[c]; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int c = threadIdx.x;
+    part[6 * blockIdx.x + c] = min(min(s_lo[0][c], s_lo[1][c]), min(s_lo[2][c], s_lo[3][c]));
+    part[6 * blockIdx.x + 3 + c] = max(max(s_hi[0][c], s_hi[1][c]), max(s_hi[2][c], s_hi[3][c]));
   }
+  if (flag && blockIdx.x == 0 && threadIdx.x == 0) *flag = 0u;
 }
 
-// 30-bit Morton code in the frame's CUBIC box (the largest extent on every axis: cells are cubes, so a run
-// of codes is compact in space whatever the box's aspect)
-__device__ inline unsigned morton(float x, float y, float z, const unsigned* ws) {
-  const float lo[3] = {fkey_inv(ws[0]), fkey_inv(ws[1]), fkey_inv(ws[2])};
-  const float ext = fmaxf(fmaxf(fkey_inv(ws[3]) - lo[0], fkey_inv(ws[4]) - lo[1]), fkey_inv(ws[5]) - lo[2]);
+// Morton code of MB bits per axis in the frame's CUBIC box (the largest extent on every axis: cells are cubes, so
+// a run of codes is compact in space whatever the box's aspect).  fr: min keys ×3, max keys ×3.
+__device__ inline unsigned morton(float x, float y, float z, const unsigned* fr, int mb) {
+  const float lo[3] = {fkey_inv(fr[0]), fkey_inv(fr[1]), fkey_inv(fr[2])};
+  const float ext = fmaxf(fmaxf(fkey_inv(fr[3]) - lo[0], fkey_inv(fr[4]) - lo[1]), fkey_inv(fr[5]) - lo[2]);
   const float v[3] = {x, y, z};
   unsigned m = 0;
 #pragma unroll
@@ -124,12 +135,22 @@ __device__ inline unsigned morton(float x, float y, float z, const unsigned* ws)
     t = fminf(fmaxf(t, 0.f), 1.f);  // NaN → 0
     m |= spread10((unsigned)(t * 1023.f)) << c;
   }
-  return m;
+  return m >> (3 * (10 - mb));
 }
 
-// Morton keys of points (centroid = false) or of face centroids (centroid = true, 9 floats a face).
+// Morton keys (mb bits per axis) of points (centroid = false) or of face centroids (centroid = true, 9 floats a
+// face), in the frame of the nb bbox partials.
 __global__ __launch_bounds__(256) void sdf_keys_kernel(const float* __restrict__ v, int64_t n, int centroid,
-                                                       const unsigned* __restrict__ ws, unsigned* keys, int* vals) {
+                                                       const unsigned* __restrict__ part, int nb, int mb,
+                                                       unsigned* keys, int* vals) {
+  __shared__ unsigned fr[6];
+  if (threadIdx.x < 6) {
+    const int c = threadIdx.x;
+    unsigned r = c < 3 ? 0xFFFFFFFFu : 0u;
+    for (int b = 0; b < nb; ++b) r = c < 3 ? min(r, part[6 * b + c]) : max(r, part[6 * b + c]);
+    fr[c] = r;
+  }
+  __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float x, y, z;
@@ -140,7 +161,7 @@ __global__ __launch_bounds__(256) void sdf_keys_kernel(const float* __restrict__
   } else {
     x = v[3 * i]; y = v[3 * i + 1]; z = v[3 * i + 2];
   }
-  keys[i] = morton(x, y, z, ws);
+  keys[i] = morton(x, y, z, fr, mb);
   vals[i] = (int)i;
 }
 
@@ -334,12 +355,16 @@ __device__ void exact_point(cdx::F3 p, const float* __restrict__ faces, int64_t 
 }
 
 
+// The bounds' square roots: v_sqrt_f32 (≤ 1 ulp, no correction sequence) — a bound's rounding is four orders
+// below its margins; the distances themselves (point_face, face_dist2) keep the correctly rounded sqrtf.
+__device__ __forceinline__ float bsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+
 // Squared distance from p to a node's cylinder (its ball: *d2 = |p − c|² for the caller's ball test).
 __device__ __forceinline__ float cyl_lb2(cdx::F3 p, float4 a, float4 b, float rc, float* d2) {
   const float dx = p.x - a.x, dy = p.y - a.y, dz = p.z - a.z;
   const float h = b.x * dx + b.y * dy + b.z * dz;
   const float ex = dx - h * b.x, ey = dy - h * b.y, ez = dz - h * b.z;
-  const float rho = sqrtf(ex * ex + ey * ey + ez * ez);
+  const float rho = bsqrt(ex * ex + ey * ey + ez * ez);
   const float dh = fmaxf(fabsf(h) - b.w, 0.f), dr = fmaxf(rho - rc, 0.f);  // (fmaxf: NaN → 0, a bound of 0)
   *d2 = dx * dx + dy * dy + dz * dz;
   return dh * dh + dr * dr;
@@ -364,7 +389,7 @@ __device__ __forceinline__ bool node_needed(cdx::F3 p, const Node& n, float sb, 
 __device__ __forceinline__ float node_lb(cdx::F3 p, const Node& n) {
   float d2;
   const float l2 = cyl_lb2(p, n.a, n.b, n.m.x, &d2);
-  return fmaxf(sqrtf(l2), sqrtf(d2) - n.a.w);
+  return fmaxf(bsqrt(l2), bsqrt(d2) - n.a.w);
 }
 
 __device__ __forceinline__ Node load_node(const Node* __restrict__ p, int i) {
@@ -390,7 +415,14 @@ __device__ inline unsigned long long pack_best(float d, int idx) {
   return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)idx;
 }
 
-// One wave per 64 Morton-sorted points, waves independent (four to a workgroup, no barrier).
+// One workgroup per 64 Morton-sorted points: its four waves hold the same 64 points (lane = point) and split
+// the work — the greedy seed's tops / chunks / faces four ways, then the chunks of every top node some lane
+// cannot rule out (wave w takes chunks w, w + 4, … of the top) — and share each point's packed best in LDS,
+// so a face one wave evaluates tightens the bounds the others test.  Grid: ⌈P/64⌉ workgroups of 4 waves.
+__device__ __forceinline__ void sel_min(float& lb, int& sel, float l, int i) {
+  if (l < lb || (l == lb && i < sel)) { lb = l; sel = i; }
+}
+
 __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
     const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
     int64_t F, const cdx::FaceRec* __restrict__ rec, const Slab* __restrict__ slab, const Node* __restrict__ chunk,
@@ -399,73 +431,91 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
     int32_t* __restrict__ out_face, int count) {
   if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
   __shared__ float4 s_rec[4][REC_WORDS * CHUNK / 4];  // per wave: the visited chunk's face records
-  __shared__ unsigned long long s_best[4][64];        // … each lane's packed (distance, face) best
-  __shared__ unsigned short s_pair[4][128];           // … and its pending (lane << 5 | face) pairs
+  __shared__ unsigned long long s_best[64];           // the group's packed (distance, face) best per point
+  __shared__ unsigned short s_pair[4][128];           // per wave: pending (lane << 5 | face) pairs
+  __shared__ float s_lb[4][64];                       // greedy seed: per wave candidate bound …
+  __shared__ int s_sel[4][64];                        // … and index
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t j0 = ((int64_t)blockIdx.x * 4 + w) * 64;
-  if (j0 >= P) return;
-  const int64_t j = j0 + lane;
+  const int64_t j = (int64_t)blockIdx.x * 64 + lane;
   const bool live = j < P;
   const int64_t pi = porder[live ? j : P - 1];  // dead lanes shadow a live point
   const cdx::F3 p = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
   const bool ok = fabsf(p.x) <= PT_LIM && fabsf(p.y) <= PT_LIM && fabsf(p.z) <= PT_LIM;
-  if (!__all(ok)) {
-    exact_point(p, faces, F, pi, out_dist, out_sign, out_nrm, out_clst, out_face, live);
-    if (count && lane == 0) atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(__ballot(live)));
+  if (!__all(ok)) {  // same points in every wave: uniform over the workgroup
+    if (w == 0) {
+      exact_point(p, faces, F, pi, out_dist, out_sign, out_nrm, out_clst, out_face, live);
+      if (count && lane == 0)
+        atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(__ballot(live)));
+    }
     return;
   }
-  const float pnorm = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+  const float pnorm = bsqrt(p.x * p.x + p.y * p.y + p.z * p.z);
+  // merge the four waves' (bound, index) candidates: the smallest bound, then the smallest index
+  auto merge = [&](float lb, int sel) {
+    s_lb[w][lane] = lb;
+    s_sel[w][lane] = sel;
+    __syncthreads();
+    float m = s_lb[0][lane];
+    int si = s_sel[0][lane];
+#pragma unroll
+    for (int v = 1; v < 4; ++v) sel_min(m, si, s_lb[v][lane], s_sel[v][lane]);
+    __syncthreads();
+    return si;
+  };
 
   // greedy seed: nearest top node, nearest chunk in it, the face of smallest slab bound in that chunk —
-  // evaluated exactly, so the lane starts with a real (distance, face) near its answer
-  int tsel = 0;
+  // evaluated exactly, so every point starts with a real (distance, face) near its answer
+  int tsel;
   {
     float tl = INFINITY;
-    for (int t = 0; t < T; ++t) {
-      const float lb = node_lb(p, load_node(top, t));
-      if (lb < tl) { tl = lb; tsel = t; }
-    }
+    int ts = 0x7fffffff;
+    for (int t = w; t < T; t += 4) sel_min(tl, ts, node_lb(p, load_node(top, t)), t);
+    tsel = merge(tl, ts);
+    if (tsel >= T) tsel = 0;
   }
-  int csel = tsel * TOPB;
+  int csel;
   {
     float cl = INFINITY;
-    const int ce = min(C, tsel * TOPB + TOPB);
-    for (int c = tsel * TOPB; c < ce; ++c) {
-      const float lb = node_lb(p, load_node(chunk, c));
-      if (lb < cl) { cl = lb; csel = c; }
+    int cs = 0x7fffffff;
+    for (int i = 0; i < TOPB / 4; ++i) {
+      const int c = tsel * TOPB + w + 4 * i;
+      if (c < C) sel_min(cl, cs, node_lb(p, load_node(chunk, c)), c);
     }
+    csel = merge(cl, cs);
+    if (csel >= C) csel = tsel * TOPB;
   }
-  int64_t fsel = (int64_t)csel * CHUNK;
   {
     float fl = INFINITY;
-    const int64_t fe = min(F, (int64_t)csel * CHUNK + CHUNK);
-    for (int64_t f = (int64_t)csel * CHUNK; f < fe; ++f) {
-      const Slab s = load_slab(slab, f);
-      float d2;
-      const float l2 = cyl_lb2(p, s.a, s.b, s.a.w, &d2);
-      if (l2 < fl) { fl = l2; fsel = f; }
+    int fs = 0x7fffffff;
+    for (int i = 0; i < CHUNK / 4; ++i) {
+      const int64_t f = (int64_t)csel * CHUNK + w + 4 * i;
+      if (f < F) {
+        const Slab sl = load_slab(slab, f);
+        float d2;
+        sel_min(fl, fs, cyl_lb2(p, sl.a, sl.b, sl.a.w, &d2), (int)f);
+      }
     }
+    const int fsel = merge(fl, fs);
+    if (w == 0) {
+      const cdx::FaceRec r = rec[fsel < F ? fsel : csel * CHUNK];
+      s_best[lane] = pack_best(cdx::face_dist2(p, r), r.idx);
+    }
+    __syncthreads();
   }
-  float best;
-  int bidx;
-  {
-    const cdx::FaceRec r = rec[fsel];
-    best = cdx::face_dist2(p, r);
-    bidx = r.idx;
-  }
-  s_best[w][lane] = pack_best(best, bidx);
-  unsigned visits = 0, pairs = 64;
+  unsigned visits = 0, pairs = 0;
+  auto best_now = [&]() { return __uint_as_float((unsigned)(s_best[lane] >> 32)); };
 
   const float4* rec4 = reinterpret_cast<const float4*>(rec);
   float4* buf = s_rec[w];
   const cdx::FaceRec* rr = reinterpret_cast<const cdx::FaceRec*>(buf);
   for (int t = 0; t < T; ++t) {
-    if (!__any(node_needed(p, load_node(top, t), sqrtf(best), pnorm))) continue;
-    const int ce = min(C, t * TOPB + TOPB);
-    for (int c = t * TOPB; c < ce; ++c) {
+    if (!__any(node_needed(p, load_node(top, t), bsqrt(best_now()), pnorm))) continue;
+    for (int i = 0; i < TOPB / 4; ++i) {
+      const int c = t * TOPB + w + 4 * i;
+      if (c >= C) break;
       const Node cn = load_node(chunk, c);
-      const float sb = sqrtf(best);
+      const float sb = bsqrt(best_now());
       if (!__any(node_needed(p, cn, sb, pnorm))) continue;
       // the chunk's faces a lane cannot rule out: slab bound against the chunk's threshold (its margins)
       const float th = node_th(cn, sb, pnorm);
@@ -474,9 +524,9 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
       unsigned lmask = 0;
 #pragma unroll 8
       for (int k = 0; k < CHUNK; ++k) {
-        const Slab s = load_slab(slab, (int64_t)c * CHUNK + k);
+        const Slab sl = load_slab(slab, (int64_t)c * CHUNK + k);
         float d2;
-        const float l2 = cyl_lb2(p, s.a, s.b, s.a.w, &d2);
+        const float l2 = cyl_lb2(p, sl.a, sl.b, sl.a.w, &d2);
         if (!(l2 > th2) && k < nf && live) lmask |= 1u << k;
       }
       unsigned mask = lmask;
@@ -489,10 +539,10 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
       {
         float4 v[REC_V4];
 #pragma unroll
-        for (int i = 0; i < REC_V4; ++i) v[i] = rec4[(int64_t)c * (REC_WORDS * CHUNK / 4) + lane + 64 * i];
+        for (int q = 0; q < REC_V4; ++q) v[q] = rec4[(int64_t)c * (REC_WORDS * CHUNK / 4) + lane + 64 * q];
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int i = 0; i < REC_V4; ++i) buf[lane + 64 * i] = v[i];
+        for (int q = 0; q < REC_V4; ++q) buf[lane + 64 * q] = v[q];
         __builtin_amdgcn_wave_barrier();
       }
       // the (lane, face) pairs, packed 64 to a round: lane i of a round evaluates pair i (its point read from
@@ -503,8 +553,7 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
         const float qx = __shfl(p.x, l), qy = __shfl(p.y, l), qz = __shfl(p.z, l);
         if (lane < n) {
           const cdx::FaceRec& r = rr[e & 31u];
-          const float d = cdx::face_dist2(cdx::f3(qx, qy, qz), r);
-          atomicMin(&s_best[w][l], pack_best(d, r.idx));
+          atomicMin(&s_best[l], pack_best(cdx::face_dist2(cdx::f3(qx, qy, qz), r), r.idx));
         }
         pairs += (unsigned)n;
       };
@@ -530,22 +579,19 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
       __builtin_amdgcn_wave_barrier();
       if (cnt > 0) eval_round(cnt);
       __builtin_amdgcn_wave_barrier();
-      {
-        const unsigned long long bb = s_best[w][lane];
-        best = __uint_as_float((unsigned)(bb >> 32));
-        bidx = (int)(unsigned)bb;
-      }
     }
   }
   if (count) {
     const unsigned long long nl = __popcll(__ballot(live));
     if (lane == 0) {
-      atomicAdd(&g_sdf_stats[0], (unsigned long long)pairs - 64 + nl);
-      atomicAdd(&g_sdf_stats[2], nl);
+      atomicAdd(&g_sdf_stats[0], (unsigned long long)pairs + (w == 0 ? nl : 0ull));
+      if (w == 0) atomicAdd(&g_sdf_stats[2], nl);
       atomicAdd(&g_sdf_stats[3], (unsigned long long)visits);
     }
   }
-  if (!live) return;
+  __syncthreads();
+  if (w != 0 || !live) return;
+  const int bidx = (int)(unsigned)s_best[lane];
   const float* v = faces + 9 * (int64_t)bidx;
   cdx::F3 cc, n;
   int sg;
@@ -707,7 +753,7 @@ void mesh_fill(const float* faces, int64_t F, const int* order, char* mesh, hipS
                      reinterpret_cast<Node*>(mesh + mesh_top_off(C)));
 }
 
-// One-shot build on the device: face centroids in Morton order of the faces' cubic frame.
+// One-shot build on the device: face centroids in Morton order (10 bits per axis) of the faces' cubic frame.
 int mesh_build_morton(const float* faces, int64_t F, char* mesh, hipStream_t s) {
   const int n = (int)F;
   size_t tf = 0;
@@ -715,19 +761,20 @@ int mesh_build_morton(const float* faces, int64_t F, char* mesh, hipStream_t s) 
                                          (int*)nullptr, n, 0, 30, s) != hipSuccess)
     return CDX_ELAUNCH;
   size_t off = 0;
+  const size_t o_part = off; off = align256(off + 6 * BBOX_BLOCKS * sizeof(unsigned));
   const size_t o_fk = off; off = align256(off + 2 * (size_t)n * sizeof(unsigned));
   const size_t o_fv = off; off = align256(off + 2 * (size_t)n * sizeof(int));
   const size_t o_tmp = off; off = align256(off + tf);
   char* base = nullptr;
   if (hipMallocAsync(reinterpret_cast<void**>(&base), off, s) != hipSuccess) return CDX_ELAUNCH;
   unsigned* ws = reinterpret_cast<unsigned*>(mesh);
+  unsigned* part = reinterpret_cast<unsigned*>(base + o_part);
   unsigned* fk = reinterpret_cast<unsigned*>(base + o_fk);
   int* fv = reinterpret_cast<int*>(base + o_fv);
-  hipLaunchKernelGGL(sdf_init_kernel, dim3(1), dim3(64), 0, s, ws);
-  const unsigned bbb = (unsigned)std::min<int64_t>((3 * F + 255) / 256, 1024);
-  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(bbb), dim3(256), 0, s, faces, 3 * F, ws);
+  const int nb = (int)std::min<int64_t>((3 * F + 255) / 256, BBOX_BLOCKS);
+  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(nb), dim3(256), 0, s, faces, 3 * F, part, ws + 6);
   hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((F + 255) / 256)), dim3(256), 0, s, faces, F, 1,
-                     (const unsigned*)ws, fk, fv);
+                     (const unsigned*)part, nb, 10, fk, fv);
   size_t t1 = tf;
   bool ok = hipcub::DeviceRadixSort::SortPairs(base + o_tmp, t1, fk, fk + n, fv, fv + n, n, 0, 30, s) == hipSuccess;
   mesh_fill(faces, F, fv + n, mesh, s);
@@ -788,25 +835,25 @@ int mesh_build_kd(const float* faces, int64_t F, char* mesh, hipStream_t s) {
   if (hipMallocAsync(reinterpret_cast<void**>(&order), (size_t)F * sizeof(int), s) != hipSuccess) return CDX_ELAUNCH;
   bool ok = hipMemcpyAsync(order, idx.data(), (size_t)F * sizeof(int), hipMemcpyHostToDevice, s) == hipSuccess &&
             hipStreamSynchronize(s) == hipSuccess;  // (idx is freed on return)
-  unsigned* ws = reinterpret_cast<unsigned*>(mesh);
-  hipLaunchKernelGGL(sdf_init_kernel, dim3(1), dim3(64), 0, s, ws);
-  const unsigned bbb = (unsigned)std::min<int64_t>((3 * F + 255) / 256, 1024);
-  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(bbb), dim3(256), 0, s, faces, 3 * F, ws);
+  hipLaunchKernelGGL(sdf_init_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<unsigned*>(mesh));  // (may-NaN flag)
   mesh_fill(faces, F, order, mesh, s);
   ok = ok && hipGetLastError() == hipSuccess;
   ok = (hipFreeAsync(order, s) == hipSuccess) && ok;
   return ok ? CDX_OK : CDX_ELAUNCH;
 }
 
-// Query workspace: [point frame words ×8][keys 2P][values 2P][radix-sort scratch].
+// Query workspace: [bbox partials 6·BBOX_BLOCKS words][keys 2P][values 2P][radix-sort scratch]; the points' order
+// stays at values + P for a later query of the same points (CDX_SDF_REUSE_ORDER).
+constexpr int POINT_MB = 6;  // Morton bits per axis of the point order (64³ cells over the points' box; finer
+                             // levels only reorder points within a wave's neighbourhood)
 struct QueryWs { size_t o_pk, o_pv, o_tmp, bytes, tp; };
 bool query_ws(int64_t P, hipStream_t s, QueryWs& q) {
   const int m = (int)P;
   q.tp = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, q.tp, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
-                                         (int*)nullptr, m, 0, 30, s) != hipSuccess)
+                                         (int*)nullptr, m, 0, 3 * POINT_MB, s) != hipSuccess)
     return false;
-  size_t off = align256(8 * sizeof(unsigned));
+  size_t off = align256(6 * BBOX_BLOCKS * sizeof(unsigned));
   q.o_pk = off; off = align256(off + 2 * (size_t)m * sizeof(unsigned));
   q.o_pv = off; off = align256(off + 2 * (size_t)m * sizeof(int));
   q.o_tmp = off; off = align256(off + q.tp);
@@ -814,50 +861,58 @@ bool query_ws(int64_t P, hipStream_t s, QueryWs& q) {
   return true;
 }
 
-// Points in Morton order of their own cubic frame (a wave then holds nearby points), the tree kernel, and
-// the brute-force tile rule when the mesh may produce NaN distances (decided on the device).
+// Points in Morton order of their own cubic frame (a workgroup then holds nearby points; skipped with
+// CDX_SDF_REUSE_ORDER), the tree kernel (skipped with CDX_SDF_MESH_EXACT), and the brute-force tile rule when the
+// mesh may produce NaN distances (decided on the device; skipped with CDX_SDF_MESH_CULLED).
 int mesh_query(const char* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
-               int32_t* sign, float* normals, float* clst, int32_t* face_idx, char* base, const QueryWs& q,
+               int32_t* sign, float* normals, float* clst, int32_t* face_idx, char* base, const QueryWs& q, int flags,
                hipStream_t s) {
   const int m = (int)P;
   const int64_t C = n_chunks(F), T = n_tops(F);
   const unsigned* mws = reinterpret_cast<const unsigned*>(mesh);
-  unsigned* pws = reinterpret_cast<unsigned*>(base);
+  unsigned* part = reinterpret_cast<unsigned*>(base);
   unsigned* pk = reinterpret_cast<unsigned*>(base + q.o_pk);
   int* pv = reinterpret_cast<int*>(base + q.o_pv);
-  hipLaunchKernelGGL(sdf_init_kernel, dim3(1), dim3(64), 0, s, pws);
-  const unsigned bbb = (unsigned)std::min<int64_t>((P + 255) / 256, 1024);
-  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(bbb), dim3(256), 0, s, points, P, pws);
-  hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P, 0,
-                     (const unsigned*)pws, pk, pv);
-  size_t t2 = q.tp;
-  bool ok = hipcub::DeviceRadixSort::SortPairs(base + q.o_tmp, t2, pk, pk + m, pv, pv + m, m, 0, 30, s) == hipSuccess;
-  hipLaunchKernelGGL(sdf_tree_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0, s, points,
-                     P, (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
-                     reinterpret_cast<const Slab*>(mesh + mesh_slab_off(C)),
-                     reinterpret_cast<const Node*>(mesh + mesh_chunk_off(C)),
-                     reinterpret_cast<const Node*>(mesh + mesh_top_off(C)), (int)C, (int)T, mws, sqdist, sign, normals,
-                     clst, face_idx, (int)g_sdf_count);
-  hipLaunchKernelGGL(sdf_exact_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0, s, points,
-                     P, faces, F, mws, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
+  bool ok = true;
+  if (!(flags & CDX_SDF_REUSE_ORDER) && !(flags & CDX_SDF_MESH_EXACT)) {
+    const int nb = (int)std::min<int64_t>((P + 255) / 256, BBOX_BLOCKS);
+    hipLaunchKernelGGL(sdf_bbox_kernel, dim3(nb), dim3(256), 0, s, points, P, part, (unsigned*)nullptr);
+    hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P, 0,
+                       (const unsigned*)part, nb, POINT_MB, pk, pv);
+    size_t t2 = q.tp;
+    ok = hipcub::DeviceRadixSort::SortPairs(base + q.o_tmp, t2, pk, pk + m, pv, pv + m, m, 0, 3 * POINT_MB, s) ==
+         hipSuccess;
+  }
+  if (!(flags & CDX_SDF_MESH_EXACT))
+    hipLaunchKernelGGL(sdf_tree_kernel, dim3((unsigned)((P + 63) / 64)), dim3(SDF_BLOCK), 0, s, points, P,
+                       (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
+                       reinterpret_cast<const Slab*>(mesh + mesh_slab_off(C)),
+                       reinterpret_cast<const Node*>(mesh + mesh_chunk_off(C)),
+                       reinterpret_cast<const Node*>(mesh + mesh_top_off(C)), (int)C, (int)T, mws, sqdist, sign,
+                       normals, clst, face_idx, (int)g_sdf_count);
+  if (!(flags & CDX_SDF_MESH_CULLED))
+    hipLaunchKernelGGL(sdf_exact_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0, s,
+                       points, P, faces, F, mws, sqdist, sign, normals, clst, face_idx, (int)g_sdf_count);
   ok = ok && hipGetLastError() == hipSuccess;
   return ok ? CDX_OK : CDX_ELAUNCH;
 }
 
 // mesh_query with workspace `ws` (ws_bytes ≥ cdx_sdf_query_workspace(P)), or stream-ordered scratch when ws is
-// NULL.
+// NULL (then the order cannot be reused).
 int mesh_query_ws(const char* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
-                  int32_t* sign, float* normals, float* clst, int32_t* face_idx, void* ws, size_t ws_bytes,
+                  int32_t* sign, float* normals, float* clst, int32_t* face_idx, void* ws, size_t ws_bytes, int flags,
                   hipStream_t s) {
   QueryWs q;
   if (!query_ws(P, s, q)) return CDX_ELAUNCH;
   if (ws) {
     if (ws_bytes < q.bytes) return CDX_EINVAL;
-    return mesh_query(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, static_cast<char*>(ws), q, s);
+    return mesh_query(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, static_cast<char*>(ws), q,
+                      flags, s);
   }
+  if (flags & CDX_SDF_REUSE_ORDER) return CDX_EINVAL;
   char* base = nullptr;
   if (hipMallocAsync(reinterpret_cast<void**>(&base), q.bytes, s) != hipSuccess) return CDX_ELAUNCH;
-  int rc = mesh_query(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, base, q, s);
+  int rc = mesh_query(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, base, q, flags, s);
   if (hipFreeAsync(base, s) != hipSuccess && !rc) rc = CDX_ELAUNCH;
   return rc;
 }
@@ -887,7 +942,7 @@ int cdx_sdf_forward(const float* points, int64_t P, const float* faces, int64_t 
   char* mesh = nullptr;
   if (hipMallocAsync(reinterpret_cast<void**>(&mesh), mesh_bytes(F), s) != hipSuccess) return CDX_ELAUNCH;
   int rc = mesh_build_morton(faces, F, mesh, s);
-  if (!rc) rc = mesh_query_ws(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, nullptr, 0, s);
+  if (!rc) rc = mesh_query_ws(mesh, faces, F, points, P, sqdist, sign, normals, clst, face_idx, nullptr, 0, 0, s);
   if (hipFreeAsync(mesh, s) != hipSuccess && !rc) rc = CDX_ELAUNCH;
   return rc;
 }
@@ -905,16 +960,28 @@ size_t cdx_sdf_query_workspace(int64_t P) {
   return query_ws(P, nullptr, q) ? q.bytes : 0;
 }
 
+int cdx_sdf_mesh_flags(const void* mesh, int32_t* flags, cdx_stream_t stream) {
+  if (!mesh || !flags) return CDX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  unsigned w = 0;
+  if (hipMemcpyAsync(&w, static_cast<const unsigned*>(mesh) + 6, sizeof(unsigned), hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return CDX_ELAUNCH;
+  *flags = w ? CDX_SDF_MESH_EXACT : CDX_SDF_MESH_CULLED;
+  return CDX_OK;
+}
+
 int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
                   int32_t* sign, float* normals, float* clst, int32_t* face_idx, void* workspace,
-                  size_t workspace_bytes, cdx_stream_t stream) {
-  if (P < 0 || F < 0 || !mesh) return CDX_EINVAL;
+                  size_t workspace_bytes, int32_t flags, cdx_stream_t stream) {
+  if (P < 0 || F < 0 || !mesh || (flags & ~7) || (flags & 6) == 6) return CDX_EINVAL;
   if (P == 0) return CDX_OK;
   if (!sdf_args_ok(P, points, faces, F, sqdist, sign, normals, clst)) return CDX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (sdf_mode() == 1) return cdx_sdf_forward(points, P, faces, F, sqdist, sign, normals, clst, face_idx, stream);
   return mesh_query_ws(static_cast<const char*>(mesh), faces, F, points, P, sqdist, sign, normals, clst, face_idx,
-                       workspace, workspace_bytes, s);
+                       workspace, workspace_bytes, flags, s);
 }
 
 int cdx_sdf_chunk_visits(uint64_t* out, cdx_stream_t stream) {

@@ -24,7 +24,7 @@ from . import _native as N
 from .force_eq import force_eq_descriptor, force_eq_reward
 from .optimizer import EE_OFFSETS, FINGERTIP_LB, FINGERTIP_UB, WRIST_OFFSET
 from .robot_model import DifferentiableRobotModel
-from .torchsdf import PreparedMesh, compute_sdf
+from .torchsdf import PreparedMesh, QueryWorkspace, compute_sdf
 
 
 class TriangleMesh:
@@ -113,6 +113,7 @@ class _FusedLoop:
     def __init__(self, E, T, pose, target, comp, faces, faces_deflate, dev):
         f32 = dict(dtype=torch.float32, device=dev)
         self.mesh, self.mesh_def = PreparedMesh(faces), PreparedMesh(faces_deflate)
+        self.ws_tips, self.ws_tgt = QueryWorkspace(), QueryWorkspace()
         self.pose, self.target, self.comp = pose, target, comp
         self.loss = torch.empty(E, dtype=torch.float64, device=dev)
         self.margin = [torch.zeros(E, T, dtype=torch.float64, device=dev) for _ in range(2)]
@@ -139,9 +140,10 @@ class _FusedLoop:
         self.buffers = b
 
     def queries(self, tips, target):
-        _, sign1, n1, _, _ = self.mesh_def.query(tips)
-        dist, sign2, n2, clst, _ = self.mesh.query(tips)
-        tdist, tsign, _, tclst, _ = self.mesh.query(target.view(-1, 3))
+        """The iteration's three TorchSDF calls (:186-188); the fingertips are sorted once for both meshes."""
+        _, sign1, n1, _, _ = self.mesh_def.query(tips, workspace=self.ws_tips)
+        dist, sign2, n2, clst, _ = self.mesh.query(tips, workspace=self.ws_tips, reuse_order=True)
+        tdist, tsign, _, tclst, _ = self.mesh.query(target.view(-1, 3), workspace=self.ws_tgt)
         return sign1, n1, dist, sign2, n2, clst, tdist, tsign, tclst
 
     def best(self):

@@ -10,6 +10,8 @@ argmin face index.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from . import _native as N
@@ -53,16 +55,21 @@ class PreparedMesh:
         self.faces = face_vertices.detach().contiguous().clone()
         F = self.faces.shape[0]
         self.buf = torch.empty(lib.cdx_sdf_mesh_bytes(F), dtype=torch.uint8, device=self.faces.device)
-        N.check(lib.cdx_sdf_mesh_prepare(N.ptr(self.faces), F, N.ptr(self.buf), N.stream_ptr(self.faces.device)),
-                "cdx_sdf_mesh_prepare")
-        self._ws = torch.empty(0, dtype=torch.uint8, device=self.faces.device)
+        stream = N.stream_ptr(self.faces.device)
+        N.check(lib.cdx_sdf_mesh_prepare(N.ptr(self.faces), F, N.ptr(self.buf), stream), "cdx_sdf_mesh_prepare")
+        kind = C.c_int32(0)
+        N.check(lib.cdx_sdf_mesh_flags(N.ptr(self.buf), C.byref(kind), stream), "cdx_sdf_mesh_flags")
+        self.kind = kind.value  # SDF_MESH_CULLED, or SDF_MESH_EXACT for a mesh with a NaN-capable face
+        self._ws = QueryWorkspace()
 
     @property
     def num_faces(self):
         return self.faces.shape[0]
 
-    def query(self, points, want_face=False):
-        """(sqdist, sign, normals, clst, face | None) of float32 points [P, 3] (cdx_sdf_query)."""
+    def query(self, points, want_face=False, workspace=None, reuse_order=False):
+        """(sqdist, sign, normals, clst, face | None) of float32 points [P, 3] (cdx_sdf_query).  ``workspace``: a
+        QueryWorkspace to sort the points in (default: the mesh's own); ``reuse_order``: the workspace's last query
+        was of these same points (another mesh may have run it) — their order is reused, not sorted again."""
         _check(points, self.faces)
         lib = N.load()
         points = points.detach().contiguous()
@@ -74,13 +81,31 @@ class PreparedMesh:
         face = torch.empty(P, dtype=torch.int32, device=dev) if want_face else None
         if P == 0:
             return dist, sign, normals, clst, face
-        need = lib.cdx_sdf_query_workspace(P)
-        if self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        ws = (workspace or self._ws).get(P, dev, reuse_order)
+        flags = self.kind | (N.SDF_REUSE_ORDER if reuse_order else 0)
         N.check(lib.cdx_sdf_query(N.ptr(self.buf), N.ptr(self.faces), self.faces.shape[0], N.ptr(points), P,
                                   N.ptr(dist), N.ptr(sign), N.ptr(normals), N.ptr(clst), N.ptr(face),
-                                  N.ptr(self._ws), self._ws.numel(), N.stream_ptr(dev)), "cdx_sdf_query")
+                                  N.ptr(ws), ws.numel(), flags, N.stream_ptr(dev)), "cdx_sdf_query")
         return dist, sign, normals, clst, face
+
+
+class QueryWorkspace:
+    """Scratch of cdx_sdf_query (the points' Morton sort), regrown to the largest point count seen; it keeps the
+    last sorted order, which a query of the same points on another mesh may reuse."""
+
+    def __init__(self):
+        self.buf, self.P = None, None
+
+    def get(self, P, dev, reuse_order=False):
+        if reuse_order and self.P != P:
+            raise RuntimeError("reuse_order: the workspace's last query had a different point count")
+        need = N.load().cdx_sdf_query_workspace(P)
+        if self.buf is None or self.buf.numel() < need or self.buf.device != torch.device(dev):
+            if reuse_order:
+                raise RuntimeError("reuse_order: the workspace holds no order for these points")
+            self.buf = torch.empty(need, dtype=torch.uint8, device=dev)
+        self.P = P
+        return self.buf
 
 
 def _forward(points, faces, want_face):

@@ -488,9 +488,18 @@ int cdx_sdf_backward_f64(const double* grad_dist, const double* points, const do
 size_t cdx_sdf_mesh_bytes(int64_t F);
 int cdx_sdf_mesh_prepare(const float* faces, int64_t F, void* mesh, cdx_stream_t stream);
 size_t cdx_sdf_query_workspace(int64_t P);
+/* flags of cdx_sdf_query: CDX_SDF_REUSE_ORDER — `workspace` still holds the order of these same points from the
+ * previous query on it (e.g. the same fingertips against a second mesh): the points are not sorted again;
+ * CDX_SDF_MESH_CULLED / CDX_SDF_MESH_EXACT — the mesh's kind as cdx_sdf_mesh_flags read it once (no NaN-capable
+ * face: the culled kernel only; else the brute-force tile rule only); without either, both kernels are launched
+ * and the device picks. */
+#define CDX_SDF_REUSE_ORDER 1
+#define CDX_SDF_MESH_CULLED 2
+#define CDX_SDF_MESH_EXACT 4
+int cdx_sdf_mesh_flags(const void* mesh, int32_t* flags, cdx_stream_t stream);  /* waits on stream */
 int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
                   int32_t* sign, float* normals, float* clst, int32_t* face_idx, void* workspace,
-                  size_t workspace_bytes, cdx_stream_t stream);
+                  size_t workspace_bytes, int32_t flags, cdx_stream_t stream);
 /* Diagnostic work counters of cdx_sdf_forward / cdx_sdf_query (float path): out3 (nullable, host) =
  * [(point, face) pairs the culled kernel evaluated exactly — each lane's greedy seed face plus the pairs
  * its slab bounds could not rule out —, pairs of brute-force scans (the exact path), points queried]; read before `enable` applies.

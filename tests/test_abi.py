@@ -40,7 +40,7 @@ def test_bad_arguments_are_rejected_without_launch():
     c = N.CdxChain()
     assert lib.cdx_fk_forward(c, None, 1, None, None, None) == -3
     assert lib.cdx_sdf_forward(None, 5, None, 0, None, None, None, None, None, None) == -1
-    assert lib.cdx_sdf_query(None, None, 0, None, 5, None, None, None, None, None, None, 0, None) == -1
+    assert lib.cdx_sdf_query(None, None, 0, None, 5, None, None, None, None, None, None, 0, 0, None) == -1
     assert lib.cdx_sdf_query_workspace(0) == 0 and lib.cdx_sdf_mesh_bytes(0) == 0
     assert lib.cdx_sdf_mesh_prepare(None, 10, None, None) == -1
     cfg, buf = N.CdxKinOpt(), N.CdxKinOptBuffers()

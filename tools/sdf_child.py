@@ -25,11 +25,13 @@ def main(reps):
     faces = _face_vertices(m, dev)
     m.scale(0.9, center=[0, 0, 0])
     full, deflated = PreparedMesh(faces), PreparedMesh(_face_vertices(m, dev))
+    from compliancedex_amd.torchsdf import QueryWorkspace
+    ws_t, ws_g = QueryWorkspace(), QueryWorkspace()
     with torch.no_grad():
         for _ in range(reps):
-            deflated.query(tips)
-            full.query(tips)
-            full.query(tg)
+            deflated.query(tips, workspace=ws_t)
+            full.query(tips, workspace=ws_t, reuse_order=True)
+            full.query(tg, workspace=ws_g)
     torch.cuda.synchronize()
 
 
