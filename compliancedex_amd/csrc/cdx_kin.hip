@@ -153,6 +153,165 @@ __global__ __launch_bounds__(64) void kin_cost_kernel(
   }
 }
 
+
+// Four-fingertip variant: four lanes per candidate (lane f = fingertip f), so E = 16 384 candidates fill 1 024
+// waves instead of 256.  Every lane of a candidate gathers the candidate's four rows (shuffles) and runs the
+// force-equilibrium reward and the cost terms forward and backward itself — identical inputs, identical
+// results, no divergence (the lanes would idle otherwise) — then takes its own fingertip's gradients and walks
+// its own FK chain backward; the four chains' joint gradients are summed across the lanes ((f0 + f1) + (f2 + f3)).
+template <int MAXD, bool FK>
+__global__ __launch_bounds__(64) void kin_cost4_kernel(
+    cdx_chain chain, cdx_kin_params p, int64_t E, const float* __restrict__ q, const float* __restrict__ tip,
+    const float* __restrict__ target, const float* __restrict__ comp, const int32_t* __restrict__ sign1,
+    const float* __restrict__ n1, const float* __restrict__ sqd, const int32_t* __restrict__ sign2,
+    const float* __restrict__ n2, const float* __restrict__ clst, const float* __restrict__ tsqd,
+    const int32_t* __restrict__ tsign, const float* __restrict__ tclst, const double* __restrict__ noise, uint64_t seed,
+    double* __restrict__ loss, double* __restrict__ margin, float* __restrict__ normal_out, float* __restrict__ g_q,
+    float* __restrict__ g_target, float* __restrict__ g_comp, float* __restrict__ g_tip) {
+  constexpr int NT = 4;
+  const int64_t tg_ = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e_raw = tg_ >> 2;
+  const int f = (int)(tg_ & 3);
+  const bool on = e_raw < E;
+  const int64_t e = on ? e_raw : E - 1;  // (lanes past E shadow the last candidate: every lane shuffles)
+  const int base = (int)(threadIdx.x & ~3u);
+  const int D = FK ? chain.n_dofs : 0;
+  const int64_t r = e * NT + f;
+  // this lane's fingertip row: ½·s1·n1 + ½·s2·n2 and its norm in float32 (the reference's tensors are float32)
+  double nro[3], tpo[3], tgo[3];
+  {
+    float n[3];
+    const float a1 = 0.5f * (float)sign1[r], a2 = 0.5f * (float)sign2[r];
+    for (int i = 0; i < 3; ++i) n[i] = a1 * n1[3 * r + i] + a2 * n2[3 * r + i];
+    const float nn = sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    for (int i = 0; i < 3; ++i) {
+      const float v = n[i] / nn;
+      nro[i] = (double)v;
+      if (normal_out && on) normal_out[3 * r + i] = v;
+      tpo[i] = (double)tip[3 * r + i];
+      tgo[i] = (double)target[3 * r + i];
+    }
+  }
+  const double cpo = (double)comp[r], sdo = sqrt((double)sqd[r]), stdo = sqrt((double)tsqd[r]);
+  const double tso = (double)tsign[r];
+  double tp[NT][3], tg[NT * 3], cp[NT], nr[NT][3], sd[NT], std_[NT], ts[NT];
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    const int l = base + k;
+    for (int i = 0; i < 3; ++i) {
+      tp[k][i] = __shfl(tpo[i], l);
+      tg[3 * k + i] = __shfl(tgo[i], l);
+      nr[k][i] = __shfl(nro[i], l);
+    }
+    cp[k] = __shfl(cpo, l);
+    sd[k] = __shfl(sdo, l);
+    std_[k] = __shfl(stdo, l);
+    ts[k] = __shfl(tso, l);
+  }
+  double nz[9];
+  if (noise) {
+    for (int i = 0; i < 9; ++i) nz[i] = noise[e * 9 + i];
+  } else {
+    for (int i = 0; i < 9; ++i) nz[i] = (double)(kin_mix(seed ^ kin_mix((uint64_t)(e * 9 + i))) >> 11) * 0x1.0p-53;
+  }
+  cdx::ForceEqParams fp;
+  fp.cos_mu = (double)p.fe.cos_mu;
+  fp.gravity = p.fe.gravity;
+  for (int i = 0; i < 3; ++i) fp.com[i] = (double)p.fe.com[i];
+  fp.dummy_target_z = (double)p.fe.dummy_target_z;
+  fp.dummy_comp = (double)p.fe.dummy_comp;
+  cdx::ForceEq<NT> fe;
+  fe.forward(fp, NT, tp, tg, cp, nr, nz);
+
+  // ---- forward
+  double ct[3] = {0, 0, 0}, cg[3] = {0, 0, 0};
+  for (int k = 0; k < NT; ++k)
+    for (int i = 0; i < 3; ++i) { ct[i] += tp[k][i]; cg[i] += tg[3 * k + i]; }
+  double cd[3];
+  for (int i = 0; i < 3; ++i) cd[i] = ct[i] / NT - cg[i] / NT;
+  const double cn = sqrt(cd[0] * cd[0] + cd[1] * cd[1] + cd[2] * cd[2]);
+  double dq2 = 0.0;
+  for (int i = 0; i < D; ++i) {
+    const double d = (double)q[e * D + i] - (double)p.ref_q[i];
+    dq2 += d * d;
+  }
+  const double qn = sqrt(dq2);
+  double dcost = 0.0, tcost = 0.0;
+  for (int k = 0; k < NT; ++k) {
+    dcost += sd[k];
+    tcost += ts[k] * std_[k];
+  }
+  const double* fn = fe.fn;
+  double zmax = -fn[0];
+  for (int k = 1; k < NT; ++k) zmax = -fn[k] > zmax ? -fn[k] : zmax;
+  double ez[NT], esum = 0.0;
+  for (int k = 0; k < NT; ++k) { ez[k] = exp(-fn[k] - zmax); esum += ez[k]; }
+  double sm[NT], v[NT], fcost = 0.0;
+  for (int k = 0; k < NT; ++k) {
+    sm[k] = ez[k] / esum;
+    v[k] = fn[k] * sm[k];
+    fcost += v[k] > 1.0 ? 1.0 : v[k];
+  }
+  if (on && f == 0) {
+    loss[e] = FK ? -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost + qn * 10.0
+                 : -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost;
+  }
+  double mo = 0.0;
+  for (int k = 0; k < NT; ++k) mo = k == f ? fe.margin[k] : mo;
+  if (on) margin[r] = mo;
+
+  // ---- backward (dl = 1)
+  double gt[NT][3], gg[NT][3], gc[NT];
+  for (int k = 0; k < NT; ++k) {
+    const int64_t rk = e * NT + k;
+    gc[k] = 0.0;
+    const double gd = 1000.0 * 0.5 / sd[k], gtd = 10.0 * ts[k] * 0.5 / std_[k];
+    for (int i = 0; i < 3; ++i) {
+      const double gcen = cn > 0 ? 10.0 * cd[i] / cn / NT : 0.0;
+      gt[k][i] = 2.0 * gd * (tp[k][i] - (double)clst[3 * rk + i]) + gcen;
+      gg[k][i] = 2.0 * gtd * (tg[3 * k + i] - (double)tclst[3 * rk + i]) - gcen;
+    }
+  }
+  double g_fn[NT], g_sm[NT], gsm_dot = 0.0;
+  for (int k = 0; k < NT; ++k) {
+    const double gv = v[k] <= 1.0 ? -1.0 : 0.0;
+    g_fn[k] = gv * sm[k];
+    g_sm[k] = gv * fn[k];
+    gsm_dot += g_sm[k] * sm[k];
+  }
+  for (int k = 0; k < NT; ++k) g_fn[k] += -(sm[k] * (g_sm[k] - gsm_dot));
+  fe.backward(-5.0, g_fn, cp, gt, gg, gc);
+  // this lane's fingertip (selects: no dynamic register indexing)
+  double gto[3] = {0, 0, 0}, ggo[3] = {0, 0, 0}, gco = 0.0;
+#pragma unroll
+  for (int k = 0; k < NT; ++k)
+    if (k == f) {
+      for (int i = 0; i < 3; ++i) { gto[i] = gt[k][i]; ggo[i] = gg[k][i]; }
+      gco = gc[k];
+    }
+  if constexpr (FK) {
+    float fk_g[CDX_MAX_DOFS];
+    for (int i = 0; i < D; ++i) fk_g[i] = 0.f;
+    const float gpos[3] = {(float)gto[0], (float)gto[1], (float)gto[2]};
+    cdx::fk_tip_bwd<MAXD>(chain, f, q + e * D, gpos, cdx::GqAdd{fk_g});
+    for (int i = 0; i < D; ++i) {
+      float s = fk_g[i];
+      s += __shfl_xor(s, 1);
+      s += __shfl_xor(s, 2);
+      if ((i & 3) == f && on) {
+        const double d = (double)q[e * D + i] - (double)p.ref_q[i];
+        const float gq = qn > 0 ? (float)(10.0 * d / qn) : 0.f;
+        g_q[e * D + i] = gq + s;
+      }
+    }
+  }
+  if (!on) return;
+  if (g_tip)
+    for (int i = 0; i < 3; ++i) g_tip[3 * r + i] = (float)gto[i];
+  g_comp[r] = (float)gco;
+  for (int i = 0; i < 3; ++i) g_target[3 * r + i] = (float)ggo[i];
+}
+
 }  // namespace
 
 extern "C" int cdx_kin_cost(const cdx_chain* chain, const cdx_kin_params* p, int64_t E, const float* q, const float* tip,
@@ -179,13 +338,25 @@ extern "C" int cdx_kin_cost(const cdx_chain* chain, const cdx_kin_params* p, int
   hipLaunchKernelGGL((kin_cost_kernel<NT, MAXD, FK>), grid, dim3(64), 0, s, c, *p, E, q, tip, target, comp, sign1, n1, \
                      sqdist, sign2, n2, clst, tsqdist, tsign, tclst, noise, seed, loss, margin, normal, g_q, g_target,    \
                      g_comp, g_tip, T)
+#define CDX_KIN4_LAUNCH(MAXD, FK)                                                                                      \
+  hipLaunchKernelGGL((kin_cost4_kernel<MAXD, FK>), dim3((unsigned)((4 * E + 63) / 64)), dim3(64), 0, s, c, *p, E, q, tip, \
+                     target, comp, sign1, n1, sqdist, sign2, n2, clst, tsqdist, tsign, tclst, noise, seed, loss, margin,   \
+                     normal, g_q, g_target, g_comp, g_tip)
+#if defined(CDX_KIN_1LANE)  // A/B: one lane per candidate for four fingertips too (round 4)
   if (!chain && T == 4) CDX_KIN_LAUNCH(4, 8, false);
   else if (!chain) CDX_KIN_LAUNCH(0, 8, false);
   else if (T == 4 && shallow) CDX_KIN_LAUNCH(4, 8, true);
   else if (T == 4) CDX_KIN_LAUNCH(4, CDX_MAX_DEPTH, true);
+#else
+  if (!chain && T == 4) CDX_KIN4_LAUNCH(8, false);
+  else if (!chain) CDX_KIN_LAUNCH(0, 8, false);
+  else if (T == 4 && shallow) CDX_KIN4_LAUNCH(8, true);
+  else if (T == 4) CDX_KIN4_LAUNCH(CDX_MAX_DEPTH, true);
+#endif
   else if (shallow) CDX_KIN_LAUNCH(0, 8, true);
   else CDX_KIN_LAUNCH(0, CDX_MAX_DEPTH, true);
 #undef CDX_KIN_LAUNCH
+#undef CDX_KIN4_LAUNCH
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 

@@ -408,6 +408,13 @@ __device__ __forceinline__ Slab load_slab(const Slab* __restrict__ p, int64_t i)
 constexpr int REC_WORDS = sizeof(cdx::FaceRec) / 4;  // 40
 static_assert(REC_WORDS * CHUNK % (64 * 4) == 0, "a chunk's records load as whole dwordx4 per lane");
 constexpr int REC_V4 = REC_WORDS * CHUNK / (64 * 4);   // dwordx4 loads per lane per chunk (5)
+static_assert(sizeof(Slab) * CHUNK == 64 * 16, "a chunk's slabs load as one dwordx4 per lane");
+#if defined(CDX_SDF_CHUNKS_LDS)
+constexpr int NODES_LDS = 512;  // chunk nodes staged in LDS (F ≤ 16 384 faces): 2 waves per SIMD, slower (r05f)
+#else
+constexpr int NODES_LDS = 0;    // chunk nodes loaded per visited top node (the wave's share, one vector load)
+#endif
+constexpr int TOPS_LDS = 64;    // top nodes staged in LDS
 
 // (distance, face) as one unsigned 64-bit word whose order is the winner rule's: a non-negative float's
 // bits order as unsigned integers, ties then go to the smaller index.
@@ -415,28 +422,77 @@ __device__ inline unsigned long long pack_best(float d, int idx) {
   return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)idx;
 }
 
-// One workgroup per 64 Morton-sorted points: its four waves hold the same 64 points (lane = point) and split
-// the work — the greedy seed's tops / chunks / faces four ways, then the chunks of every top node some lane
-// cannot rule out (wave w takes chunks w, w + 4, … of the top) — and share each point's packed best in LDS,
-// so a face one wave evaluates tightens the bounds the others test.  Grid: ⌈P/64⌉ workgroups of 4 waves.
+// One workgroup per 64 Morton-sorted points: its NW waves hold the same 64 points (lane = point) and split
+// the work — the greedy seed's tops / chunks / faces NW ways, then the chunks of every top node some lane
+// cannot rule out (wave w takes chunks w, w + NW, … of the top) — and share each point's packed best in LDS,
+// so a face one wave evaluates tightens the bounds the others test.  Grid: ⌈P/64⌉ workgroups of NW waves.
+#ifndef CDX_SDF_NW
+#define CDX_SDF_NW 4
+#endif
+constexpr int NW = CDX_SDF_NW;     // waves per point group
+constexpr int CPW = TOPB / NW;     // chunks of a top node per wave
+static_assert(TOPB % NW == 0 && CHUNK % NW == 0, "waves split a top's chunks and a chunk's faces evenly");
+#if defined(CDX_SDF_DIAG)
+// timing-only diagnostic: per workgroup [start, end] (s_memrealtime, 100 MHz) of the last tree launch
+__device__ unsigned long long g_sdf_wgtime[65536][4];  // start, end, chunk visits, pairs (summed over waves)
+#endif
 __device__ __forceinline__ void sel_min(float& lb, int& sel, float l, int i) {
   if (l < lb || (l == lb && i < sel)) { lb = l; sel = i; }
 }
 
-__global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
+__global__ __launch_bounds__(64 * NW) void sdf_tree_kernel(
     const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
     int64_t F, const cdx::FaceRec* __restrict__ rec, const Slab* __restrict__ slab, const Node* __restrict__ chunk,
     const Node* __restrict__ top, int C, int T, const unsigned* __restrict__ ws, float* __restrict__ out_dist,
     int32_t* __restrict__ out_sign, float* __restrict__ out_nrm, float* __restrict__ out_clst,
     int32_t* __restrict__ out_face, int count) {
   if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
-  __shared__ float4 s_rec[4][REC_WORDS * CHUNK / 4];  // per wave: the visited chunk's face records
+#if defined(CDX_SDF_DIAG)
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+  __shared__ float4 s_rec[NW][REC_WORDS * CHUNK / 4];  // per wave: the visited chunk's face records
+  __shared__ float4 s_slab[NW][2 * CHUNK];             // … and its face slabs
+  __shared__ float4 s_node[3 * (NODES_LDS + TOPS_LDS)];  // chunk nodes, then top nodes (when they fit)
+  __shared__ float4 s_cn[NW][3 * CPW];                // per wave: its CPW chunk nodes of the current top node
   __shared__ unsigned long long s_best[64];           // the group's packed (distance, face) best per point
-  __shared__ unsigned short s_pair[4][128];           // per wave: pending (lane << 5 | face) pairs
-  __shared__ float s_lb[4][64];                       // greedy seed: per wave candidate bound …
-  __shared__ int s_sel[4][64];                        // … and index
+  __shared__ unsigned short s_pair[NW][128];           // per wave: pending (lane << 5 | face) pairs
+  __shared__ float s_lb[NW][64];                       // greedy seed: per wave candidate bound …
+  __shared__ int s_sel[NW][64];                        // … and index
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // the upper levels of the hierarchy in LDS: one coalesced copy per workgroup instead of a dependent load per
+  // node test (the tests then read LDS; a mesh with more nodes reads the rest from global memory)
+  const bool chunks_lds = C <= NODES_LDS, tops_lds = T <= TOPS_LDS;
+  {
+    const float4* cs = reinterpret_cast<const float4*>(chunk);
+    const float4* ts = reinterpret_cast<const float4*>(top);
+    if (chunks_lds)
+      for (int i = threadIdx.x; i < 3 * C; i += 64 * NW) s_node[i] = cs[i];
+    if (tops_lds)
+      for (int i = threadIdx.x; i < 3 * T; i += 64 * NW) s_node[3 * NODES_LDS + i] = ts[i];
+    __syncthreads();
+  }
+  // the wave's chunks of top node t are t·16 + w + NW·i, i < CPW: staged per wave (one vector load) unless all
+  // chunk nodes are in LDS; wave_chunk(t, i) then reads LDS either way
+  auto stage_chunks = [&](int t) {
+    if (chunks_lds) return;
+    if (lane < 3 * CPW) {
+      const int c = t * TOPB + w + NW * (lane / 3);
+      s_cn[w][lane] = c < C ? reinterpret_cast<const float4*>(chunk)[3 * c + lane % 3] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto wave_chunk = [&](int t, int i) {
+    if (chunks_lds) {
+      const int c = t * TOPB + w + NW * i;
+      return Node{s_node[3 * c], s_node[3 * c + 1], s_node[3 * c + 2]};
+    }
+    return Node{s_cn[w][3 * i], s_cn[w][3 * i + 1], s_cn[w][3 * i + 2]};
+  };
+  auto top_node = [&](int t) {
+    if (tops_lds) return Node{s_node[3 * (NODES_LDS + t)], s_node[3 * (NODES_LDS + t) + 1], s_node[3 * (NODES_LDS + t) + 2]};
+    return load_node(top, t);
+  };
   const int64_t j = (int64_t)blockIdx.x * 64 + lane;
   const bool live = j < P;
   const int64_t pi = porder[live ? j : P - 1];  // dead lanes shadow a live point
@@ -459,7 +515,7 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
     float m = s_lb[0][lane];
     int si = s_sel[0][lane];
 #pragma unroll
-    for (int v = 1; v < 4; ++v) sel_min(m, si, s_lb[v][lane], s_sel[v][lane]);
+    for (int v = 1; v < NW; ++v) sel_min(m, si, s_lb[v][lane], s_sel[v][lane]);
     __syncthreads();
     return si;
   };
@@ -470,7 +526,7 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
   {
     float tl = INFINITY;
     int ts = 0x7fffffff;
-    for (int t = w; t < T; t += 4) sel_min(tl, ts, node_lb(p, load_node(top, t)), t);
+    for (int t = w; t < T; t += NW) sel_min(tl, ts, node_lb(p, top_node(t)), t);
     tsel = merge(tl, ts);
     if (tsel >= T) tsel = 0;
   }
@@ -478,9 +534,16 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
   {
     float cl = INFINITY;
     int cs = 0x7fffffff;
-    for (int i = 0; i < TOPB / 4; ++i) {
-      const int c = tsel * TOPB + w + 4 * i;
-      if (c < C) sel_min(cl, cs, node_lb(p, load_node(chunk, c)), c);
+    if (!chunks_lds) {  // (a per-lane top: each lane loads its own 4 nodes)
+      for (int i = 0; i < CPW; ++i) {
+        const int c = tsel * TOPB + w + NW * i;
+        if (c < C) sel_min(cl, cs, node_lb(p, load_node(chunk, c)), c);
+      }
+    } else {
+      for (int i = 0; i < CPW; ++i) {
+        const int c = tsel * TOPB + w + NW * i;
+        if (c < C) sel_min(cl, cs, node_lb(p, Node{s_node[3 * c], s_node[3 * c + 1], s_node[3 * c + 2]}), c);
+      }
     }
     csel = merge(cl, cs);
     if (csel >= C) csel = tsel * TOPB;
@@ -488,8 +551,8 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
   {
     float fl = INFINITY;
     int fs = 0x7fffffff;
-    for (int i = 0; i < CHUNK / 4; ++i) {
-      const int64_t f = (int64_t)csel * CHUNK + w + 4 * i;
+    for (int i = 0; i < CHUNK / NW; ++i) {
+      const int64_t f = (int64_t)csel * CHUNK + w + NW * i;
       if (f < F) {
         const Slab sl = load_slab(slab, f);
         float d2;
@@ -510,13 +573,27 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
   float4* buf = s_rec[w];
   const cdx::FaceRec* rr = reinterpret_cast<const cdx::FaceRec*>(buf);
   for (int t = 0; t < T; ++t) {
-    if (!__any(node_needed(p, load_node(top, t), bsqrt(best_now()), pnorm))) continue;
-    for (int i = 0; i < TOPB / 4; ++i) {
-      const int c = t * TOPB + w + 4 * i;
+    if (!__any(node_needed(p, top_node(t), bsqrt(best_now()), pnorm))) continue;
+    stage_chunks(t);
+    for (int i = 0; i < CPW; ++i) {
+      const int c = t * TOPB + w + NW * i;
       if (c >= C) break;
-      const Node cn = load_node(chunk, c);
+      const Node cn = wave_chunk(t, i);
       const float sb = bsqrt(best_now());
       if (!__any(node_needed(p, cn, sb, pnorm))) continue;
+      // the chunk's face slabs (one dwordx4 per lane) and records (5 per lane) in flight together, into the
+      // wave's LDS buffers
+      {
+        float4 v[REC_V4];
+        const float4 sv = reinterpret_cast<const float4*>(slab)[(int64_t)c * 2 * CHUNK + lane];
+#pragma unroll
+        for (int q = 0; q < REC_V4; ++q) v[q] = rec4[(int64_t)c * (REC_WORDS * CHUNK / 4) + lane + 64 * q];
+        __builtin_amdgcn_wave_barrier();
+        s_slab[w][lane] = sv;
+#pragma unroll
+        for (int q = 0; q < REC_V4; ++q) buf[lane + 64 * q] = v[q];
+        __builtin_amdgcn_wave_barrier();
+      }
       // the chunk's faces a lane cannot rule out: slab bound against the chunk's threshold (its margins)
       const float th = node_th(cn, sb, pnorm);
       const float th2 = th * th;
@@ -524,9 +601,9 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
       unsigned lmask = 0;
 #pragma unroll 8
       for (int k = 0; k < CHUNK; ++k) {
-        const Slab sl = load_slab(slab, (int64_t)c * CHUNK + k);
+        const float4 sa = s_slab[w][2 * k], sbv = s_slab[w][2 * k + 1];
         float d2;
-        const float l2 = cyl_lb2(p, sl.a, sl.b, sl.a.w, &d2);
+        const float l2 = cyl_lb2(p, sa, sbv, sa.w, &d2);
         if (!(l2 > th2) && k < nf && live) lmask |= 1u << k;
       }
       unsigned mask = lmask;
@@ -535,16 +612,6 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
       mask = __builtin_amdgcn_readfirstlane(mask);
       if (!mask) continue;
       ++visits;
-      // the chunk's 32 face records into the wave's LDS buffer (5 dwordx4 per lane)
-      {
-        float4 v[REC_V4];
-#pragma unroll
-        for (int q = 0; q < REC_V4; ++q) v[q] = rec4[(int64_t)c * (REC_WORDS * CHUNK / 4) + lane + 64 * q];
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int q = 0; q < REC_V4; ++q) buf[lane + 64 * q] = v[q];
-        __builtin_amdgcn_wave_barrier();
-      }
       // the (lane, face) pairs, packed 64 to a round: lane i of a round evaluates pair i (its point read from
       // the owner) and folds it into the owner's packed best with an LDS 64-bit minimum (the winner order)
       auto eval_round = [&](int n) {
@@ -589,7 +656,21 @@ __global__ __launch_bounds__(SDF_BLOCK) void sdf_tree_kernel(
       atomicAdd(&g_sdf_stats[3], (unsigned long long)visits);
     }
   }
+#if defined(CDX_SDF_DIAG)
+  __shared__ unsigned s_diag[2];
+  if (threadIdx.x == 0) s_diag[0] = s_diag[1] = 0u;
   __syncthreads();
+  if (lane == 0) { atomicAdd(&s_diag[0], visits); atomicAdd(&s_diag[1], pairs); }
+#endif
+  __syncthreads();
+#if defined(CDX_SDF_DIAG)
+  if (threadIdx.x == 0 && blockIdx.x < 65536) {
+    g_sdf_wgtime[blockIdx.x][0] = t_start;
+    g_sdf_wgtime[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+    g_sdf_wgtime[blockIdx.x][2] = s_diag[0];
+    g_sdf_wgtime[blockIdx.x][3] = s_diag[1];
+  }
+#endif
   if (w != 0 || !live) return;
   const int bidx = (int)(unsigned)s_best[lane];
   const float* v = faces + 9 * (int64_t)bidx;
@@ -884,7 +965,7 @@ int mesh_query(const char* mesh, const float* faces, int64_t F, const float* poi
          hipSuccess;
   }
   if (!(flags & CDX_SDF_MESH_EXACT))
-    hipLaunchKernelGGL(sdf_tree_kernel, dim3((unsigned)((P + 63) / 64)), dim3(SDF_BLOCK), 0, s, points, P,
+    hipLaunchKernelGGL(sdf_tree_kernel, dim3((unsigned)((P + 63) / 64)), dim3(64 * NW), 0, s, points, P,
                        (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
                        reinterpret_cast<const Slab*>(mesh + mesh_slab_off(C)),
                        reinterpret_cast<const Node*>(mesh + mesh_chunk_off(C)),
@@ -983,6 +1064,17 @@ int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* 
   return mesh_query_ws(static_cast<const char*>(mesh), faces, F, points, P, sqdist, sign, normals, clst, face_idx,
                        workspace, workspace_bytes, flags, s);
 }
+
+#if defined(CDX_SDF_DIAG)
+int cdx_sdf_diag_wgtime(uint64_t* out, int64_t n, cdx_stream_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (n > 65536 || hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_sdf_wgtime), (size_t)n * 32, 0, hipMemcpyDeviceToHost, s) !=
+                       hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return CDX_ELAUNCH;
+  return CDX_OK;
+}
+#endif
 
 int cdx_sdf_chunk_visits(uint64_t* out, cdx_stream_t stream) {
   if (!out) return CDX_EINVAL;

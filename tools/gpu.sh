@@ -72,6 +72,28 @@ for STEP in "$@"; do
     sdfpmc)
       bash tools/pmc_sdf.sh "$TAG" > "$OUT/pmc_sdf_$TAG.txt" 2>&1
       rc=$?; echo "sdf pmc rc=$rc"; tail -40 "$OUT/pmc_sdf_$TAG.txt"; stop_if_fault $rc ;;
+    sdfab=*)  # TorchSDF forward of the config-4 queries for each library: sdfab=base,name,... (libcdx_name.so)
+      IFS=, read -r -a LIBS <<< "${STEP#sdfab=}"
+      for r in $(seq 1 "${R:-2}"); do
+        for L in "${LIBS[@]}"; do
+          for K in around far; do
+            if [ "$L" = base ]; then LP=$ROOT/compliancedex_amd/lib/libcdx.so; else LP=$ROOT/compliancedex_amd/lib/libcdx_$L.so; fi
+            CDX_LIB=$LP timeout -k 10 120 python3 tools/sdf_child.py 6 $K > "$OUT/sdfab_run_$TAG.log" 2>&1
+            rc=$?; [ $rc -ne 0 ] && { echo "$L rc=$rc"; tail -5 "$OUT/sdfab_run_$TAG.log"; exit $rc; }
+            echo "{\"lib\": \"$L\", \"round\": $r, \"res\": $(grep '^{' "$OUT/sdfab_run_$TAG.log" | tail -1)}" | tee -a "$OUT/sdfab_$TAG.jsonl"
+          done
+        done
+      done ;;
+    c4ab=*)  # the fused config-4 Kin loop for each library: c4ab=base,name,...
+      IFS=, read -r -a LIBS <<< "${STEP#c4ab=}"
+      for r in $(seq 1 "${R:-2}"); do
+        for L in "${LIBS[@]}"; do
+          if [ "$L" = base ]; then LP=$ROOT/compliancedex_amd/lib/libcdx.so; else LP=$ROOT/compliancedex_amd/lib/libcdx_$L.so; fi
+          CDX_LIB=$LP timeout -k 10 200 python3 tools/c4_kin.py 20 3 > "$OUT/c4ab_run_$TAG.log" 2>&1
+          rc=$?; [ $rc -ne 0 ] && { echo "$L rc=$rc"; tail -5 "$OUT/c4ab_run_$TAG.log"; exit $rc; }
+          grep '^{' "$OUT/c4ab_run_$TAG.log" | python3 -c "import json,sys; [print(json.dumps({'lib': '$L', 'round': $r, 'case': d['case'], 'min_ms': d['min_ms'], 'pairs_per_point': d['pairs_per_point']})) for d in map(json.loads, sys.stdin)]" | tee -a "$OUT/c4ab_$TAG.jsonl"
+        done
+      done ;;
     configs)
       timeout -k 10 600 python -u tools/bench_configs.py > "$OUT/configs_$TAG.jsonl" 2> "$OUT/configs_$TAG.log"
       rc=$?; echo "configs rc=$rc"; tail -c 3000 "$OUT/configs_$TAG.jsonl"; stop_if_fault $rc ;;
