@@ -151,6 +151,123 @@ __device__ __forceinline__ void mean_tps_moments(const cdx_gpis& g, int64_t M, i
   }
 }
 
+// Register-blocked TPS moment form (A/B switch CDX_MEAN_QPT > 1, off): each thread carries MQ_QPT queries, so
+// one LDS read of a staged point serves MQ_QPT pairs; MQ_SPLIT lanes share a query group's points.  Same staging,
+// moments and epilogue as mean_tps_moments.  Measured slower in the closure (round 5, profiles/r05i_*: the
+// mean 85 → 92 µs at 4 queries per thread, 90 µs at 2): the loop is f64-VALU-bound, not LDS-bound, and the
+// extra accumulators cost occupancy.
+#ifndef CDX_MEAN_QPT
+#define CDX_MEAN_QPT 1
+#endif
+#ifndef CDX_MEAN_QSPLIT
+#define CDX_MEAN_QSPLIT 16
+#endif
+constexpr int MQ_QPT = CDX_MEAN_QPT, MQ_SPLIT = CDX_MEAN_QSPLIT;
+constexpr int MQ_PER_WG = (MEAN_BLOCK / MQ_SPLIT) * MQ_QPT;  // queries per workgroup
+__global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_tps_blocked_kernel(cdx_gpis g, const double* __restrict__ X,
+                                                                           int64_t M, double* __restrict__ mean,
+                                                                           double* __restrict__ gmean,
+                                                                           double* __restrict__ normal) {
+  __shared__ dbl4 sp[MEAN_BLOCK];
+  const int tid = threadIdx.x;
+  const int split = tid % MQ_SPLIT;
+  const int64_t m0 = ((int64_t)blockIdx.x * (MEAN_BLOCK / MQ_SPLIT) + tid / MQ_SPLIT) * MQ_QPT;
+  double xq[MQ_QPT][3];
+#pragma unroll
+  for (int q = 0; q < MQ_QPT; ++q) {
+    const int64_t m = m0 + q;
+    for (int i = 0; i < 3; ++i) xq[q][i] = m < M ? X[3 * m + i] : 0.0;
+  }
+  const double c0 = g.X1[0], c1 = g.X1[1], c2 = g.X1[2];
+  double a3[MQ_QPT], h0[MQ_QPT], h1[MQ_QPT], h2[MQ_QPT];
+#pragma unroll
+  for (int q = 0; q < MQ_QPT; ++q) a3[q] = h0[q] = h1[q] = h2[q] = 0.0;
+  double s0 = 0, s1x = 0, s1y = 0, s1z = 0, s2 = 0;
+  for (int j0 = 0; j0 < g.N; j0 += MEAN_BLOCK) {
+    const int j = j0 + tid;
+    __syncthreads();
+    dbl4 v;
+    if (j < g.N) {
+      v.x = g.X1[3 * j]; v.y = g.X1[3 * j + 1]; v.z = g.X1[3 * j + 2]; v.w = g.alpha[j];
+      const double px = v.x - c0, py = v.y - c1, pz = v.z - c2;
+      s0 += v.w;
+      s1x += v.w * px; s1y += v.w * py; s1z += v.w * pz;
+      s2 += v.w * (px * px + py * py + pz * pz);
+    } else {
+      v.x = xq[0][0] + 1.0; v.y = v.z = 0.0; v.w = 0.0;  // any finite point; α = 0
+    }
+    sp[tid] = v;
+    __syncthreads();
+#pragma unroll 2
+    for (int jj = split; jj < MEAN_BLOCK; jj += MQ_SPLIT) {
+      const dbl4 p = sp[jj];
+#pragma unroll
+      for (int q = 0; q < MQ_QPT; ++q) {
+        const double dx = xq[q][0] - p.x, dy = xq[q][1] - p.y, dz = xq[q][2] - p.z;
+        const double r2 = dx * dx + dy * dy + dz * dz;
+#if defined(CDX_MEAN_RSQ32)
+        const double ar = p.w * cdx::sqrt_r2_f32seed(r2);
+#else
+        const double ar = p.w * cdx::sqrt_r2_gen(r2);
+#endif
+        a3[q] += ar * r2;
+        h0[q] += ar * dx;
+        h1[q] += ar * dy;
+        h2[q] += ar * dz;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MQ_QPT; ++q)
+#pragma unroll
+    for (int w = 1; w < MQ_SPLIT; w <<= 1) {
+      a3[q] += __shfl_xor(a3[q], w);
+      h0[q] += __shfl_xor(h0[q], w);
+      h1[q] += __shfl_xor(h1[q], w);
+      h2[q] += __shfl_xor(h2[q], w);
+    }
+#pragma unroll
+  for (int w = 1; w < 64; w <<= 1) {
+    s0 += __shfl_xor(s0, w);
+    s1x += __shfl_xor(s1x, w);
+    s1y += __shfl_xor(s1y, w);
+    s1z += __shfl_xor(s1z, w);
+    s2 += __shfl_xor(s2, w);
+  }
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(sp);
+  const int wave = tid >> 6;
+  if ((tid & 63) == 0) {
+    red[wave * 5 + 0] = s0; red[wave * 5 + 1] = s1x; red[wave * 5 + 2] = s1y; red[wave * 5 + 3] = s1z;
+    red[wave * 5 + 4] = s2;
+  }
+  __syncthreads();
+  s0 = s1x = s1y = s1z = s2 = 0;
+#pragma unroll
+  for (int w = 0; w < MEAN_BLOCK / 64; ++w) {
+    s0 += red[w * 5 + 0]; s1x += red[w * 5 + 1]; s1y += red[w * 5 + 2]; s1z += red[w * 5 + 3];
+    s2 += red[w * 5 + 4];
+  }
+  if (split != 0) return;
+  const double R = g.R;
+#pragma unroll
+  for (int q = 0; q < MQ_QPT; ++q) {
+    const int64_t m = m0 + q;
+    if (m >= M) break;
+    const double qx = xq[q][0] - c0, qy = xq[q][1] - c1, qz = xq[q][2] - c2;
+    const double sr2 = (qx * qx + qy * qy + qz * qz) * s0 - 2.0 * (qx * s1x + qy * s1y + qz * s1z) + s2;
+    mean[m] = 2.0 * a3[q] - 3.0 * R * sr2 + R * R * R * s0 + g.bias;
+    const double gx = 6.0 * h0[q] - 6.0 * R * (qx * s0 - s1x);
+    const double gy = 6.0 * h1[q] - 6.0 * R * (qy * s0 - s1y);
+    const double gz = 6.0 * h2[q] - 6.0 * R * (qz * s0 - s1z);
+    if (gmean) { gmean[3 * m] = gx; gmean[3 * m + 1] = gy; gmean[3 * m + 2] = gz; }
+    if (normal) {
+      const double nn = sqrt(gx * gx + gy * gy + gz * gz) + 1e-8;
+      normal[3 * m] = gx / nn; normal[3 * m + 1] = gy / nn; normal[3 * m + 2] = gz / nn;
+    }
+  }
+}
+
 template <int KT>
 __global__ __launch_bounds__(MEAN_BLOCK) void gpis_mean_kernel(cdx_gpis g, const double* __restrict__ X, int64_t M,
                                                                double* __restrict__ mean, double* __restrict__ gmean,
@@ -1570,7 +1687,14 @@ int cdx_gpis_mean(const cdx_gpis* g, const double* X, int64_t M, double* mean, d
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   cdx::prof_mark(cdx::PROF_GPIS_MEAN, true, s);
   switch (g->kernel) {
-    case CDX_KERNEL_TPS: hipLaunchKernelGGL(gpis_mean_kernel<CDX_KERNEL_TPS>, grid, dim3(MEAN_BLOCK), 0, s, *g, X, M, mean, grad_mean, normal); break;
+    case CDX_KERNEL_TPS:
+#if !defined(CDX_MEAN_DIRECT) && CDX_MEAN_QPT > 1
+      hipLaunchKernelGGL(gpis_mean_tps_blocked_kernel, dim3((unsigned)((M + MQ_PER_WG - 1) / MQ_PER_WG)), dim3(MEAN_BLOCK), 0, s,
+                         *g, X, M, mean, grad_mean, normal);
+#else
+      hipLaunchKernelGGL(gpis_mean_kernel<CDX_KERNEL_TPS>, grid, dim3(MEAN_BLOCK), 0, s, *g, X, M, mean, grad_mean, normal);
+#endif
+      break;
     case CDX_KERNEL_RBF: hipLaunchKernelGGL(gpis_mean_kernel<CDX_KERNEL_RBF>, grid, dim3(MEAN_BLOCK), 0, s, *g, X, M, mean, grad_mean, normal); break;
     default: hipLaunchKernelGGL(gpis_mean_kernel<CDX_KERNEL_JOINT>, grid, dim3(MEAN_BLOCK), 0, s, *g, X, M, mean, grad_mean, normal); break;
   }

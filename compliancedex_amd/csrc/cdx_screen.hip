@@ -627,10 +627,14 @@ __global__ __launch_bounds__(CB_GROUPS) void screen_count_kernel(int64_t G, int 
   __shared__ int red[4], s_cut;
   __shared__ unsigned s_zmin[4];
   const int t = threadIdx.x, lane = t & 63;
-  if (A > 0) {
-    int v = 0;
-    for (int b = 0; b < nsel; ++b) v += hist[(int64_t)b * cdx::AUDIT_BINS + t];
-    s_hist[t] = v;
+  if (A > 0) {  // (eight independent loads in flight per step: the sum is latency-bound, not bandwidth-bound)
+    int v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int b = 0;
+    for (; b + 8 <= nsel; b += 8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] += hist[(int64_t)(b + u) * cdx::AUDIT_BINS + t];
+    for (; b < nsel; ++b) v[0] += hist[(int64_t)b * cdx::AUDIT_BINS + t];
+    s_hist[t] = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
   }
   if (t == 0) s_cut = A > 0 ? cdx::AUDIT_BINS : 0;
   __syncthreads();
