@@ -3,8 +3,8 @@
 // brute-force scan (unbatched_triangle_distance_cuda.cu:186-246) and to oracle/sdf_oracle.c.
 //
 // Culled path (meshes without NaN-capable faces, the normal case), round 5:
-//   * a mesh is a two-level hierarchy over its faces in a spatially compact order: 32-face chunks
-//     (leaves), 16 chunks to a top node.  Prepared meshes (cdx_sdf_mesh_prepare, queried every
+//   * a mesh is a three-level hierarchy over its faces in a spatially compact order: 8-face runs, 32-face
+//     chunks (4 runs), 16 chunks to a top node.  Prepared meshes (cdx_sdf_mesh_prepare, queried every
 //     iteration by the SDF/Kin optimisers) take the order of a median-split k-d tree on the face
 //     centroids, built on the host once (chunk radius 5.3 mm median on the 16 384-face banana, against
 //     10.5 mm for the round-4 Morton chunks — tools/sdf_cull_sim.py); the one-shot cdx_sdf_forward
@@ -17,10 +17,14 @@
 //     rounded outward.
 //   * one wave per 64 points (Morton-sorted in the points' own cubic frame): each lane first descends
 //     greedily (nearest top node → nearest chunk → face of smallest slab bound) and evaluates that one
-//     face, which gives it a near-final best; then the wave walks the top nodes and chunks some lane
-//     cannot rule out, tests the chunk's 32 slab bounds per lane, and evaluates only the (lane, face)
-//     pairs a lane needs, packed 64 to a round (ballot/mbcnt into LDS, an LDS 64-bit minimum on
-//     (distance bits, face index) into the owner's best).
+//     face, which gives it a near-final best; the top nodes some lane cannot rule out against those seeds
+//     are tested once per workgroup (waves split them, an LDS mask); then each wave walks those top nodes
+//     and the chunks some lane cannot rule out, tests the chunk's run nodes and, inside the runs some lane
+//     needs, the faces' slab bounds per lane, and evaluates only the (lane, face) pairs a lane needs,
+//     packed 64 to a round (ballot/mbcnt into LDS, an LDS 64-bit minimum on (distance bits, face index)
+//     into the owner's best).  Runs and the shared top mask: config-4 forward 0.71 → 0.61 ms (points
+//     around the mesh) and 0.775 → 0.725 ms (far), CDX_SDF_NO_RUNS / CDX_SDF_NO_TMASK build the A/B
+//     (profiles/r05l_sdf_runs_tmask_ab.jsonl).
 // A skip needs bound·(1 − α) − β > sqrt(best): α = 1e-4 + 1e-5·κ (κ = the worst face's 1/sinθ in the
 // node; α ≥ 1 or a NaN κ never skips) and β = (1e-4 + 1e-8·κ)·(|p| + |c| + 3R) exceed every rounding error
 // of point_face and of the bound (tests/test_sdf_bounds_cpu.py), so a skipped face's computed
@@ -47,6 +51,8 @@ constexpr int SDF_BLOCK = 256;
 constexpr int SDF_TILE = CDX_SDF_REF_TILE;
 constexpr int CHUNK = 32;           // faces per chunk (leaf node)
 constexpr int TOPB = 16;            // chunks per top node
+constexpr int RUN = 8;              // faces per run (a chunk's sub-group with its own node)
+constexpr int RPC = 32 / RUN;       // runs per chunk
 constexpr float PT_LIM = 1e4f;      // |p| bound of the culled path (face_may_nan's premise)
 
 // Bounding volume of a node: a = (centre xyz, ball radius R), b = (cylinder axis xyz, half-thickness t),
@@ -443,7 +449,8 @@ __device__ __forceinline__ void sel_min(float& lb, int& sel, float l, int i) {
 __global__ __launch_bounds__(64 * NW) void sdf_tree_kernel(
     const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
     int64_t F, const cdx::FaceRec* __restrict__ rec, const Slab* __restrict__ slab, const Node* __restrict__ chunk,
-    const Node* __restrict__ top, int C, int T, const unsigned* __restrict__ ws, float* __restrict__ out_dist,
+    const Node* __restrict__ top, const Node* __restrict__ run, int C, int T, const unsigned* __restrict__ ws,
+    float* __restrict__ out_dist,
     int32_t* __restrict__ out_sign, float* __restrict__ out_nrm, float* __restrict__ out_clst,
     int32_t* __restrict__ out_face, int count) {
   if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
@@ -452,6 +459,8 @@ __global__ __launch_bounds__(64 * NW) void sdf_tree_kernel(
 #endif
   __shared__ float4 s_rec[NW][REC_WORDS * CHUNK / 4];  // per wave: the visited chunk's face records
   __shared__ float4 s_slab[NW][2 * CHUNK];             // … and its face slabs
+  __shared__ float4 s_run[NW][3 * RPC];               // … and its runs' nodes
+  __shared__ unsigned long long s_tmask;              // top nodes some lane cannot rule out (T ≤ 64)
   __shared__ float4 s_node[3 * (NODES_LDS + TOPS_LDS)];  // chunk nodes, then top nodes (when they fit)
   __shared__ float4 s_cn[NW][3 * CPW];                // per wave: its CPW chunk nodes of the current top node
   __shared__ unsigned long long s_best[64];           // the group's packed (distance, face) best per point
@@ -572,7 +581,24 @@ __global__ __launch_bounds__(64 * NW) void sdf_tree_kernel(
   const float4* rec4 = reinterpret_cast<const float4*>(rec);
   float4* buf = s_rec[w];
   const cdx::FaceRec* rr = reinterpret_cast<const cdx::FaceRec*>(buf);
+  // the top nodes some lane cannot rule out against the seeds, tested once per workgroup (waves split them) when
+  // they fit one mask word; each is re-tested against the current best before its chunks are walked
+#if defined(CDX_SDF_NO_TMASK)
+  const bool shared_tops = false;
+#else
+  const bool shared_tops = tops_lds && T <= 64;
+#endif
+  if (shared_tops) {
+    if (threadIdx.x == 0) s_tmask = 0ull;
+    __syncthreads();
+    const float sb0 = bsqrt(best_now());
+    for (int t = w; t < T; t += NW)
+      if (__any(node_needed(p, top_node(t), sb0, pnorm)) && lane == 0) atomicOr(&s_tmask, 1ull << t);
+    __syncthreads();
+  }
+  const unsigned long long tmask = shared_tops ? s_tmask : ~0ull;
   for (int t = 0; t < T; ++t) {
+    if (shared_tops && !((tmask >> t) & 1ull)) continue;
     if (!__any(node_needed(p, top_node(t), bsqrt(best_now()), pnorm))) continue;
     stage_chunks(t);
     for (int i = 0; i < CPW; ++i) {
@@ -586,25 +612,38 @@ __global__ __launch_bounds__(64 * NW) void sdf_tree_kernel(
       {
         float4 v[REC_V4];
         const float4 sv = reinterpret_cast<const float4*>(slab)[(int64_t)c * 2 * CHUNK + lane];
+        const float4 rv = lane < 3 * RPC ? reinterpret_cast<const float4*>(run)[(int64_t)c * 3 * RPC + lane]
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int q = 0; q < REC_V4; ++q) v[q] = rec4[(int64_t)c * (REC_WORDS * CHUNK / 4) + lane + 64 * q];
         __builtin_amdgcn_wave_barrier();
         s_slab[w][lane] = sv;
+        if (lane < 3 * RPC) s_run[w][lane] = rv;
 #pragma unroll
         for (int q = 0; q < REC_V4; ++q) buf[lane + 64 * q] = v[q];
         __builtin_amdgcn_wave_barrier();
       }
-      // the chunk's faces a lane cannot rule out: slab bound against the chunk's threshold (its margins)
+      // the chunk's faces a lane cannot rule out: the runs first (their own nodes), then the slab bound of each
+      // face of a run some lane needs, against the chunk's threshold (its margins)
       const float th = node_th(cn, sb, pnorm);
       const float th2 = th * th;
       const int nf = (int)min((int64_t)CHUNK, F - (int64_t)c * CHUNK);
       unsigned lmask = 0;
-#pragma unroll 8
-      for (int k = 0; k < CHUNK; ++k) {
-        const float4 sa = s_slab[w][2 * k], sbv = s_slab[w][2 * k + 1];
-        float d2;
-        const float l2 = cyl_lb2(p, sa, sbv, sa.w, &d2);
-        if (!(l2 > th2) && k < nf && live) lmask |= 1u << k;
+#pragma unroll
+      for (int rr = 0; rr < RPC; ++rr) {
+        if (rr * RUN >= nf) break;
+#if !defined(CDX_SDF_NO_RUNS)
+        const Node rn = Node{s_run[w][3 * rr], s_run[w][3 * rr + 1], s_run[w][3 * rr + 2]};
+        if (!__any(node_needed(p, rn, sb, pnorm))) continue;
+#endif
+#pragma unroll
+        for (int kk = 0; kk < RUN; ++kk) {
+          const int k = RUN * rr + kk;
+          const float4 sa = s_slab[w][2 * k], sbv = s_slab[w][2 * k + 1];
+          float d2;
+          const float l2 = cyl_lb2(p, sa, sbv, sa.w, &d2);
+          if (!(l2 > th2) && k < nf && live) lmask |= 1u << k;
+        }
       }
       unsigned mask = lmask;
 #pragma unroll
@@ -811,14 +850,16 @@ int sdf_mode() {  // CDX_SDF_MODE=exact forces the brute-force kernel (benchmark
 // Mesh: [header words: frame keys ×6, may-NaN flag, 0][face records: C·CHUNK FaceRec][slabs: C·CHUNK Slab]
 // [chunk nodes: C Node][top nodes: T Node], C = ⌈F/32⌉, T = ⌈C/16⌉, faces in the build's order.
 int64_t n_chunks(int64_t F) { return (F + CHUNK - 1) / CHUNK; }
+// (runs: RUN-face groups of a chunk, RPC per chunk, each with its own node — tested before the run's faces)
 int64_t n_tops(int64_t F) { return (n_chunks(F) + TOPB - 1) / TOPB; }
 size_t mesh_rec_off() { return align256(8 * sizeof(unsigned)); }
 size_t mesh_slab_off(int64_t C) { return mesh_rec_off() + align256((size_t)C * CHUNK * sizeof(cdx::FaceRec)); }
 size_t mesh_chunk_off(int64_t C) { return mesh_slab_off(C) + align256((size_t)C * CHUNK * sizeof(Slab)); }
 size_t mesh_top_off(int64_t C) { return mesh_chunk_off(C) + align256((size_t)C * sizeof(Node)); }
+size_t mesh_run_off(int64_t C) { return mesh_top_off(C) + align256((size_t)((C + TOPB - 1) / TOPB) * sizeof(Node)); }
 size_t mesh_bytes(int64_t F) {
   const int64_t C = n_chunks(F);
-  return mesh_top_off(C) + align256((size_t)n_tops(F) * sizeof(Node));
+  return mesh_run_off(C) + align256((size_t)C * RPC * sizeof(Node));
 }
 
 // Records, slabs and nodes of the faces in `order` (device int[F]).
@@ -832,6 +873,8 @@ void mesh_fill(const float* faces, int64_t F, const int* order, char* mesh, hipS
                      reinterpret_cast<Node*>(mesh + mesh_chunk_off(C)));
   hipLaunchKernelGGL(sdf_node_kernel, dim3((unsigned)T), dim3(64), 0, s, (const cdx::FaceRec*)rec, F, CHUNK * TOPB,
                      reinterpret_cast<Node*>(mesh + mesh_top_off(C)));
+  hipLaunchKernelGGL(sdf_node_kernel, dim3((unsigned)(C * RPC)), dim3(64), 0, s, (const cdx::FaceRec*)rec, F, RUN,
+                     reinterpret_cast<Node*>(mesh + mesh_run_off(C)));
 }
 
 // One-shot build on the device: face centroids in Morton order (10 bits per axis) of the faces' cubic frame.
@@ -864,9 +907,9 @@ int mesh_build_morton(const float* faces, int64_t F, char* mesh, hipStream_t s) 
   return ok ? CDX_OK : CDX_ELAUNCH;
 }
 
-// Face order of a median-split k-d tree on the centroids: split the longest extent of the
-// node's centroids at a left size that is a multiple of a top node (512 faces) while the node is larger than
-// one, else of a chunk (32), so every chunk and every top node is one subtree (a compact cluster).
+// Face order of a median-split k-d tree on the centroids: split the longest extent of the node's centroids at
+// a left size that is a multiple of a top node (512 faces) while the node is larger than one, else of a chunk
+// (32), else of a run (8), so every run, chunk and top node is one subtree (a compact cluster).
 void kd_order(const std::vector<float>& cen, std::vector<int>& idx) {
   struct Range { int lo, hi; };
   std::vector<Range> stack{{0, (int)idx.size()}};
@@ -874,7 +917,7 @@ void kd_order(const std::vector<float>& cen, std::vector<int>& idx) {
     const Range r = stack.back();
     stack.pop_back();
     const int n = r.hi - r.lo;
-    if (n <= CHUNK) continue;
+    if (n <= RUN) continue;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = r.lo; i < r.hi; ++i)
       for (int c = 0; c < 3; ++c) {
@@ -885,7 +928,7 @@ void kd_order(const std::vector<float>& cen, std::vector<int>& idx) {
     int ax = 0;
     for (int c = 1; c < 3; ++c)
       if (hi[c] - lo[c] > hi[ax] - lo[ax]) ax = c;
-    const int unit = n > CHUNK * TOPB ? CHUNK * TOPB : CHUNK;
+    const int unit = n > CHUNK * TOPB ? CHUNK * TOPB : (n > CHUNK ? CHUNK : RUN);
     const int half = std::min(((n + 1) / 2 + unit - 1) / unit * unit, n - 1);
     std::nth_element(idx.begin() + r.lo, idx.begin() + r.lo + half, idx.begin() + r.hi, [&](int a, int b) {
       const float ka = cen[3 * (size_t)a + ax], kb = cen[3 * (size_t)b + ax];
@@ -969,7 +1012,8 @@ int mesh_query(const char* mesh, const float* faces, int64_t F, const float* poi
                        (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
                        reinterpret_cast<const Slab*>(mesh + mesh_slab_off(C)),
                        reinterpret_cast<const Node*>(mesh + mesh_chunk_off(C)),
-                       reinterpret_cast<const Node*>(mesh + mesh_top_off(C)), (int)C, (int)T, mws, sqdist, sign,
+                       reinterpret_cast<const Node*>(mesh + mesh_top_off(C)),
+                       reinterpret_cast<const Node*>(mesh + mesh_run_off(C)), (int)C, (int)T, mws, sqdist, sign,
                        normals, clst, face_idx, (int)g_sdf_count);
   if (!(flags & CDX_SDF_MESH_CULLED))
     hipLaunchKernelGGL(sdf_exact_kernel, dim3((unsigned)((P + SDF_BLOCK - 1) / SDF_BLOCK)), dim3(SDF_BLOCK), 0, s,

@@ -142,7 +142,7 @@ def _node(faces):
 
 def test_node_cylinder_bound_premise():
     """Every face of a node against the node's cylinder ∩ ball bound with the node's margins (the largest α of
-    its faces, β = 1e-4·(|p| + |c| + 3R)): groups of 32 and 512 faces of the banana mesh in k-d order, points
+    its faces, β = 1e-4·(|p| + |c| + 3R)): groups of 8, 32 and 512 faces of the banana mesh in k-d order, points
     around and far from the mesh."""
     import os
     from compliancedex_amd.workloads import DATA
@@ -151,7 +151,7 @@ def test_node_cylinder_bound_premise():
     order = np.argsort(faces.mean(1)[:, 1], kind="stable")  # slabs along the banana's long axis
     lo, hi = faces.reshape(-1, 3).min(0), faces.reshape(-1, 3).max(0)
     pts = (lo - 2.0 * (hi - lo) + 5.0 * (hi - lo) * rng.random((4000, 3))).astype(F32)
-    for size in (32, 512):
+    for size in (8, 32, 512):
         for k in range(0, 8 * size, size):
             grp = faces[order[k * 3:k * 3 + size]]
             c, a, t, rc, R = _node(grp)

@@ -46,18 +46,18 @@ for STEP in "$@"; do
       rc=$?; echo "bench rc=$rc"; tail -c 3000 "$OUT/bench_$TAG.log"; stop_if_fault $rc ;;
     trace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
-        python3 "$ROOT/bench.py" --steps 30 --warmup 20 --no-cpu-baseline > "$OUT/rocprof_$TAG.log" 2>&1
+        python3 "$ROOT/bench.py" --steps 30 --warmup 20 --no-cpu-baseline --no-config4 > "$OUT/rocprof_$TAG.log" 2>&1
       rc=$?; echo "rocprof rc=$rc"; tail -2 "$OUT/rocprof_$TAG.log"; stop_if_fault $rc ;;
     pmc)
       for C in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${C}_$TAG" -o run -- \
-          python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_${C}_$TAG.log" 2>&1
+          python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-config4 > "$OUT/pmc_${C}_$TAG.log" 2>&1
         rc=$?; echo "pmc $C rc=$rc"; stop_if_fault $rc
       done ;;
     mfma)
       timeout -k 10 -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA \
         SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_mfma_$TAG" -o run -- \
-        python3 "$ROOT/bench.py" --steps 3 --warmup 2 --no-cpu-baseline > "$OUT/pmc_mfma_$TAG.log" 2>&1
+        python3 "$ROOT/bench.py" --steps 3 --warmup 2 --no-cpu-baseline --no-config4 > "$OUT/pmc_mfma_$TAG.log" 2>&1
       rc=$?; echo "pmc mfma rc=$rc"; stop_if_fault $rc ;;
     timeline)
       python3 tools/closure_timeline.py "$OUT/prof_$TAG/run_kernel_trace.csv" > "$OUT/closure_timeline_$TAG.txt" 2>&1
@@ -107,7 +107,7 @@ for STEP in "$@"; do
             if [ -n "$ENVS" ]; then for kv in ${ENVS//+/ }; do export "$kv"; done; fi
             if [ "$L" = base ]; then export CDX_LIB=$ROOT/compliancedex_amd/lib/libcdx.so
             else export CDX_LIB=$ROOT/compliancedex_amd/lib/libcdx_$L.so; fi
-            timeout -k 10 200 python3 "$ROOT/bench.py" --steps "$STEPS" --warmup "$WARMUP" --no-cpu-baseline \
+            timeout -k 10 200 python3 "$ROOT/bench.py" --steps "$STEPS" --warmup "$WARMUP" --no-cpu-baseline --no-config4 \
               > "$OUT/ab_run_$TAG.log" 2>&1
           )
           rc=$?; [ $rc -ne 0 ] && { echo "$SPEC rc=$rc"; tail -5 "$OUT/ab_run_$TAG.log"; exit $rc; }
