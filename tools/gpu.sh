@@ -94,6 +94,14 @@ for STEP in "$@"; do
           grep '^{' "$OUT/c4ab_run_$TAG.log" | python3 -c "import json,sys; [print(json.dumps({'lib': '$L', 'round': $r, 'case': d['case'], 'min_ms': d['min_ms'], 'pairs_per_point': d['pairs_per_point']})) for d in map(json.loads, sys.stdin)]" | tee -a "$OUT/c4ab_$TAG.jsonl"
         done
       done ;;
+    digest=*)  # config-2 closure output digests per library (bit-identity across builds): digest=base,name,...
+      IFS=, read -r -a LIBS <<< "${STEP#digest=}"
+      for L in "${LIBS[@]}"; do
+        if [ "$L" = base ]; then LP=$ROOT/compliancedex_amd/lib/libcdx.so; else LP=$ROOT/compliancedex_amd/lib/libcdx_$L.so; fi
+        CDX_LIB=$LP timeout -k 10 120 python3 tools/closure_digest.py 3 > "$OUT/digest_run_$TAG.log" 2>&1
+        rc=$?; [ $rc -ne 0 ] && { echo "$L rc=$rc"; tail -5 "$OUT/digest_run_$TAG.log"; exit $rc; }
+        grep '^{' "$OUT/digest_run_$TAG.log" | tail -1 | tee -a "$OUT/digest_$TAG.jsonl"
+      done ;;
     configs)
       timeout -k 10 600 python -u tools/bench_configs.py > "$OUT/configs_$TAG.jsonl" 2> "$OUT/configs_$TAG.log"
       rc=$?; echo "configs rc=$rc"; tail -c 3000 "$OUT/configs_$TAG.jsonl"; stop_if_fault $rc ;;
