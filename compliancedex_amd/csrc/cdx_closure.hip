@@ -635,16 +635,16 @@ int mean_sched() {
   }();
   return m;
 }
-// The side stream runs mean A before the Kabsch records (round 4 default; CDX_MEAN_FIRST=0: records
-// first): the mean starts right after the screen, in the window of the latency-bound selection and
-// compaction, instead of 25 µs later, and the refine pass then shares the chip with less of it.  With the
-// side stream at normal priority (below): 1.013 vs 1.036 ms per closure over 4 interleaved rounds
-// (profiles/r04q_ab_mean_first_side_prio.jsonl; at the highest priority the mean's workgroups also take
-// the CUs the one-workgroup compaction needs: −4 µs only, r04p).
+// Order on the side stream (CDX_MEAN_FIRST): 0 (round 5 default) the Kabsch records, then mean A; 1 mean A
+// first (round 4's default, with the one-workgroup compaction: the mean then started in the window of the
+// latency-bound selection and compaction, 1.013 vs 1.036 ms, profiles/r04q_ab_mean_first_side_prio.jsonl).
+// With the compaction spread over the chip (screen_count / screen_place kernels, round 5) the mean's
+// workgroups arriving first stretch those two kernels instead: records first measured 0.984–0.989 vs
+// 0.996–0.998 ms per closure over 3 interleaved rounds (profiles/r05n_ab_side_order.jsonl).
 bool mean_first() {
   static const bool on = [] {
     const char* e = getenv("CDX_MEAN_FIRST");
-    return !e || atoi(e) != 0;
+    return e && atoi(e) != 0;
   }();
   return on;
 }
