@@ -403,7 +403,7 @@ def main():
                                  "(informational)"},
             "step_ms": ({"min": min(step_ms), "median": statistics.median(step_ms), "max": max(step_ms),
                          "first5_mean": statistics.fmean(step_ms[:5]), "last5_mean": statistics.fmean(step_ms[-5:]),
-                         "steps_marked": len(step_ms),
+                         "steps_marked": len(step_ms), **({"all": step_ms} if mode == "all" else {}),
                          "note": "rank 0's stream time of the first and last 5 timed steps (HIP events between "
                                  "them): the clock ramp shows as first5_mean > last5_mean"} if step_ms else None),
             "native": N.build_info(),
