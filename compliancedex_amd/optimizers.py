@@ -17,6 +17,8 @@ of scope.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -114,6 +116,8 @@ class _FusedLoop:
         f32 = dict(dtype=torch.float32, device=dev)
         self.mesh, self.mesh_def = PreparedMesh(faces), PreparedMesh(faces_deflate)
         self.ws_tips, self.ws_tgt = QueryWorkspace(), QueryWorkspace()
+        self.iteration = 0
+        self.resort = max(1, int(os.environ.get("CDX_SDF_RESORT", "4")))  # iterations per point sort (A/B: 1)
         self.pose, self.target, self.comp = pose, target, comp
         self.loss = torch.empty(E, dtype=torch.float64, device=dev)
         self.margin = [torch.zeros(E, T, dtype=torch.float64, device=dev) for _ in range(2)]
@@ -140,10 +144,15 @@ class _FusedLoop:
         self.buffers = b
 
     def queries(self, tips, target):
-        """The iteration's three TorchSDF calls (:186-188); the fingertips are sorted once for both meshes."""
-        _, sign1, n1, _, _ = self.mesh_def.query(tips, workspace=self.ws_tips)
+        """The iteration's three TorchSDF calls (:186-188).  The fingertips are sorted once for both meshes, and the
+        fingertips' and targets' orders are re-sorted only every ``resort`` iterations: a query's results do not
+        depend on the order its points are walked in (each point's winner is exact), only the culling's speed does,
+        and the points move little between iterations."""
+        fresh = self.iteration % self.resort == 0
+        self.iteration += 1
+        _, sign1, n1, _, _ = self.mesh_def.query(tips, workspace=self.ws_tips, reuse_order=not fresh)
         dist, sign2, n2, clst, _ = self.mesh.query(tips, workspace=self.ws_tips, reuse_order=True)
-        tdist, tsign, _, tclst, _ = self.mesh.query(target.view(-1, 3), workspace=self.ws_tgt)
+        tdist, tsign, _, tclst, _ = self.mesh.query(target.view(-1, 3), workspace=self.ws_tgt, reuse_order=not fresh)
         return sign1, n1, dist, sign2, n2, clst, tdist, tsign, tclst
 
     def best(self):

@@ -68,8 +68,10 @@ class PreparedMesh:
 
     def query(self, points, want_face=False, workspace=None, reuse_order=False):
         """(sqdist, sign, normals, clst, face | None) of float32 points [P, 3] (cdx_sdf_query).  ``workspace``: a
-        QueryWorkspace to sort the points in (default: the mesh's own); ``reuse_order``: the workspace's last query
-        was of these same points (another mesh may have run it) — their order is reused, not sorted again."""
+        QueryWorkspace to sort the points in (default: the mesh's own); ``reuse_order``: walk the points in the order
+        the workspace's last sort left (of P points — these same points on another mesh, or earlier positions of
+        them) instead of sorting them again.  The results are the same for any order; only the culling's speed
+        depends on how close the order keeps nearby points."""
         _check(points, self.faces)
         lib = N.load()
         points = points.detach().contiguous()
@@ -91,7 +93,8 @@ class PreparedMesh:
 
 class QueryWorkspace:
     """Scratch of cdx_sdf_query (the points' Morton sort), regrown to the largest point count seen; it keeps the
-    last sorted order, which a query of the same points on another mesh may reuse."""
+    last sorted order, which a later query of P points may reuse (the same points on another mesh, or the same
+    points moved a little — a fused loop's next iterations)."""
 
     def __init__(self):
         self.buf, self.P = None, None

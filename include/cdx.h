@@ -488,8 +488,10 @@ int cdx_sdf_backward_f64(const double* grad_dist, const double* points, const do
 size_t cdx_sdf_mesh_bytes(int64_t F);
 int cdx_sdf_mesh_prepare(const float* faces, int64_t F, void* mesh, cdx_stream_t stream);
 size_t cdx_sdf_query_workspace(int64_t P);
-/* flags of cdx_sdf_query: CDX_SDF_REUSE_ORDER — `workspace` still holds the order of these same points from the
- * previous query on it (e.g. the same fingertips against a second mesh): the points are not sorted again;
+/* flags of cdx_sdf_query: CDX_SDF_REUSE_ORDER — walk the points in the order the last sort on `workspace` left,
+ * which must have been of P points (the same fingertips against a second mesh, or the same points a few optimiser
+ * iterations earlier): the points are not sorted again.  The results do not depend on the order, only the
+ * culling's speed does;
  * CDX_SDF_MESH_CULLED / CDX_SDF_MESH_EXACT — the mesh's kind as cdx_sdf_mesh_flags read it once (no NaN-capable
  * face: the culled kernel only; else the brute-force tile rule only); without either, both kernels are launched
  * and the device picks. */

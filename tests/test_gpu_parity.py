@@ -510,6 +510,31 @@ def test_sdf_prepared_mesh_equals_one_shot_and_owns_its_faces():
     assert torch.equal(g, 2 * (pts - c))
 
 
+def test_sdf_stale_order_gives_the_same_results():
+    """CDX_SDF_REUSE_ORDER with an order sorted for OTHER points (a fused loop re-sorts its query points only every
+    few iterations): the results equal a fresh sort's bit for bit — moved points, shuffled points, and points
+    with a non-finite entry (their waves take the tile rule wherever the stale order puts them)."""
+    from compliancedex_amd import PreparedMesh
+    from compliancedex_amd.torchsdf import QueryWorkspace
+    faces = torch.from_numpy(np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))).to(DEV)
+    rng = np.random.default_rng(23)
+    lo, hi = faces.reshape(-1, 3).min(0)[0], faces.reshape(-1, 3).max(0)[0]
+    a = (lo - 0.1 + (hi - lo + 0.2) * torch.from_numpy(rng.random((8192, 3))).to(DEV).float()).contiguous()
+    moved = (a + 0.01 * torch.from_numpy(rng.standard_normal((8192, 3))).to(DEV).float()).contiguous()
+    shuffled = a[torch.from_numpy(rng.permutation(8192)).to(DEV)].contiguous()
+    bad = moved.clone()
+    bad[77] = float("nan")
+    bad[4000, 1] = 2e4
+    mesh = PreparedMesh(faces)
+    for pts in (moved, shuffled, bad):
+        ws = QueryWorkspace()
+        mesh.query(a, workspace=ws)  # sorts a
+        stale = [t.cpu().numpy() for t in mesh.query(pts, want_face=True, workspace=ws, reuse_order=True)]
+        fresh = [t.cpu().numpy() for t in mesh.query(pts, want_face=True, workspace=QueryWorkspace())]
+        for x, y in zip(stale, fresh):
+            assert _bitwise_equal_nan_aware(x, y)
+
+
 @pytest.mark.parametrize("path", SDF_PATHS)
 def test_sdf_nonfinite_points_take_exact_path(path):
     """A wave holding a NaN / inf / |p| > 1e4 point runs the reference tile rule."""
