@@ -610,17 +610,16 @@ __global__ __launch_bounds__(64 * NW) void sdf_tree_kernel(
       // the chunk's face slabs (one dwordx4 per lane) and records (5 per lane) in flight together, into the
       // wave's LDS buffers
       {
-        float4 v[REC_V4];
+        static_assert(REC_V4 == 5, "five record loads per lane");
+        const float4* rc = rec4 + (int64_t)c * (REC_WORDS * CHUNK / 4) + lane;
+        const float4 v0 = rc[0], v1 = rc[64], v2 = rc[128], v3 = rc[192], v4 = rc[256];
         const float4 sv = reinterpret_cast<const float4*>(slab)[(int64_t)c * 2 * CHUNK + lane];
         const float4 rv = lane < 3 * RPC ? reinterpret_cast<const float4*>(run)[(int64_t)c * 3 * RPC + lane]
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int q = 0; q < REC_V4; ++q) v[q] = rec4[(int64_t)c * (REC_WORDS * CHUNK / 4) + lane + 64 * q];
         __builtin_amdgcn_wave_barrier();
         s_slab[w][lane] = sv;
         if (lane < 3 * RPC) s_run[w][lane] = rv;
-#pragma unroll
-        for (int q = 0; q < REC_V4; ++q) buf[lane + 64 * q] = v[q];
+        buf[lane] = v0; buf[lane + 64] = v1; buf[lane + 128] = v2; buf[lane + 192] = v3; buf[lane + 256] = v4;
         __builtin_amdgcn_wave_barrier();
       }
       // the chunk's faces a lane cannot rule out: the runs first (their own nodes), then the slab bound of each
