@@ -987,25 +987,32 @@ bool query_ws(int64_t P, hipStream_t s, QueryWs& q) {
 // Points in Morton order of their own cubic frame (a workgroup then holds nearby points; skipped with
 // CDX_SDF_REUSE_ORDER), the tree kernel (skipped with CDX_SDF_MESH_EXACT), and the brute-force tile rule when the
 // mesh may produce NaN distances (decided on the device; skipped with CDX_SDF_MESH_CULLED).
+// The points' Morton order into workspace `base` (bbox partials, keys, an 18-bit radix sort): the order stays at
+// values + P for the tree kernel of this and later CDX_SDF_REUSE_ORDER queries.
+bool mesh_order(const float* points, int64_t P, char* base, const QueryWs& q, hipStream_t s) {
+  const int m = (int)P;
+  unsigned* part = reinterpret_cast<unsigned*>(base);
+  unsigned* pk = reinterpret_cast<unsigned*>(base + q.o_pk);
+  int* pv = reinterpret_cast<int*>(base + q.o_pv);
+  const int nb = (int)std::min<int64_t>((P + 255) / 256, BBOX_BLOCKS);
+  hipLaunchKernelGGL(sdf_bbox_kernel, dim3(nb), dim3(256), 0, s, points, P, part, (unsigned*)nullptr);
+  hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P, 0,
+                     (const unsigned*)part, nb, POINT_MB, pk, pv);
+  size_t t2 = q.tp;
+  return hipcub::DeviceRadixSort::SortPairs(base + q.o_tmp, t2, pk, pk + m, pv, pv + m, m, 0, 3 * POINT_MB, s) ==
+             hipSuccess &&
+         hipGetLastError() == hipSuccess;
+}
+
 int mesh_query(const char* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
                int32_t* sign, float* normals, float* clst, int32_t* face_idx, char* base, const QueryWs& q, int flags,
                hipStream_t s) {
   const int m = (int)P;
   const int64_t C = n_chunks(F), T = n_tops(F);
   const unsigned* mws = reinterpret_cast<const unsigned*>(mesh);
-  unsigned* part = reinterpret_cast<unsigned*>(base);
-  unsigned* pk = reinterpret_cast<unsigned*>(base + q.o_pk);
   int* pv = reinterpret_cast<int*>(base + q.o_pv);
   bool ok = true;
-  if (!(flags & CDX_SDF_REUSE_ORDER) && !(flags & CDX_SDF_MESH_EXACT)) {
-    const int nb = (int)std::min<int64_t>((P + 255) / 256, BBOX_BLOCKS);
-    hipLaunchKernelGGL(sdf_bbox_kernel, dim3(nb), dim3(256), 0, s, points, P, part, (unsigned*)nullptr);
-    hipLaunchKernelGGL(sdf_keys_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, points, P, 0,
-                       (const unsigned*)part, nb, POINT_MB, pk, pv);
-    size_t t2 = q.tp;
-    ok = hipcub::DeviceRadixSort::SortPairs(base + q.o_tmp, t2, pk, pk + m, pv, pv + m, m, 0, 3 * POINT_MB, s) ==
-         hipSuccess;
-  }
+  if (!(flags & CDX_SDF_REUSE_ORDER) && !(flags & CDX_SDF_MESH_EXACT)) ok = mesh_order(points, P, base, q, s);
   if (!(flags & CDX_SDF_MESH_EXACT))
     hipLaunchKernelGGL(sdf_tree_kernel, dim3((unsigned)((P + 63) / 64)), dim3(64 * NW), 0, s, points, P,
                        (const int*)(pv + m), faces, F, reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off()),
@@ -1118,6 +1125,17 @@ int cdx_sdf_diag_wgtime(uint64_t* out, int64_t n, cdx_stream_t stream) {
   return CDX_OK;
 }
 #endif
+
+int cdx_sdf_query_order(const float* points, int64_t P, void* workspace, size_t workspace_bytes, cdx_stream_t stream) {
+  if (P < 0 || P > INT32_MAX) return CDX_EINVAL;
+  if (P == 0) return CDX_OK;
+  if (!points || !workspace) return CDX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  QueryWs q;
+  if (!query_ws(P, s, q)) return CDX_ELAUNCH;
+  if (workspace_bytes < q.bytes) return CDX_EINVAL;
+  return mesh_order(points, P, static_cast<char*>(workspace), q, s) ? CDX_OK : CDX_ELAUNCH;
+}
 
 int cdx_sdf_chunk_visits(uint64_t* out, cdx_stream_t stream) {
   if (!out) return CDX_EINVAL;

@@ -118,6 +118,14 @@ class _FusedLoop:
         self.ws_tips, self.ws_tgt = QueryWorkspace(), QueryWorkspace()
         self.iteration = 0
         self.resort = max(1, int(os.environ.get("CDX_SDF_RESORT", "4")))  # iterations per point sort (A/B: 1)
+        # the three queries' outputs (dist, sign, normals, clst), and the two side streams the second and third
+        # query run on beside the first (CDX_SDF_CONCURRENT=0: all three on the caller's stream)
+        self.q_out = [(torch.empty(E * T, **f32), torch.empty(E * T, dtype=torch.int32, device=dev),
+                       torch.empty(E * T, 3, **f32), torch.empty(E * T, 3, **f32)) for _ in range(3)]
+        self.concurrent = os.environ.get("CDX_SDF_CONCURRENT", "1") != "0"
+        if self.concurrent:
+            self.side = [torch.cuda.Stream(device=dev) for _ in range(2)]
+            self.ev = [torch.cuda.Event() for _ in range(3)]
         self.pose, self.target, self.comp = pose, target, comp
         self.loss = torch.empty(E, dtype=torch.float64, device=dev)
         self.margin = [torch.zeros(E, T, dtype=torch.float64, device=dev) for _ in range(2)]
@@ -150,10 +158,31 @@ class _FusedLoop:
         and the points move little between iterations."""
         fresh = self.iteration % self.resort == 0
         self.iteration += 1
-        _, sign1, n1, _, _ = self.mesh_def.query(tips, workspace=self.ws_tips, reuse_order=not fresh)
-        dist, sign2, n2, clst, _ = self.mesh.query(tips, workspace=self.ws_tips, reuse_order=True)
-        tdist, tsign, _, tclst, _ = self.mesh.query(target.view(-1, 3), workspace=self.ws_tgt, reuse_order=not fresh)
-        return sign1, n1, dist, sign2, n2, clst, tdist, tsign, tclst
+        tgt = target.view(-1, 3)
+        o = self.q_out
+        if not self.concurrent:
+            self.mesh_def.query(tips, workspace=self.ws_tips, reuse_order=not fresh, out=o[0])
+            self.mesh.query(tips, workspace=self.ws_tips, reuse_order=True, out=o[1])
+            self.mesh.query(tgt, workspace=self.ws_tgt, reuse_order=not fresh, out=o[2])
+        else:
+            # The three queries are independent: each culled kernel's tail (a few point groups far from the mesh)
+            # leaves most of the chip idle, which the others fill.  Orders first, then the full mesh's two queries
+            # on the side streams and the deflated mesh's on the caller's, which waits for both before cdx_kin_cost.
+            if fresh:
+                self.ws_tips.sort(tips)
+                self.ws_tgt.sort(tgt)
+            main = torch.cuda.current_stream(tips.device)
+            self.ev[0].record(main)
+            for k, (pts, ws) in enumerate(((tips, self.ws_tips), (tgt, self.ws_tgt))):
+                st = self.side[k]
+                st.wait_event(self.ev[0])
+                with torch.cuda.stream(st):
+                    self.mesh.query(pts, workspace=ws, reuse_order=True, out=o[k + 1])
+                self.ev[k + 1].record(st)
+            self.mesh_def.query(tips, workspace=self.ws_tips, reuse_order=True, out=o[0])
+            main.wait_event(self.ev[1])
+            main.wait_event(self.ev[2])
+        return o[0][1], o[0][2], o[1][0], o[1][1], o[1][2], o[1][3], o[2][0], o[2][1], o[2][3]
 
     def best(self):
         return self.opt[0], self.opt[2], self.opt[1], (self.opt_margin > 0.0).all()

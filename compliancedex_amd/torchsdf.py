@@ -66,7 +66,7 @@ class PreparedMesh:
     def num_faces(self):
         return self.faces.shape[0]
 
-    def query(self, points, want_face=False, workspace=None, reuse_order=False):
+    def query(self, points, want_face=False, workspace=None, reuse_order=False, out=None):
         """(sqdist, sign, normals, clst, face | None) of float32 points [P, 3] (cdx_sdf_query).  ``workspace``: a
         QueryWorkspace to sort the points in (default: the mesh's own); ``reuse_order``: walk the points in the order
         the workspace's last sort left (of P points — these same points on another mesh, or earlier positions of
@@ -76,10 +76,17 @@ class PreparedMesh:
         lib = N.load()
         points = points.detach().contiguous()
         P, dev = points.shape[0], points.device
-        dist = torch.empty(P, dtype=torch.float32, device=dev)
-        sign = torch.empty(P, dtype=torch.int32, device=dev)
-        normals = torch.empty(P, 3, dtype=torch.float32, device=dev)
-        clst = torch.empty(P, 3, dtype=torch.float32, device=dev)
+        if out is not None:  # (dist [P] f32, sign [P] i32, normals [P, 3] f32, clst [P, 3] f32), contiguous
+            dist, sign, normals, clst = out
+            if not (dist.shape == (P,) and sign.shape == (P,) and normals.shape == (P, 3) and clst.shape == (P, 3) and
+                    dist.dtype == normals.dtype == clst.dtype == torch.float32 and sign.dtype == torch.int32 and
+                    all(t.is_contiguous() and t.device == dev for t in out)):
+                raise RuntimeError("query: out must be (dist [P], sign [P] int32, normals [P, 3], clst [P, 3]) float32")
+        else:
+            dist = torch.empty(P, dtype=torch.float32, device=dev)
+            sign = torch.empty(P, dtype=torch.int32, device=dev)
+            normals = torch.empty(P, 3, dtype=torch.float32, device=dev)
+            clst = torch.empty(P, 3, dtype=torch.float32, device=dev)
         face = torch.empty(P, dtype=torch.int32, device=dev) if want_face else None
         if P == 0:
             return dist, sign, normals, clst, face
@@ -98,6 +105,20 @@ class QueryWorkspace:
 
     def __init__(self):
         self.buf, self.P = None, None
+
+    def sort(self, points):
+        """The points' order alone (cdx_sdf_query_order): later queries of these points with ``reuse_order`` — on
+        other meshes, on other streams ordered after this call — walk them in it."""
+        _check(points, points.new_zeros(1, 3, 3))
+        if points.dtype != torch.float32:
+            raise RuntimeError("QueryWorkspace.sort takes float32 points")
+        points = points.detach().contiguous()
+        P, dev = points.shape[0], points.device
+        if P == 0:
+            return
+        buf = self.get(P, dev)
+        N.check(N.load().cdx_sdf_query_order(N.ptr(points), P, N.ptr(buf), buf.numel(), N.stream_ptr(dev)),
+                "cdx_sdf_query_order")
 
     def get(self, P, dev, reuse_order=False):
         if reuse_order and self.P != P:

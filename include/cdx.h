@@ -495,6 +495,10 @@ size_t cdx_sdf_query_workspace(int64_t P);
  * CDX_SDF_MESH_CULLED / CDX_SDF_MESH_EXACT — the mesh's kind as cdx_sdf_mesh_flags read it once (no NaN-capable
  * face: the culled kernel only; else the brute-force tile rule only); without either, both kernels are launched
  * and the device picks. */
+/* The points' Morton order alone, into `workspace` (what cdx_sdf_query does first without CDX_SDF_REUSE_ORDER):
+ * several queries of these points may then run with CDX_SDF_REUSE_ORDER concurrently on other streams, each
+ * ordered after this call. */
+int cdx_sdf_query_order(const float* points, int64_t P, void* workspace, size_t workspace_bytes, cdx_stream_t stream);
 #define CDX_SDF_REUSE_ORDER 1
 #define CDX_SDF_MESH_CULLED 2
 #define CDX_SDF_MESH_EXACT 4

@@ -254,8 +254,8 @@ def _spy_prepared_queries(monkeypatch):
     calls = []
     real = torchsdf.PreparedMesh.query
 
-    def spy(self, points, want_face=False, workspace=None, reuse_order=False):
-        out = real(self, points, want_face, workspace, reuse_order)
+    def spy(self, points, want_face=False, workspace=None, reuse_order=False, out=None):
+        out = real(self, points, want_face, workspace, reuse_order, out)
         calls.append((points.detach().clone(), self.faces, [t.detach().clone() for t in out[:4]]))
         return out
     monkeypatch.setattr(torchsdf.PreparedMesh, "query", spy)
