@@ -163,14 +163,29 @@ def config4_kin(args, dev):
     full = PreparedMesh(faces)
     meshes = (PreparedMesh(_face_vertices(m, dev)), full, full)
     ws_t, ws_g = QueryWorkspace(), QueryWorkspace()
-    wss, reuse = (ws_t, ws_t, ws_g), (False, True, False)  # the loop's pattern: fingertips sorted once
+    wss = (ws_t, ws_t, ws_g)
     from compliancedex_amd import DifferentiableRobotModel
     tips = (DifferentiableRobotModel("iiwa7_allegro", device=dev).compute_forward_kinematics(
         res[0].detach(), links, offsets=offs)[0].view(-1, 3) + torch.from_numpy(palm).to(dev)).contiguous()
     pts = (tips, tips, res[2].detach().reshape(-1, 3).contiguous())
+    side = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    evs = [torch.cuda.Event() for _ in range(3)]
+
     def three():
-        for mh, pt, w, r in zip(meshes, pts, wss, reuse):
-            mh.query(pt, workspace=w, reuse_order=r)
+        """The loop's pattern (optimizers._FusedLoop.queries): both point sets sorted, then the full mesh's two
+        queries on side streams beside the deflated mesh's."""
+        ws_t.sort(tips)
+        ws_g.sort(pts[2])
+        main = torch.cuda.current_stream(dev)
+        evs[0].record(main)
+        for k in (1, 2):
+            side[k - 1].wait_event(evs[0])
+            with torch.cuda.stream(side[k - 1]):
+                meshes[k].query(pts[k], workspace=wss[k], reuse_order=True)
+            evs[k].record(side[k - 1])
+        meshes[0].query(pts[0], workspace=wss[0], reuse_order=True)
+        main.wait_event(evs[1])
+        main.wait_event(evs[2])
     three()
     st = (ctypes.c_uint64 * 3)()
     visits = ctypes.c_uint64(0)
@@ -193,11 +208,12 @@ def config4_kin(args, dev):
     return {"workload": "config 4: KinGraspOptimizer (fused) on iiwa7_allegro (23 DOF, chain depth 13), "
                         f"E={E} candidates, 16 384-face banana mesh, optimize_target, 3 TorchSDF queries per iteration",
             "iterations": iters, "ms_per_iteration": ms_iter, "evals_per_s": E / (ms_iter * 1e-3),
-            "launches_per_iteration": "3 TorchSDF queries (sdf_tree_kernel each; the fingertips' and the targets' "
-                                      "Morton order: bbox partials, keys, an 18-bit radix sort) + cdx_kin_cost + "
-                                      "cdx_kin_step + the loss sum",
+            "launches_per_iteration": "3 TorchSDF queries (sdf_tree_kernel each, concurrently on three streams; the "
+                                      "fingertips' and the targets' Morton order — bbox partials, keys, an 18-bit "
+                                      "radix sort — every 4th iteration) + cdx_kin_cost + cdx_kin_step + the loss sum",
             "roofline_sdf": {"bound": "valu", "kernel": "sdf_tree_kernel (+ per-query bbox, Morton keys, radix sort)",
-                             "fwd_3calls_ms": fwd_ms, "points": n_pts, "faces": F, "brute_force_pairs": brute,
+                             "fwd_3calls_ms": fwd_ms, "fwd_pattern": "both point sets sorted, three queries concurrently (the loop's "
+                                                               "iterations re-sort every 4th)", "points": n_pts, "faces": F, "brute_force_pairs": brute,
                              "pairs_evaluated": int(st[0]), "pairs_exact_path": int(st[1]),
                              "pairs_per_point": int(st[0]) / max(1, n_pts),
                              "chunk_visits_per_wave": int(visits.value) / max(1, (n_pts + 63) // 64),
