@@ -250,6 +250,76 @@ CDX_HD void fk_tip_bwd(const cdx_chain& c, int k, const Q& q, const float* gpos,
   }
 }
 
+// fk_tip_bwd in closed form, no per-level storage: every joint is a revolute joint about a body axis (axis_rot)
+// or fixed, so with M_j = R_parent·F_j (orthonormal), ω_j = M_j·e_axis and o_j the joint's world origin,
+// dR/dθ_j = [ω_j]×R and dt/dθ_j = ω_j × (t − o_j) for the final pose (R, t).  Hence
+//   dL/dθ_j = <G_R, [ω_j]×R> + G_t·(ω_j × (t − o_j)) = ω_j·(w − o_j × G_t),  w = Σ_c R[:,c] × G_R[:,c] + t × G_t,
+// with G_R the tip offset's rotation gradient (the detached-scale quaternion path as in fk_tip_bwd).  Two forward
+// walks (the second recomputes the poses) instead of a forward walk that keeps every level's rotation plus a
+// backward walk: the same gradient to f32 rounding, ≈ 10 registers of state instead of 9 per level.
+template <int MAXD, class Q, class GQ>
+CDX_HD void fk_tip_bwd2(const cdx_chain& c, int k, const Q& q, const float* gpos, GQ&& g_q, float* pos = nullptr) {
+  const uint32_t mask = chain_path_mask(c, c.tip_body[k]);
+  const int n = path_depth(mask);
+  float R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f}, t[3] = {0.f, 0.f, 0.f};
+  uint32_t m = mask;
+#pragma unroll
+  for (int l = 0; l < MAXD; ++l) {
+    if (l < n) {
+      float Rn[9], tn[3];
+      chain_step(c.bodies[low_bit(m)], q, R, t, Rn, tn);
+      m &= m - 1;
+      for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+      for (int i = 0; i < 3; ++i) t[i] = tn[i];
+    }
+  }
+  if (pos) tip_from_pose(c, k, R, t, pos, nullptr);
+  float GR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const float Gt[3] = {gpos[0], gpos[1], gpos[2]};
+  if (c.has_offsets) {
+    float raw[4], sc;
+    const int br = quat_raw(R, raw, &sc);
+    float qt[4] = {raw[0] * sc, raw[1] * sc, raw[2] * sc, raw[3] * sc};
+    float gq[4] = {0, 0, 0, 0};
+    quat_rotate_bwd(qt, c.tip_offset[k], gpos, gq);
+    for (int i = 0; i < 4; ++i) gq[i] *= sc;  // scale is detached: only d raw flows
+    quat_raw_bwd(br, gq, GR);
+  }
+  float w[3] = {t[1] * Gt[2] - t[2] * Gt[1], t[2] * Gt[0] - t[0] * Gt[2], t[0] * Gt[1] - t[1] * Gt[0]};
+#pragma unroll
+  for (int cc = 0; cc < 3; ++cc) {
+    const float r0 = R[cc], r1 = R[3 + cc], r2 = R[6 + cc], g0 = GR[cc], g1 = GR[3 + cc], g2 = GR[6 + cc];
+    w[0] += r1 * g2 - r2 * g1;
+    w[1] += r2 * g0 - r0 * g2;
+    w[2] += r0 * g1 - r1 * g0;
+  }
+  for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.f : 0.f;
+  t[0] = t[1] = t[2] = 0.f;
+  m = mask;
+#pragma unroll
+  for (int l = 0; l < MAXD; ++l) {
+    if (l < n) {
+      const cdx_body& b = c.bodies[low_bit(m)];
+      m &= m - 1;
+      float M[9], tt[3];
+      mat3_mul(R, b.F, M);
+      mat3_vec(R, b.t, tt);
+      for (int i = 0; i < 3; ++i) t[i] = tt[i] + t[i];
+      if (b.dof >= 0) {
+        const float om[3] = {M[b.axis], M[3 + b.axis], M[6 + b.axis]};
+        const float ox[3] = {t[1] * Gt[2] - t[2] * Gt[1], t[2] * Gt[0] - t[0] * Gt[2], t[0] * Gt[1] - t[1] * Gt[0]};
+        const float dth = om[0] * (w[0] - ox[0]) + om[1] * (w[1] - ox[1]) + om[2] * (w[2] - ox[2]);
+        g_q(b.dof, b.sign * dth);
+        float A[9], dA[9];
+        axis_rot(b.axis, b.sign * q[b.dof], A, dA);
+        mat3_mul(M, A, R);
+      } else {
+        for (int i = 0; i < 9; ++i) R[i] = M[i];
+      }
+    }
+  }
+}
+
 // Deepest tip path of a chain (host: picks the fk_tip_bwd register bound).
 CDX_HD int chain_max_depth(const cdx_chain& c) {
   int d = 0;

@@ -221,7 +221,9 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
   fp.dummy_target_z = (double)p.fe.dummy_target_z;
   fp.dummy_comp = (double)p.fe.dummy_comp;
   cdx::ForceEq<NT> fe;
+#if !defined(CDX_KIN_DIAG_NOFE)
   fe.forward(fp, NT, tp, tg, cp, nr, nz);
+#endif
 
   // ---- forward
   double ct[3] = {0, 0, 0}, cg[3] = {0, 0, 0};
@@ -280,7 +282,9 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
     gsm_dot += g_sm[k] * sm[k];
   }
   for (int k = 0; k < NT; ++k) g_fn[k] += -(sm[k] * (g_sm[k] - gsm_dot));
+#if !defined(CDX_KIN_DIAG_NOFE)
   fe.backward(-5.0, g_fn, cp, gt, gg, gc);
+#endif
   // this lane's fingertip (selects: no dynamic register indexing)
   double gto[3] = {0, 0, 0}, ggo[3] = {0, 0, 0}, gco = 0.0;
 #pragma unroll
@@ -290,12 +294,32 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
       gco = gc[k];
     }
   if constexpr (FK) {
+#if defined(CDX_KIN_FK_BWD1)  // (A/B: the stored-rotations backward walk, per-DOF sums in a register array)
     float fk_g[CDX_MAX_DOFS];
     for (int i = 0; i < D; ++i) fk_g[i] = 0.f;
     const float gpos[3] = {(float)gto[0], (float)gto[1], (float)gto[2]};
+#if !defined(CDX_KIN_DIAG_NOFK)  // (timing-only diagnostic builds: outputs wrong)
     cdx::fk_tip_bwd<MAXD>(chain, f, q + e * D, gpos, cdx::GqAdd{fk_g});
+#endif
+#else  // the closed-form backward (fk_tip_bwd2), per-DOF sums in LDS (a register array indexed by DOF spilled)
+    __shared__ float s_fk[CDX_MAX_DOFS][64];
+    for (int i = 0; i < D; ++i) s_fk[i][threadIdx.x] = 0.f;
+    const float gpos[3] = {(float)gto[0], (float)gto[1], (float)gto[2]};
+#if !defined(CDX_KIN_DIAG_NOFK)
+    // the chain read in place from the kernel-argument segment (it is the first argument, at offset 0): indexed by a
+    // per-lane body index, the by-value copy went to scratch (≈ 2 KB per lane) in the deep-chain instantiation
+    const cdx_chain& kc = *(const cdx_chain*)(__builtin_amdgcn_kernarg_segment_ptr());
+    cdx::fk_tip_bwd2<MAXD>(kc, f, q + e * D, gpos, [&](int d, float v) { s_fk[d][threadIdx.x] += v; });
+#endif
+    float* fk_g = nullptr;
+    (void)fk_g;
+#endif
     for (int i = 0; i < D; ++i) {
+#if defined(CDX_KIN_FK_BWD1)
       float s = fk_g[i];
+#else
+      float s = s_fk[i][threadIdx.x];
+#endif
       s += __shfl_xor(s, 1);
       s += __shfl_xor(s, 2);
       if ((i & 3) == f && on) {
