@@ -48,8 +48,11 @@ __global__ __launch_bounds__(64) void fk_backward_kernel(cdx_chain c, const floa
   if (b >= B) return;
   float* g = gq + b * c.n_dofs;
   for (int i = 0; i < c.n_dofs; ++i) g[i] = 0.f;
+  // (the chain read in place from the kernel-argument segment — the first argument, offset 0: indexed per body, the
+  // by-value copy went to scratch in the deep-chain instantiation)
+  const cdx_chain& kc = *(const cdx_chain*)(__builtin_amdgcn_kernarg_segment_ptr());
   for (int k = 0; k < c.n_tips; ++k)
-    cdx::fk_tip_bwd<MAXD>(c, k, q + b * c.n_dofs, gpos + (b * c.n_tips + k) * 3, cdx::GqAdd{g});
+    cdx::fk_tip_bwd<MAXD>(kc, k, q + b * c.n_dofs, gpos + (b * c.n_tips + k) * 3, cdx::GqAdd{g});
 }
 
 // --------------------------------------------------------------- collision loss
@@ -435,9 +438,15 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
   const float gtl[3] = {(float)gl[0], (float)gl[1], (float)gl[2]};
   for (int i = 0; i < D; ++i) gcon[i][tid] = 0.f;
   float tl[3] = {0.f, 0.f, 0.f};
-  if (live)
-    cdx::fk_tip_bwd<MAXD>(P.chain, f, cdx::QRowD{q + ec * D}, gtl,
-                          [&](int d, float v) { gcon[d][tid] += v; }, tl);
+  if (live) {
+    // the chain read in place from the kernel-argument segment (P is the first argument, at offset 0)
+    const cdx_chain& kc = (*(const cdx_problem*)(__builtin_amdgcn_kernarg_segment_ptr())).chain;
+#if defined(CDX_COMBINE_FK_BWD1)  // (A/B: the stored-rotations backward walk)
+    cdx::fk_tip_bwd<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
+#else
+    cdx::fk_tip_bwd2<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
+#endif
+  }
   double red[12];  // g_palm_pos (3) + g_Rp (9)
   for (int i = 0; i < 3; ++i) red[i] = gt[i];
   for (int r = 0; r < 3; ++r)

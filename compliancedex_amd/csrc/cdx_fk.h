@@ -306,7 +306,9 @@ CDX_HD void fk_tip_bwd2(const cdx_chain& c, int k, const Q& q, const float* gpos
       mat3_vec(R, b.t, tt);
       for (int i = 0; i < 3; ++i) t[i] = tt[i] + t[i];
       if (b.dof >= 0) {
-        const float om[3] = {M[b.axis], M[3 + b.axis], M[6 + b.axis]};
+        const int ax = b.axis;  // (selects, not an index into M: a register array indexed at run time goes to scratch)
+        const float om[3] = {ax == 0 ? M[0] : (ax == 1 ? M[1] : M[2]), ax == 0 ? M[3] : (ax == 1 ? M[4] : M[5]),
+                             ax == 0 ? M[6] : (ax == 1 ? M[7] : M[8])};
         const float ox[3] = {t[1] * Gt[2] - t[2] * Gt[1], t[2] * Gt[0] - t[0] * Gt[2], t[0] * Gt[1] - t[1] * Gt[0]};
         const float dth = om[0] * (w[0] - ox[0]) + om[1] * (w[1] - ox[1]) + om[2] * (w[2] - ox[2]);
         g_q(b.dof, b.sign * dth);
