@@ -470,18 +470,34 @@ __global__ __launch_bounds__(64) void kin_step_kernel(cdx_chain chain, cdx_kin_o
                : rmsprop_f32(p[k], g[k], v[k], b2, w2, eps, sz[grp]);
   };
   // pose: Kin — the joint angles this thread owns, and the whole updated row into LDS for the FK; SDF — tip f
-  if (kin) {
+  if (kin) {  // the DOFs i ≡ f (mod T) of the row, each into LDS for the FK below (loads issued ahead of the updates)
     float* qs = s_q + gl * D;
-    for (int i = 0; i < D; ++i) {
-      const int64_t k = e * D + i;
-      float qn = b.pose[k];
-      if (cfg.lr[0] != 0.0) {
-        float m = b.m_pose[k], v = b.v_pose[k];
-        qn = adam_f32(qn, b.g_pose[k], m, v, w1, b2, w2, bc2s, eps, sz[0]);
-        if (i % T == f) { b.m_pose[k] = m; b.v_pose[k] = v; }
+    constexpr int U = 4;
+    for (int i0 = f; i0 < D; i0 += U * T) {
+      float pv[U], gv[U], mv[U], vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * T;
+        const int64_t k = e * D + (i < D ? i : f);
+        pv[u] = b.pose[k];
+        gv[u] = b.g_pose[k];
+        mv[u] = b.m_pose[k];
+        vv[u] = b.v_pose[k];
       }
-      if (i % T == f) b.pose[k] = qn;
-      if (f == 0) qs[i] = qn;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * T;
+        if (i >= D) break;
+        const int64_t k = e * D + i;
+        float qn = pv[u];
+        if (cfg.lr[0] != 0.0) {
+          qn = adam_f32(qn, gv[u], mv[u], vv[u], w1, b2, w2, bc2s, eps, sz[0]);
+          b.m_pose[k] = mv[u];
+          b.v_pose[k] = vv[u];
+        }
+        b.pose[k] = qn;
+        qs[i] = qn;
+      }
     }
   } else {
     for (int i = 0; i < 3; ++i) upd(b.pose, b.g_pose, b.m_pose, b.v_pose, 3 * r + i, 0);
