@@ -510,6 +510,33 @@ def test_sdf_prepared_mesh_equals_one_shot_and_owns_its_faces():
     assert torch.equal(g, 2 * (pts - c))
 
 
+def test_fused_loop_concurrent_queries_equal_sequential(monkeypatch):
+    """The fused Kin / SDF loop's three TorchSDF queries on three streams (points sorted once by
+    QueryWorkspace.sort, the full mesh's two queries on side streams) give the same bits as the three run one
+    after the other, over several iterations (fresh and reused orders, moved points)."""
+    from compliancedex_amd.optimizers import _FusedLoop
+    faces = torch.from_numpy(np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))).to(DEV)
+    rng = np.random.default_rng(29)
+    E, T = 3000, 4
+    lo, hi = faces.reshape(-1, 3).min(0)[0], faces.reshape(-1, 3).max(0)[0]
+    tips = (lo - 0.05 + (hi - lo + 0.1) * torch.from_numpy(rng.random((E * T, 3))).to(DEV).float()).contiguous()
+    tgt = (lo + (hi - lo) * torch.from_numpy(rng.random((E, T, 3))).to(DEV).float()).contiguous()
+    z = torch.zeros(E, 3, device=DEV)
+    outs = {}
+    for conc in ("1", "0"):
+        monkeypatch.setenv("CDX_SDF_CONCURRENT", conc)
+        loop = _FusedLoop(E, T, z, tgt.clone(), torch.zeros(E, T, device=DEV), faces, faces * 0.9, DEV)
+        res = []
+        for it in range(6):
+            moved = (tips + 1e-3 * it).contiguous()
+            res.append([t.clone().cpu().numpy() for t in loop.queries(moved, tgt + 1e-3 * it)])
+        torch.cuda.synchronize()
+        outs[conc] = res
+    for a_it, b_it in zip(outs["1"], outs["0"]):
+        for a, b in zip(a_it, b_it):
+            assert _bitwise_equal_nan_aware(a, b)
+
+
 def test_sdf_stale_order_gives_the_same_results():
     """CDX_SDF_REUSE_ORDER with an order sorted for OTHER points (a fused loop re-sorts its query points only every
     few iterations): the results equal a fresh sort's bit for bit — moved points, shuffled points, and points
