@@ -436,6 +436,9 @@ __device__ inline unsigned long long pack_best(float d, int idx) {
 #define CDX_SDF_NW 4
 #endif
 constexpr int NW = CDX_SDF_NW;     // waves per point group
+#ifndef CDX_SDF_MINW
+#define CDX_SDF_MINW 5  // waves per SIMD the tree kernel is compiled for: 96 VGPRs, 30.7 KB LDS per group → 5 (1: 101 VGPRs, 4)
+#endif
 constexpr int CPW = TOPB / NW;     // chunks of a top node per wave
 static_assert(TOPB % NW == 0 && CHUNK % NW == 0, "waves split a top's chunks and a chunk's faces evenly");
 #if defined(CDX_SDF_DIAG)
@@ -446,7 +449,7 @@ __device__ __forceinline__ void sel_min(float& lb, int& sel, float l, int i) {
   if (l < lb || (l == lb && i < sel)) { lb = l; sel = i; }
 }
 
-__global__ __launch_bounds__(64 * NW) void sdf_tree_kernel(
+__global__ __launch_bounds__(64 * NW, CDX_SDF_MINW) void sdf_tree_kernel(
     const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
     int64_t F, const cdx::FaceRec* __restrict__ rec, const Slab* __restrict__ slab, const Node* __restrict__ chunk,
     const Node* __restrict__ top, const Node* __restrict__ run, int C, int T, const unsigned* __restrict__ ws,
@@ -465,8 +468,10 @@ __global__ __launch_bounds__(64 * NW) void sdf_tree_kernel(
   __shared__ float4 s_cn[NW][3 * CPW];                // per wave: its CPW chunk nodes of the current top node
   __shared__ unsigned long long s_best[64];           // the group's packed (distance, face) best per point
   __shared__ unsigned short s_pair[NW][128];           // per wave: pending (lane << 5 | face) pairs
-  __shared__ float s_lb[NW][64];                       // greedy seed: per wave candidate bound …
-  __shared__ int s_sel[NW][64];                        // … and index
+  // greedy seed: per wave candidate bound and index — in the record buffers, which the seed phase does not use
+  static_assert(sizeof(s_rec) >= NW * 64 * (sizeof(float) + sizeof(int)), "seed scratch fits the record buffers");
+  float (*s_lb)[64] = reinterpret_cast<float (*)[64]>(&s_rec[0][0]);
+  int (*s_sel)[64] = reinterpret_cast<int (*)[64]>(reinterpret_cast<float*>(&s_rec[0][0]) + NW * 64);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // the upper levels of the hierarchy in LDS: one coalesced copy per workgroup instead of a dependent load per
@@ -612,6 +617,7 @@ __global__ __launch_bounds__(64 * NW) void sdf_tree_kernel(
       {
         static_assert(REC_V4 == 5, "five record loads per lane");
         const float4* rc = rec4 + (int64_t)c * (REC_WORDS * CHUNK / 4) + lane;
+#if defined(CDX_SDF_REG_STAGE)  // (A/B: through registers — 28 VGPRs in flight)
         const float4 v0 = rc[0], v1 = rc[64], v2 = rc[128], v3 = rc[192], v4 = rc[256];
         const float4 sv = reinterpret_cast<const float4*>(slab)[(int64_t)c * 2 * CHUNK + lane];
         const float4 rv = lane < 3 * RPC ? reinterpret_cast<const float4*>(run)[(int64_t)c * 3 * RPC + lane]
@@ -621,6 +627,20 @@ __global__ __launch_bounds__(64 * NW) void sdf_tree_kernel(
         if (lane < 3 * RPC) s_run[w][lane] = rv;
         buf[lane] = v0; buf[lane + 64] = v1; buf[lane + 128] = v2; buf[lane + 192] = v3; buf[lane + 256] = v4;
         __builtin_amdgcn_wave_barrier();
+#else  // LDS-DMA (global_load_lds_dwordx4: lane l's 16 bytes to base + 16·l, no VGPRs, no ds_write)
+        typedef __attribute__((address_space(3))) void* lds_ptr;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the previous chunk's LDS reads are done)
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const float4*>(slab) + (int64_t)c * 2 * CHUNK + lane,
+                                         (lds_ptr)&s_slab[w][0], 16, 0, 0);
+        if (lane < 3 * RPC)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const float4*>(run) + (int64_t)c * 3 * RPC + lane,
+                                           (lds_ptr)&s_run[w][0], 16, 0, 0);
+#pragma unroll
+        for (int q = 0; q < REC_V4; ++q) __builtin_amdgcn_global_load_lds(rc + 64 * q, (lds_ptr)(buf + 64 * q), 16, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#endif
       }
       // the chunk's faces a lane cannot rule out: the runs first (their own nodes), then the slab bound of each
       // face of a run some lane needs, against the chunk's threshold (its margins)
