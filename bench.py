@@ -169,22 +169,27 @@ def config4_kin(args, dev):
         res[0].detach(), links, offsets=offs)[0].view(-1, 3) + torch.from_numpy(palm).to(dev)).contiguous()
     pts = (tips, tips, res[2].detach().reshape(-1, 3).contiguous())
     side = [torch.cuda.Stream(device=dev) for _ in range(2)]
-    evs = [torch.cuda.Event() for _ in range(3)]
+    evs = [torch.cuda.Event() for _ in range(4)]
 
     def three():
-        """The loop's pattern (optimizers._FusedLoop.queries): both point sets sorted, then the full mesh's two
-        queries on side streams beside the deflated mesh's."""
-        ws_t.sort(tips)
-        ws_g.sort(pts[2])
+        """The loop's pattern on a re-sorting iteration (optimizers._FusedLoop.queries): the targets sorted and
+        queried on a side stream, the fingertips sorted on the caller's stream, then queried against the full mesh on
+        a second side stream and against the deflated mesh on the caller's."""
         main = torch.cuda.current_stream(dev)
         evs[0].record(main)
-        for k in (1, 2):
-            side[k - 1].wait_event(evs[0])
-            with torch.cuda.stream(side[k - 1]):
-                meshes[k].query(pts[k], workspace=wss[k], reuse_order=True)
-            evs[k].record(side[k - 1])
-        meshes[0].query(pts[0], workspace=wss[0], reuse_order=True)
-        main.wait_event(evs[1])
+        side[1].wait_event(evs[0])
+        with torch.cuda.stream(side[1]):
+            ws_g.sort(pts[2])
+            meshes[2].query(pts[2], workspace=ws_g, reuse_order=True)
+        evs[2].record(side[1])
+        ws_t.sort(tips)
+        evs[1].record(main)
+        side[0].wait_event(evs[1])
+        with torch.cuda.stream(side[0]):
+            meshes[1].query(pts[1], workspace=ws_t, reuse_order=True)
+        evs[3].record(side[0])
+        meshes[0].query(pts[0], workspace=ws_t, reuse_order=True)
+        main.wait_event(evs[3])
         main.wait_event(evs[2])
     three()
     st = (ctypes.c_uint64 * 3)()

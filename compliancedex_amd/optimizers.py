@@ -122,10 +122,10 @@ class _FusedLoop:
         # query run on beside the first (CDX_SDF_CONCURRENT=0: all three on the caller's stream)
         self.q_out = [(torch.empty(E * T, **f32), torch.empty(E * T, dtype=torch.int32, device=dev),
                        torch.empty(E * T, 3, **f32), torch.empty(E * T, 3, **f32)) for _ in range(3)]
-        self.concurrent = os.environ.get("CDX_SDF_CONCURRENT", "1") != "0"
+        self.concurrent = int(os.environ.get("CDX_SDF_CONCURRENT", "1"))  # 2 (A/B): only the targets' query on a side stream
         if self.concurrent:
             self.side = [torch.cuda.Stream(device=dev) for _ in range(2)]
-            self.ev = [torch.cuda.Event() for _ in range(3)]
+            self.ev = [torch.cuda.Event() for _ in range(4)]
         self.pose, self.target, self.comp = pose, target, comp
         self.loss = torch.empty(E, dtype=torch.float64, device=dev)
         self.margin = [torch.zeros(E, T, dtype=torch.float64, device=dev) for _ in range(2)]
@@ -166,22 +166,33 @@ class _FusedLoop:
             self.mesh.query(tgt, workspace=self.ws_tgt, reuse_order=not fresh, out=o[2])
         else:
             # The three queries are independent: each culled kernel's tail (a few point groups far from the mesh)
-            # leaves most of the chip idle, which the others fill.  Orders first, then the full mesh's two queries
-            # on the side streams and the deflated mesh's on the caller's, which waits for both before cdx_kin_cost.
+            # leaves most of the chip idle, which the others fill.  The targets are sorted (when fresh) and queried
+            # on side stream 2, the fingertips sorted on the caller's stream and queried against the full mesh on
+            # side stream 1 and against the deflated mesh on the caller's, which waits for both before cdx_kin_cost.
+            main = torch.cuda.current_stream(tips.device)
+            ev_start, ev_tips, ev_full, ev_tgt = self.ev
+            ev_start.record(main)
+            s1, s2 = self.side
+            s2.wait_event(ev_start)
+            with torch.cuda.stream(s2):
+                if fresh:
+                    self.ws_tgt.sort(tgt)
+                self.mesh.query(tgt, workspace=self.ws_tgt, reuse_order=True, out=o[2])
+            ev_tgt.record(s2)
             if fresh:
                 self.ws_tips.sort(tips)
-                self.ws_tgt.sort(tgt)
-            main = torch.cuda.current_stream(tips.device)
-            self.ev[0].record(main)
-            for k, (pts, ws) in enumerate(((tips, self.ws_tips), (tgt, self.ws_tgt))):
-                st = self.side[k]
-                st.wait_event(self.ev[0])
-                with torch.cuda.stream(st):
-                    self.mesh.query(pts, workspace=ws, reuse_order=True, out=o[k + 1])
-                self.ev[k + 1].record(st)
+            if self.concurrent == 1:
+                ev_tips.record(main)
+                s1.wait_event(ev_tips)
+                with torch.cuda.stream(s1):
+                    self.mesh.query(tips, workspace=self.ws_tips, reuse_order=True, out=o[1])
+                ev_full.record(s1)
             self.mesh_def.query(tips, workspace=self.ws_tips, reuse_order=True, out=o[0])
-            main.wait_event(self.ev[1])
-            main.wait_event(self.ev[2])
+            if self.concurrent == 1:
+                main.wait_event(ev_full)
+            else:  # (A/B: the full mesh's fingertip query on the caller's stream too)
+                self.mesh.query(tips, workspace=self.ws_tips, reuse_order=True, out=o[1])
+            main.wait_event(ev_tgt)
         return o[0][1], o[0][2], o[1][0], o[1][1], o[1][2], o[1][3], o[2][0], o[2][1], o[2][3]
 
     def best(self):
