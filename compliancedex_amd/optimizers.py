@@ -117,6 +117,7 @@ class _FusedLoop:
         self.mesh, self.mesh_def = PreparedMesh(faces), PreparedMesh(faces_deflate)
         self.ws_tips, self.ws_tgt = QueryWorkspace(), QueryWorkspace()
         self.iteration = 0
+        self.hist = None
         self.resort = max(1, int(os.environ.get("CDX_SDF_RESORT", "4")))  # iterations per point sort (A/B: 1)
         # the three queries' outputs (dist, sign, normals, clst), and the two side streams the second and third
         # query run on beside the first (CDX_SDF_CONCURRENT=0: all three on the caller's stream)
@@ -194,6 +195,22 @@ class _FusedLoop:
                 self.mesh.query(tips, workspace=self.ws_tips, reuse_order=True, out=o[1])
             main.wait_event(ev_tgt)
         return o[0][1], o[0][2], o[1][0], o[1][1], o[1][2], o[1][3], o[2][0], o[2][1], o[2][3]
+
+    def loss_slot(self, s, iters):
+        """Iteration s's loss vector: a row of a per-call [iters, E] history (the per-iteration sums are taken in one
+        reduction after the loop, not one per iteration), or the single buffer when the history would pass 1 GiB."""
+        E = self.loss.shape[0]
+        if s == 0:
+            self.hist = (torch.empty(iters, E, dtype=torch.float64, device=self.loss.device)
+                         if iters * E * 8 <= (1 << 30) else None)
+        row = self.hist[s] if self.hist is not None else self.loss
+        self.buffers.loss = N.ptr(row)
+        return row
+
+    def loss_sums(self, history):
+        """Append the loop's per-iteration loss sums (device scalars) to ``history``."""
+        if getattr(self, "hist", None) is not None:
+            history.extend(self.hist.sum(dim=1).unbind(0))
 
     def best(self):
         return self.opt[0], self.opt[2], self.opt[1], (self.opt_margin > 0.0).all()
@@ -314,17 +331,20 @@ class KinGraspOptimizer:
             nz = _noise(kabsch_noise, s)
             nz = None if nz is None else nz.detach().to(device=dev, dtype=torch.float64).contiguous()
             self._seed += 1
+            loss = st.loss_slot(s, self.num_iters)
             N.check(lib.cdx_kin_cost(chain, prm, E, N.ptr(q), N.ptr(st.tips), N.ptr(tgt), N.ptr(comp),
                                      *(N.ptr(t) for t in st.queries(st.tips, tgt)), N.ptr(nz), self._seed,
-                                     N.ptr(st.loss), N.ptr(st.margin[s & 1]), N.ptr(st.normal[s & 1]), N.ptr(st.g[0]),
+                                     N.ptr(loss), N.ptr(st.margin[s & 1]), N.ptr(st.normal[s & 1]), N.ptr(st.g[0]),
                                      N.ptr(st.g[1]), N.ptr(st.g[2]), None, stream), "cdx_kin_cost")
-            self.loss_history.append(st.loss.sum())  # device scalar, no sync
+            if st.hist is None:
+                self.loss_history.append(loss.sum())  # device scalar, no sync
             if trace_rows:
-                self.loss_rows.append(st.loss.clone())
+                self.loss_rows.append(loss.clone())
             if verbose:
-                print("Loss:", float(st.loss.sum()), comp)
+                print("Loss:", float(loss.sum()), comp)
             N.check(lib.cdx_kin_step(chain, cfg, st.buffers, E, T, s, 0, stream), "cdx_kin_step")
         N.check(lib.cdx_kin_step(chain, cfg, st.buffers, E, T, self.num_iters, 1, stream), "cdx_kin_step")
+        st.loss_sums(self.loss_history)
         if self.loop_events:
             self.loop_events[1].record()
         if verbose:
@@ -429,17 +449,20 @@ class SDFGraspOptimizer:
             nz = None if nz is None else nz.detach().to(device=dev, dtype=torch.float64).contiguous()
             self._seed += 1
             pts = tips.view(-1, 3)
+            loss = st.loss_slot(s, self.num_iters)
             N.check(lib.cdx_kin_cost(None, prm, E, None, N.ptr(pts), N.ptr(tgt), N.ptr(comp),
-                                     *(N.ptr(t) for t in st.queries(pts, tgt)), N.ptr(nz), self._seed, N.ptr(st.loss),
+                                     *(N.ptr(t) for t in st.queries(pts, tgt)), N.ptr(nz), self._seed, N.ptr(loss),
                                      N.ptr(st.margin[s & 1]), N.ptr(st.normal[s & 1]), None, N.ptr(st.g[1]),
                                      N.ptr(st.g[2]), N.ptr(st.g[0]), stream), "cdx_kin_cost")
-            self.loss_history.append(st.loss.sum())  # device scalar, no sync
+            if st.hist is None:
+                self.loss_history.append(loss.sum())  # device scalar, no sync
             if trace_rows:
-                self.loss_rows.append(st.loss.clone())
+                self.loss_rows.append(loss.clone())
             if verbose:
-                print("Loss:", float(st.loss.sum()))
+                print("Loss:", float(loss.sum()))
             N.check(lib.cdx_kin_step(None, cfg, st.buffers, E, T, s, 0, stream), "cdx_kin_step")
         N.check(lib.cdx_kin_step(None, cfg, st.buffers, E, T, self.num_iters, 1, stream), "cdx_kin_step")
+        st.loss_sums(self.loss_history)
         if self.loop_events:
             self.loop_events[1].record()
         if verbose:
