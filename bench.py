@@ -168,29 +168,17 @@ def config4_kin(args, dev):
     tips = (DifferentiableRobotModel("iiwa7_allegro", device=dev).compute_forward_kinematics(
         res[0].detach(), links, offsets=offs)[0].view(-1, 3) + torch.from_numpy(palm).to(dev)).contiguous()
     pts = (tips, tips, res[2].detach().reshape(-1, 3).contiguous())
-    side = [torch.cuda.Stream(device=dev) for _ in range(2)]
-    evs = [torch.cuda.Event() for _ in range(4)]
+    from compliancedex_amd.torchsdf import query_batch
+    P = pts[0].shape[0]
+    outs = [(torch.empty(P, device=dev), torch.empty(P, dtype=torch.int32, device=dev), torch.empty(P, 3, device=dev),
+             torch.empty(P, 3, device=dev)) for _ in range(3)]
 
     def three():
-        """The loop's pattern on a re-sorting iteration (optimizers._FusedLoop.queries): the targets sorted and
-        queried on a side stream, the fingertips sorted on the caller's stream, then queried against the full mesh on
-        a second side stream and against the deflated mesh on the caller's."""
-        main = torch.cuda.current_stream(dev)
-        evs[0].record(main)
-        side[1].wait_event(evs[0])
-        with torch.cuda.stream(side[1]):
-            ws_g.sort(pts[2])
-            meshes[2].query(pts[2], workspace=ws_g, reuse_order=True)
-        evs[2].record(side[1])
+        """The loop's pattern on a re-sorting iteration (optimizers._FusedLoop.queries): both point sets sorted, then
+        the three queries in one launch (cdx_sdf_query_batch)."""
         ws_t.sort(tips)
-        evs[1].record(main)
-        side[0].wait_event(evs[1])
-        with torch.cuda.stream(side[0]):
-            meshes[1].query(pts[1], workspace=ws_t, reuse_order=True)
-        evs[3].record(side[0])
-        meshes[0].query(pts[0], workspace=ws_t, reuse_order=True)
-        main.wait_event(evs[3])
-        main.wait_event(evs[2])
+        ws_g.sort(pts[2])
+        query_batch([(meshes[k], pts[k], wss[k], outs[k]) for k in range(3)])
     three()
     st = (ctypes.c_uint64 * 3)()
     visits = ctypes.c_uint64(0)
@@ -213,12 +201,12 @@ def config4_kin(args, dev):
     return {"workload": "config 4: KinGraspOptimizer (fused) on iiwa7_allegro (23 DOF, chain depth 13), "
                         f"E={E} candidates, 16 384-face banana mesh, optimize_target, 3 TorchSDF queries per iteration",
             "iterations": iters, "ms_per_iteration": ms_iter, "evals_per_s": E / (ms_iter * 1e-3),
-            "launches_per_iteration": "3 TorchSDF queries (sdf_tree_kernel each, concurrently on three streams; the "
-                                      "fingertips' and the targets' Morton order — bbox partials, keys, an 18-bit "
-                                      "radix sort — every 4th iteration) + cdx_kin_cost + cdx_kin_step + the loss sum",
+            "launches_per_iteration": "3 TorchSDF queries in one launch (sdf_tree_batch_kernel; the fingertips' and the "
+                                      "targets' Morton order — bbox partials, keys, an 18-bit radix sort — every 4th "
+                                      "iteration) + cdx_kin_cost + cdx_kin_step",
             "roofline_sdf": {"bound": "valu", "kernel": "sdf_tree_kernel (+ per-query bbox, Morton keys, radix sort)",
-                             "fwd_3calls_ms": fwd_ms, "fwd_pattern": "both point sets sorted, three queries concurrently (the loop's "
-                                                               "iterations re-sort every 4th)", "points": n_pts, "faces": F, "brute_force_pairs": brute,
+                             "fwd_3calls_ms": fwd_ms, "fwd_pattern": "both point sets sorted, the three queries in one launch (the "
+                                                               "loop's iterations re-sort every 4th)", "points": n_pts, "faces": F, "brute_force_pairs": brute,
                              "pairs_evaluated": int(st[0]), "pairs_exact_path": int(st[1]),
                              "pairs_per_point": int(st[0]) / max(1, n_pts),
                              "chunk_visits_per_wave": int(visits.value) / max(1, (n_pts + 63) // 64),

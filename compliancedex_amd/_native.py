@@ -82,6 +82,13 @@ class CdxKinOptBuffers(C.Structure):
                                             "opt_comp", "any", "tips")])
 
 
+class CdxSdfBatchQuery(C.Structure):
+    _fields_ = [("mesh", C.c_void_p), ("faces", C.c_void_p), ("F", C.c_int64), ("points", C.c_void_p), ("P", C.c_int64),
+                ("sqdist", C.c_void_p), ("sign", C.c_void_p), ("normals", C.c_void_p), ("clst", C.c_void_p),
+                ("face_idx", C.c_void_p), ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
+                ("flags", C.c_int32), ("_pad", C.c_int32)]
+
+
 class CdxAdam(C.Structure):
     _fields_ = [("lr", C.c_double * 5), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double),
                 ("comp_min", C.c_double), ("target_lb", C.c_double * (MAX_TIPS * 3)),
@@ -156,6 +163,7 @@ _SIGS = {
     "cdx_sdf_mesh_prepare": (C.c_int, [_P, _I64, _P, _P]),
     "cdx_sdf_query_workspace": (C.c_size_t, [_I64]),
     "cdx_sdf_query_order": (C.c_int, [_P, _I64, _P, C.c_size_t, _P]),
+    "cdx_sdf_query_batch": (C.c_int, [C.c_int32, _P, _P]),
     "cdx_sdf_query": (C.c_int, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, C.c_size_t, C.c_int32, _P]),
     "cdx_sdf_mesh_flags": (C.c_int, [_P, C.POINTER(C.c_int32), _P]),
     "cdx_version": (C.c_char_p, []),
@@ -192,11 +200,12 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        sizes = (C.c_size_t * 12)()
+        sizes = (C.c_size_t * 13)()
         lib.cdx_abi_sizes(sizes)
         mine = [C.sizeof(CdxGpis), C.sizeof(CdxBody), C.sizeof(CdxChain), C.sizeof(CdxProblem),
                 C.sizeof(CdxCollision), C.sizeof(CdxAdam), C.sizeof(CdxOptBuffers), C.sizeof(CdxForceEq),
-                C.sizeof(CdxScreenReport), C.sizeof(CdxKinParams), C.sizeof(CdxKinOpt), C.sizeof(CdxKinOptBuffers)]
+                C.sizeof(CdxScreenReport), C.sizeof(CdxKinParams), C.sizeof(CdxKinOpt), C.sizeof(CdxKinOptBuffers),
+                C.sizeof(CdxSdfBatchQuery)]
         if list(sizes) != mine:
             raise ImportError(f"ABI struct size mismatch: library {list(sizes)} vs binding {mine}")
         info = build_info()

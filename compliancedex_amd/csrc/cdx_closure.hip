@@ -1359,4 +1359,5 @@ extern "C" void cdx_abi_sizes(size_t* out) {
   out[9] = sizeof(cdx_kin_params);
   out[10] = sizeof(cdx_kin_opt);
   out[11] = sizeof(cdx_kin_opt_buffers);
+  out[12] = sizeof(cdx_sdf_batch_query);
 }

@@ -449,13 +449,13 @@ __device__ __forceinline__ void sel_min(float& lb, int& sel, float l, int i) {
   if (l < lb || (l == lb && i < sel)) { lb = l; sel = i; }
 }
 
-__global__ __launch_bounds__(64 * NW, CDX_SDF_MINW) void sdf_tree_kernel(
+__device__ __forceinline__ void sdf_tree_body(
     const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
     int64_t F, const cdx::FaceRec* __restrict__ rec, const Slab* __restrict__ slab, const Node* __restrict__ chunk,
     const Node* __restrict__ top, const Node* __restrict__ run, int C, int T, const unsigned* __restrict__ ws,
     float* __restrict__ out_dist,
     int32_t* __restrict__ out_sign, float* __restrict__ out_nrm, float* __restrict__ out_clst,
-    int32_t* __restrict__ out_face, int count) {
+    int32_t* __restrict__ out_face, int count, int64_t grp) {
   if (ws[6]) return;  // mesh has a NaN-capable face: sdf_exact_kernel does this call
 #if defined(CDX_SDF_DIAG)
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(64 * NW, CDX_SDF_MINW) void sdf_tree_kernel(
     if (tops_lds) return Node{s_node[3 * (NODES_LDS + t)], s_node[3 * (NODES_LDS + t) + 1], s_node[3 * (NODES_LDS + t) + 2]};
     return load_node(top, t);
   };
-  const int64_t j = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t j = grp * 64 + lane;
   const bool live = j < P;
   const int64_t pi = porder[live ? j : P - 1];  // dead lanes shadow a live point
   const cdx::F3 p = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
@@ -741,6 +741,54 @@ __global__ __launch_bounds__(64 * NW, CDX_SDF_MINW) void sdf_tree_kernel(
   out_nrm[3 * pi] = n.x; out_nrm[3 * pi + 1] = n.y; out_nrm[3 * pi + 2] = n.z;
   out_clst[3 * pi] = cc.x; out_clst[3 * pi + 1] = cc.y; out_clst[3 * pi + 2] = cc.z;
   if (out_face) out_face[pi] = bidx;
+}
+
+__global__ __launch_bounds__(64 * NW, CDX_SDF_MINW) void sdf_tree_kernel(
+    const float* __restrict__ points, int64_t P, const int* __restrict__ porder, const float* __restrict__ faces,
+    int64_t F, const cdx::FaceRec* __restrict__ rec, const Slab* __restrict__ slab, const Node* __restrict__ chunk,
+    const Node* __restrict__ top, const Node* __restrict__ run, int C, int T, const unsigned* __restrict__ ws,
+    float* __restrict__ out_dist, int32_t* __restrict__ out_sign, float* __restrict__ out_nrm,
+    float* __restrict__ out_clst, int32_t* __restrict__ out_face, int count) {
+  sdf_tree_body(points, P, porder, faces, F, rec, slab, chunk, top, run, C, T, ws, out_dist, out_sign, out_nrm, out_clst,
+                out_face, count, blockIdx.x);
+}
+
+// Several queries (ordered, culled meshes) in one launch: workgroup b runs point group b − first[q] of query q.  The
+// queries' tails (the few groups far from each mesh) overlap in one grid, with no stream or event between them.
+constexpr int SDF_BATCH_MAX = 4;
+struct SdfBatchQ {
+  const float* points;
+  int64_t P;
+  const int* porder;
+  const float* faces;
+  int64_t F;
+  const cdx::FaceRec* rec;
+  const Slab* slab;
+  const Node *chunk, *top, *run;
+  int C, T;
+  const unsigned* ws;
+  float* out_dist;
+  int32_t* out_sign;
+  float *out_nrm, *out_clst;
+  int32_t* out_face;
+};
+struct SdfBatch {
+  SdfBatchQ q[SDF_BATCH_MAX];
+  unsigned first[SDF_BATCH_MAX];
+  int n, count;
+};
+__global__ __launch_bounds__(64 * NW, CDX_SDF_MINW) void sdf_tree_batch_kernel(SdfBatch b) {
+  // the descriptors read in place from the kernel-argument segment (indexed per workgroup, a by-value copy would go
+  // to scratch)
+  const SdfBatch& kb = *(const SdfBatch*)(__builtin_amdgcn_kernarg_segment_ptr());
+  int qi = 0;
+#pragma unroll
+  for (int i = 1; i < SDF_BATCH_MAX; ++i)
+    if (i < kb.n && blockIdx.x >= kb.first[i]) qi = i;
+  qi = __builtin_amdgcn_readfirstlane(qi);
+  const SdfBatchQ& q = kb.q[qi];
+  sdf_tree_body(q.points, q.P, q.porder, q.faces, q.F, q.rec, q.slab, q.chunk, q.top, q.run, q.C, q.T, q.ws,
+                q.out_dist, q.out_sign, q.out_nrm, q.out_clst, q.out_face, kb.count, (int64_t)blockIdx.x - kb.first[qi]);
 }
 
 // Brute force with the reference's tile rule: one point per lane, faces streamed through LDS
@@ -1145,6 +1193,60 @@ int cdx_sdf_diag_wgtime(uint64_t* out, int64_t n, cdx_stream_t stream) {
   return CDX_OK;
 }
 #endif
+
+int cdx_sdf_query_batch(int32_t n, const cdx_sdf_batch_query* qs, cdx_stream_t stream) {
+  if (n < 0 || n > SDF_BATCH_MAX || (n > 0 && !qs)) return CDX_EINVAL;
+  SdfBatch b{};
+  unsigned groups = 0;
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    const cdx_sdf_batch_query& d = qs[i];
+    if (d.P < 0 || d.F < 0 || !d.mesh || d.flags != (CDX_SDF_REUSE_ORDER | CDX_SDF_MESH_CULLED)) return CDX_EINVAL;
+    if (d.P == 0) continue;
+    if (!sdf_args_ok(d.P, d.points, d.faces, d.F, d.sqdist, d.sign, d.normals, d.clst) || !d.workspace) return CDX_EINVAL;
+    QueryWs q;
+    if (!query_ws(d.P, reinterpret_cast<hipStream_t>(stream), q)) return CDX_ELAUNCH;
+    if (d.workspace_bytes < q.bytes) return CDX_EINVAL;
+    const char* mesh = static_cast<const char*>(d.mesh);
+    const int64_t C = n_chunks(d.F), T = n_tops(d.F);
+    SdfBatchQ& o = b.q[m];
+    o.points = d.points;
+    o.P = d.P;
+    o.porder = reinterpret_cast<const int*>(static_cast<const char*>(d.workspace) + q.o_pv) + d.P;
+    o.faces = d.faces;
+    o.F = d.F;
+    o.rec = reinterpret_cast<const cdx::FaceRec*>(mesh + mesh_rec_off());
+    o.slab = reinterpret_cast<const Slab*>(mesh + mesh_slab_off(C));
+    o.chunk = reinterpret_cast<const Node*>(mesh + mesh_chunk_off(C));
+    o.top = reinterpret_cast<const Node*>(mesh + mesh_top_off(C));
+    o.run = reinterpret_cast<const Node*>(mesh + mesh_run_off(C));
+    o.C = (int)C;
+    o.T = (int)T;
+    o.ws = reinterpret_cast<const unsigned*>(mesh);
+    o.out_dist = d.sqdist;
+    o.out_sign = d.sign;
+    o.out_nrm = d.normals;
+    o.out_clst = d.clst;
+    o.out_face = d.face_idx;
+    b.first[m] = groups;
+    groups += (unsigned)((d.P + 63) / 64);
+    ++m;
+  }
+  if (m == 0) return CDX_OK;
+  b.n = m;
+  b.count = (int)g_sdf_count;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (sdf_mode() == 1) {  // (the exact-path debug mode: one call per query)
+    for (int i = 0; i < n; ++i) {
+      const cdx_sdf_batch_query& d = qs[i];
+      const int rc = cdx_sdf_forward(d.points, d.P, d.faces, d.F, d.sqdist, d.sign, d.normals, d.clst, d.face_idx, stream);
+      if (rc) return rc;
+    }
+    return CDX_OK;
+  }
+  hipLaunchKernelGGL(sdf_tree_batch_kernel, dim3(groups), dim3(64 * NW), 0, s, b);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
 
 int cdx_sdf_query_order(const float* points, int64_t P, void* workspace, size_t workspace_bytes, cdx_stream_t stream) {
   if (P < 0 || P > INT32_MAX) return CDX_EINVAL;

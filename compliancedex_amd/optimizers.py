@@ -26,7 +26,7 @@ from . import _native as N
 from .force_eq import force_eq_descriptor, force_eq_reward
 from .optimizer import EE_OFFSETS, FINGERTIP_LB, FINGERTIP_UB, WRIST_OFFSET
 from .robot_model import DifferentiableRobotModel
-from .torchsdf import PreparedMesh, QueryWorkspace, compute_sdf
+from .torchsdf import PreparedMesh, QueryWorkspace, compute_sdf, query_batch
 
 
 class TriangleMesh:
@@ -123,8 +123,12 @@ class _FusedLoop:
         # query run on beside the first (CDX_SDF_CONCURRENT=0: all three on the caller's stream)
         self.q_out = [(torch.empty(E * T, **f32), torch.empty(E * T, dtype=torch.int32, device=dev),
                        torch.empty(E * T, 3, **f32), torch.empty(E * T, 3, **f32)) for _ in range(3)]
-        self.concurrent = int(os.environ.get("CDX_SDF_CONCURRENT", "1"))  # 2 (A/B): only the targets' query on a side stream
-        if self.concurrent:
+        # 3 (default): the three queries in one launch (cdx_sdf_query_batch); 1: on three streams; 2: the targets' on
+        # a side stream only; 0: one after the other (A/B switch CDX_SDF_CONCURRENT)
+        self.concurrent = int(os.environ.get("CDX_SDF_CONCURRENT", "3"))
+        if self.concurrent == 3 and not (self.mesh.kind == N.SDF_MESH_CULLED and self.mesh_def.kind == N.SDF_MESH_CULLED):
+            self.concurrent = 1  # (a mesh with NaN-capable faces: the batch launch has no exact path)
+        if self.concurrent in (1, 2):
             self.side = [torch.cuda.Stream(device=dev) for _ in range(2)]
             self.ev = [torch.cuda.Event() for _ in range(4)]
         self.pose, self.target, self.comp = pose, target, comp
@@ -161,7 +165,15 @@ class _FusedLoop:
         self.iteration += 1
         tgt = target.view(-1, 3)
         o = self.q_out
-        if not self.concurrent:
+        if self.concurrent == 3:
+            # one launch: each culled kernel's tail (a few point groups far from the mesh) leaves most of the chip idle,
+            # which the other queries' groups fill — no side stream, no event
+            if fresh:
+                self.ws_tips.sort(tips)
+                self.ws_tgt.sort(tgt)
+            query_batch([(self.mesh_def, tips, self.ws_tips, o[0]), (self.mesh, tips, self.ws_tips, o[1]),
+                         (self.mesh, tgt, self.ws_tgt, o[2])])
+        elif not self.concurrent:
             self.mesh_def.query(tips, workspace=self.ws_tips, reuse_order=not fresh, out=o[0])
             self.mesh.query(tips, workspace=self.ws_tips, reuse_order=True, out=o[1])
             self.mesh.query(tgt, workspace=self.ws_tgt, reuse_order=not fresh, out=o[2])

@@ -98,6 +98,39 @@ class PreparedMesh:
         return dist, sign, normals, clst, face
 
 
+def query_batch(items):
+    """Several PreparedMesh queries in one launch (cdx_sdf_query_batch, ≤ 4): ``items`` = [(mesh, points, workspace,
+    out)], each workspace already holding its points' order (QueryWorkspace.sort, or a query of the same P points),
+    each mesh free of NaN-capable faces (``mesh.kind == SDF_MESH_CULLED``), ``out`` = (dist, sign, normals, clst)
+    preallocated as for PreparedMesh.query.  Outputs identical to the separate queries."""
+    if not 0 < len(items) <= 4:
+        raise RuntimeError("query_batch takes 1 to 4 queries")
+    qs = (N.CdxSdfBatchQuery * len(items))()
+    keep = []
+    dev = None
+    for d, (mesh, points, ws, out) in zip(qs, items):
+        _check(points, mesh.faces)
+        if mesh.kind != N.SDF_MESH_CULLED:
+            raise RuntimeError("query_batch: a mesh with NaN-capable faces takes PreparedMesh.query")
+        points = points.detach().contiguous()
+        P = points.shape[0]
+        dev = points.device
+        if ws.buf is None or ws.P != P:
+            raise RuntimeError("query_batch: the workspace holds no order for these points (QueryWorkspace.sort)")
+        dist, sign, normals, clst = out
+        if not (dist.shape == (P,) and sign.shape == (P,) and normals.shape == (P, 3) and clst.shape == (P, 3) and
+                dist.dtype == normals.dtype == clst.dtype == torch.float32 and sign.dtype == torch.int32 and
+                all(t.is_contiguous() and t.device == dev for t in out)):
+            raise RuntimeError("query_batch: out must be (dist [P], sign [P] int32, normals [P, 3], clst [P, 3]) float32")
+        keep.append(points)
+        d.mesh, d.faces, d.F = N.ptr(mesh.buf), N.ptr(mesh.faces), mesh.faces.shape[0]
+        d.points, d.P = N.ptr(points), P
+        d.sqdist, d.sign, d.normals, d.clst, d.face_idx = N.ptr(dist), N.ptr(sign), N.ptr(normals), N.ptr(clst), None
+        d.workspace, d.workspace_bytes = N.ptr(ws.buf), ws.buf.numel()
+        d.flags = N.SDF_REUSE_ORDER | N.SDF_MESH_CULLED
+    N.check(N.load().cdx_sdf_query_batch(len(items), C.cast(qs, C.c_void_p), N.stream_ptr(dev)), "cdx_sdf_query_batch")
+
+
 class QueryWorkspace:
     """Scratch of cdx_sdf_query (the points' Morton sort), regrown to the largest point count seen; it keeps the
     last sorted order, which a later query of P points may reuse (the same points on another mesh, or the same

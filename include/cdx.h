@@ -503,6 +503,26 @@ int cdx_sdf_query_order(const float* points, int64_t P, void* workspace, size_t 
 #define CDX_SDF_MESH_CULLED 2
 #define CDX_SDF_MESH_EXACT 4
 int cdx_sdf_mesh_flags(const void* mesh, int32_t* flags, cdx_stream_t stream);  /* waits on stream */
+/* Up to four cdx_sdf_query calls in one launch (the SDF / Kin optimisers' three queries per iteration): each with
+ * flags CDX_SDF_REUSE_ORDER | CDX_SDF_MESH_CULLED (its workspace already holds its points' order —
+ * cdx_sdf_query_order — and its mesh has no NaN-capable face); outputs identical to the separate calls. */
+typedef struct cdx_sdf_batch_query {
+  const void* mesh;
+  const float* faces;
+  int64_t F;
+  const float* points;
+  int64_t P;
+  float* sqdist;
+  int32_t* sign;
+  float* normals;
+  float* clst;
+  int32_t* face_idx; /* nullable */
+  void* workspace;
+  size_t workspace_bytes;
+  int32_t flags;
+  int32_t _pad;
+} cdx_sdf_batch_query;
+int cdx_sdf_query_batch(int32_t n, const cdx_sdf_batch_query* queries, cdx_stream_t stream);
 int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
                   int32_t* sign, float* normals, float* clst, int32_t* face_idx, void* workspace,
                   size_t workspace_bytes, int32_t flags, cdx_stream_t stream);
@@ -534,7 +554,7 @@ int cdx_profile_read(double* ms6, int64_t* count6);
  * sizeof(cdx_collision), sizeof(cdx_adam), sizeof(cdx_opt_buffers), sizeof(cdx_force_eq),
  * sizeof(cdx_screen_report), sizeof(cdx_kin_params), sizeof(cdx_kin_opt), sizeof(cdx_kin_opt_buffers)
  * — lets a binding verify its struct layouts before the first call. */
-void cdx_abi_sizes(size_t* out12);
+void cdx_abi_sizes(size_t* out13);
 
 /* Test hook: D[16×16] = A[16×4]·B[4×16] through one v_mfma_f64_16x16x4_f64 (checks the
  * fragment layout the GPIS std kernel relies on). */

@@ -258,7 +258,16 @@ def _spy_prepared_queries(monkeypatch):
         out = real(self, points, want_face, workspace, reuse_order, out)
         calls.append((points.detach().clone(), self.faces, [t.detach().clone() for t in out[:4]]))
         return out
+    real_batch = torchsdf.query_batch
+
+    def spy_batch(items):  # the fused loop's one-launch path (cdx_sdf_query_batch)
+        real_batch(items)
+        for mesh, points, _, out in items:
+            calls.append((points.detach().clone(), mesh.faces, [t.detach().clone() for t in out]))
     monkeypatch.setattr(torchsdf.PreparedMesh, "query", spy)
+    from compliancedex_amd import optimizers
+    monkeypatch.setattr(torchsdf, "query_batch", spy_batch)
+    monkeypatch.setattr(optimizers, "query_batch", spy_batch)
     return calls
 
 

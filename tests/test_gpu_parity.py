@@ -511,9 +511,9 @@ def test_sdf_prepared_mesh_equals_one_shot_and_owns_its_faces():
 
 
 def test_fused_loop_concurrent_queries_equal_sequential(monkeypatch):
-    """The fused Kin / SDF loop's three TorchSDF queries on three streams (points sorted once by
-    QueryWorkspace.sort, the full mesh's two queries on side streams) give the same bits as the three run one
-    after the other, over several iterations (fresh and reused orders, moved points)."""
+    """The fused Kin / SDF loop's three TorchSDF queries in one launch (cdx_sdf_query_batch) and on three streams
+    (points sorted once by QueryWorkspace.sort) give the same bits as the three run one after the other, over
+    several iterations (fresh and reused orders, moved points)."""
     from compliancedex_amd.optimizers import _FusedLoop
     faces = torch.from_numpy(np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))).to(DEV)
     rng = np.random.default_rng(29)
@@ -523,7 +523,7 @@ def test_fused_loop_concurrent_queries_equal_sequential(monkeypatch):
     tgt = (lo + (hi - lo) * torch.from_numpy(rng.random((E, T, 3))).to(DEV).float()).contiguous()
     z = torch.zeros(E, 3, device=DEV)
     outs = {}
-    for conc in ("1", "0"):
+    for conc in ("3", "1", "0"):
         monkeypatch.setenv("CDX_SDF_CONCURRENT", conc)
         loop = _FusedLoop(E, T, z, tgt.clone(), torch.zeros(E, T, device=DEV), faces, faces * 0.9, DEV)
         res = []
@@ -532,9 +532,10 @@ def test_fused_loop_concurrent_queries_equal_sequential(monkeypatch):
             res.append([t.clone().cpu().numpy() for t in loop.queries(moved, tgt + 1e-3 * it)])
         torch.cuda.synchronize()
         outs[conc] = res
-    for a_it, b_it in zip(outs["1"], outs["0"]):
-        for a, b in zip(a_it, b_it):
-            assert _bitwise_equal_nan_aware(a, b)
+    for conc in ("3", "1"):
+        for a_it, b_it in zip(outs[conc], outs["0"]):
+            for a, b in zip(a_it, b_it):
+                assert _bitwise_equal_nan_aware(a, b)
 
 
 def test_sdf_stale_order_gives_the_same_results():
