@@ -103,7 +103,7 @@ for STEP in "$@"; do
         grep '^{' "$OUT/digest_run_$TAG.log" | tail -1 | tee -a "$OUT/digest_$TAG.jsonl"
       done ;;
     configs)
-      timeout -k 10 600 python -u tools/bench_configs.py > "$OUT/configs_$TAG.jsonl" 2> "$OUT/configs_$TAG.log"
+      timeout -k 10 600 python -u tools/bench_configs.py --only "${CONFIGS:-c1,c2opt,c3,c4,c4loop,c5,fit}" > "$OUT/configs_$TAG.jsonl" 2> "$OUT/configs_$TAG.log"
       rc=$?; echo "configs rc=$rc"; tail -c 3000 "$OUT/configs_$TAG.jsonl"; stop_if_fault $rc ;;
     ab=*)
       IFS=, read -r -a SPECS <<< "${STEP#ab=}"
