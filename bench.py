@@ -168,17 +168,18 @@ def config4_kin(args, dev):
     tips = (DifferentiableRobotModel("iiwa7_allegro", device=dev).compute_forward_kinematics(
         res[0].detach(), links, offsets=offs)[0].view(-1, 3) + torch.from_numpy(palm).to(dev)).contiguous()
     pts = (tips, tips, res[2].detach().reshape(-1, 3).contiguous())
-    from compliancedex_amd.torchsdf import query_batch
+    from compliancedex_amd.torchsdf import BatchSchedule, query_batch
+    sched = BatchSchedule()
     P = pts[0].shape[0]
     outs = [(torch.empty(P, device=dev), torch.empty(P, dtype=torch.int32, device=dev), torch.empty(P, 3, device=dev),
              torch.empty(P, 3, device=dev)) for _ in range(3)]
 
     def three():
         """The loop's pattern on a re-sorting iteration (optimizers._FusedLoop.queries): both point sets sorted, then
-        the three queries in one launch (cdx_sdf_query_batch)."""
+        the three queries in one launch (cdx_sdf_query_batch) with the loop's schedule (heaviest groups first)."""
         ws_t.sort(tips)
         ws_g.sort(pts[2])
-        query_batch([(meshes[k], pts[k], wss[k], outs[k]) for k in range(3)])
+        query_batch([(meshes[k], pts[k], wss[k], outs[k]) for k in range(3)], schedule=sched)
     three()
     st = (ctypes.c_uint64 * 3)()
     visits = ctypes.c_uint64(0)

@@ -163,7 +163,8 @@ _SIGS = {
     "cdx_sdf_mesh_prepare": (C.c_int, [_P, _I64, _P, _P]),
     "cdx_sdf_query_workspace": (C.c_size_t, [_I64]),
     "cdx_sdf_query_order": (C.c_int, [_P, _I64, _P, C.c_size_t, _P]),
-    "cdx_sdf_query_batch": (C.c_int, [C.c_int32, _P, _P]),
+    "cdx_sdf_batch_schedule_bytes": (C.c_size_t, [C.c_int32, _P]),
+    "cdx_sdf_query_batch": (C.c_int, [C.c_int32, _P, _P, C.c_size_t, _P]),
     "cdx_sdf_query": (C.c_int, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, C.c_size_t, C.c_int32, _P]),
     "cdx_sdf_mesh_flags": (C.c_int, [_P, C.POINTER(C.c_int32), _P]),
     "cdx_version": (C.c_char_p, []),

@@ -776,19 +776,73 @@ struct SdfBatch {
   SdfBatchQ q[SDF_BATCH_MAX];
   unsigned first[SDF_BATCH_MAX];
   int n, count;
+  unsigned* sched;  // nullable: the launch schedule (below)
+  unsigned cap;     // groups the schedule holds
 };
+// Launch schedule of a batch (cdx_sdf_query_batch's `schedule`, uint32 words): [0] the group count the order below
+// is for (0: none yet), [1..3] reserved, cost[cap] (each group's duration in the last launch, 100 MHz ticks),
+// order[cap] (a permutation of the groups: heaviest first).  A group's walk time spreads 2-3× (the groups far from a
+// mesh test many more nodes); dispatched in point order, the heavy groups that start last set the launch's end.
+// Workgroup b runs group order[b], so the heaviest groups of the previous launch — the same points, or points a sort
+// later, an optimiser step away — start first and the light ones fill the tail.  Any permutation gives the same
+// outputs: every group writes only its own points.
+constexpr int SDF_SCHED_HDR = 4;
 __global__ __launch_bounds__(64 * NW, CDX_SDF_MINW) void sdf_tree_batch_kernel(SdfBatch b) {
   // the descriptors read in place from the kernel-argument segment (indexed per workgroup, a by-value copy would go
   // to scratch)
   const SdfBatch& kb = *(const SdfBatch*)(__builtin_amdgcn_kernarg_segment_ptr());
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned grp = blockIdx.x;
+  if (kb.sched && kb.sched[0] == gridDim.x) {
+    const unsigned v = kb.sched[SDF_SCHED_HDR + kb.cap + blockIdx.x];
+    grp = v < gridDim.x ? v : grp;
+  }
+  grp = __builtin_amdgcn_readfirstlane(grp);
   int qi = 0;
 #pragma unroll
   for (int i = 1; i < SDF_BATCH_MAX; ++i)
-    if (i < kb.n && blockIdx.x >= kb.first[i]) qi = i;
+    if (i < kb.n && grp >= kb.first[i]) qi = i;
   qi = __builtin_amdgcn_readfirstlane(qi);
   const SdfBatchQ& q = kb.q[qi];
   sdf_tree_body(q.points, q.P, q.porder, q.faces, q.F, q.rec, q.slab, q.chunk, q.top, q.run, q.C, q.T, q.ws,
-                q.out_dist, q.out_sign, q.out_nrm, q.out_clst, q.out_face, kb.count, (int64_t)blockIdx.x - kb.first[qi]);
+                q.out_dist, q.out_sign, q.out_nrm, q.out_clst, q.out_face, kb.count, (int64_t)grp - kb.first[qi]);
+  if (kb.sched && threadIdx.x == 0)  // (after the body's last barrier: every wave's walk is done)
+    kb.sched[SDF_SCHED_HDR + grp] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t0);
+}
+
+// The next launch's order from this launch's group durations: a counting sort on SCHED_BINS duration bins, heaviest
+// bin first (one workgroup; the order inside a bin is whatever the LDS atomics give — any order is correct).
+constexpr int SCHED_BINS = 64, SCHED_THREADS = 1024;
+__global__ __launch_bounds__(SCHED_THREADS) void sdf_batch_sched_kernel(unsigned* __restrict__ sch, unsigned G,
+                                                                        unsigned cap) {
+  __shared__ unsigned s_hist[SCHED_BINS], s_max;
+  const unsigned* cost = sch + SDF_SCHED_HDR;
+  unsigned* order = sch + SDF_SCHED_HDR + cap;
+  const unsigned t = threadIdx.x;
+  if (t < SCHED_BINS) s_hist[t] = 0u;
+  if (t == 0) s_max = 0u;
+  __syncthreads();
+  unsigned m = 0u;
+  for (unsigned g = t; g < G; g += SCHED_THREADS) m = max(m, cost[g]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+  if ((t & 63) == 0) atomicMax(&s_max, m);
+  __syncthreads();
+  const unsigned long long span = (unsigned long long)s_max + 1ull;
+  auto bin = [&](unsigned c) { return (unsigned)(SCHED_BINS - 1) - (unsigned)((unsigned long long)c * SCHED_BINS / span); };
+  for (unsigned g = t; g < G; g += SCHED_THREADS) atomicAdd(&s_hist[bin(cost[g])], 1u);
+  __syncthreads();
+  if (t == 0) {  // exclusive prefix: each bin's first position
+    unsigned acc = 0u;
+    for (int i = 0; i < SCHED_BINS; ++i) {
+      const unsigned c = s_hist[i];
+      s_hist[i] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  for (unsigned g = t; g < G; g += SCHED_THREADS) order[atomicAdd(&s_hist[bin(cost[g])], 1u)] = g;
+  if (t == 0) sch[0] = G;
 }
 
 // Brute force with the reference's tile rule: one point per lane, faces streamed through LDS
@@ -904,6 +958,14 @@ __global__ __launch_bounds__(256) void sdf_backward_kernel(const float* __restri
 }
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+bool sched_on() {  // CDX_SDF_SCHED=0: a batch ignores its schedule (point order, the A/B base)
+  static const bool on = [] {
+    const char* e = getenv("CDX_SDF_SCHED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 int sdf_mode() {  // CDX_SDF_MODE=exact forces the brute-force kernel (benchmarks, A/B tests)
   static const int m = [] {
@@ -1194,7 +1256,18 @@ int cdx_sdf_diag_wgtime(uint64_t* out, int64_t n, cdx_stream_t stream) {
 }
 #endif
 
-int cdx_sdf_query_batch(int32_t n, const cdx_sdf_batch_query* qs, cdx_stream_t stream) {
+size_t cdx_sdf_batch_schedule_bytes(int32_t n, const int64_t* P) {
+  if (n < 0 || n > SDF_BATCH_MAX || (n > 0 && !P)) return 0;
+  uint64_t groups = 0;
+  for (int i = 0; i < n; ++i) {
+    if (P[i] < 0 || P[i] > INT32_MAX) return 0;
+    groups += (uint64_t)((P[i] + 63) / 64);
+  }
+  return (size_t)(SDF_SCHED_HDR + 2 * groups) * sizeof(unsigned);
+}
+
+int cdx_sdf_query_batch(int32_t n, const cdx_sdf_batch_query* qs, void* schedule, size_t schedule_bytes,
+                        cdx_stream_t stream) {
   if (n < 0 || n > SDF_BATCH_MAX || (n > 0 && !qs)) return CDX_EINVAL;
   SdfBatch b{};
   unsigned groups = 0;
@@ -1244,7 +1317,13 @@ int cdx_sdf_query_batch(int32_t n, const cdx_sdf_batch_query* qs, cdx_stream_t s
     }
     return CDX_OK;
   }
+  if (schedule && sched_on()) {
+    if (schedule_bytes < (size_t)(SDF_SCHED_HDR + 2 * (size_t)groups) * sizeof(unsigned)) return CDX_EINVAL;
+    b.sched = static_cast<unsigned*>(schedule);
+    b.cap = groups;
+  }
   hipLaunchKernelGGL(sdf_tree_batch_kernel, dim3(groups), dim3(64 * NW), 0, s, b);
+  if (b.sched) hipLaunchKernelGGL(sdf_batch_sched_kernel, dim3(1), dim3(SCHED_THREADS), 0, s, b.sched, groups, b.cap);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 

@@ -26,7 +26,7 @@ from . import _native as N
 from .force_eq import force_eq_descriptor, force_eq_reward
 from .optimizer import EE_OFFSETS, FINGERTIP_LB, FINGERTIP_UB, WRIST_OFFSET
 from .robot_model import DifferentiableRobotModel
-from .torchsdf import PreparedMesh, QueryWorkspace, compute_sdf, query_batch
+from .torchsdf import BatchSchedule, PreparedMesh, QueryWorkspace, compute_sdf, query_batch
 
 
 class TriangleMesh:
@@ -116,6 +116,8 @@ class _FusedLoop:
         f32 = dict(dtype=torch.float32, device=dev)
         self.mesh, self.mesh_def = PreparedMesh(faces), PreparedMesh(faces_deflate)
         self.ws_tips, self.ws_tgt = QueryWorkspace(), QueryWorkspace()
+        # the batched launch's schedule (heaviest point groups of the last iteration first; CDX_SDF_SCHED=0: none)
+        self.sched = BatchSchedule()
         self.iteration = 0
         self.hist = None
         self.resort = max(1, int(os.environ.get("CDX_SDF_RESORT", "4")))  # iterations per point sort (A/B: 1)
@@ -172,7 +174,7 @@ class _FusedLoop:
                 self.ws_tips.sort(tips)
                 self.ws_tgt.sort(tgt)
             query_batch([(self.mesh_def, tips, self.ws_tips, o[0]), (self.mesh, tips, self.ws_tips, o[1]),
-                         (self.mesh, tgt, self.ws_tgt, o[2])])
+                         (self.mesh, tgt, self.ws_tgt, o[2])], schedule=self.sched)
         elif not self.concurrent:
             self.mesh_def.query(tips, workspace=self.ws_tips, reuse_order=not fresh, out=o[0])
             self.mesh.query(tips, workspace=self.ws_tips, reuse_order=True, out=o[1])

@@ -98,11 +98,30 @@ class PreparedMesh:
         return dist, sign, normals, clst, face
 
 
-def query_batch(items):
+class BatchSchedule:
+    """Device state a repeated query_batch carries from one launch to the next (cdx_sdf_query_batch's schedule): each
+    point group's walk time, and from it the next launch's order, heaviest groups first.  Regrown (zeroed) when a
+    batch with more groups comes; the outputs never depend on it."""
+
+    def __init__(self):
+        self.buf = None
+
+    def get(self, Ps, dev):
+        arr = (C.c_int64 * len(Ps))(*Ps)
+        need = N.load().cdx_sdf_batch_schedule_bytes(len(Ps), arr)
+        if need == 0:
+            raise RuntimeError("BatchSchedule: bad point counts")
+        if self.buf is None or self.buf.numel() < need or self.buf.device != dev:
+            self.buf = torch.zeros(need, dtype=torch.uint8, device=dev)
+        return self.buf
+
+
+def query_batch(items, schedule=None):
     """Several PreparedMesh queries in one launch (cdx_sdf_query_batch, ≤ 4): ``items`` = [(mesh, points, workspace,
     out)], each workspace already holding its points' order (QueryWorkspace.sort, or a query of the same P points),
     each mesh free of NaN-capable faces (``mesh.kind == SDF_MESH_CULLED``), ``out`` = (dist, sign, normals, clst)
-    preallocated as for PreparedMesh.query.  Outputs identical to the separate queries."""
+    preallocated as for PreparedMesh.query.  ``schedule``: a BatchSchedule kept across the calls of a loop (the
+    heaviest point groups of the last launch start first).  Outputs identical to the separate queries."""
     if not 0 < len(items) <= 4:
         raise RuntimeError("query_batch takes 1 to 4 queries")
     qs = (N.CdxSdfBatchQuery * len(items))()
@@ -128,7 +147,9 @@ def query_batch(items):
         d.sqdist, d.sign, d.normals, d.clst, d.face_idx = N.ptr(dist), N.ptr(sign), N.ptr(normals), N.ptr(clst), None
         d.workspace, d.workspace_bytes = N.ptr(ws.buf), ws.buf.numel()
         d.flags = N.SDF_REUSE_ORDER | N.SDF_MESH_CULLED
-    N.check(N.load().cdx_sdf_query_batch(len(items), C.cast(qs, C.c_void_p), N.stream_ptr(dev)), "cdx_sdf_query_batch")
+    sb = schedule.get([d.P for d in qs], dev) if schedule is not None else None
+    N.check(N.load().cdx_sdf_query_batch(len(items), C.cast(qs, C.c_void_p), N.ptr(sb), 0 if sb is None else sb.numel(),
+                                         N.stream_ptr(dev)), "cdx_sdf_query_batch")
 
 
 class QueryWorkspace:

@@ -522,7 +522,14 @@ typedef struct cdx_sdf_batch_query {
   int32_t flags;
   int32_t _pad;
 } cdx_sdf_batch_query;
-int cdx_sdf_query_batch(int32_t n, const cdx_sdf_batch_query* queries, cdx_stream_t stream);
+/* schedule (nullable): device bytes, all zero before their first use (at least
+ * cdx_sdf_batch_schedule_bytes(n, P) for the queries' point counts P[n]) that carry each point group's walk time from
+ * one launch to the next — the next launch of a batch with as many groups starts the heaviest groups first (the
+ * optimiser loops' same points, an iteration apart); used in stream order only, by this function only.  The outputs do
+ * not depend on it. */
+size_t cdx_sdf_batch_schedule_bytes(int32_t n, const int64_t* P);
+int cdx_sdf_query_batch(int32_t n, const cdx_sdf_batch_query* queries, void* schedule, size_t schedule_bytes,
+                        cdx_stream_t stream);
 int cdx_sdf_query(const void* mesh, const float* faces, int64_t F, const float* points, int64_t P, float* sqdist,
                   int32_t* sign, float* normals, float* clst, int32_t* face_idx, void* workspace,
                   size_t workspace_bytes, int32_t flags, cdx_stream_t stream);

@@ -44,10 +44,14 @@ def test_bad_arguments_are_rejected_without_launch():
     assert lib.cdx_sdf_query_workspace(0) == 0 and lib.cdx_sdf_mesh_bytes(0) == 0
     assert lib.cdx_sdf_mesh_prepare(None, 10, None, None) == -1
     assert lib.cdx_sdf_query_order(None, 5, None, 0, None) == -1 and lib.cdx_sdf_query_order(None, -1, None, 0, None) == -1
-    assert lib.cdx_sdf_query_batch(5, None, None) == -1 and lib.cdx_sdf_query_batch(1, None, None) == -1
+    assert lib.cdx_sdf_query_batch(5, None, None, 0, None) == -1 and lib.cdx_sdf_query_batch(1, None, None, 0, None) == -1
     q = N.CdxSdfBatchQuery()
     q.P, q.F, q.flags = 10, 4, N.SDF_REUSE_ORDER  # (not marked culled)
-    assert lib.cdx_sdf_query_batch(1, ctypes.cast(ctypes.pointer(q), ctypes.c_void_p), None) == -1
+    assert lib.cdx_sdf_query_batch(1, ctypes.cast(ctypes.pointer(q), ctypes.c_void_p), None, 0, None) == -1
+    # the launch schedule: 4 header words, then a duration and an order slot per 64-point group
+    Ps = (ctypes.c_int64 * 3)(65536, 65536, 100)
+    assert lib.cdx_sdf_batch_schedule_bytes(3, Ps) == 4 * (4 + 2 * (1024 + 1024 + 2))
+    assert lib.cdx_sdf_batch_schedule_bytes(5, Ps) == 0 and lib.cdx_sdf_batch_schedule_bytes(1, None) == 0
     cfg, buf = N.CdxKinOpt(), N.CdxKinOptBuffers()
     cfg.rule = 2
     assert lib.cdx_kin_step(None, cfg, buf, 4, 4, 0, 0, None) == -1  # unknown rule

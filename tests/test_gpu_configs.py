@@ -260,8 +260,8 @@ def _spy_prepared_queries(monkeypatch):
         return out
     real_batch = torchsdf.query_batch
 
-    def spy_batch(items):  # the fused loop's one-launch path (cdx_sdf_query_batch)
-        real_batch(items)
+    def spy_batch(items, schedule=None):  # the fused loop's one-launch path (cdx_sdf_query_batch)
+        real_batch(items, schedule=schedule)
         for mesh, points, _, out in items:
             calls.append((points.detach().clone(), mesh.faces, [t.detach().clone() for t in out]))
     monkeypatch.setattr(torchsdf.PreparedMesh, "query", spy)

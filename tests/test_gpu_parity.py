@@ -563,6 +563,44 @@ def test_sdf_stale_order_gives_the_same_results():
             assert _bitwise_equal_nan_aware(x, y)
 
 
+def test_sdf_batch_schedule_gives_the_same_results():
+    """cdx_sdf_query_batch with a launch schedule (heaviest point groups of the previous launch first): over several
+    launches — the first in point order, later ones in the schedule's order, one whose schedule was built by a
+    different batch of as many groups, and one with more groups (the schedule regrown) — every query's outputs equal
+    the separate queries' bit for bit, and the schedule's order is a permutation of the groups."""
+    from compliancedex_amd import PreparedMesh
+    from compliancedex_amd.torchsdf import BatchSchedule, QueryWorkspace, query_batch
+    faces = torch.from_numpy(np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))).to(DEV)
+    rng = np.random.default_rng(29)
+    lo, hi = faces.reshape(-1, 3).min(0)[0], faces.reshape(-1, 3).max(0)[0]
+
+    def cloud(n, pad):
+        return (lo - pad + (hi - lo + 2 * pad) * torch.from_numpy(rng.random((n, 3))).to(DEV).float()).contiguous()
+    full, small = PreparedMesh(faces), PreparedMesh((0.9 * faces).contiguous())
+
+    def outs(P):
+        return (torch.empty(P, device=DEV), torch.empty(P, dtype=torch.int32, device=DEV),
+                torch.empty(P, 3, device=DEV), torch.empty(P, 3, device=DEV))
+    sched = BatchSchedule()
+    for pts_a, pts_b in ((cloud(6000, 0.3), cloud(3000, 0.02)), (cloud(6000, 0.1), cloud(3000, 0.3)),
+                         (cloud(3000, 0.05), cloud(6000, 0.5)), (cloud(9000, 0.2), cloud(4100, 0.05))):
+        for _ in range(2):  # the second launch runs in the first one's schedule
+            wa, wb = QueryWorkspace(), QueryWorkspace()
+            wa.sort(pts_a)
+            wb.sort(pts_b)
+            items = [(small, pts_a, wa, outs(pts_a.shape[0])), (full, pts_a, wa, outs(pts_a.shape[0])),
+                     (full, pts_b, wb, outs(pts_b.shape[0]))]
+            query_batch(items, schedule=sched)
+            for mesh, pts, _, o in items:
+                ref = mesh.query(pts, workspace=QueryWorkspace())
+                for x, y in zip(o, ref[:4]):
+                    assert _bitwise_equal_nan_aware(x.cpu().numpy(), y.cpu().numpy())
+            G = sum((p.shape[0] + 63) // 64 for p in (pts_a, pts_a, pts_b))
+            words = sched.buf.view(torch.int32).cpu().numpy()
+            assert words[0] == G
+            assert np.array_equal(np.sort(words[4 + G:4 + 2 * G]), np.arange(G))  # (order after G durations)
+
+
 @pytest.mark.parametrize("path", SDF_PATHS)
 def test_sdf_nonfinite_points_take_exact_path(path):
     """A wave holding a NaN / inf / |p| > 1e4 point runs the reference tile rule."""
