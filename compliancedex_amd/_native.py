@@ -176,6 +176,9 @@ _SIGS = {
     "cdx_profile_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "cdx_kin_step": (C.c_int, [C.POINTER(CdxChain), C.POINTER(CdxKinOpt), C.POINTER(CdxKinOptBuffers), _I64, C.c_int32,
                                C.c_int32, C.c_int32, _P]),
+    "cdx_kin_iteration": (C.c_int, [C.POINTER(CdxChain), C.POINTER(CdxKinParams), C.POINTER(CdxKinOpt),
+                                    C.POINTER(CdxKinOptBuffers), _I64, C.c_int32] + [_P] * 10 +
+                          [C.c_uint64, C.c_int32, _P]),
 }
 
 _lib = None

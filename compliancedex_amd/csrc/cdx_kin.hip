@@ -27,6 +27,47 @@ __device__ __forceinline__ uint64_t kin_mix(uint64_t x) {
   return x ^ (x >> 31);
 }
 
+// Joint-angle reader over the workgroup's LDS copy of the candidate's updated row.
+struct QRowLds {
+  const float* p;
+  __device__ __forceinline__ float operator[](int i) const { return p[i]; }
+};
+
+__device__ __forceinline__ float adam_f32(float p, float g, float& m, float& v, float w1, float b2, float w2, float bc2s,
+                                          float eps, float step) {
+  // torch.optim.Adam's single-tensor / foreach update in float32 opmath: m.lerp_(g, 1 − β1);
+  // v.mul_(β2).addcmul_(g, g, 1 − β2); p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, −lr/bc1)
+  m = m + w1 * (g - m);
+  v = v * b2 + (w2 * g) * g;
+  const float denom = sqrtf(v) / bc2s + eps;
+  return p + step * (m / denom);
+}
+
+__device__ __forceinline__ float rmsprop_f32(float p, float g, float& v, float a, float w2, float eps, float lr) {
+  // torch.optim.RMSprop (no momentum, not centred): v.mul_(α).addcmul_(g, g, 1 − α); p.addcdiv_(g, sqrt(v) + eps, −lr)
+  v = v * a + (w2 * g) * g;
+  const float avg = sqrtf(v) + eps;
+  return p + lr * (g / avg);
+}
+
+// Adam's per-iteration constants (torch.optim.Adam, step count s + 1): 1 − β1, β2, 1 − β2, √(1 − β2^t) and the
+// −lr/(1 − β1^t) step sizes of the three groups, as cdx_kin_step and the fused iteration both take them.
+struct AdamConst {
+  float w1, b2, w2, bc2s, eps, sz[3];
+};
+__device__ __forceinline__ AdamConst adam_const(const cdx_kin_opt& cfg, int s) {
+  const double step = (double)(s + 1);
+  const double bc1 = 1.0 - pow(cfg.beta1, step), bc2 = 1.0 - pow(cfg.beta2, step);
+  AdamConst a;
+  a.w1 = (float)(1.0 - cfg.beta1);
+  a.b2 = (float)cfg.beta2;
+  a.w2 = (float)(1.0 - cfg.beta2);
+  a.bc2s = (float)sqrt(bc2);
+  a.eps = (float)cfg.eps;
+  for (int g = 0; g < 3; ++g) a.sz[g] = (float)(-(cfg.lr[g] / bc1));
+  return a;
+}
+
 template <int NT, int MAXD, bool FK>
 __global__ __launch_bounds__(64) void kin_cost_kernel(
     cdx_chain chain, cdx_kin_params p, int64_t E, const float* __restrict__ q, const float* __restrict__ tip,
@@ -159,16 +200,32 @@ __global__ __launch_bounds__(64) void kin_cost_kernel(
 // force-equilibrium reward and the cost terms forward and backward itself — identical inputs, identical
 // results, no divergence (the lanes would idle otherwise) — then takes its own fingertip's gradients and walks
 // its own FK chain backward; the four chains' joint gradients are summed across the lanes ((f0 + f1) + (f2 + f3)).
-template <int MAXD, bool FK>
+//
+// STEP (cdx_kin_iteration: Kin mode, Adam, no box clamp): the iteration's cdx_kin_step in the same launch — the
+// candidate's four lanes hold its loss and every gradient when the cost is done, so the best-iterate update, the
+// Adam step of the DOFs / targets / compliances each lane owns and the next fingertip's FK follow without a second
+// launch or a gradient round trip through memory.  Same operations in the same order as the two launches:
+// bit-identical parameters, best iterate and fingertips.  (q / tip / target / comp alias sb's pose / tips / target /
+// comp: a lane reads its candidate's rows before any of the candidate's lanes rewrites them.)
+template <int MAXD, bool FK, bool STEP = false>
 __global__ __launch_bounds__(64) void kin_cost4_kernel(
-    cdx_chain chain, cdx_kin_params p, int64_t E, const float* __restrict__ q, const float* __restrict__ tip,
-    const float* __restrict__ target, const float* __restrict__ comp, const int32_t* __restrict__ sign1,
+    cdx_chain chain, cdx_kin_params p, int64_t E, const float* q, const float* tip, const float* target,
+    const float* comp, const int32_t* __restrict__ sign1,
     const float* __restrict__ n1, const float* __restrict__ sqd, const int32_t* __restrict__ sign2,
     const float* __restrict__ n2, const float* __restrict__ clst, const float* __restrict__ tsqd,
     const int32_t* __restrict__ tsign, const float* __restrict__ tclst, const double* __restrict__ noise, uint64_t seed,
     double* __restrict__ loss, double* __restrict__ margin, float* __restrict__ normal_out, float* __restrict__ g_q,
-    float* __restrict__ g_target, float* __restrict__ g_comp, float* __restrict__ g_tip) {
+    float* __restrict__ g_target, float* __restrict__ g_comp, float* __restrict__ g_tip, cdx_kin_opt cfg,
+    cdx_kin_opt_buffers sb, int it) {
   constexpr int NT = 4;
+#if !defined(CDX_KIN_FK_BWD1)
+  __shared__ float s_fk[CDX_MAX_DOFS][64];  // per-DOF FK gradient contributions (then, with STEP, the summed ones)
+#endif
+  // STEP: the step's operands, prefetched (DOFs f + 4u of the candidate's row, this lane's target / compliance)
+  constexpr int PF_DOFS = CDX_MAX_DOFS / NT;
+  float pf_p[PF_DOFS], pf_m[PF_DOFS], pf_v[PF_DOFS], pf_t[3], pf_tm[3], pf_tv[3], pf_c = 0.f, pf_cm = 0.f, pf_cv = 0.f;
+  float pf_ov = 0.f;
+  unsigned pf_any = 0u;
   const int64_t tg_ = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t e_raw = tg_ >> 2;
   const int f = (int)(tg_ & 3);
@@ -254,10 +311,9 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
     v[k] = fn[k] * sm[k];
     fcost += v[k] > 1.0 ? 1.0 : v[k];
   }
-  if (on && f == 0) {
-    loss[e] = FK ? -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost + qn * 10.0
-                 : -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost;
-  }
+  const double lval = FK ? -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost + qn * 10.0
+                         : -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost;
+  if (on && f == 0) loss[e] = lval;
   double mo = 0.0;
   for (int k = 0; k < NT; ++k) mo = k == f ? fe.margin[k] : mo;
   if (on) margin[r] = mo;
@@ -302,13 +358,35 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
     cdx::fk_tip_bwd<MAXD>(chain, f, q + e * D, gpos, cdx::GqAdd{fk_g});
 #endif
 #else  // the closed-form backward (fk_tip_bwd2), per-DOF sums in LDS (a register array indexed by DOF spilled)
-    __shared__ float s_fk[CDX_MAX_DOFS][64];
     for (int i = 0; i < D; ++i) s_fk[i][threadIdx.x] = 0.f;
     const float gpos[3] = {(float)gto[0], (float)gto[1], (float)gto[2]};
 #if !defined(CDX_KIN_DIAG_NOFK)
     // the chain read in place from the kernel-argument segment (it is the first argument, at offset 0): indexed by a
     // per-lane body index, the by-value copy went to scratch (≈ 2 KB per lane) in the deep-chain instantiation
     const cdx_chain& kc = *(const cdx_chain*)(__builtin_amdgcn_kernarg_segment_ptr());
+    if constexpr (STEP) {
+      // the step's operands, loaded now so that their latency hides under the FK backward (the kernel runs at one
+      // wave per SIMD): none of them is written before the step reads it
+      pf_any = it > 0 ? sb.any[(it - 1) % 3] : 0u;
+      pf_ov = sb.opt_value[e];
+#pragma unroll
+      for (int u = 0; u < PF_DOFS; ++u) {
+        const int i = f + NT * u;
+        const int64_t k = e * D + (i < D ? i : f);
+        pf_p[u] = sb.pose[k];
+        pf_m[u] = sb.m_pose[k];
+        pf_v[u] = sb.v_pose[k];
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        pf_t[i] = sb.target[3 * r + i];
+        pf_tm[i] = sb.m_target[3 * r + i];
+        pf_tv[i] = sb.v_target[3 * r + i];
+      }
+      pf_c = sb.comp[r];
+      pf_cm = sb.m_comp[r];
+      pf_cv = sb.v_comp[r];
+    }
     cdx::fk_tip_bwd2<MAXD>(kc, f, q + e * D, gpos, [&](int d, float v) { s_fk[d][threadIdx.x] += v; });
 #endif
     float* fk_g = nullptr;
@@ -322,18 +400,87 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
 #endif
       s += __shfl_xor(s, 1);
       s += __shfl_xor(s, 2);
-      if ((i & 3) == f && on) {
+      if ((i & 3) == f) {
         const double d = (double)q[e * D + i] - (double)p.ref_q[i];
         const float gq = qn > 0 ? (float)(10.0 * d / qn) : 0.f;
-        g_q[e * D + i] = gq + s;
+        if (on) g_q[e * D + i] = gq + s;
+#if !defined(CDX_KIN_FK_BWD1)
+        if constexpr (STEP) s_fk[i][threadIdx.x] = gq + s;  // (this lane's own slot: the step below reads it)
+#endif
       }
     }
   }
-  if (!on) return;
-  if (g_tip)
-    for (int i = 0; i < 3; ++i) g_tip[3 * r + i] = (float)gto[i];
-  g_comp[r] = (float)gco;
-  for (int i = 0; i < 3; ++i) g_target[3 * r + i] = (float)ggo[i];
+  if (on) {
+    if (g_tip)
+      for (int i = 0; i < 3; ++i) g_tip[3 * r + i] = (float)gto[i];
+    g_comp[r] = (float)gco;
+    for (int i = 0; i < 3; ++i) g_target[3 * r + i] = (float)ggo[i];
+  }
+#if !defined(CDX_KIN_FK_BWD1)
+  if constexpr (STEP && FK) {
+    // ---- cdx_kin_step's iteration `it` (kin_step_kernel, rule 0, T = 4): the previous iteration's margin / normal
+    // commit, the best iterate, Adam, the next fingertip
+    if (pf_any && on) {
+      const bool ps = ((it - 1) & 1) != 0;
+      const double* mg = ps ? sb.margin[1] : sb.margin[0];
+      const float* nm = ps ? sb.normal[1] : sb.normal[0];
+      sb.opt_margin[r] = mg[r];
+      for (int i = 0; i < 3; ++i) sb.opt_normal[3 * r + i] = nm[3 * r + i];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) sb.any[(it + 1) % 3] = 0u;
+    const bool flag = on && lval < (double)pf_ov;
+    if (flag) {
+      if (f == 0) sb.opt_value[e] = (float)lval;
+#pragma unroll
+      for (int u = 0; u < PF_DOFS; ++u)
+        if (f + NT * u < D) sb.opt_pose[e * D + f + NT * u] = pf_p[u];
+      for (int i = 0; i < 3; ++i) sb.opt_target[3 * r + i] = pf_t[i];
+      sb.opt_comp[r] = pf_c;
+    }
+    if (__any(flag) && threadIdx.x == 0) atomicOr(sb.any + it % 3, 1u);
+    const AdamConst ac = adam_const(cfg, it);
+    __shared__ float s_qn[64 / NT][CDX_MAX_DOFS];  // the candidates' updated joint rows, for the FK
+    float* qs = s_qn[threadIdx.x / NT];
+#pragma unroll
+    for (int u = 0; u < PF_DOFS; ++u) {
+      const int i = f + NT * u;
+      if (i >= D) break;
+      float qv = pf_p[u];
+      if (cfg.lr[0] != 0.0) {
+        float m = pf_m[u], v = pf_v[u];
+        qv = adam_f32(qv, s_fk[i][threadIdx.x], m, v, ac.w1, ac.b2, ac.w2, ac.bc2s, ac.eps, ac.sz[0]);
+        if (on) {
+          sb.m_pose[e * D + i] = m;
+          sb.v_pose[e * D + i] = v;
+        }
+      }
+      if (on) sb.pose[e * D + i] = qv;
+      qs[i] = qv;
+    }
+    if (on) {
+      if (cfg.lr[1] != 0.0)
+        for (int i = 0; i < 3; ++i) {
+          float m = pf_tm[i], v = pf_tv[i];
+          sb.target[3 * r + i] = adam_f32(pf_t[i], (float)ggo[i], m, v, ac.w1, ac.b2, ac.w2, ac.bc2s, ac.eps, ac.sz[1]);
+          sb.m_target[3 * r + i] = m;
+          sb.v_target[3 * r + i] = v;
+        }
+      if (cfg.lr[2] != 0.0) {
+        float m = pf_cm, v = pf_cv;
+        sb.comp[r] = adam_f32(pf_c, (float)gco, m, v, ac.w1, ac.b2, ac.w2, ac.bc2s, ac.eps, ac.sz[2]);
+        sb.m_comp[r] = m;
+        sb.v_comp[r] = v;
+      }
+    }
+    __syncthreads();
+    if (on && sb.tips) {
+      const cdx_chain& kc = *(const cdx_chain*)(__builtin_amdgcn_kernarg_segment_ptr());
+      float pos[3];
+      cdx::fk_tip(kc, f, QRowLds{qs}, pos, nullptr);
+      for (int i = 0; i < 3; ++i) sb.tips[3 * r + i] = pos[i] + cfg.palm_offset[i];
+    }
+  }
+#endif
 }
 
 }  // namespace
@@ -365,7 +512,7 @@ extern "C" int cdx_kin_cost(const cdx_chain* chain, const cdx_kin_params* p, int
 #define CDX_KIN4_LAUNCH(MAXD, FK)                                                                                      \
   hipLaunchKernelGGL((kin_cost4_kernel<MAXD, FK>), dim3((unsigned)((4 * E + 63) / 64)), dim3(64), 0, s, c, *p, E, q, tip, \
                      target, comp, sign1, n1, sqdist, sign2, n2, clst, tsqdist, tsign, tclst, noise, seed, loss, margin,   \
-                     normal, g_q, g_target, g_comp, g_tip)
+                     normal, g_q, g_target, g_comp, g_tip, cdx_kin_opt{}, cdx_kin_opt_buffers{}, 0)
 #if defined(CDX_KIN_1LANE)  // A/B: one lane per candidate for four fingertips too (round 4)
   if (!chain && T == 4) CDX_KIN_LAUNCH(4, 8, false);
   else if (!chain) CDX_KIN_LAUNCH(0, 8, false);
@@ -389,28 +536,6 @@ extern "C" int cdx_kin_cost(const cdx_chain* chain, const cdx_kin_params* p, int
 // (candidate e, tip f), T to a candidate, 64 / T candidates to a 64-thread workgroup.
 namespace {
 
-// Joint-angle reader over the workgroup's LDS copy of the candidate's updated row.
-struct QRowLds {
-  const float* p;
-  __device__ __forceinline__ float operator[](int i) const { return p[i]; }
-};
-
-__device__ __forceinline__ float adam_f32(float p, float g, float& m, float& v, float w1, float b2, float w2, float bc2s,
-                                          float eps, float step) {
-  // torch.optim.Adam's single-tensor / foreach update in float32 opmath: m.lerp_(g, 1 − β1);
-  // v.mul_(β2).addcmul_(g, g, 1 − β2); p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, −lr/bc1)
-  m = m + w1 * (g - m);
-  v = v * b2 + (w2 * g) * g;
-  const float denom = sqrtf(v) / bc2s + eps;
-  return p + step * (m / denom);
-}
-
-__device__ __forceinline__ float rmsprop_f32(float p, float g, float& v, float a, float w2, float eps, float lr) {
-  // torch.optim.RMSprop (no momentum, not centred): v.mul_(α).addcmul_(g, g, 1 − α); p.addcdiv_(g, sqrt(v) + eps, −lr)
-  v = v * a + (w2 * g) * g;
-  const float avg = sqrtf(v) + eps;
-  return p + lr * (g / avg);
-}
 
 __global__ __launch_bounds__(64) void kin_step_kernel(cdx_chain chain, cdx_kin_opt cfg, cdx_kin_opt_buffers b, int64_t E,
                                                       int T, int D, int s, int finalize) {
@@ -547,5 +672,54 @@ extern "C" int cdx_kin_step(const cdx_chain* chain, const cdx_kin_opt* cfg, cons
   const cdx_chain c = chain ? *chain : cdx_chain{};
   hipLaunchKernelGGL(kin_step_kernel, dim3((unsigned)((E + G - 1) / G)), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
                      c, *cfg, b, E, (int)n_tips, kin ? (int)chain->n_dofs : 0, (int)iteration, (int)finalize);
+  return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
+}
+
+// One optimiser iteration: cdx_kin_cost then cdx_kin_step on the parameters / slots in `buf` — in ONE launch
+// (kin_cost4_kernel<…, STEP>) for the Kin optimiser's case (chain, four fingertips, Adam, no box clamp), else the two
+// launches.
+
+extern "C" int cdx_kin_iteration(const cdx_chain* chain, const cdx_kin_params* p, const cdx_kin_opt* cfg,
+                                 const cdx_kin_opt_buffers* buf, int64_t E, int32_t n_tips, const int32_t* sign1,
+                                 const float* n1, const float* sqdist, const int32_t* sign2, const float* n2,
+                                 const float* clst, const float* tsqdist, const int32_t* tsign, const float* tclst,
+                                 const double* noise, uint64_t seed, int32_t iteration, cdx_stream_t stream) {
+  if (!p || !cfg || !buf || iteration < 0 || (cfg->rule != 0 && cfg->rule != 1) || n_tips != p->fe.n_tips) return CDX_EINVAL;
+  const cdx_kin_opt_buffers& b = *buf;
+  const bool kin = cfg->rule == 0;
+  if (kin && (!chain || !b.tips)) return CDX_EINVAL;
+  float* g_pose = const_cast<float*>(b.g_pose);
+  float* g_target = const_cast<float*>(b.g_target);
+  float* g_comp = const_cast<float*>(b.g_comp);
+  double* loss = const_cast<double*>(b.loss);
+  double* margin = b.margin[iteration & 1];
+  float* normal = b.normal[iteration & 1];
+  const bool fuse = kin && n_tips == 4 && !cfg->clamp_box;
+  if (!fuse) {
+    int rc = cdx_kin_cost(kin ? chain : nullptr, p, E, kin ? b.pose : nullptr, kin ? b.tips : b.pose, b.target, b.comp,
+                          sign1, n1, sqdist, sign2, n2, clst, tsqdist, tsign, tclst, noise, seed, loss, margin, normal,
+                          kin ? g_pose : nullptr, g_target, g_comp, kin ? nullptr : g_pose, stream);
+    if (rc) return rc;
+    return cdx_kin_step(kin ? chain : nullptr, cfg, buf, E, n_tips, iteration, 0, stream);
+  }
+  // the two calls' argument checks
+  if (chain->n_tips != 4 || chain->n_dofs < 1 || chain->n_dofs > CDX_MAX_DOFS || chain->n_bodies < 1 ||
+      chain->n_bodies > CDX_MAX_BODIES || E < 0)
+    return CDX_EINVAL;
+  if (E == 0) return CDX_OK;
+  if (!b.pose || !b.target || !b.comp || !g_pose || !g_target || !g_comp || !b.m_pose || !b.v_pose || !b.m_target ||
+      !b.v_target || !b.m_comp || !b.v_comp || !loss || !margin || !normal || !b.margin[0] || !b.margin[1] ||
+      !b.normal[0] || !b.normal[1] || !b.opt_value || !b.opt_margin || !b.opt_normal || !b.opt_pose || !b.opt_target ||
+      !b.opt_comp || !b.any || !sign1 || !n1 || !sqdist || !sign2 || !n2 || !clst || !tsqdist || !tsign || !tclst)
+    return CDX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)((4 * E + 63) / 64));
+#define CDX_KIN4_STEP_LAUNCH(MAXD)                                                                                    \
+  hipLaunchKernelGGL((kin_cost4_kernel<MAXD, true, true>), grid, dim3(64), 0, s, *chain, *p, E, b.pose, b.tips,        \
+                     b.target, b.comp, sign1, n1, sqdist, sign2, n2, clst, tsqdist, tsign, tclst, noise, seed, loss,     \
+                     margin, normal, g_pose, g_target, g_comp, nullptr, *cfg, b, (int)iteration)
+  if (cdx::chain_max_depth(*chain) <= 8) CDX_KIN4_STEP_LAUNCH(8);
+  else CDX_KIN4_STEP_LAUNCH(CDX_MAX_DEPTH);
+#undef CDX_KIN4_STEP_LAUNCH
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }

@@ -336,6 +336,7 @@ class KinGraspOptimizer:
             cfg.palm_offset[i] = off[i]
         st = _FusedLoop(E, T, q, tgt, comp, faces, faces_deflate, dev)
         st.buffers.tips = N.ptr(st.tips)
+        one_launch = os.environ.get("CDX_KIN_FUSED_STEP", "1") != "0"  # (A/B: cdx_kin_cost + cdx_kin_step)
         stream = N.stream_ptr(dev)
         N.check(lib.cdx_fk_forward(chain, N.ptr(q), E, N.ptr(st.tips), None, stream), "cdx_fk_forward")
         st.tips.add_(self.palm_offset.float())  # FK + palm offset (:148); later iterations: cdx_kin_step
@@ -346,17 +347,22 @@ class KinGraspOptimizer:
             nz = None if nz is None else nz.detach().to(device=dev, dtype=torch.float64).contiguous()
             self._seed += 1
             loss = st.loss_slot(s, self.num_iters)
-            N.check(lib.cdx_kin_cost(chain, prm, E, N.ptr(q), N.ptr(st.tips), N.ptr(tgt), N.ptr(comp),
-                                     *(N.ptr(t) for t in st.queries(st.tips, tgt)), N.ptr(nz), self._seed,
-                                     N.ptr(loss), N.ptr(st.margin[s & 1]), N.ptr(st.normal[s & 1]), N.ptr(st.g[0]),
-                                     N.ptr(st.g[1]), N.ptr(st.g[2]), None, stream), "cdx_kin_cost")
+            qr = [N.ptr(t) for t in st.queries(st.tips, tgt)]
+            if not verbose and one_launch:  # cost, backward and step in one launch (cdx_kin_iteration)
+                N.check(lib.cdx_kin_iteration(chain, prm, cfg, st.buffers, E, T, *qr, N.ptr(nz), self._seed, s, stream),
+                        "cdx_kin_iteration")
+            else:  # two launches (verbose: the compliances printed before the step, as the reference prints them)
+                N.check(lib.cdx_kin_cost(chain, prm, E, N.ptr(q), N.ptr(st.tips), N.ptr(tgt), N.ptr(comp), *qr,
+                                         N.ptr(nz), self._seed, N.ptr(loss), N.ptr(st.margin[s & 1]),
+                                         N.ptr(st.normal[s & 1]), N.ptr(st.g[0]), N.ptr(st.g[1]), N.ptr(st.g[2]), None,
+                                         stream), "cdx_kin_cost")
+                if verbose:
+                    print("Loss:", float(loss.sum()), comp)
+                N.check(lib.cdx_kin_step(chain, cfg, st.buffers, E, T, s, 0, stream), "cdx_kin_step")
             if st.hist is None:
                 self.loss_history.append(loss.sum())  # device scalar, no sync
             if trace_rows:
                 self.loss_rows.append(loss.clone())
-            if verbose:
-                print("Loss:", float(loss.sum()), comp)
-            N.check(lib.cdx_kin_step(chain, cfg, st.buffers, E, T, s, 0, stream), "cdx_kin_step")
         N.check(lib.cdx_kin_step(chain, cfg, st.buffers, E, T, self.num_iters, 1, stream), "cdx_kin_step")
         st.loss_sums(self.loss_history)
         if self.loop_events:

@@ -395,6 +395,15 @@ typedef struct {                          /* device pointers, candidate-major */
 
 int cdx_kin_step(const cdx_chain* chain, const cdx_kin_opt* cfg, const cdx_kin_opt_buffers* buf, int64_t E,
                  int32_t n_tips, int32_t iteration, int32_t finalize, cdx_stream_t stream);
+/* One whole optimiser iteration on the loop state in `buf`: cdx_kin_cost (q = pose, tip = tips for rule 0 / tip = pose
+ * for rule 1; loss, margin[iteration & 1], normal[iteration & 1] and the g_* gradients into buf's buffers) followed by
+ * cdx_kin_step(iteration, finalize = 0).  The Kin optimiser's case (chain, four fingertips, rule 0, no clamp_box) runs
+ * as ONE launch with the same results as the two; other cases run the two launches.  chain: rule 0 only. */
+int cdx_kin_iteration(const cdx_chain* chain, const cdx_kin_params* p, const cdx_kin_opt* cfg,
+                      const cdx_kin_opt_buffers* buf, int64_t E, int32_t n_tips, const int32_t* sign1, const float* n1,
+                      const float* sqdist, const int32_t* sign2, const float* n2, const float* clst,
+                      const float* tsqdist, const int32_t* tsign, const float* tclst, const double* noise,
+                      uint64_t seed, int32_t iteration, cdx_stream_t stream);
 
 /* ------------------------------------------------------------ collision loss -------
  * Replaces ProbabilisticGraspOptimizer.compute_collision_loss (optimize_pregrasp.py:671-701):

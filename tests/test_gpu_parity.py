@@ -538,6 +538,43 @@ def test_fused_loop_concurrent_queries_equal_sequential(monkeypatch):
                 assert _bitwise_equal_nan_aware(a, b)
 
 
+@pytest.mark.parametrize("robot", ["iiwa7_allegro", "allegro"])
+def test_kin_one_launch_iteration_equals_two_launches(monkeypatch, robot):
+    """cdx_kin_iteration's one-launch Kin iteration (cost, backward, best iterate, Adam and the next fingertips in
+    kin_cost4_kernel<…, STEP>) against cdx_kin_cost + cdx_kin_step (CDX_KIN_FUSED_STEP=0): the per-iteration losses,
+    the best iterate, its loss, margins and normals and the final parameters are the same bits — on the deep
+    iiwa7_allegro chain (MAXD 16) and the shallow Allegro hand (MAXD 8)."""
+    from compliancedex_amd import KinGraspOptimizer
+    from compliancedex_amd.urdf import load_robot
+    from compliancedex_amd.workloads import banana_mesh, config4_kin_inputs
+    E = 3000
+    links, offs, palm, q, target, comp = config4_kin_inputs(E, device=DEV, q_scale=0.3)
+    if robot == "allegro":
+        cfg = load_robot("allegro")["config"]
+        links, offs = cfg["ee_link_name"], cfg["ee_link_offset"]
+        q = q[:, :16].copy()
+    D = q.shape[1]
+    outs = {}
+    for one in ("1", "0"):
+        monkeypatch.setenv("CDX_KIN_FUSED_STEP", one)
+        kin = KinGraspOptimizer(robot, links, offs, palm_offset=palm.tolist(), num_iters=7, optimize_target=True,
+                                ref_q=[0.0] * D, seed=5)
+        args = [torch.from_numpy(a).to(DEV) for a in (q, target, comp)]
+        res = kin.optimize(*args, 1.0, banana_mesh(), verbose=False, trace_rows=True)
+        torch.cuda.synchronize()
+        outs[one] = ([t.cpu().numpy() for t in res[:3]] + [bool(res[3])] + [kin.best_loss.cpu().numpy()] +
+                     [r.cpu().numpy() for r in kin.loss_rows])
+    assert len(outs["1"]) == len(outs["0"])
+    for a, b in zip(outs["1"], outs["0"]):
+        if isinstance(a, bool):
+            assert a == b
+        elif a.dtype == np.float64:
+            assert np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(a.view(np.uint64)[~np.isnan(a)],
+                                                                                b.view(np.uint64)[~np.isnan(b)])
+        else:
+            assert _bitwise_equal_nan_aware(a, b)
+
+
 def test_sdf_stale_order_gives_the_same_results():
     """CDX_SDF_REUSE_ORDER with an order sorted for OTHER points (a fused loop re-sorts its query points only every
     few iterations): the results equal a fresh sort's bit for bit — moved points, shuffled points, and points
