@@ -59,6 +59,12 @@ def test_bad_arguments_are_rejected_without_launch():
     assert lib.cdx_kin_step(None, cfg, buf, 4, 4, 0, 0, None) == -1  # Adam (Kin) without a chain
     cfg.rule = 1
     assert lib.cdx_kin_step(None, cfg, buf, 4, 4, 0, 0, None) == -1  # null buffers
+    prm = N.CdxKinParams()
+    prm.fe.n_tips = 4
+    assert lib.cdx_kin_iteration(None, None, cfg, buf, 4, 4, *[None] * 10, 0, 0, None) == -1  # no params
+    cfg.rule = 0
+    assert lib.cdx_kin_iteration(None, prm, cfg, buf, 4, 4, *[None] * 10, 0, 0, None) == -1  # Kin without a chain
+    assert lib.cdx_kin_iteration(c, prm, cfg, buf, 4, 3, *[None] * 10, 0, 0, None) == -1  # tip count mismatch
     p = N.CdxProblem()
     assert lib.cdx_closure_workspace(p, 10) == 0
     assert lib.cdx_closure(p, 10, *([None] * 6), ctypes.c_uint64(0), *([None] * 11)) == -1
