@@ -126,7 +126,7 @@ SDF_FLOPS_PER_PAIR = 46       # face_dist2's usual branch, 3 IEEE divisions coun
 def config4_kin(args, dev):
     """Config 4's SDF leg (BASELINE configs[3]: iiwa7_allegro arm + hand, TorchSDF on): the fused KinGraspOptimizer
     loop (optimize_pregrasp.py:183-223) at E = 16 384 candidates on the 16 384-face banana — per iteration three
-    TorchSDF queries on prepared meshes (3 × 65 536 points), cdx_kin_cost, cdx_kin_step — timed over
+    TorchSDF queries on prepared meshes (3 × 65 536 points) and cdx_kin_iteration (cost, backward and step) — timed over
     ``--config4-iters`` iterations after a warm-up call (HIP events on the loop's stream), then the three queries
     of one iteration alone (the TorchSDF forward) and the culled kernel's work counters."""
     import copy
@@ -202,12 +202,14 @@ def config4_kin(args, dev):
     return {"workload": "config 4: KinGraspOptimizer (fused) on iiwa7_allegro (23 DOF, chain depth 13), "
                         f"E={E} candidates, 16 384-face banana mesh, optimize_target, 3 TorchSDF queries per iteration",
             "iterations": iters, "ms_per_iteration": ms_iter, "evals_per_s": E / (ms_iter * 1e-3),
-            "launches_per_iteration": "3 TorchSDF queries in one launch (sdf_tree_batch_kernel; the fingertips' and the "
-                                      "targets' Morton order — bbox partials, keys, an 18-bit radix sort — every 4th "
-                                      "iteration) + cdx_kin_cost + cdx_kin_step",
+            "launches_per_iteration": "3 TorchSDF queries in one launch (sdf_tree_batch_kernel, heaviest point groups of "
+                                      "the last iteration first, + its one-workgroup schedule kernel; the fingertips' and "
+                                      "the targets' Morton order — bbox partials, keys, an 18-bit radix sort — every 16th "
+                                      "iteration) + cdx_kin_iteration (cost, backward, best iterate, Adam, next "
+                                      "fingertips: one launch)",
             "roofline_sdf": {"bound": "valu", "kernel": "sdf_tree_kernel (+ per-query bbox, Morton keys, radix sort)",
                              "fwd_3calls_ms": fwd_ms, "fwd_pattern": "both point sets sorted, the three queries in one launch (the "
-                                                               "loop's iterations re-sort every 4th)", "points": n_pts, "faces": F, "brute_force_pairs": brute,
+                                                               "loop's iterations re-sort every 16th)", "points": n_pts, "faces": F, "brute_force_pairs": brute,
                              "pairs_evaluated": int(st[0]), "pairs_exact_path": int(st[1]),
                              "pairs_per_point": int(st[0]) / max(1, n_pts),
                              "chunk_visits_per_wave": int(visits.value) / max(1, (n_pts + 63) // 64),

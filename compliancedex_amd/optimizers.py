@@ -120,7 +120,9 @@ class _FusedLoop:
         self.sched = BatchSchedule()
         self.iteration = 0
         self.hist = None
-        self.resort = max(1, int(os.environ.get("CDX_SDF_RESORT", "4")))  # iterations per point sort (A/B: 1)
+        # iterations per point sort: 16 (A/B with the batched launch's schedule, profiles/r05ba_config4_resort_sched_ab.jsonl:
+        # 4 / 8 / 16 / never = 0.327 / 0.316 / 0.316 / 0.311 ms around the mesh, 0.461 / 0.445 / 0.442 / 0.469 far)
+        self.resort = max(1, int(os.environ.get("CDX_SDF_RESORT", "16")))
         # the three queries' outputs (dist, sign, normals, clst), and the two side streams the second and third
         # query run on beside the first (CDX_SDF_CONCURRENT=0: all three on the caller's stream)
         self.q_out = [(torch.empty(E * T, **f32), torch.empty(E * T, dtype=torch.int32, device=dev),
