@@ -409,7 +409,11 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
           ssel = gv.std_[qsel];
           lsel = log(100 * ssel);  // the level loss's max_f log(100·std_f)
           if (qsel == cdx::q_alltip(u, e, f, E, T)) {
+#if defined(CDX_COMBINE_DIAG_NOFOLD)  // (timing-only diagnostic build: outputs wrong)
+            if (false)
+#else
             if (gv.fold.partial)
+#endif
               cdx::grad_fold_gstd(gv.fold, m, gv.var[qsel], gs3);
             else
               for (int i = 0; i < 3; ++i) gs3[i] = gv.gstd[3 * qsel + i];
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
     const cdx_chain& kc = (*(const cdx_problem*)(__builtin_amdgcn_kernarg_segment_ptr())).chain;
 #if defined(CDX_COMBINE_FK_BWD1)  // (A/B: the stored-rotations backward walk)
     cdx::fk_tip_bwd<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
-#else
+#elif !defined(CDX_COMBINE_DIAG_NOFK)  // (timing-only diagnostic build without the FK backward: outputs wrong)
     cdx::fk_tip_bwd2<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
 #endif
   }
