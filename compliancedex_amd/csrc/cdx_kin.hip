@@ -481,6 +481,54 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
     }
   }
 #endif
+  if constexpr (STEP && !FK) {
+    // ---- cdx_kin_step's iteration `it` for the SDF optimiser (kin_step_kernel, rule 1, T = 4): the previous
+    // iteration's margin / normal commit, the best iterate, RMSprop on this lane's fingertip / target / compliance,
+    // the box clamps
+    const float pv[3] = {sb.pose[3 * r], sb.pose[3 * r + 1], sb.pose[3 * r + 2]};
+    const float tv[3] = {sb.target[3 * r], sb.target[3 * r + 1], sb.target[3 * r + 2]};
+    const float cv = sb.comp[r];
+    if (it > 0 && sb.any[(it - 1) % 3] && on) {
+      const bool ps = ((it - 1) & 1) != 0;
+      const double* mg = ps ? sb.margin[1] : sb.margin[0];
+      const float* nm = ps ? sb.normal[1] : sb.normal[0];
+      sb.opt_margin[r] = mg[r];
+      for (int i = 0; i < 3; ++i) sb.opt_normal[3 * r + i] = nm[3 * r + i];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) sb.any[(it + 1) % 3] = 0u;
+    const bool flag = on && lval < (double)sb.opt_value[e];
+    if (flag) {
+      if (f == 0) sb.opt_value[e] = (float)lval;
+      for (int i = 0; i < 3; ++i) {
+        sb.opt_pose[3 * r + i] = pv[i];
+        sb.opt_target[3 * r + i] = tv[i];
+      }
+      sb.opt_comp[r] = cv;
+    }
+    if (__any(flag) && threadIdx.x == 0) atomicOr(sb.any + it % 3, 1u);
+    if (on) {
+      const float a = (float)cfg.alpha, w2 = (float)(1.0 - cfg.alpha), eps = (float)cfg.eps;
+      auto upd = [&](float* pp, float p0, float g, float* vv, int64_t k, int grp) {
+        if (cfg.lr[grp] == 0.0) return;
+        float v = vv[k];
+        pp[k] = rmsprop_f32(p0, g, v, a, w2, eps, (float)(-cfg.lr[grp]));
+        vv[k] = v;
+      };
+      for (int i = 0; i < 3; ++i) upd(sb.pose, pv[i], (float)gto[i], sb.v_pose, 3 * r + i, 0);
+      for (int i = 0; i < 3; ++i) upd(sb.target, tv[i], (float)ggo[i], sb.v_target, 3 * r + i, 1);
+      upd(sb.comp, cv, (float)gco, sb.v_comp, r, 2);
+      if (cfg.clamp_box)  // (:312-314) torch.clamp: NaN stays NaN
+        for (int i = 0; i < 3; ++i) {
+          const float lo = cfg.box_lb[3 * f + i], hi = cfg.box_ub[3 * f + i];
+          float x = sb.target[3 * r + i];
+          x = x < lo ? lo : x;
+          sb.target[3 * r + i] = x > hi ? hi : x;
+          float y = sb.pose[3 * r + i];
+          y = y < lo ? lo : y;
+          sb.pose[3 * r + i] = y > hi ? hi : y;
+        }
+    }
+  }
 }
 
 }  // namespace
@@ -694,7 +742,8 @@ extern "C" int cdx_kin_iteration(const cdx_chain* chain, const cdx_kin_params* p
   double* loss = const_cast<double*>(b.loss);
   double* margin = b.margin[iteration & 1];
   float* normal = b.normal[iteration & 1];
-  const bool fuse = kin && n_tips == 4 && !cfg->clamp_box;
+  // one launch: the Kin optimiser (chain, Adam, no box clamp) or the SDF optimiser (no chain, RMSprop), four tips
+  const bool fuse = n_tips == 4 && (kin ? !cfg->clamp_box : !chain);
   if (!fuse) {
     int rc = cdx_kin_cost(kin ? chain : nullptr, p, E, kin ? b.pose : nullptr, kin ? b.tips : b.pose, b.target, b.comp,
                           sign1, n1, sqdist, sign2, n2, clst, tsqdist, tsign, tclst, noise, seed, loss, margin, normal,
@@ -703,12 +752,13 @@ extern "C" int cdx_kin_iteration(const cdx_chain* chain, const cdx_kin_params* p
     return cdx_kin_step(kin ? chain : nullptr, cfg, buf, E, n_tips, iteration, 0, stream);
   }
   // the two calls' argument checks
-  if (chain->n_tips != 4 || chain->n_dofs < 1 || chain->n_dofs > CDX_MAX_DOFS || chain->n_bodies < 1 ||
-      chain->n_bodies > CDX_MAX_BODIES || E < 0)
+  if (E < 0 || (kin && (chain->n_tips != 4 || chain->n_dofs < 1 || chain->n_dofs > CDX_MAX_DOFS ||
+                        chain->n_bodies < 1 || chain->n_bodies > CDX_MAX_BODIES)))
     return CDX_EINVAL;
   if (E == 0) return CDX_OK;
-  if (!b.pose || !b.target || !b.comp || !g_pose || !g_target || !g_comp || !b.m_pose || !b.v_pose || !b.m_target ||
-      !b.v_target || !b.m_comp || !b.v_comp || !loss || !margin || !normal || !b.margin[0] || !b.margin[1] ||
+  if (!b.pose || !b.target || !b.comp || !g_pose || !g_target || !g_comp || (kin && (!b.m_pose || !b.m_target)) ||
+      !b.v_pose ||
+      !b.v_target || (kin && !b.m_comp) || !b.v_comp || !loss || !margin || !normal || !b.margin[0] || !b.margin[1] ||
       !b.normal[0] || !b.normal[1] || !b.opt_value || !b.opt_margin || !b.opt_normal || !b.opt_pose || !b.opt_target ||
       !b.opt_comp || !b.any || !sign1 || !n1 || !sqdist || !sign2 || !n2 || !clst || !tsqdist || !tsign || !tclst)
     return CDX_EINVAL;
@@ -718,7 +768,11 @@ extern "C" int cdx_kin_iteration(const cdx_chain* chain, const cdx_kin_params* p
   hipLaunchKernelGGL((kin_cost4_kernel<MAXD, true, true>), grid, dim3(64), 0, s, *chain, *p, E, b.pose, b.tips,        \
                      b.target, b.comp, sign1, n1, sqdist, sign2, n2, clst, tsqdist, tsign, tclst, noise, seed, loss,     \
                      margin, normal, g_pose, g_target, g_comp, nullptr, *cfg, b, (int)iteration)
-  if (cdx::chain_max_depth(*chain) <= 8) CDX_KIN4_STEP_LAUNCH(8);
+  if (!kin)
+    hipLaunchKernelGGL((kin_cost4_kernel<8, false, true>), grid, dim3(64), 0, s, cdx_chain{}, *p, E, nullptr, b.pose,
+                       b.target, b.comp, sign1, n1, sqdist, sign2, n2, clst, tsqdist, tsign, tclst, noise, seed, loss,
+                       margin, normal, nullptr, g_target, g_comp, g_pose, *cfg, b, (int)iteration);
+  else if (cdx::chain_max_depth(*chain) <= 8) CDX_KIN4_STEP_LAUNCH(8);
   else CDX_KIN4_STEP_LAUNCH(CDX_MAX_DEPTH);
 #undef CDX_KIN4_STEP_LAUNCH
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;

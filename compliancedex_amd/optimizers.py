@@ -464,6 +464,7 @@ class SDFGraspOptimizer:
             cfg.box_lb[i], cfg.box_ub[i] = lb[i], ub[i]
         st = _FusedLoop(E, T, tips, tgt, comp, faces, faces_deflate, dev)
         stream = N.stream_ptr(dev)
+        one_launch = os.environ.get("CDX_KIN_FUSED_STEP", "1") != "0"  # (A/B: cdx_kin_cost + cdx_kin_step)
         if self.loop_events:
             self.loop_events[0].record()
         for s in range(self.num_iters):
@@ -472,17 +473,21 @@ class SDFGraspOptimizer:
             self._seed += 1
             pts = tips.view(-1, 3)
             loss = st.loss_slot(s, self.num_iters)
-            N.check(lib.cdx_kin_cost(None, prm, E, None, N.ptr(pts), N.ptr(tgt), N.ptr(comp),
-                                     *(N.ptr(t) for t in st.queries(pts, tgt)), N.ptr(nz), self._seed, N.ptr(loss),
-                                     N.ptr(st.margin[s & 1]), N.ptr(st.normal[s & 1]), None, N.ptr(st.g[1]),
-                                     N.ptr(st.g[2]), N.ptr(st.g[0]), stream), "cdx_kin_cost")
+            qr = [N.ptr(t) for t in st.queries(pts, tgt)]
+            if not verbose and one_launch:  # cost, backward and step in one launch (cdx_kin_iteration)
+                N.check(lib.cdx_kin_iteration(None, prm, cfg, st.buffers, E, T, *qr, N.ptr(nz), self._seed, s, stream),
+                        "cdx_kin_iteration")
+            else:
+                N.check(lib.cdx_kin_cost(None, prm, E, None, N.ptr(pts), N.ptr(tgt), N.ptr(comp), *qr, N.ptr(nz),
+                                         self._seed, N.ptr(loss), N.ptr(st.margin[s & 1]), N.ptr(st.normal[s & 1]),
+                                         None, N.ptr(st.g[1]), N.ptr(st.g[2]), N.ptr(st.g[0]), stream), "cdx_kin_cost")
+                if verbose:
+                    print("Loss:", float(loss.sum()))
+                N.check(lib.cdx_kin_step(None, cfg, st.buffers, E, T, s, 0, stream), "cdx_kin_step")
             if st.hist is None:
                 self.loss_history.append(loss.sum())  # device scalar, no sync
             if trace_rows:
                 self.loss_rows.append(loss.clone())
-            if verbose:
-                print("Loss:", float(loss.sum()))
-            N.check(lib.cdx_kin_step(None, cfg, st.buffers, E, T, s, 0, stream), "cdx_kin_step")
         N.check(lib.cdx_kin_step(None, cfg, st.buffers, E, T, self.num_iters, 1, stream), "cdx_kin_step")
         st.loss_sums(self.loss_history)
         if self.loop_events:

@@ -575,6 +575,41 @@ def test_kin_one_launch_iteration_equals_two_launches(monkeypatch, robot):
             assert _bitwise_equal_nan_aware(a, b)
 
 
+def test_sdf_one_launch_iteration_equals_two_launches(monkeypatch):
+    """The SDF optimiser's one-launch iteration (kin_cost4_kernel<8, false, STEP>: cost, backward, best iterate, RMSprop
+    and the box clamps) against cdx_kin_cost + cdx_kin_step (CDX_KIN_FUSED_STEP=0): the same bits, with fingertips
+    both inside and outside the clamp box."""
+    from compliancedex_amd import SDFGraspOptimizer
+    from compliancedex_amd.optimizer import FINGERTIP_LB, FINGERTIP_UB
+    from compliancedex_amd.workloads import banana_mesh
+    from tests.conftest import REPO
+    E = 3000
+    center = np.load(os.path.join(REPO, "compliancedex_amd", "data", "banana_center.npy"))
+    rng = np.random.default_rng(47)
+    dirs = rng.standard_normal((E, 4, 3))
+    dirs /= np.linalg.norm(dirs, axis=-1, keepdims=True)
+    tips = (center + dirs * rng.uniform(0.01, 0.2, (E, 4, 1))).astype(np.float32)
+    target = (np.tile(center, (E, 4, 1)) + 0.01 * rng.standard_normal((E, 4, 3))).astype(np.float32)
+    comp = np.tile(np.array([10.0, 10.0, 10.0, 20.0], np.float32), (E, 1))
+    outs = {}
+    for one in ("1", "0"):
+        monkeypatch.setenv("CDX_KIN_FUSED_STEP", one)
+        opt = SDFGraspOptimizer([FINGERTIP_LB, FINGERTIP_UB], num_iters=7, optimize_target=True, seed=5)
+        res = opt.optimize(*(torch.from_numpy(a).to(DEV) for a in (tips, target, comp)), 1, banana_mesh(),
+                           verbose=False, trace_rows=True)
+        torch.cuda.synchronize()
+        outs[one] = ([t.cpu().numpy() for t in res[:3]] + [bool(res[3])] + [opt.best_loss.cpu().numpy()] +
+                     [r.cpu().numpy() for r in opt.loss_rows])
+    for a, b in zip(outs["1"], outs["0"]):
+        if isinstance(a, bool):
+            assert a == b
+        elif a.dtype == np.float64:
+            assert np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(a.view(np.uint64)[~np.isnan(a)],
+                                                                                b.view(np.uint64)[~np.isnan(b)])
+        else:
+            assert _bitwise_equal_nan_aware(a, b)
+
+
 def test_sdf_stale_order_gives_the_same_results():
     """CDX_SDF_REUSE_ORDER with an order sorted for OTHER points (a fused loop re-sorts its query points only every
     few iterations): the results equal a fresh sort's bit for bit — moved points, shuffled points, and points
