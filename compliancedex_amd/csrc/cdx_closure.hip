@@ -448,7 +448,12 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
 #if defined(CDX_COMBINE_FK_BWD1)  // (A/B: the stored-rotations backward walk)
     cdx::fk_tip_bwd<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
 #elif !defined(CDX_COMBINE_DIAG_NOFK)  // (timing-only diagnostic build without the FK backward: outputs wrong)
-    cdx::fk_tip_bwd2<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
+#if !defined(CDX_COMBINE_FK_BWD2)
+    if constexpr (MAXD <= 8)  // one walk, the joints' axes and origins kept (CDX_COMBINE_FK_BWD2: two walks, A/B)
+      cdx::fk_tip_bwd3<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
+    else
+#endif
+      cdx::fk_tip_bwd2<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
 #endif
   }
   double red[12];  // g_palm_pos (3) + g_Rp (9)

@@ -322,6 +322,70 @@ CDX_HD void fk_tip_bwd2(const cdx_chain& c, int k, const Q& q, const float* gpos
   }
 }
 
+// fk_tip_bwd2's gradient from ONE walk: each moving joint's world axis ω_j = R_parent·F_j·e_axis and origin o_j are kept
+// (6 floats per level, MAXD levels in registers) during the forward walk, and dθ_j = ω_j·(w − o_j × G_t) is taken for
+// every joint once w is known — no second walk (its sin / cos and matrix products), and the per-joint products are
+// independent of each other.  For shallow chains (MAXD ≤ 8: the hands), where the registers are affordable.
+template <int MAXD, class Q, class GQ>
+CDX_HD void fk_tip_bwd3(const cdx_chain& c, int k, const Q& q, const float* gpos, GQ&& g_q, float* pos = nullptr) {
+  const uint32_t mask = chain_path_mask(c, c.tip_body[k]);
+  const int n = path_depth(mask);
+  float R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f}, t[3] = {0.f, 0.f, 0.f};
+  float om[MAXD][3], og[MAXD][3], sgn[MAXD];
+  int dof[MAXD];
+  uint32_t m = mask;
+#pragma unroll
+  for (int l = 0; l < MAXD; ++l) {
+    dof[l] = -1;
+    if (l < n) {
+      const cdx_body& b = c.bodies[low_bit(m)];
+      m &= m - 1;
+      float Rn[9], tn[3];
+      chain_step(b, q, R, t, Rn, tn);
+      if (b.dof >= 0) {
+        const int ax = b.axis;  // (selects: a register array indexed at run time goes to scratch)
+        const float fa[3] = {ax == 0 ? b.F[0] : (ax == 1 ? b.F[1] : b.F[2]), ax == 0 ? b.F[3] : (ax == 1 ? b.F[4] : b.F[5]),
+                             ax == 0 ? b.F[6] : (ax == 1 ? b.F[7] : b.F[8])};
+        mat3_vec(R, fa, om[l]);
+        for (int i = 0; i < 3; ++i) og[l][i] = tn[i];
+        dof[l] = b.dof;
+        sgn[l] = b.sign;
+      }
+      for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+      for (int i = 0; i < 3; ++i) t[i] = tn[i];
+    }
+  }
+  if (pos) tip_from_pose(c, k, R, t, pos, nullptr);
+  float GR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const float Gt[3] = {gpos[0], gpos[1], gpos[2]};
+  if (c.has_offsets) {
+    float raw[4], sc;
+    const int br = quat_raw(R, raw, &sc);
+    float qt[4] = {raw[0] * sc, raw[1] * sc, raw[2] * sc, raw[3] * sc};
+    float gq[4] = {0, 0, 0, 0};
+    quat_rotate_bwd(qt, c.tip_offset[k], gpos, gq);
+    for (int i = 0; i < 4; ++i) gq[i] *= sc;  // scale is detached: only d raw flows
+    quat_raw_bwd(br, gq, GR);
+  }
+  float w[3] = {t[1] * Gt[2] - t[2] * Gt[1], t[2] * Gt[0] - t[0] * Gt[2], t[0] * Gt[1] - t[1] * Gt[0]};
+#pragma unroll
+  for (int cc = 0; cc < 3; ++cc) {
+    const float r0 = R[cc], r1 = R[3 + cc], r2 = R[6 + cc], g0 = GR[cc], g1 = GR[3 + cc], g2 = GR[6 + cc];
+    w[0] += r1 * g2 - r2 * g1;
+    w[1] += r2 * g0 - r0 * g2;
+    w[2] += r0 * g1 - r1 * g0;
+  }
+#pragma unroll
+  for (int l = 0; l < MAXD; ++l) {
+    if (dof[l] >= 0) {
+      const float* o = og[l];
+      const float ox[3] = {o[1] * Gt[2] - o[2] * Gt[1], o[2] * Gt[0] - o[0] * Gt[2], o[0] * Gt[1] - o[1] * Gt[0]};
+      const float dth = om[l][0] * (w[0] - ox[0]) + om[l][1] * (w[1] - ox[1]) + om[l][2] * (w[2] - ox[2]);
+      g_q(dof[l], sgn[l] * dth);
+    }
+  }
+}
+
 // Deepest tip path of a chain (host: picks the fk_tip_bwd register bound).
 CDX_HD int chain_max_depth(const cdx_chain& c) {
   int d = 0;
