@@ -1553,6 +1553,13 @@ static void grad_launch_kt(const cdx_gpis& g, const double* X, int64_t M, const 
       fold->Nt = n_tiles;
       fold->N = g.N;
       fold->gc = gc;
+      fold->n_slots = 0;
+#if !defined(CDX_FOLD_CUTS)  // (A/B: the consumer walks the cuts itself)
+      if (slots.n <= GF_MAX_SLOTS) {
+        fold->n_slots = slots.n;
+        for (int i = 0; i < slots.n; ++i) fold->slot[i] = slots.t[i];
+      }
+#endif
       return;
     }
   } else {

@@ -110,16 +110,33 @@ __device__ __host__ inline int gradv_cut(int p, int parts, int W, int N, int Nt,
   return W;
 }
 
+constexpr int GF_MAX_SLOTS = 32;
 struct GradFold {
   const double* partial = nullptr;  // [slots][M_pad][4]
   int64_t M_pad = 0;
   int parts = 0, W = 0, Nt = 0, N = 0;
   GradCosts gc;
+  // the slots the pieces wrote, in the order the loop below visits them (host-computed by the launcher; 0: none
+  // listed, the consumer walks the cuts itself)
+  int n_slots = 0;
+  unsigned short slot[GF_MAX_SLOTS] = {};
 };
 // gstd (3) of query m scaled by the signed variance v: −sign(v)/sqrt|v| · Σ_slots partial[slot][m][1..3]
 // (all indices uniform: scalar integer work, the 2·(parts + Nt) loads issued together).
 __device__ inline void grad_fold_gstd(const GradFold& f, int64_t m, double v, double* out) {
   double g0 = 0, g1 = 0, g2 = 0;
+  if (f.n_slots > 0) {  // the listed slots: the same sums in the same order, without the cut arithmetic
+#pragma unroll
+    for (int i = 0; i < GF_MAX_SLOTS; ++i) {
+      if (i >= f.n_slots) break;
+      const double* pp = f.partial + ((int64_t)f.slot[i] * f.M_pad + m) * 4;
+      g0 += pp[1]; g1 += pp[2]; g2 += pp[3];
+    }
+    const double sg = v > 0 ? 1.0 : (v < 0 ? -1.0 : 0.0);
+    const double fct = -sg / sqrt(fabs(v));
+    out[0] = fct * g0; out[1] = fct * g1; out[2] = fct * g2;
+    return;
+  }
   int q0 = 0;
   for (int p = 0; p < f.parts; ++p) {
     const int q1 = gradv_cut(p + 1, f.parts, f.W, f.N, f.Nt, f.gc.uc, f.gc.n);
