@@ -361,6 +361,59 @@ __device__ void exact_point(cdx::F3 p, const float* __restrict__ faces, int64_t 
 }
 
 
+// The reference tile rule for lane b's point with the faces split over the wave's lanes (all 64 lanes call it):
+// per 512-face tile, the sequential rule `s == 0 || best > d` picks the tile's first face when its distance is NaN,
+// else the first minimum over the tile's non-NaN distances — a (distance, face) minimum over the lanes' partial
+// minima reproduces it; across tiles the same rule runs on the (uniform) tile results.  The winner's sign, normal and
+// closest point are recomputed from the same point_face call the sequential scan kept.
+__device__ void exact_point_wave(int b, cdx::F3 p0, int64_t pi, bool live0, const float* __restrict__ faces, int64_t F,
+                                 float* out_dist, int32_t* out_sign, float* out_nrm, float* out_clst,
+                                 int32_t* out_face) {
+  const int lane = threadIdx.x & 63;
+  const cdx::F3 p = cdx::f3(__shfl(p0.x, b), __shfl(p0.y, b), __shfl(p0.z, b));
+  const int64_t pib = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(pi >> 32), b) << 32) |
+                                (uint64_t)(uint32_t)__shfl((int)(uint32_t)pi, b));
+  const bool wr = __shfl((int)live0, b) != 0;
+  float best = 0.f;
+  int64_t bface = 0;
+  for (int64_t f0 = 0; f0 < F; f0 += SDF_TILE) {
+    const int nt = (int)min((int64_t)SDF_TILE, F - f0);
+    float ld = 0.f;
+    int ls = -1;  // this lane's first minimum over its non-NaN faces of the tile (−1: none)
+    bool first_nan = false;
+    for (int s = lane; s < nt; s += 64) {
+      const float* v = faces + 9 * (f0 + s);
+      cdx::F3 c, n;
+      int sg;
+      const float d = cdx::point_face(p, cdx::f3(v[0], v[1], v[2]), cdx::f3(v[3], v[4], v[5]),
+                                      cdx::f3(v[6], v[7], v[8]), c, n, sg);
+      if (s == 0) first_nan = d != d;
+      if (d == d && (ls < 0 || d < ld)) { ld = d; ls = s; }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float od = __shfl_xor(ld, o);
+      const int os = __shfl_xor(ls, o);
+      if (os >= 0 && (ls < 0 || od < ld || (od == ld && os < ls))) { ld = od; ls = os; }
+    }
+    const bool t_nan = __shfl((int)first_nan, 0) != 0;
+    const float tbest = t_nan ? __builtin_nanf("") : ld;
+    const int64_t tface = f0 + (t_nan ? 0 : ls);
+    if (f0 == 0 || best > tbest) { best = tbest; bface = tface; }
+  }
+  if (lane != 0 || !wr) return;
+  const float* v = faces + 9 * bface;
+  cdx::F3 c, n;
+  int sg;
+  const float d = cdx::point_face(p, cdx::f3(v[0], v[1], v[2]), cdx::f3(v[3], v[4], v[5]), cdx::f3(v[6], v[7], v[8]),
+                                  c, n, sg);
+  out_dist[pib] = d;
+  out_sign[pib] = sg;
+  out_nrm[3 * pib] = n.x; out_nrm[3 * pib + 1] = n.y; out_nrm[3 * pib + 2] = n.z;
+  out_clst[3 * pib] = c.x; out_clst[3 * pib + 1] = c.y; out_clst[3 * pib + 2] = c.z;
+  if (out_face) out_face[pib] = (int32_t)bface;
+}
+
 // The bounds' square roots: v_sqrt_f32 (≤ 1 ulp, no correction sequence) — a bound's rounding is four orders
 // below its margins; the distances themselves (point_face, face_dist2) keep the correctly rounded sqrtf.
 __device__ __forceinline__ float bsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
@@ -508,18 +561,37 @@ __device__ __forceinline__ void sdf_tree_body(
     return load_node(top, t);
   };
   const int64_t j = grp * 64 + lane;
-  const bool live = j < P;
-  const int64_t pi = porder[live ? j : P - 1];  // dead lanes shadow a live point
-  const cdx::F3 p = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
-  const bool ok = fabsf(p.x) <= PT_LIM && fabsf(p.y) <= PT_LIM && fabsf(p.z) <= PT_LIM;
-  if (!__all(ok)) {  // same points in every wave: uniform over the workgroup
+  const bool live0 = j < P;
+  const int64_t pi = porder[live0 ? j : P - 1];  // dead lanes shadow a live point
+  const cdx::F3 p0 = cdx::f3(points[3 * pi], points[3 * pi + 1], points[3 * pi + 2]);
+  const bool ok = fabsf(p0.x) <= PT_LIM && fabsf(p0.y) <= PT_LIM && fabsf(p0.z) <= PT_LIM;
+  const unsigned long long badm = __ballot(!ok);  // same points in every wave: uniform over the workgroup
+  if (badm) {
+#if defined(CDX_SDF_EXACT_GROUP)  // (A/B: the whole group by the tile rule, one point per lane of wave 0)
     if (w == 0) {
-      exact_point(p, faces, F, pi, out_dist, out_sign, out_nrm, out_clst, out_face, live);
+      exact_point(p0, faces, F, pi, out_dist, out_sign, out_nrm, out_clst, out_face, live0);
       if (count && lane == 0)
-        atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(__ballot(live)));
+        atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(__ballot(live0)));
     }
     return;
+#else
+    // a non-finite or out-of-range point (an optimiser's diverged candidate) takes the reference's tile rule, its
+    // faces split over the lanes of one wave (the waves take such points in turn); the group's other points walk
+    // the tree as usual
+    const unsigned long long todo = badm & __ballot(live0);  // (dead lanes shadowing a bad point: nothing to write)
+    int k = 0;
+    for (unsigned long long m = todo; m; m &= m - 1, ++k)
+      if (k % NW == w) exact_point_wave(__builtin_ctzll(m), p0, pi, live0, faces, F, out_dist, out_sign, out_nrm,
+                                        out_clst, out_face);
+    if (count && threadIdx.x == 0)
+      atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(todo));
+    if (!~badm) return;
+#endif
   }
+  // the walk: a bad lane shadows the first good lane's point and writes nothing
+  const int sh = __builtin_ctzll(~badm);
+  const cdx::F3 p = ok ? p0 : cdx::f3(__shfl(p0.x, sh), __shfl(p0.y, sh), __shfl(p0.z, sh));
+  const bool live = live0 && ok;
   const float pnorm = bsqrt(p.x * p.x + p.y * p.y + p.z * p.z);
   // merge the four waves' (bound, index) candidates: the smallest bound, then the smallest index
   auto merge = [&](float lb, int sel) {
