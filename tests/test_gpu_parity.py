@@ -690,6 +690,28 @@ def test_sdf_nonfinite_points_take_exact_path(path):
 
 
 @pytest.mark.parametrize("path", SDF_PATHS)
+def test_sdf_bad_point_groups(path):
+    """Point groups holding non-finite / out-of-range points (their faces split over a wave's lanes, the group's other
+    points walking the tree): a group of only bad points, groups mixing bad and good ones, and a last partial group
+    whose dead lanes shadow a bad point — bit-exact against the C oracle's tile rule, the 'banana' mesh's 16 384
+    faces (32 tiles) included."""
+    from tests import _sdf_oracle
+    faces = np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))
+    rng = np.random.default_rng(31)
+    lo, hi = faces.reshape(-1, 3).min(0), faces.reshape(-1, 3).max(0)
+    pts = (lo - 0.05 + (hi - lo + 0.1) * rng.random((300, 3))).astype(np.float32)
+    pts[:70] = np.nan                      # (in point order these land together, whatever the sort does with them)
+    pts[70:80, 1] = np.inf
+    pts[80:90] = [3e4, 0.0, 0.0]
+    pts[[120, 170, 233]] = np.nan
+    pts[-1] = [np.nan, 0.0, 1.0]           # the shadow point of the last group's dead lanes
+    got = _sdf_run(pts, faces, path)
+    o = _sdf_oracle.forward(pts, faces)
+    for a, b in zip(got, o):
+        assert _bitwise_equal_nan_aware(a, b)
+
+
+@pytest.mark.parametrize("path", SDF_PATHS)
 def test_sdf_degenerate_and_autograd(path):
     from compliancedex_amd import compute_sdf
     from tests import _sdf_oracle
