@@ -18,6 +18,7 @@ NPAD_ALIGN = 256  # CDX_NPAD_ALIGN
 SCREEN_BANDS = 24  # CDX_SCREEN_BANDS
 PROF_STAGES = 6   # cdx_profile_read array length
 SDF_REUSE_ORDER, SDF_MESH_CULLED, SDF_MESH_EXACT = 1, 2, 4  # cdx_sdf_query flags
+SDF_SCHED_KEEP = 8  # cdx_sdf_query_batch, first query: keep the schedule's order
 ERRORS = {-1: "invalid argument", -2: "unsupported GPIS kernel", -3: "chain exceeds descriptor capacity",
           -10: "HIP launch failed"}
 

@@ -1346,7 +1346,8 @@ int cdx_sdf_query_batch(int32_t n, const cdx_sdf_batch_query* qs, void* schedule
   int m = 0;
   for (int i = 0; i < n; ++i) {
     const cdx_sdf_batch_query& d = qs[i];
-    if (d.P < 0 || d.F < 0 || !d.mesh || d.flags != (CDX_SDF_REUSE_ORDER | CDX_SDF_MESH_CULLED)) return CDX_EINVAL;
+    const int32_t fl = i == 0 ? (d.flags & ~CDX_SDF_SCHED_KEEP) : d.flags;
+    if (d.P < 0 || d.F < 0 || !d.mesh || fl != (CDX_SDF_REUSE_ORDER | CDX_SDF_MESH_CULLED)) return CDX_EINVAL;
     if (d.P == 0) continue;
     if (!sdf_args_ok(d.P, d.points, d.faces, d.F, d.sqdist, d.sign, d.normals, d.clst) || !d.workspace) return CDX_EINVAL;
     QueryWs q;
@@ -1395,7 +1396,8 @@ int cdx_sdf_query_batch(int32_t n, const cdx_sdf_batch_query* qs, void* schedule
     b.cap = groups;
   }
   hipLaunchKernelGGL(sdf_tree_batch_kernel, dim3(groups), dim3(64 * NW), 0, s, b);
-  if (b.sched) hipLaunchKernelGGL(sdf_batch_sched_kernel, dim3(1), dim3(SCHED_THREADS), 0, s, b.sched, groups, b.cap);
+  if (b.sched && !(qs[0].flags & CDX_SDF_SCHED_KEEP))
+    hipLaunchKernelGGL(sdf_batch_sched_kernel, dim3(1), dim3(SCHED_THREADS), 0, s, b.sched, groups, b.cap);
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 

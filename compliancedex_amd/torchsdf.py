@@ -11,6 +11,7 @@ argmin face index.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -103,8 +104,18 @@ class BatchSchedule:
     point group's walk time, and from it the next launch's order, heaviest groups first.  Regrown (zeroed) when a
     batch with more groups comes; the outputs never depend on it."""
 
-    def __init__(self):
+    def __init__(self, every=None):
+        """``every``: launches per recomputation of the order (the durations are recorded on every launch; the
+        order from a few launches back serves as well, and each recomputation is a launch of its own)."""
         self.buf = None
+        self.every = max(1, int(os.environ.get("CDX_SDF_SCHED_EVERY", "4") if every is None else every))
+        self.launches = 0
+
+    def keep_order(self):
+        """Whether this launch keeps the current order (the count advances)."""
+        keep = self.launches % self.every != 0
+        self.launches += 1
+        return keep
 
     def get(self, Ps, dev):
         arr = (C.c_int64 * len(Ps))(*Ps)
@@ -113,6 +124,10 @@ class BatchSchedule:
             raise RuntimeError("BatchSchedule: bad point counts")
         if self.buf is None or self.buf.numel() < need or self.buf.device != dev:
             self.buf = torch.zeros(need, dtype=torch.uint8, device=dev)
+            self.launches = 0
+        groups = sum((P + 63) // 64 for P in Ps)
+        if groups != getattr(self, "groups", None):  # (an order for another group count is not used: recompute)
+            self.groups, self.launches = groups, 0
         return self.buf
 
 
@@ -148,6 +163,8 @@ def query_batch(items, schedule=None):
         d.workspace, d.workspace_bytes = N.ptr(ws.buf), ws.buf.numel()
         d.flags = N.SDF_REUSE_ORDER | N.SDF_MESH_CULLED
     sb = schedule.get([d.P for d in qs], dev) if schedule is not None else None
+    if sb is not None and schedule.keep_order():
+        qs[0].flags |= N.SDF_SCHED_KEEP
     N.check(N.load().cdx_sdf_query_batch(len(items), C.cast(qs, C.c_void_p), N.ptr(sb), 0 if sb is None else sb.numel(),
                                          N.stream_ptr(dev)), "cdx_sdf_query_batch")
 

@@ -511,6 +511,8 @@ int cdx_sdf_query_order(const float* points, int64_t P, void* workspace, size_t 
 #define CDX_SDF_REUSE_ORDER 1
 #define CDX_SDF_MESH_CULLED 2
 #define CDX_SDF_MESH_EXACT 4
+#define CDX_SDF_SCHED_KEEP 8 /* cdx_sdf_query_batch, first query's flags: keep the schedule's order (durations still
+                                recorded; the order is recomputed on the next launch without it) */
 int cdx_sdf_mesh_flags(const void* mesh, int32_t* flags, cdx_stream_t stream);  /* waits on stream */
 /* Up to four cdx_sdf_query calls in one launch (the SDF / Kin optimisers' three queries per iteration): each with
  * flags CDX_SDF_REUSE_ORDER | CDX_SDF_MESH_CULLED (its workspace already holds its points' order —
