@@ -386,6 +386,77 @@ CDX_HD void fk_tip_bwd3(const cdx_chain& c, int k, const Q& q, const float* gpos
   }
 }
 
+// fk_tip_bwd3 with the joints' axes and origins in caller-provided LDS instead of registers (deep chains, where the
+// registers are spent): slot (l, i) of this lane at st[(6·l + i)·64 + lane] (64-lane interleave, conflict-free).
+template <int MAXD, class Q, class GQ>
+CDX_HD void fk_tip_bwd3s(const cdx_chain& c, int k, const Q& q, const float* gpos, GQ&& g_q, float* st, int lane) {
+  const uint32_t mask = chain_path_mask(c, c.tip_body[k]);
+  const int n = path_depth(mask);
+  float R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f}, t[3] = {0.f, 0.f, 0.f};
+  uint32_t dofs = 0u;  // levels with a moving joint
+  uint32_t m = mask;
+#pragma unroll
+  for (int l = 0; l < MAXD; ++l) {
+    if (l < n) {
+      const cdx_body& b = c.bodies[low_bit(m)];
+      m &= m - 1;
+      float Rn[9], tn[3];
+      chain_step(b, q, R, t, Rn, tn);
+      if (b.dof >= 0) {
+        const int ax = b.axis;
+        const float fa[3] = {ax == 0 ? b.F[0] : (ax == 1 ? b.F[1] : b.F[2]), ax == 0 ? b.F[3] : (ax == 1 ? b.F[4] : b.F[5]),
+                             ax == 0 ? b.F[6] : (ax == 1 ? b.F[7] : b.F[8])};
+        float om[3];
+        mat3_vec(R, fa, om);
+        for (int i = 0; i < 3; ++i) {
+          st[(6 * l + i) * 64 + lane] = om[i];
+          st[(6 * l + 3 + i) * 64 + lane] = tn[i];
+        }
+        dofs |= 1u << l;
+      }
+      for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+      for (int i = 0; i < 3; ++i) t[i] = tn[i];
+    }
+  }
+  float GR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const float Gt[3] = {gpos[0], gpos[1], gpos[2]};
+  if (c.has_offsets) {
+    float raw[4], sc;
+    const int br = quat_raw(R, raw, &sc);
+    float qt[4] = {raw[0] * sc, raw[1] * sc, raw[2] * sc, raw[3] * sc};
+    float gq[4] = {0, 0, 0, 0};
+    quat_rotate_bwd(qt, c.tip_offset[k], gpos, gq);
+    for (int i = 0; i < 4; ++i) gq[i] *= sc;  // scale is detached: only d raw flows
+    quat_raw_bwd(br, gq, GR);
+  }
+  float w[3] = {t[1] * Gt[2] - t[2] * Gt[1], t[2] * Gt[0] - t[0] * Gt[2], t[0] * Gt[1] - t[1] * Gt[0]};
+#pragma unroll
+  for (int cc = 0; cc < 3; ++cc) {
+    const float r0 = R[cc], r1 = R[3 + cc], r2 = R[6 + cc], g0 = GR[cc], g1 = GR[3 + cc], g2 = GR[6 + cc];
+    w[0] += r1 * g2 - r2 * g1;
+    w[1] += r2 * g0 - r0 * g2;
+    w[2] += r0 * g1 - r1 * g0;
+  }
+  m = mask;
+#pragma unroll
+  for (int l = 0; l < MAXD; ++l) {
+    if (l < n) {
+      const cdx_body& b = c.bodies[low_bit(m)];
+      m &= m - 1;
+      if ((dofs >> l) & 1u) {
+        float om[3], o[3];
+        for (int i = 0; i < 3; ++i) {
+          om[i] = st[(6 * l + i) * 64 + lane];
+          o[i] = st[(6 * l + 3 + i) * 64 + lane];
+        }
+        const float ox[3] = {o[1] * Gt[2] - o[2] * Gt[1], o[2] * Gt[0] - o[0] * Gt[2], o[0] * Gt[1] - o[1] * Gt[0]};
+        const float dth = om[0] * (w[0] - ox[0]) + om[1] * (w[1] - ox[1]) + om[2] * (w[2] - ox[2]);
+        g_q(b.dof, b.sign * dth);
+      }
+    }
+  }
+}
+
 // Deepest tip path of a chain (host: picks the fk_tip_bwd register bound).
 CDX_HD int chain_max_depth(const cdx_chain& c) {
   int d = 0;

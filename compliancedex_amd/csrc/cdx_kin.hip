@@ -387,7 +387,13 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
       pf_cm = sb.m_comp[r];
       pf_cv = sb.v_comp[r];
     }
+#if defined(CDX_KIN_FK_BWD2)  // (A/B: two walks, no per-level state)
     cdx::fk_tip_bwd2<MAXD>(kc, f, q + e * D, gpos, [&](int d, float v) { s_fk[d][threadIdx.x] += v; });
+#else  // one walk, each joint's world axis and origin kept in LDS
+    __shared__ float s_jst[6 * MAXD * 64];
+    cdx::fk_tip_bwd3s<MAXD>(kc, f, q + e * D, gpos, [&](int d, float v) { s_fk[d][threadIdx.x] += v; }, s_jst,
+                            (int)threadIdx.x);
+#endif
 #endif
     float* fk_g = nullptr;
     (void)fk_g;
