@@ -578,13 +578,30 @@ __device__ __forceinline__ void sdf_tree_body(
     // a non-finite or out-of-range point (an optimiser's diverged candidate) takes the reference's tile rule, its
     // faces split over the lanes of one wave (the waves take such points in turn); the group's other points walk
     // the tree as usual
-    const unsigned long long todo = badm & __ballot(live0);  // (dead lanes shadowing a bad point: nothing to write)
+    // A point with a NaN coordinate has a NaN distance to every face (p − c carries the NaN), so the rule keeps the
+    // first face of the first tile: face 0's point_face, no scan (diverged candidates are mostly NaN, and the sort
+    // gathers them into the same groups)
+    const bool nanp = p0.x != p0.x || p0.y != p0.y || p0.z != p0.z;
+    if (w == 0 && live0 && nanp) {
+      cdx::F3 c, n;
+      int sg;
+      const float d = cdx::point_face(p0, cdx::f3(faces[0], faces[1], faces[2]), cdx::f3(faces[3], faces[4], faces[5]),
+                                      cdx::f3(faces[6], faces[7], faces[8]), c, n, sg);
+      out_dist[pi] = d;
+      out_sign[pi] = sg;
+      out_nrm[3 * pi] = n.x; out_nrm[3 * pi + 1] = n.y; out_nrm[3 * pi + 2] = n.z;
+      out_clst[3 * pi] = c.x; out_clst[3 * pi + 1] = c.y; out_clst[3 * pi + 2] = c.z;
+      if (out_face) out_face[pi] = 0;
+    }
+    // the others (an infinite or out-of-range coordinate) scan every face (dead lanes shadowing a bad point: nothing
+    // to write)
+    const unsigned long long todo = badm & __ballot(live0) & ~__ballot(nanp);
     int k = 0;
     for (unsigned long long m = todo; m; m &= m - 1, ++k)
       if (k % NW == w) exact_point_wave(__builtin_ctzll(m), p0, pi, live0, faces, F, out_dist, out_sign, out_nrm,
                                         out_clst, out_face);
-    if (count && threadIdx.x == 0)
-      atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(todo));
+    if (count && threadIdx.x == 0)  // (the brute-force pairs the tile rule stands for, NaN points included)
+      atomicAdd(&g_sdf_stats[1], (unsigned long long)F * (unsigned long long)__popcll(badm & __ballot(live0)));
     if (!~badm) return;
 #endif
   }
