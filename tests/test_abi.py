@@ -78,3 +78,20 @@ def test_product_refuses_cpu_tensors():
     g.load_state_data("banana_state", device="cpu")
     with pytest.raises(RuntimeError, match="no CPU path"):
         g.pred(torch.zeros(4, 3, dtype=torch.float64))
+
+
+def test_batch_schedule_host_logic():
+    """torchsdf.BatchSchedule (host side of cdx_sdf_query_batch's schedule): sized by cdx_sdf_batch_schedule_bytes,
+    zeroed when (re)allocated, the order recomputed on every `every`-th launch and whenever the group count changes."""
+    import torch
+    from compliancedex_amd.torchsdf import BatchSchedule
+    dev = torch.device("cpu")
+    sch = BatchSchedule(every=4)
+    buf = sch.get([65536, 65536, 100], dev)
+    assert buf.numel() == 4 * (4 + 2 * (1024 + 1024 + 2)) and int(buf.sum()) == 0
+    keeps = [sch.keep_order() for _ in range(9)]
+    assert keeps == [False, True, True, True, False, True, True, True, False]
+    sch.get([6000, 6000, 3000], dev)  # fewer groups: the same buffer, the order recomputed next
+    assert sch.buf is buf and sch.keep_order() is False and sch.keep_order() is True
+    big = sch.get([1 << 20], dev)  # more groups than the buffer holds: a new, zeroed buffer
+    assert big is not buf and big.numel() == 4 * (4 + 2 * 16384) and sch.keep_order() is False
