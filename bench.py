@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--cpu-E", type=int, default=256)
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal on one GPU)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 SDF/Kin block (N = 1)")
-    ap.add_argument("--config4-iters", type=int, default=100)  # (the reference's Kin loop runs 1000 per call)
+    ap.add_argument("--config4-iters", type=int, default=1000)  # (the reference's Kin loop default: 1000 per call)
     return ap.parse_args()
 
 
