@@ -148,6 +148,7 @@ _SIGS = {
     "cdx_closure_screen_report": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, C.POINTER(CdxScreenReport), _P]),
     "cdx_closure_screen_reset": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, _P]),
     "cdx_debug_fail_next_closure": (C.c_int, [C.c_int32]),
+    "cdx_ab_switches": (C.c_int, []),
     "cdx_closure": (C.c_int, [C.POINTER(CdxProblem), _I64, _P, _P, _P, _P, _P, _P, C.c_uint64, _P,
                               _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cdx_pack_survivors": (C.c_int, [_I64, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_double,

@@ -14,6 +14,8 @@
 //                               and the five parameter gradients        — :713-769, :49-118
 #include <hip/hip_runtime.h>
 
+#include "cdx_ab.h"
+
 #include <atomic>
 #include <cstdlib>
 
@@ -556,7 +558,7 @@ struct ClosureWs {
 //   0: no fork.  Values above 4 are taken as 0.
 int fork_point() {
   static const int at = [] {
-    const char* e = getenv("CDX_FORK_MEAN");
+    const char* e = cdx::ab_env("CDX_FORK_MEAN");
     const int v = e ? std::max(0, atoi(e)) : 2;
     return v > 4 ? 0 : v;
   }();
@@ -578,7 +580,7 @@ bool screen_on(const cdx_problem* p, int64_t E) {
 #if defined(CDX_GRAD_EXPLICIT)
   return false;  // the screened path keeps V for the ∇std pass, which this build does not allocate
 #endif
-  static const bool off = getenv("CDX_NO_SCREEN") != nullptr;
+  static const bool off = cdx::ab_env("CDX_NO_SCREEN") != nullptr;
   const int64_t Ms = (int64_t)p->n_query_levels * E * p->chain.n_tips;
   return !off && p->gpis.screen && p->gpis.screen_delta > 0 && p->chain.n_tips <= CDX_MAX_TIPS &&
          Ms >= SCREEN_MIN_ROWS;
@@ -648,7 +650,7 @@ struct SideStream {
 // exact selection after the refine pass; the level kernel follows the all-tip and target rows.
 int mean_sched() {
   static const int m = [] {
-    const char* e = getenv("CDX_MEAN_SCHED");
+    const char* e = cdx::ab_env("CDX_MEAN_SCHED");
     return e ? atoi(e) : 1;
   }();
   return m;
@@ -661,7 +663,7 @@ int mean_sched() {
 // 0.996–0.998 ms per closure over 3 interleaved rounds (profiles/r05n_ab_side_order.jsonl).
 bool mean_first() {
   static const bool on = [] {
-    const char* e = getenv("CDX_MEAN_FIRST");
+    const char* e = cdx::ab_env("CDX_MEAN_FIRST");
     return e && atoi(e) != 0;
   }();
   return on;
@@ -671,14 +673,14 @@ bool mean_first() {
 // wait in front of the combine costs ≈ 7 µs of gap (A/B).
 bool join_early() {
   static const bool on = [] {
-    const char* e = getenv("CDX_JOIN_EARLY");
+    const char* e = cdx::ab_env("CDX_JOIN_EARLY");
     return e && atoi(e) != 0;
   }();
   return on;
 }
 double mean_chunk1() {
   static const double f = [] {
-    const char* e = getenv("CDX_MEAN_CHUNK1");
+    const char* e = cdx::ab_env("CDX_MEAN_CHUNK1");
     const double v = e ? atof(e) : 0.3;
     return v < 0 ? 0.0 : (v > 1 ? 1.0 : v);
   }();
@@ -692,7 +694,7 @@ double mean_chunk1() {
 // — mean B's waves share SIMDs with the level kernel's long dependent chains and stretch them.
 bool mean_split() {
   static const bool on = [] {
-    const char* e = getenv("CDX_MEAN_SPLIT");
+    const char* e = cdx::ab_env("CDX_MEAN_SPLIT");
     return e && atoi(e) != 0;
   }();
   return on;
@@ -714,7 +716,7 @@ int kabsch_mode() {
 // sums the ∇std pieces of its group itself (GpisView::fold) — one launch fewer.
 bool grad_fold() {
   static const bool on = [] {
-    const char* e = getenv("CDX_GRAD_FOLD");
+    const char* e = cdx::ab_env("CDX_GRAD_FOLD");
     return !e || atoi(e) != 0;
   }();
   return on;
@@ -724,7 +726,7 @@ bool grad_fold() {
 // two streams of one device, whose kernels see each other's writes at kernel boundaries anyway.
 unsigned side_event_flags() {
   static const unsigned f = [] {
-    const char* e = getenv("CDX_SIDE_EVENT_FENCE");
+    const char* e = cdx::ab_env("CDX_SIDE_EVENT_FENCE");
     return (e && atoi(e) != 0) ? (unsigned)hipEventDisableTiming
                                : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
   }();
@@ -744,7 +746,7 @@ bool side_stream(SideStream& out) {
     // default, with the mean first: the highest priority lets the mean's workgroups starve the main
     // stream's compaction; 1.013 vs 1.016 (lowest) vs 1.036 ms (highest, records first),
     // r04q_ab_mean_first_side_prio.jsonl).
-    const char* pe = getenv("CDX_SIDE_PRIO");
+    const char* pe = cdx::ab_env("CDX_SIDE_PRIO");
     const int want = pe ? atoi(pe) : 0;
     int least = 0, greatest = 0;
     hipError_t ce;
@@ -774,7 +776,7 @@ bool side_stream(SideStream& out) {
   if (mean_sched() >= 2 && !ss.s2) {
     // CDX_SIDEB_PRIO: the mean chunks' stream priority (0 normal, default: the merge's workgroups are
     // dispatched first and the mean fills the CUs around them; > 0 highest, < 0 lowest)
-    const char* pe = getenv("CDX_SIDEB_PRIO");
+    const char* pe = cdx::ab_env("CDX_SIDEB_PRIO");
     const int want = pe ? atoi(pe) : 0;
     int least = 0, greatest = 0;
     hipStream_t st;
@@ -879,7 +881,7 @@ bool inject_fail(int stage) {
 // host sync, hipGraph-capturable).
 bool screen_repair() {
   static const bool on = [] {
-    const char* e = getenv("CDX_SCREEN_REPAIR");
+    const char* e = cdx::ab_env("CDX_SCREEN_REPAIR");
     return !e || atoi(e) != 0;
   }();
   return on;
@@ -1228,6 +1230,14 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
 
+int cdx_ab_switches(void) {
+#if defined(CDX_AB_SWITCHES)
+  return 1;
+#else
+  return 0;
+#endif
+}
+
 int cdx_debug_fail_next_closure(int32_t stage) {
   if (stage < 0 || stage > 3) return CDX_EINVAL;
   g_fail_stage.store(stage, std::memory_order_relaxed);
@@ -1334,7 +1344,7 @@ extern "C" int cdx_profile_enable(int stages) {
     // timing-only events: no system-scope fence (L2 writeback) at each record; CDX_PROF_EVENT_FLAGS
     // (hex) overrides the flags for A/B runs
     unsigned flags = hipEventDisableSystemFence;
-    if (const char* f = getenv("CDX_PROF_EVENT_FLAGS")) flags = (unsigned)strtoul(f, nullptr, 16);
+    if (const char* f = cdx::ab_env("CDX_PROF_EVENT_FLAGS")) flags = (unsigned)strtoul(f, nullptr, 16);
     const int total = cdx::PROF_STAGES * cdx::PROF_POOL * 2;
     hipEvent_t* evs = &g_prof.ev[0][0][0];
     for (int e = 0; e < total; ++e)

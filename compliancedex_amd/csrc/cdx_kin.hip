@@ -201,7 +201,8 @@ __global__ __launch_bounds__(64) void kin_cost_kernel(
 // results, no divergence (the lanes would idle otherwise) — then takes its own fingertip's gradients and walks
 // its own FK chain backward; the four chains' joint gradients are summed across the lanes ((f0 + f1) + (f2 + f3)).
 //
-// STEP (cdx_kin_iteration: Kin mode, Adam, no box clamp): the iteration's cdx_kin_step in the same launch — the
+// STEP (cdx_kin_iteration: Kin mode — FK, Adam, no box clamp — or SDF mode — no FK, RMSprop, box clamps): the
+// iteration's cdx_kin_step in the same launch — the
 // candidate's four lanes hold its loss and every gradient when the cost is done, so the best-iterate update, the
 // Adam step of the DOFs / targets / compliances each lane owns and the next fingertip's FK follow without a second
 // launch or a gradient round trip through memory.  Same operations in the same order as the two launches:
@@ -372,7 +373,7 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
 #pragma unroll
       for (int u = 0; u < PF_DOFS; ++u) {
         const int i = f + NT * u;
-        const int64_t k = e * D + (i < D ? i : f);
+        const int64_t k = e * D + (i < D ? i : 0);  // (padded slots re-read DOF 0 of the row)
         pf_p[u] = sb.pose[k];
         pf_m[u] = sb.m_pose[k];
         pf_v[u] = sb.v_pose[k];
@@ -657,7 +658,7 @@ __global__ __launch_bounds__(64) void kin_step_kernel(cdx_chain chain, cdx_kin_o
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = i0 + u * T;
-        const int64_t k = e * D + (i < D ? i : f);
+        const int64_t k = e * D + (i < D ? i : 0);  // (padded slots re-read DOF 0 of the row)
         pv[u] = b.pose[k];
         gv[u] = b.g_pose[k];
         mv[u] = b.m_pose[k];
@@ -730,8 +731,8 @@ extern "C" int cdx_kin_step(const cdx_chain* chain, const cdx_kin_opt* cfg, cons
 }
 
 // One optimiser iteration: cdx_kin_cost then cdx_kin_step on the parameters / slots in `buf` — in ONE launch
-// (kin_cost4_kernel<…, STEP>) for the Kin optimiser's case (chain, four fingertips, Adam, no box clamp), else the two
-// launches.
+// (kin_cost4_kernel<…, STEP>) for the Kin optimiser's case (chain, four fingertips, Adam, no box clamp) and the SDF
+// optimiser's (no chain, four fingertips, RMSprop, box clamps), else the two launches.
 
 extern "C" int cdx_kin_iteration(const cdx_chain* chain, const cdx_kin_params* p, const cdx_kin_opt* cfg,
                                  const cdx_kin_opt_buffers* buf, int64_t E, int32_t n_tips, const int32_t* sign1,

@@ -113,10 +113,15 @@ __device__ __host__ inline unsigned audit_bin_floor(int b) {  // float bits of t
   return b >= AUDIT_BINS ? 0x7F800000u : 0x3F800000u + ((unsigned)b << 20);
 }
 
+// Groups per workgroup of the screen's selection kernel and of its count / place (compaction) kernels: the scratch
+// below and the launches in cdx_screen.hip are both sized from these.
+constexpr int SCREEN_SEL_BLOCK = 64;
+constexpr int SCREEN_CB_GROUPS = 256;
+
 // Words of compaction scratch the caller allocates right behind zkey's M words (select blocks' z histograms,
 // compaction block counts).
 inline int64_t screen_compact_words(int64_t G) {
-  return (G + 63) / 64 * AUDIT_BINS + 4 * ((G + 255) / 256) + 1;
+  return (G + SCREEN_SEL_BLOCK - 1) / SCREEN_SEL_BLOCK * AUDIT_BINS + 4 * ((G + SCREEN_CB_GROUPS - 1) / SCREEN_CB_GROUPS) + 1;
 }
 
 // Closure screening of the all-tip rows (G groups of T, M = G·T): screen partials in ws

@@ -25,6 +25,8 @@
 // on the CPU (max |Δstd²|/k0 = 1.5e-6 on the config-2 workload).
 #include <hip/hip_runtime.h>
 
+#include "cdx_ab.h"
+
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -519,7 +521,7 @@ __global__ __launch_bounds__(256) void gpis_screen_finalize(cdx_gpis g, const do
 // sqrt(a_f), below the exact std of the group's maximum, so the level kernel's argmax is unchanged.
 // The per-group selection kernels (one thread per group, latency-bound loads of the stripe partials)
 // run in 64-thread workgroups: G = 4096 groups spread over 64 CUs instead of 16.
-constexpr int SEL_BLOCK = 64;
+constexpr int SEL_BLOCK = cdx::SCREEN_SEL_BLOCK;  // (screen_compact_words sizes the histograms from it)
 
 using cdx::screen_margin;
 
@@ -603,7 +605,7 @@ __global__ __launch_bounds__(SEL_BLOCK) void screen_select_kernel(cdx_gpis g, co
 //                        block 0 writes the per-closure statistics and the cumulative block.
 // Audited beyond the cut: an input-keyed sample of ~1/SAMPLE of the other discarded rows (hash of the row and its
 // z), so the audit's checks also reach rows far below the keep threshold.
-constexpr int CB_GROUPS = 256;
+constexpr int CB_GROUPS = cdx::SCREEN_CB_GROUPS;  // (screen_compact_words sizes the block counts from it)
 constexpr unsigned AUDIT_SAMPLE_SHIFT = 9;  // 1 in 512
 __device__ __forceinline__ bool audit_sampled(int64_t q, unsigned z) {
   unsigned h = (unsigned)q * 0x9E3779B1u ^ z;
@@ -1013,7 +1015,7 @@ size_t screen_select_ws_bytes(const cdx_gpis& g, int64_t Ms) { return screen_ws_
 
 int screen_audit_rows() {
   static const int n = [] {
-    const char* e = getenv("CDX_SCREEN_AUDIT");
+    const char* e = cdx::ab_env("CDX_SCREEN_AUDIT");
     return e ? std::max(0, atoi(e)) : 64;
   }();
   return n;

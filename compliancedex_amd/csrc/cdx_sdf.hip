@@ -35,6 +35,8 @@
 // kernel (512-face LDS tiles); a wave holding a non-finite or |p| > 1e4 point runs the tile rule itself.
 // The choice is made on the device (no host sync).
 #include <hip/hip_runtime.h>
+
+#include "cdx_ab.h"
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -1050,7 +1052,7 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 bool sched_on() {  // CDX_SDF_SCHED=0: a batch ignores its schedule (point order, the A/B base)
   static const bool on = [] {
-    const char* e = getenv("CDX_SDF_SCHED");
+    const char* e = cdx::ab_env("CDX_SDF_SCHED");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -1058,7 +1060,7 @@ bool sched_on() {  // CDX_SDF_SCHED=0: a batch ignores its schedule (point order
 
 int sdf_mode() {  // CDX_SDF_MODE=exact forces the brute-force kernel (benchmarks, A/B tests)
   static const int m = [] {
-    const char* e = getenv("CDX_SDF_MODE");
+    const char* e = cdx::ab_env("CDX_SDF_MODE");
     return (e && e[0] == 'e') ? 1 : 0;
   }();
   return m;

@@ -23,8 +23,8 @@ from . import _native as N
 
 _PKG_STATES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "gpis_states")
 # Closure screening margin Δ = SCREEN_MARGIN × the calibrated max error of the split-precision estimate of std²
-# (cdx_gpis.screen_delta); CDX_SCREEN_MARGIN overrides it, 0 disables screening.
-SCREEN_MARGIN = float(os.environ.get("CDX_SCREEN_MARGIN", "32"))
+# (cdx_gpis.screen_delta).  A constant: no environment variable can shrink the margin of the shipped path.
+SCREEN_MARGIN = 32.0
 CALIB_QUERIES = 8192      # near the object (displaced inducing points, bounding box ± 5 cm)
 CALIB_FAR_QUERIES = 4096  # 5 cm … 3.5R from the inducing points (the screen's whole finite range)
 

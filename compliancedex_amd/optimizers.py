@@ -178,9 +178,12 @@ class _FusedLoop:
             query_batch([(self.mesh_def, tips, self.ws_tips, o[0]), (self.mesh, tips, self.ws_tips, o[1]),
                          (self.mesh, tgt, self.ws_tgt, o[2])], schedule=self.sched)
         elif not self.concurrent:
-            self.mesh_def.query(tips, workspace=self.ws_tips, reuse_order=not fresh, out=o[0])
+            if fresh:  # (sorted explicitly: a query on a mesh with NaN-capable faces neither sorts nor walks)
+                self.ws_tips.sort(tips)
+                self.ws_tgt.sort(tgt)
+            self.mesh_def.query(tips, workspace=self.ws_tips, reuse_order=True, out=o[0])
             self.mesh.query(tips, workspace=self.ws_tips, reuse_order=True, out=o[1])
-            self.mesh.query(tgt, workspace=self.ws_tgt, reuse_order=not fresh, out=o[2])
+            self.mesh.query(tgt, workspace=self.ws_tgt, reuse_order=True, out=o[2])
         else:
             # The three queries are independent: each culled kernel's tail (a few point groups far from the mesh)
             # leaves most of the chip idle, which the others fill.  The targets are sorted (when fresh) and queried

@@ -91,11 +91,18 @@ class PreparedMesh:
         face = torch.empty(P, dtype=torch.int32, device=dev) if want_face else None
         if P == 0:
             return dist, sign, normals, clst, face
-        ws = (workspace or self._ws).get(P, dev, reuse_order)
+        wsp = workspace or self._ws
+        # a mesh with NaN-capable faces (SDF_MESH_EXACT) scans every face: it neither reads nor writes a point order
+        walks = self.kind != N.SDF_MESH_EXACT
+        ws = wsp.get(P, dev, reuse_order and walks)
         flags = self.kind | (N.SDF_REUSE_ORDER if reuse_order else 0)
+        if not reuse_order and walks:
+            wsp.order_P = None  # (overwritten by this query's sort; valid again once it is enqueued)
         N.check(lib.cdx_sdf_query(N.ptr(self.buf), N.ptr(self.faces), self.faces.shape[0], N.ptr(points), P,
                                   N.ptr(dist), N.ptr(sign), N.ptr(normals), N.ptr(clst), N.ptr(face),
                                   N.ptr(ws), ws.numel(), flags, N.stream_ptr(dev)), "cdx_sdf_query")
+        if not reuse_order and walks:
+            wsp.order_P = P  # this query sorted its points: later reuse_order queries of P points may walk that order
         return dist, sign, normals, clst, face
 
 
@@ -149,7 +156,7 @@ def query_batch(items, schedule=None):
         points = points.detach().contiguous()
         P = points.shape[0]
         dev = points.device
-        if ws.buf is None or ws.P != P:
+        if ws.buf is None or ws.order_P != P:
             raise RuntimeError("query_batch: the workspace holds no order for these points (QueryWorkspace.sort)")
         dist, sign, normals, clst = out
         if not (dist.shape == (P,) and sign.shape == (P,) and normals.shape == (P, 3) and clst.shape == (P, 3) and
@@ -172,10 +179,13 @@ def query_batch(items, schedule=None):
 class QueryWorkspace:
     """Scratch of cdx_sdf_query (the points' Morton sort), regrown to the largest point count seen; it keeps the
     last sorted order, which a later query of P points may reuse (the same points on another mesh, or the same
-    points moved a little — a fused loop's next iterations)."""
+    points moved a little — a fused loop's next iterations).  ``order_P`` is the point count of the order it holds
+    (None: none) — set only by a sort (``sort``, or a query that sorts: not ``reuse_order``, a mesh without
+    NaN-capable faces), cleared when the buffer is regrown; ``reuse_order`` queries and ``query_batch`` require it
+    to match, so no walk ever reads an order that was never written."""
 
     def __init__(self):
-        self.buf, self.P = None, None
+        self.buf, self.order_P = None, None
 
     def sort(self, points):
         """The points' order alone (cdx_sdf_query_order): later queries of these points with ``reuse_order`` — on
@@ -188,18 +198,22 @@ class QueryWorkspace:
         if P == 0:
             return
         buf = self.get(P, dev)
+        self.order_P = None
         N.check(N.load().cdx_sdf_query_order(N.ptr(points), P, N.ptr(buf), buf.numel(), N.stream_ptr(dev)),
                 "cdx_sdf_query_order")
+        self.order_P = P
 
     def get(self, P, dev, reuse_order=False):
-        if reuse_order and self.P != P:
-            raise RuntimeError("reuse_order: the workspace's last query had a different point count")
+        """The scratch buffer for a query of P points (regrown if needed); ``reuse_order``: the query walks the held
+        order, which must be one of P points."""
+        if reuse_order and self.order_P != P:
+            raise RuntimeError("reuse_order: the workspace holds no order for these points (sort them first)")
         need = N.load().cdx_sdf_query_workspace(P)
         if self.buf is None or self.buf.numel() < need or self.buf.device != torch.device(dev):
             if reuse_order:
                 raise RuntimeError("reuse_order: the workspace holds no order for these points")
             self.buf = torch.empty(need, dtype=torch.uint8, device=dev)
-        self.P = P
+            self.order_P = None
         return self.buf
 
 

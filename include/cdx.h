@@ -285,6 +285,10 @@ int cdx_closure_screen_reset(const cdx_problem* p, int64_t E, void* workspace, c
  * screen / selection and the side-stream fork, 2: after the exact pass, 3: after the ∇std pass; 0 clears),
  * through the error path of a failed launch — which joins the side stream before returning. */
 int cdx_debug_fail_next_closure(int32_t stage);
+/* 1 if this library was built with -DCDX_AB_SWITCHES (an A/B build: it reads the CDX_* run-time switches of
+ * csrc/cdx_ab.h, including CDX_SCREEN_AUDIT / CDX_SCREEN_REPAIR / CDX_NO_SCREEN), 0 for the shipped build, which
+ * ignores them: every screened closure audits its discarded rows and repairs itself on a failed check. */
+int cdx_ab_switches(void);
 
 /* ------------------------------------------------------------ survivor exchange ------
  * Multi-GPU record pack (no reference counterpart — the reference is single-GPU):
@@ -397,8 +401,9 @@ int cdx_kin_step(const cdx_chain* chain, const cdx_kin_opt* cfg, const cdx_kin_o
                  int32_t n_tips, int32_t iteration, int32_t finalize, cdx_stream_t stream);
 /* One whole optimiser iteration on the loop state in `buf`: cdx_kin_cost (q = pose, tip = tips for rule 0 / tip = pose
  * for rule 1; loss, margin[iteration & 1], normal[iteration & 1] and the g_* gradients into buf's buffers) followed by
- * cdx_kin_step(iteration, finalize = 0).  The Kin optimiser's case (chain, four fingertips, rule 0, no clamp_box) runs
- * as ONE launch with the same results as the two; other cases run the two launches.  chain: rule 0 only. */
+ * cdx_kin_step(iteration, finalize = 0).  Two cases run as ONE launch with the same results as the two: the Kin
+ * optimiser's (rule 0 = Adam, a chain, four fingertips, no clamp_box) and the SDF optimiser's (rule 1 = RMSprop, no
+ * chain, four fingertips, box clamps allowed); other cases run the two launches.  chain: rule 0 only. */
 int cdx_kin_iteration(const cdx_chain* chain, const cdx_kin_params* p, const cdx_kin_opt* cfg,
                       const cdx_kin_opt_buffers* buf, int64_t E, int32_t n_tips, const int32_t* sign1, const float* n1,
                       const float* sqdist, const int32_t* sign2, const float* n2, const float* clst,

@@ -27,6 +27,17 @@ def test_library_exports_every_declared_symbol():
     assert lib.cdx_version().startswith(b"compliancedex_amd")
 
 
+def test_shipped_library_ignores_ab_switches():
+    """the shipped libcdx.so is built without -DCDX_AB_SWITCHES, so CDX_SCREEN_AUDIT / CDX_SCREEN_REPAIR /
+    CDX_NO_SCREEN and the schedule switches in a user's environment are ignored (csrc/cdx_ab.h); the default build's
+    -D list carries no A/B switch.  (tests/test_screen.py::test_env_switches_cannot_disable_the_repair runs the
+    closure with them set on the GPU.)"""
+    from compliancedex_amd import _native
+    from compliancedex_amd.build import DEFAULT_DEFINES
+    assert _native.load().cdx_ab_switches() == 0
+    assert "CDX_AB_SWITCHES" not in DEFAULT_DEFINES
+
+
 def test_bad_arguments_are_rejected_without_launch():
     import ctypes
     from compliancedex_amd import _native as N

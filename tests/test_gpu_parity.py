@@ -635,6 +635,59 @@ def test_sdf_stale_order_gives_the_same_results():
             assert _bitwise_equal_nan_aware(x, y)
 
 
+def test_sdf_workspace_order_only_from_a_sort(monkeypatch):
+    """a query on a mesh with NaN-capable faces (SDF_MESH_EXACT: brute-force tile rule) neither sorts nor
+    walks, so it must not leave a workspace looking as if it held an order.  A reuse_order query or a query_batch on
+    a culled mesh through that workspace raises instead of walking an unwritten order; the fused loop's sequential
+    variant (CDX_SDF_CONCURRENT=0) with an EXACT deflated mesh and a CULLED full mesh sorts explicitly and gives the
+    same bits as fresh one-shot queries."""
+    from compliancedex_amd import PreparedMesh, compute_sdf_with_faces
+    from compliancedex_amd import _native as N
+    from compliancedex_amd.optimizers import _FusedLoop
+    from compliancedex_amd.torchsdf import QueryWorkspace, query_batch
+    base = np.load(os.path.join(DATA, "meshes", "banana_faces.npy"))
+    bad_face = np.repeat(base[:1, :1], 3, axis=1)  # a zero-length-edge face: NaN-capable
+    faces = torch.from_numpy(base).to(DEV)
+    faces_exact = torch.from_numpy(np.concatenate([base * 0.9, bad_face]).astype(np.float32)).to(DEV)
+    culled, exact = PreparedMesh(faces), PreparedMesh(faces_exact)
+    assert culled.kind == N.SDF_MESH_CULLED and exact.kind == N.SDF_MESH_EXACT
+    rng = np.random.default_rng(31)
+    lo, hi = faces.reshape(-1, 3).min(0)[0], faces.reshape(-1, 3).max(0)[0]
+    P = 4096
+    pts = (lo - 0.05 + (hi - lo + 0.1) * torch.from_numpy(rng.random((P, 3))).to(DEV).float()).contiguous()
+    ws = QueryWorkspace()
+    exact.query(pts, workspace=ws)  # sizes the buffer, writes no order
+    assert ws.order_P is None
+    with pytest.raises(RuntimeError):
+        culled.query(pts, workspace=ws, reuse_order=True)
+    out = (torch.empty(P, device=DEV), torch.empty(P, dtype=torch.int32, device=DEV), torch.empty(P, 3, device=DEV),
+           torch.empty(P, 3, device=DEV))
+    with pytest.raises(RuntimeError):
+        query_batch([(culled, pts, ws, out)])
+    exact.query(pts, workspace=ws, reuse_order=True)  # the EXACT scan reads no order: allowed
+    culled.query(pts, workspace=ws)  # a walking query sorts: the order is held now
+    assert ws.order_P == P
+    a = [t.cpu().numpy() for t in culled.query(pts, workspace=ws, reuse_order=True)[:4]]
+    b = [t.cpu().numpy() for t in compute_sdf_with_faces(pts, faces)[:4]]
+    for x, y in zip(a, b):
+        assert _bitwise_equal_nan_aware(x, y)
+    monkeypatch.setenv("CDX_SDF_CONCURRENT", "0")
+    E, T = P // 4, 4
+    tgt = (lo + (hi - lo) * torch.from_numpy(rng.random((E, T, 3))).to(DEV).float()).contiguous()
+    loop = _FusedLoop(E, T, torch.zeros(E, 3, device=DEV), tgt.clone(), torch.zeros(E, T, device=DEV), faces,
+                      faces_exact, DEV)
+    assert loop.mesh_def.kind == N.SDF_MESH_EXACT and loop.concurrent == 0
+    for it in range(3):
+        moved = (pts + 1e-3 * it).contiguous()
+        got = [t.clone().cpu().numpy() for t in loop.queries(moved, tgt + 1e-3 * it)]
+        d_e = compute_sdf_with_faces(moved, faces_exact)
+        d_c = compute_sdf_with_faces(moved, faces)
+        d_t = compute_sdf_with_faces((tgt + 1e-3 * it).view(-1, 3).contiguous(), faces)
+        want = [d_e[1], d_e[2], d_c[0], d_c[1], d_c[2], d_c[3], d_t[0], d_t[1], d_t[3]]
+        for x, y in zip(got, want):
+            assert _bitwise_equal_nan_aware(x, y.cpu().numpy())
+
+
 def test_sdf_batch_schedule_gives_the_same_results():
     """cdx_sdf_query_batch with a launch schedule (heaviest point groups of the previous launch first): over several
     launches — the first in point order, later ones in the schedule's order, one whose schedule was built by a

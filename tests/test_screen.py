@@ -574,6 +574,43 @@ def test_failed_checks_repair_the_closure(scale, banana2000):
         assert rel_err(c[k], b[k]) <= TOL_EQ, (k, rel_err(c[k], b[k]))
 
 
+_ENV_REPAIR_CHILD = r"""
+import sys, json, numpy as np
+sys.path.insert(0, {repo!r})
+from tests.test_screen import _closure, _opt, _report, OUTS
+from compliancedex_amd.workloads import prob_inputs, synthetic_banana_gpis
+from tests._helpers import rel_err
+g = synthetic_banana_gpis(2000, device="cuda")
+cfg, opt = _opt()
+E = 4096
+inputs = prob_inputs(cfg["ref_q"], E, seed=1000, spread=True)
+a, st = _closure(opt, g, inputs, screen=True, delta_scale=1e-3)
+r = _report(opt, g, E)
+b, _ = _closure(opt, g, inputs, screen=False)
+err = max(rel_err(a[k], b[k]) for k in OUTS)
+print(json.dumps(dict(repaired=r["repaired"], audited=r["audited_rows"], exact=r["exact_rows"], err=err,
+                      flips_equal=bool(np.array_equal(a["flip"], b["flip"])))))
+"""
+
+
+def test_env_switches_cannot_disable_the_repair():
+    """with CDX_SCREEN_REPAIR=0, CDX_SCREEN_AUDIT=0 and CDX_NO_SCREEN=1 in the environment, the shipped
+    library still screens, audits the discarded rows and repairs a closure whose checks fail (margins 1e-3 × Δ), so it
+    returns the unscreened fp64 closure's results (TOL_EQ).  (Read once per process: a child process.)"""
+    import json
+    import os
+    import subprocess
+    import sys
+    from tests.conftest import REPO
+    env = dict(os.environ, CDX_SCREEN_REPAIR="0", CDX_SCREEN_AUDIT="0", CDX_NO_SCREEN="1")
+    r = subprocess.run([sys.executable, "-c", _ENV_REPAIR_CHILD.format(repo=REPO)], capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["repaired"] == 1 and res["audited"] > 0 and 0 < res["exact"] < 4 * 4096, res
+    assert res["flips_equal"] and res["err"] <= TOL_EQ, res
+
+
 @pytest.mark.parametrize("fused", [True, False])
 def test_optimize_with_failed_checks_equals_unscreened(fused, banana2000):
     """A 30-iteration optimise loop with injected misses (margins 1e-3 × Δ), through the fused loop and
