@@ -149,10 +149,26 @@ def config4_kin(args, dev):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     # the timed region: the iterations (the two meshes are prepared once per optimize call, before it)
     kin.loop_events = ev[:2]
-    res = kin.optimize(*x, 1, copy.deepcopy(mesh), verbose=False)
-    kin.loop_events = None
+    mesh_c = copy.deepcopy(mesh)
     torch.cuda.synchronize()
+    t_call = time.perf_counter()
+    res = kin.optimize(*x, 1, mesh_c, verbose=False)
+    torch.cuda.synchronize()
+    t_call = time.perf_counter() - t_call
+    kin.loop_events = None
     ms_iter = ev[0].elapsed_time(ev[1]) / iters
+    # the reference's non-finite case (:212-213): candidates whose last-iteration loss is not finite, and fingertips
+    # with a non-finite coordinate after the last step
+    nonfinite = int((~torch.isfinite(kin.last_loss)).sum())
+    nonfinite_tips = int((~torch.isfinite(kin.last_tips)).any(dim=1).sum())
+    # the same loop over 20 iterations (before any candidate diverges: DESIGN §5b), timed the same way
+    kin20 = KinGraspOptimizer("iiwa7_allegro", links, offs, palm_offset=palm.tolist(), num_iters=20,
+                              optimize_target=True, ref_q=[0.0] * 23, device=dev)
+    kin20.loop_events = ev[2:]
+    kin20.optimize(*x, 1, copy.deepcopy(mesh), verbose=False)
+    torch.cuda.synchronize()
+    ms_iter20 = ev[2].elapsed_time(ev[3]) / 20
+    nonfinite20 = int((~torch.isfinite(kin20.last_loss)).sum())
     # the TorchSDF forward of one iteration alone (the loop's three queries on its final fingertips / targets)
     from compliancedex_amd import PreparedMesh
     from compliancedex_amd.optimizers import _face_vertices
@@ -202,6 +218,13 @@ def config4_kin(args, dev):
     return {"workload": "config 4: KinGraspOptimizer (fused) on iiwa7_allegro (23 DOF, chain depth 13), "
                         f"E={E} candidates, 16 384-face banana mesh, optimize_target, 3 TorchSDF queries per iteration",
             "iterations": iters, "ms_per_iteration": ms_iter, "evals_per_s": E / (ms_iter * 1e-3),
+            "nonfinite_candidates": nonfinite, "nonfinite_fingertips": nonfinite_tips,
+            "call_ms": t_call * 1e3, "setup_ms": t_call * 1e3 - ms_iter * iters,
+            "ms_per_iteration_20": ms_iter20, "nonfinite_candidates_20": nonfinite20,
+            "timing_note": "ms_per_iteration: HIP events around the iterations of one optimize call (device Kabsch "
+                           "noise); call_ms: host wall time of that whole call (setup_ms = call_ms − the iterations: "
+                           "the two meshes' preparation with their host k-d builds and uploads, the loop state, one "
+                           "host wait); ms_per_iteration_20: a 20-iteration call timed the same way",
             "launches_per_iteration": "3 TorchSDF queries in one launch (sdf_tree_batch_kernel, heaviest point groups of "
                                       "the last iteration first, + its one-workgroup schedule kernel; the fingertips' and "
                                       "the targets' Morton order — bbox partials, keys, an 18-bit radix sort — every 16th "
@@ -221,6 +244,101 @@ def config4_kin(args, dev):
                                      "queries' whole forward (sorts and culling tests included), so it falls as the "
                                      "culling improves; brute_force_equivalent = the reference's brute-force pair "
                                      "flops (P·F·46) over the same time"}}
+
+
+def config4_closure(args, dev, gpis):
+    """Config 4 as BASELINE states it (configs[3]: "AllegroHand on kuka_allegro arm FK chain + TorchSDF self-collision
+    enabled, 16 384 candidates, bf16 GPIS kernel-matrix on MFMA"): the prob-mode closure (optimize_pregrasp.py:741-769)
+    with compute_collision_loss fused in (:671-701; the reference leaves the call commented out at :765) on iiwa7_allegro
+    (23 DOF, chain depth 13), E = 16 384 candidates around config 2's N = 2000 banana GPIS.  The GPIS kernel-matrix
+    product's low-precision MFMA leg is the fp16 2-slice screen (gpis_screen_kernel); every value that reaches the loss
+    comes from the fp64 MFMA passes.  Timed over 10 closures after 5 warm-up (HIP events on the closure's
+    stream), then a 5-closure all-stage pass for the three GEMM kernels' rooflines."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from compliancedex_amd import DifferentiableRobotModel, ProbabilisticGraspOptimizer
+    from compliancedex_amd import _native as N
+    from compliancedex_amd.urdf import load_robot
+    from compliancedex_amd.workloads import CONFIG4_OFFSETS, prob_inputs
+
+    E, D = 16384, 23
+    links = load_robot("iiwa7_allegro")["config"]["ee_link_name"]
+    ref_q = [0.0] * D
+    _, comp, target, _ = prob_inputs(ref_q, E, seed=8, spread=True)
+    rng = np.random.default_rng(9)
+    q = 0.05 * rng.standard_normal((E, D))
+    # the "palm" pose is the arm base: placed so the fingertips at q = 0 surround the banana
+    tips0 = DifferentiableRobotModel("iiwa7_allegro", device=dev).compute_forward_kinematics(
+        torch.zeros(1, D, device=dev), links, offsets=CONFIG4_OFFSETS)[0].view(4, 3).double().mean(0).cpu().numpy()
+    center = np.load(os.path.join(REPO, "compliancedex_amd", "data", "banana_center.npy"))
+    palm = np.concatenate([center - tips0 + 0.005 * rng.standard_normal((E, 3)), 0.02 * rng.standard_normal((E, 3))], 1)
+    pairs = [[0, 1], [0, 2], [0, 3], [1, 2], [1, 3], [2, 3]]
+    opt = ProbabilisticGraspOptimizer("iiwa7_allegro", links, CONFIG4_OFFSETS, palm_offset=palm, ref_q=ref_q,
+                                      optimize_target=True, optimize_palm=True, device=dev, anchor_link_names=links,
+                                      anchor_link_offsets=CONFIG4_OFFSETS, collision_pairs=pairs, collision=True)
+    t = [torch.from_numpy(np.ascontiguousarray(a)).to(dev).requires_grad_(True)
+         for a in (q, comp, target, palm[:, :3], palm[:, 3:])]
+
+    def step():
+        for x in t:
+            x.grad = None
+        opt.closure(*t, 1, gpis, E)
+    for _ in range(5):
+        step()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    reps = 10
+    torch.cuda.synchronize()
+    ev[0].record()
+    for _ in range(reps):
+        step()
+    ev[1].record()
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    lib = N.load()
+    msa = (ctypes.c_double * N.PROF_STAGES)()
+    cnt = (ctypes.c_int64 * N.PROF_STAGES)()
+    N.check(lib.cdx_profile_read(msa, cnt), "cdx_profile_read")  # (clears the main run's counts)
+    N.check(lib.cdx_profile_enable((1 << N.PROF_STAGES) - 1), "cdx_profile_enable")
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    N.check(lib.cdx_profile_read(msa, cnt), "cdx_profile_read")
+    lib.cdx_profile_enable(0)
+    names = ["queries", "gpis_mean", "gpis_std_var", "cost_bwd", "gpis_std_grad", "gpis_screen"]
+    stage = {n: (msa[i] / cnt[i] if cnt[i] else None) for i, n in enumerate(names)}
+    n_ind = args.n_inducing
+    lq = opt.problem(gpis, 1).n_query_levels
+    m_std, m_grad = lq * E * 4, lq * E
+    scr = opt.screen_stats(gpis, E)
+    m_exact = scr["exact_rows"] if scr else m_std
+    tri = float(n_ind) * (n_ind + 1)
+
+    def roof(kernel, flops, ms_k, peak, note):
+        a = flops / (ms_k * 1e-3) / 1e12 if ms_k else None
+        return {"bound": "mfma", "kernel": kernel, "achieved": a, "peak": peak, "unit": "TFLOP/s",
+                "frac": (a / peak) if a else None, "flops_per_launch": flops, "ms": ms_k, "note": note}
+    out = {"workload": "config 4: prob-mode closure fwd+bwd with compute_collision_loss fused (6 fingertip pairs, anchor "
+                       f"and palm floor terms), iiwa7_allegro (23 DOF, chain depth 13), E={E} candidates, N={n_ind} banana "
+                       "GPIS (config 2's), 3 pregrasp levels; fp16 2-slice MFMA screen + exact fp64 MFMA passes",
+           "ms_per_closure": ms, "evals_per_s": E / (ms * 1e-3), "closures_timed": reps,
+           "nan_candidates": int((~torch.isfinite(opt.total_loss)).sum()), "stage_ms": stage,
+           "roofline": roof("gpis_std_kernel<VARL> (v_mfma_f64_16x16x4_f64, K*·L⁻ᵀ, screened rows)" if scr else
+                            "gpis_std_kernel<VAR> (v_mfma_f64_16x16x4_f64, K*·L⁻ᵀ)", m_exact * tri,
+                            stage["gpis_std_var"], FP64_MFMA_PEAK_TFLOPS,
+                            f"{m_exact} of {m_std} all-tip rows x N(N+1), exact fp64 whitened form"),
+           "roofline_grad": roof("gpis_std_kernel<GRADV> (∇std)", m_grad * tri, stage["gpis_std_grad"],
+                                 FP64_MFMA_PEAK_TFLOPS, f"{m_grad} argmax-fingertip queries x N(N+1)"),
+           "timing_note": "ms_per_closure: HIP events over 10 closures after 5 warm-up; stage ms (rooflines) from a "
+                          "5-closure pass with every stage's events on, after it"}
+    if scr:
+        out["roofline_screen"] = roof("gpis_screen_kernel (v_mfma_f32_32x32x16_f16, 2-slice fp16 split)",
+                                      3 * m_std * tri, stage["gpis_screen"], F16_MFMA_PEAK_TFLOPS,
+                                      f"{m_std} all-tip rows x 3 x N(N+1) fp16 MFMA flops")
+        out["exact_rows"] = m_exact
+    return out
 
 
 def main():
@@ -482,6 +600,7 @@ def main():
         out["roofline"] = dict(out[dom], which=dom)
         if world == 1 and not args.no_config4:
             out["config4_kin"] = config4_kin(args, dev)
+            out["config4_closure"] = config4_closure(args, dev, gpis)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, ref_q, cfg)
         print(json.dumps(out), flush=True)

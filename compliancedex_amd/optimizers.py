@@ -375,6 +375,12 @@ class KinGraspOptimizer:
         if verbose:
             print(st.opt_margin, st.opt_normal)
         self.best_loss = st.opt_value
+        # the last iteration's per-candidate loss and fingertips (device, no copy; the reference prints the
+        # non-finite case at :212-213)
+        self.last_loss, self.last_tips = (loss if self.num_iters else None), st.tips
+        self.last_params = (q, tgt, comp)  # the parameters after the last step (device, updated in place)
+        # (trace_rows: the loop's device state too — moments, best iterate — for state-injection checks)
+        self.last_loop = st if trace_rows else None
         return st.best()
 
 

@@ -263,7 +263,17 @@ def kabsch(S1, S2, w, noise):
     c1 = S1.mean(dim=1, keepdim=True)
     c2 = S2.mean(dim=1, keepdim=True)
     H = (w * (S1 - c1)).transpose(1, 2) @ (w * (S2 - c2))
-    U, _, Vh = torch.linalg.svd(H + 1e-6 * noise)
+    Hn = H + 1e-6 * noise
+    # A non-finite batch element (a diverged candidate) comes out NaN on the reference's CUDA path and the loop goes
+    # on (its `isnan` print, :212-213); torch's CPU LAPACK path raises instead, so only the finite rows are factored
+    fin = torch.isfinite(Hn).flatten(1).all(dim=1)
+    if bool(fin.all()):
+        U, _, Vh = torch.linalg.svd(Hn)
+    else:
+        U = torch.full_like(Hn, float("nan"))
+        Vh = torch.full_like(Hn, float("nan"))
+        if bool(fin.any()):
+            U[fin], _, Vh[fin] = torch.linalg.svd(Hn[fin])
     V = Vh.mH
     flip = torch.linalg.det(V @ U.transpose(1, 2)) < 0.0
     sign = torch.ones(S1.shape[0], 3, 3, dtype=F32)
@@ -429,7 +439,7 @@ def closure_with_grads(problem, q, comp, target, palm, noise):
 
 # ----------------------------------------------------------------------------- Kin mode (config 4)
 def kin_sdf_loop(chain, ee_links, ee_offsets, palm_offset, ref_q, q0, target0, comp0, mu, faces, faces_deflate, sdf,
-                 noise_tape, iters, mass=0.1, com=(0.0, 0.0, 0.0), gravity=True):
+                 noise_tape, iters, mass=0.1, com=(0.0, 0.0, 0.0), gravity=True, adam_state=None):
     """KinGraspOptimizer.optimize with optimize_target=True (optimize_pregrasp.py:152-227), in the
     reference's float32: FK (:143-150, fresh-state — the loop only calls it recursively), the three
     TorchSDF calls per iteration (:186-188) through ``sdf(points, faces) -> (sqdist, sign, normals,
@@ -437,7 +447,10 @@ def kin_sdf_loop(chain, ee_links, ee_offsets, palm_offset, ref_q, q0, target0, c
     signed normals (:190-191), force_eq_reward with the replayed Kabsch noise (:192-198), the six cost
     terms (:199-208), backward, best-iterate tracking (:214-222) and Adam (:171-173, :223).
     ``tar_sign`` is read as [E, T] (the reference's [E·T] broadcast at :207 runs only for E = 1, where
-    the two agree).  Returns (loss [iters, E], opt_q, opt_comp, opt_target, success flag)."""
+    the two agree).  ``adam_state`` (optional): (step, m_q, v_q, m_target, v_target, m_comp, v_comp) — resume from
+    another implementation's loop state after ``step`` iterations (Adam's moments and step count, as torch.optim.Adam
+    keeps them), so the loop continues from exactly that state (``noise_tape`` then holds the draws from that
+    iteration on).  Returns (loss [iters, E], opt_q, opt_comp, opt_target, success flag)."""
     q = torch.as_tensor(q0, dtype=F32).clone().requires_grad_(True)
     comp = torch.as_tensor(comp0, dtype=F32).clone().requires_grad_(True)
     target = torch.as_tensor(target0, dtype=F32).clone().requires_grad_(True)
@@ -445,6 +458,11 @@ def kin_sdf_loop(chain, ee_links, ee_offsets, palm_offset, ref_q, q0, target0, c
     ref = torch.tensor(list(map(float, ref_q)))
     optim = torch.optim.Adam([{"params": q, "lr": 2e-3}, {"params": target, "lr": 1e-5},
                               {"params": comp, "lr": 0.2}])
+    if adam_state is not None:
+        step, *mv = adam_state
+        for prm, m, v in zip((q, target, comp), mv[0::2], mv[1::2]):
+            optim.state[prm] = {"step": torch.tensor(float(step)), "exp_avg": torch.as_tensor(m, dtype=F32).clone(),
+                                "exp_avg_sq": torch.as_tensor(v, dtype=F32).clone()}
     E, T = target.shape[0], target.shape[1]
     opt_q, opt_comp, opt_target = q.detach().clone(), comp.detach().clone(), target.detach().clone()
     opt_value = torch.full((E,), float("inf"))

@@ -339,6 +339,90 @@ def test_config4_kin_fused_at_size_vs_oracle(monkeypatch):
         assert rel_err(x.detach().cpu().double().numpy()[sl], y.double().numpy()) < 1e-4
 
 
+def test_config4_kin_divergence_vs_oracle():
+    """VERDICT r5 (top item): the regime where config 4's timed Kin loop (workloads.config4_kin_inputs, E = 16 384,
+    the bench's workload) loses candidates to NaN, pinned against the oracle.  200 iterations with a recorded Kabsch
+    noise tape (float32 seed-7 draws, as tools/c4_divergence_gpu.py):
+    (a) candidates do diverge (3 by iteration 200 on this tape, the first at 163), each from a finite loss to NaN;
+    (b) every diverged candidate hit the reference's own NaN: at its last finite iteration s − 1 (the loop re-run to
+        exactly that state) one of its fingertips lies ON the mesh — the C oracle of TorchSDF gives sqdist == 0 for the
+        GPU's fingertip bits — where the reference's dist_cost = 1000·sqrt(dist) (optimize_pregrasp.py:206) has an
+        infinite derivative and TorchSDF's backward 2·g·(p − clst) (sdf.py:56-64, .cu:256-270) gives inf·0 = NaN:
+        the oracle's autograd through that step returns a non-finite joint-angle gradient, so Adam makes q NaN and the
+        loss at s is NaN — the reference prints exactly this case (:212-213);
+    (c) from the same dumped state (parameters, Adam moments and step count injected into oracle.kin_sdf_loop), the
+        controls' losses at s − 1, s and s + 1 equal the GPU's within 1e-4 (a diverged candidate's own loss at s − 1
+        is not compared: TorchSDF's normal of a point ON the mesh is 0/0, which the reward reads);
+    (d) from the start, the diverged candidates and 8 finite controls follow the oracle within 1e-4 for 80 iterations.
+    Which candidates land exactly on the mesh is decided by the last ulp of the float32 fingertip (the oracle's FK and
+    the device FK differ by an ulp or two, as two reference runs on CPU and CUDA would), and past ≈ 100 iterations
+    single trajectories separate at the 1e-4 level by the same rounding (tools/c4_divergence_cpu.py): the test pins
+    the mechanism per candidate, not the identity of the candidates."""
+    import os
+    import compliancedex_amd.optimizers as opts
+    from compliancedex_amd import KinGraspOptimizer, TriangleMesh
+    from compliancedex_amd.workloads import config4_kin_inputs
+    from oracle.cdx_oracle import kin_sdf_loop
+    from tests import _sdf_oracle
+    from tests.conftest import REPO
+    E, iters = 16384, 200
+    links, offs, palm, q, target, comp = config4_kin_inputs(E, device=DEV)
+    tape = np.random.default_rng(7).random((iters, E, 3, 3), dtype=np.float32)
+    mesh_path = os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_mesh.npz")
+    x = [torch.from_numpy(a).to(DEV) for a in (q, target, comp)]
+
+    def run(n):
+        kin = KinGraspOptimizer("iiwa7_allegro", links, offs, palm_offset=palm.tolist(), num_iters=n,
+                                optimize_target=True, ref_q=[0.0] * 23, device=DEV)
+        kin.optimize(*[t.clone() for t in x], 1, TriangleMesh.from_npz(mesh_path), verbose=False,
+                     kabsch_noise=[torch.from_numpy(tape[s]).to(DEV) for s in range(n)], trace_rows=True, fused=True)
+        torch.cuda.synchronize()
+        return kin, torch.stack(kin.loss_rows).cpu().numpy()
+
+    _, L = run(iters)
+    bad = ~np.isfinite(L)
+    div = np.nonzero(bad.any(0))[0]
+    first = bad.argmax(0)
+    assert 0 < len(div) <= 64, len(div)  # (a) the regime is exercised, and it is rare
+    for c in div:
+        s = first[c]
+        assert s > 0 and np.isfinite(L[:s, c]).all() and bad[s:, c].all()
+    mesh = TriangleMesh.from_npz(mesh_path)
+    faces = opts._face_vertices(mesh, "cpu")
+    faces_def = opts._face_vertices(mesh.scale(0.9, center=[0, 0, 0]), "cpu")
+    chain, _ = oracle_chain("iiwa7_allegro")
+    rng = np.random.default_rng(5)
+    ctrl = np.setdiff1d(rng.choice(E, 12, replace=False), div)[:8]
+    for s in sorted(set(int(first[c]) for c in div))[:4]:
+        kin, Ls = run(s - 1)  # the loop's state at iteration s − 1 (the last finite loss of the candidates below)
+        assert np.array_equal(Ls[:, ~bad[s - 1]], L[:s - 1, ~bad[s - 1]])  # (deterministic: the same run)
+        st = kin.last_loop
+        cs = np.concatenate([div[first[div] == s], ctrl])
+        ct = torch.from_numpy(cs).to(DEV)
+        tips = st.tips.view(E, 4, 3)[ct].cpu().numpy()
+        for k, c in enumerate(cs[:(first[div] == s).sum()]):  # (b) a fingertip exactly on the mesh, NaN gradient
+            o = _sdf_oracle.forward(tips[k], faces.numpy())
+            on = np.nonzero(o[0] == 0.0)[0]
+            assert len(on) > 0, (c, o[0])
+            p = torch.from_numpy(tips[k]).requires_grad_(True)
+            d = _sdf_oracle.oracle_sdf(p, faces)[0]
+            (1000 * torch.sqrt(d)).sum().backward()
+            assert not torch.isfinite(p.grad[on]).all(), (c, p.grad)
+        # (c) the oracle from the dumped state (Adam's moments and step count injected), the tape from iteration s − 1
+        g = [t[ct].cpu().numpy() for t in (st.pose, st.target, st.comp)]
+        mv = [t[ct].cpu().numpy() for t in (st.m[0], st.v[0], st.m[1], st.v[1], st.m[2], st.v[2])]
+        lo, *_ = kin_sdf_loop(chain, links, offs, palm, [0.0] * 23, *g, 1, faces, faces_def, _sdf_oracle.oracle_sdf,
+                              tape[s - 1:s + 2][:, cs], 3, adam_state=(s - 1, *mv))
+        lo = lo.double().numpy()
+        nd = (first[div] == s).sum()
+        assert rel_err(lo[:, nd:], L[s - 1:s + 2, cs[nd:]]) < 1e-4, (lo[:, nd:], L[s - 1:s + 2, cs[nd:]])
+    # (d) from the start, 80 iterations
+    sl = np.concatenate([div, ctrl])
+    lo, *_ = kin_sdf_loop(chain, links, offs, palm, [0.0] * 23, q[sl], target[sl], comp[sl], 1, faces, faces_def,
+                          _sdf_oracle.oracle_sdf, tape[:80][:, sl], 80)
+    assert rel_err(L[:80, sl], lo.double().numpy()) < 1e-4
+
+
 def test_config4_sdf_mode_fused_at_size_vs_oracle(monkeypatch):
     """The fused SDF-mode loop (SDFGraspOptimizer: three TorchSDF queries on prepared meshes, cdx_kin_cost
     without a chain, cdx_kin_step's RMSprop and box clamps) at config 4's batch, E = 16 384 candidates (fingertips

@@ -3,7 +3,7 @@ go non-finite on config 4's inputs (workloads.config4_kin_inputs: iiwa7_allegro,
 candidate slices for ITERS iterations with a random Kabsch noise tape and prints, per iteration, the count of
 candidates whose loss is non-finite, and the first iteration of each diverged candidate.
 
-  python tools/c4_divergence_cpu.py [n_candidates] [iters] [start]
+  python tools/c4_divergence_cpu.py [n_candidates] [iters] [start] [comma-separated candidate list]
 """
 import json
 import os
@@ -44,16 +44,19 @@ def main():
     torch.set_num_threads(8)
     E = 16384
     chain, links, palm, q, target, comp = inputs(E)
-    sl = np.arange(start, start + n)
+    sl = np.arange(start, start + n) if len(sys.argv) <= 4 else np.array([int(v) for v in sys.argv[4].split(',')])
+    n = len(sl)
     mesh = TriangleMesh.from_npz(os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_mesh.npz"))
     faces = _face_vertices(mesh, "cpu")
     faces_def = _face_vertices(mesh.scale(0.9, center=[0, 0, 0]), "cpu")
-    noise = np.random.default_rng(7).random((iters, n, 3, 3)).astype(np.float32)
+    # the GPU tool's tape (tools/c4_divergence_gpu.py): the same draw for all E candidates, sliced
+    noise = np.random.default_rng(7).random((iters, E, 3, 3), dtype=np.float32)[:, sl]
     loss, oq, oc, ot, _ = kin_sdf_loop(chain, links, CONFIG4_OFFSETS, palm, [0.0] * 23, q[sl], target[sl], comp[sl], 1,
                                        faces, faces_def, _sdf_oracle.oracle_sdf, noise, iters)
     L = loss.numpy()
     bad = ~np.isfinite(L)
     first = np.where(bad.any(0), bad.argmax(0), -1)
+    np.save(f"/tmp/c4_oracle_loss_{iters}_{start}_{n}.npy", L)
     print(json.dumps({"n": n, "iters": iters, "start": start,
                       "nonfinite_by_iter": [int(b) for b in bad.sum(1)],
                       "diverged": {int(sl[i]): int(first[i]) for i in range(n) if first[i] >= 0}}))
