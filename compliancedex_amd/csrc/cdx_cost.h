@@ -20,16 +20,17 @@ namespace cdx {
 // ---------------------------------------------------------------- 3×3 SVD (f64)
 // Compare-exchange of singular value j and j+1 (descending) with their columns of A and V, by
 // selects: static register indices, where a permutation array would put A and V in scratch.
-CDX_HD void svd3_cswap(double* s, double* A, double* V, int j) {
+template <class Real = double>
+CDX_HD void svd3_cswap(Real* s, Real* A, Real* V, int j) {
   const bool sw = s[j] < s[j + 1];
-  const double a = s[j], b = s[j + 1];
+  const Real a = s[j], b = s[j + 1];
   s[j] = sw ? b : a;
   s[j + 1] = sw ? a : b;
   for (int i = 0; i < 3; ++i) {
-    const double x = A[3 * i + j], y = A[3 * i + j + 1];
+    const Real x = A[3 * i + j], y = A[3 * i + j + 1];
     A[3 * i + j] = sw ? y : x;
     A[3 * i + j + 1] = sw ? x : y;
-    const double v = V[3 * i + j], w = V[3 * i + j + 1];
+    const Real v = V[3 * i + j], w = V[3 * i + j + 1];
     V[3 * i + j] = sw ? w : v;
     V[3 * i + j + 1] = sw ? v : w;
   }
@@ -37,44 +38,57 @@ CDX_HD void svd3_cswap(double* s, double* A, double* V, int j) {
 
 // One-sided Jacobi on the columns of A: A·V = U·diag(S), S descending.  Backward-stable
 // with high relative accuracy for the small singular values the rank-1-plus-noise
-// Kabsch matrices of the reference's initial configuration have.
-CDX_HD void svd3(const double* H, double* U, double* S, double* V) {
+// Kabsch matrices of the reference's initial configuration have.  Real = double (the prob-mode closure: the
+// reference's float64 tensors) or float (the Kin / SDF optimisers: the reference's float32 tensors), with the
+// rotation-skip and convergence thresholds at the type's epsilon.
+template <class Real>
+struct Svd3Tol;
+template <>
+struct Svd3Tol<double> {
+  static constexpr double skip = 1e-17, stop = 1e-16;
+};
+template <>
+struct Svd3Tol<float> {
+  static constexpr float skip = 1e-8f, stop = 6e-8f;
+};
+template <class Real = double>
+CDX_HD void svd3(const Real* H, Real* U, Real* S, Real* V) {
 #if defined(CDX_DIAG_NOSVD)  // timing-only diagnostic build (outputs wrong): the level kernel without its SVD
-  for (int i = 0; i < 9; ++i) { U[i] = V[i] = (i % 4 == 0) ? 1.0 : 0.0; }
-  S[0] = 3.0 + H[0]; S[1] = 2.0 + H[4]; S[2] = 1.0 + H[8];
+  for (int i = 0; i < 9; ++i) { U[i] = V[i] = (i % 4 == 0) ? Real(1) : Real(0); }
+  S[0] = Real(3) + H[0]; S[1] = Real(2) + H[4]; S[2] = Real(1) + H[8];
   return;
 #endif
-  double A[9];
-  for (int i = 0; i < 9; ++i) { A[i] = H[i]; V[i] = (i % 4 == 0) ? 1.0 : 0.0; }
+  Real A[9];
+  for (int i = 0; i < 9; ++i) { A[i] = H[i]; V[i] = (i % 4 == 0) ? Real(1) : Real(0); }
   for (int sweep = 0; sweep < 12; ++sweep) {
-    double off = 0.0;
+    Real off = Real(0);
     for (int pr = 0; pr < 3; ++pr) {
       const int p = pr == 2 ? 1 : 0, qq = pr == 0 ? 1 : 2;
-      double a = 0, b = 0, g = 0;
+      Real a = 0, b = 0, g = 0;
       for (int i = 0; i < 3; ++i) {
         a += A[3 * i + p] * A[3 * i + p];
         b += A[3 * i + qq] * A[3 * i + qq];
         g += A[3 * i + p] * A[3 * i + qq];
       }
-      if (g == 0.0) continue;
-      const double rel = fabs(g) / sqrt(a * b);
+      if (g == Real(0)) continue;
+      const Real rel = fabs(g) / sqrt(a * b);
       off = rel > off ? rel : off;
-      if (rel < 1e-17) continue;
-      const double zeta = (b - a) / (2.0 * g);
-      const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-      const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+      if (rel < Svd3Tol<Real>::skip) continue;
+      const Real zeta = (b - a) / (Real(2) * g);
+      const Real t = (zeta >= 0 ? Real(1) : Real(-1)) / (fabs(zeta) + sqrt(Real(1) + zeta * zeta));
+      const Real c = Real(1) / sqrt(Real(1) + t * t), s = c * t;
       for (int i = 0; i < 3; ++i) {
-        const double ap = A[3 * i + p], aq = A[3 * i + qq];
+        const Real ap = A[3 * i + p], aq = A[3 * i + qq];
         A[3 * i + p] = c * ap - s * aq;
         A[3 * i + qq] = s * ap + c * aq;
-        const double vp = V[3 * i + p], vq = V[3 * i + qq];
+        const Real vp = V[3 * i + p], vq = V[3 * i + qq];
         V[3 * i + p] = c * vp - s * vq;
         V[3 * i + qq] = s * vp + c * vq;
       }
     }
-    if (off < 1e-16) break;
+    if (off < Svd3Tol<Real>::stop) break;
   }
-  double s[3];
+  Real s[3];
   for (int j = 0; j < 3; ++j) s[j] = sqrt(A[j] * A[j] + A[3 + j] * A[3 + j] + A[6 + j] * A[6 + j]);
   // descending bubble network (0,1), (1,2), (0,1) with strict comparisons: the permutation of a
   // bubble sort of the column indices by s
@@ -83,7 +97,7 @@ CDX_HD void svd3(const double* H, double* U, double* S, double* V) {
   svd3_cswap(s, A, V, 0);
   for (int j = 0; j < 3; ++j) {
     S[j] = s[j];
-    for (int i = 0; i < 3; ++i) U[3 * i + j] = s[j] > 0 ? A[3 * i + j] / s[j] : 0.0;
+    for (int i = 0; i < 3; ++i) U[3 * i + j] = s[j] > 0 ? A[3 * i + j] / s[j] : Real(0);
   }
   if (!(S[2] > 0)) {  // exactly singular: complete U with the cross product
     U[2] = U[3] * U[7] - U[6] * U[4];
@@ -92,52 +106,57 @@ CDX_HD void svd3(const double* H, double* U, double* S, double* V) {
   }
 }
 
-CDX_HD double det3(const double* m) {
+template <class Real = double>
+CDX_HD Real det3(const Real* m) {
   return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) + m[2] * (m[3] * m[7] - m[4] * m[6]);
 }
 
 // Kabsch state kept for the backward pass.
-struct KabschTape {
-  double U[9], S[3], V[9];
-  double d;  // +1, or -1 when det(V·Uᵀ) < 0 (the reference's `mask`, :64-66)
+template <class Real = double>
+struct KabschTapeT {
+  Real U[9], S[3], V[9];
+  Real d;  // +1, or -1 when det(V·Uᵀ) < 0 (the reference's `mask`, :64-66)
 };
+using KabschTape = KabschTapeT<double>;
 
-// R = V·diag(1,1,d)·Uᵀ of H' = H + 1e-6·noise.
-CDX_HD void kabsch_rotation(const double* H, const double* noise, KabschTape& tp, double* R) {
-  double Hn[9];
-  for (int i = 0; i < 9; ++i) Hn[i] = H[i] + 1e-6 * noise[i];
+// R = V·diag(1,1,d)·Uᵀ of H' = H + 1e-6·noise (the noise draw in Real, as the reference's rand_like(H)).
+template <class Real = double>
+CDX_HD void kabsch_rotation(const Real* H, const double* noise, KabschTapeT<Real>& tp, Real* R) {
+  Real Hn[9];
+  for (int i = 0; i < 9; ++i) Hn[i] = H[i] + Real(1e-6) * (Real)noise[i];
   svd3(Hn, tp.U, tp.S, tp.V);
-  double R0[9];
+  Real R0[9];
   mat3_mul_nt(tp.V, tp.U, R0);
-  tp.d = det3(R0) < 0.0 ? -1.0 : 1.0;
-  double Vd[9];
+  tp.d = det3(R0) < Real(0) ? Real(-1) : Real(1);
+  Real Vd[9];
   for (int i = 0; i < 3; ++i) { Vd[3 * i] = tp.V[3 * i]; Vd[3 * i + 1] = tp.V[3 * i + 1]; Vd[3 * i + 2] = tp.V[3 * i + 2] * tp.d; }
   mat3_mul_nt(Vd, tp.U, R);
 }
 
 // gH from gR through R = V·D·Uᵀ and the SVD.
-CDX_HD void kabsch_rotation_bwd(const KabschTape& tp, const double* gR, double* gH) {
-  const double* U = tp.U;
-  const double* V = tp.V;
-  const double* S = tp.S;
+template <class Real = double>
+CDX_HD void kabsch_rotation_bwd(const KabschTapeT<Real>& tp, const Real* gR, Real* gH) {
+  const Real* U = tp.U;
+  const Real* V = tp.V;
+  const Real* S = tp.S;
   // gU = gRᵀ·V·D ; gV = gR·U·D
-  double gU[9], gV[9], t[9];
+  Real gU[9], gV[9], t[9];
   mat3_mul_tn(gR, V, t);
   for (int i = 0; i < 3; ++i) { gU[3 * i] = t[3 * i]; gU[3 * i + 1] = t[3 * i + 1]; gU[3 * i + 2] = t[3 * i + 2] * tp.d; }
   mat3_mul(gR, U, t);
   for (int i = 0; i < 3; ++i) { gV[3 * i] = t[3 * i]; gV[3 * i + 1] = t[3 * i + 1]; gV[3 * i + 2] = t[3 * i + 2] * tp.d; }
-  double UgU[9], VgV[9];
+  Real UgU[9], VgV[9];
   mat3_mul_tn(U, gU, UgU);
   mat3_mul_tn(V, gV, VgV);
-  double X[9];
+  Real X[9];
   for (int j = 0; j < 3; ++j)
     for (int k = 0; k < 3; ++k) {
-      if (j == k) { X[3 * j + k] = 0.0; continue; }
-      const double sku = UgU[3 * j + k] - UgU[3 * k + j];
-      const double skv = VgV[3 * j + k] - VgV[3 * k + j];
+      if (j == k) { X[3 * j + k] = Real(0); continue; }
+      const Real sku = UgU[3 * j + k] - UgU[3 * k + j];
+      const Real skv = VgV[3 * j + k] - VgV[3 * k + j];
       X[3 * j + k] = (sku * S[k] + S[j] * skv) / (S[k] * S[k] - S[j] * S[j]);
     }
-  double UX[9];
+  Real UX[9];
   mat3_mul(U, X, UX);
   mat3_mul_nt(UX, V, gH);
 }
@@ -265,24 +284,24 @@ CDX_HD ForceEqParams force_eq_params(const cdx_problem& P) {
 
 // NT: fingertip count at compile time (0: runtime, up to CDX_MAX_TIPS); G: gravity spring at
 // compile time (0 / 1; -1: runtime) — with both fixed every loop has a constant trip count.
-template <int NT, int G = -1>
+template <int NT, int G = -1, class Real = double>
 struct ForceEq {
   static constexpr int NTA = NT > 0 ? NT : CDX_MAX_TIPS;
   int T_rt, NP_rt;
   // The tape keeps what backward cannot cheaply recompute; the weighted centred points, R·S1,
   // the residuals, directions, rotated normals and forces are recomputed there by the same
   // expressions (bit-identical values) — keeping them made the level kernel spill to scratch.
-  double S1[NTA + 1][3], S2[NTA + 1][3], w[NTA + 1], n[NTA][3];
-  double c1[3], c2[3];
-  KabschTape tp;
-  double R[9], W, t[3];
-  double dn[NTA], ang[NTA], mpre[NTA], margin[NTA], fn[NTA];
-  double reward;
+  Real S1[NTA + 1][3], S2[NTA + 1][3], w[NTA + 1], n[NTA][3];
+  Real c1[3], c2[3];
+  KabschTapeT<Real> tp;
+  Real R[9], W, t[3];
+  Real dn[NTA], ang[NTA], mpre[NTA], margin[NTA], fn[NTA];
+  Real reward;
   int flip;
 
   // The points, weights and centroids of the weighted Kabsch fit (everything before the SVD).
-  CDX_HDM void setup(const ForceEqParams& fp, int T_, const double (*tip)[3], const double* target, const double* comp,
-                     const double (*nrm)[3]) {
+  CDX_HDM void setup(const ForceEqParams& fp, int T_, const Real (*tip)[3], const Real* target, const Real* comp,
+                     const Real (*nrm)[3]) {
     T_rt = T_;
     const int T = NT > 0 ? NT : T_;
     const bool grav = G >= 0 ? G != 0 : fp.gravity != 0;
@@ -290,13 +309,13 @@ struct ForceEq {
     const int NP = (NT > 0 && G >= 0) ? (G ? NT + 1 : NT) : NP_rt;
 #pragma unroll
     for (int f = 0; f < T; ++f) {
-      for (int i = 0; i < 3; ++i) { S1[f][i] = tip[f][i]; S2[f][i] = target[3 * f + i]; n[f][i] = nrm ? nrm[f][i] : 0.0; }
+      for (int i = 0; i < 3; ++i) { S1[f][i] = tip[f][i]; S2[f][i] = target[3 * f + i]; n[f][i] = nrm ? nrm[f][i] : Real(0); }
       w[f] = comp[f];
     }
     if (grav) {
-      for (int i = 0; i < 3; ++i) S1[T][i] = fp.com[i];
-      S2[T][0] = 0.0; S2[T][1] = 0.0; S2[T][2] = fp.dummy_target_z;
-      w[T] = fp.dummy_comp;
+      for (int i = 0; i < 3; ++i) S1[T][i] = (Real)fp.com[i];
+      S2[T][0] = 0.0; S2[T][1] = 0.0; S2[T][2] = (Real)fp.dummy_target_z;
+      w[T] = (Real)fp.dummy_comp;
     }
     c1[0] = c1[1] = c1[2] = 0.0;
     c2[0] = c2[1] = c2[2] = 0.0;
@@ -309,15 +328,15 @@ struct ForceEq {
   // H = Σ w_i (S1_i − c1)(w_i (S2_i − c2))ᵀ, then the rotation and its tape (R = V·D·Uᵀ of H + 1e-6·noise).
   CDX_HDM void rotation(const double* noise) {
     const int NP = (NT > 0 && G >= 0) ? (G ? NT + 1 : NT) : NP_rt;
-    double H[9];
+    Real H[9];
     {
-      double Pm[NTA + 1][3], Qm[NTA + 1][3];
+      Real Pm[NTA + 1][3], Qm[NTA + 1][3];
 #pragma unroll
       for (int i = 0; i < NP; ++i)
         for (int j = 0; j < 3; ++j) { Pm[i][j] = w[i] * (S1[i][j] - c1[j]); Qm[i][j] = w[i] * (S2[i][j] - c2[j]); }
       for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) {
-          double acc = 0.0;
+          Real acc = 0.0;
 #pragma unroll
           for (int i = 0; i < NP; ++i) acc += Pm[i][r] * Qm[i][c];
           H[3 * r + c] = acc;
@@ -326,7 +345,7 @@ struct ForceEq {
     {
       // svd3 sorts with data-dependent indices: run it on a separate tape so that only this small
       // object, not the whole ForceEq, has to live in scratch
-      KabschTape t_;
+      KabschTapeT<Real> t_;
       kabsch_rotation(H, noise, t_, R);
       tp = t_;
     }
@@ -341,22 +360,22 @@ struct ForceEq {
     rec[21] = tp.d;
   }
   CDX_HDM void load_rotation(const double* rec) {
-    for (int i = 0; i < 9; ++i) { tp.U[i] = rec[i]; tp.V[i] = rec[12 + i]; R[i] = rec[22 + i]; }
-    for (int i = 0; i < 3; ++i) tp.S[i] = rec[9 + i];
-    tp.d = rec[21];
+    for (int i = 0; i < 9; ++i) { tp.U[i] = (Real)rec[i]; tp.V[i] = (Real)rec[12 + i]; R[i] = (Real)rec[22 + i]; }
+    for (int i = 0; i < 3; ++i) tp.S[i] = (Real)rec[9 + i];
+    tp.d = (Real)rec[21];
   }
 
   // Everything after the rotation: translation, equilibrium residuals, friction margins, reward.
-  CDX_HDM void finish(const ForceEqParams& fp, const double* comp) {
+  CDX_HDM void finish(const ForceEqParams& fp, const Real* comp) {
     const int T = NT > 0 ? NT : T_rt;
     const int NP = (NT > 0 && G >= 0) ? (G ? NT + 1 : NT) : NP_rt;
-    flip = tp.d < 0 ? 1 : 0;
+    flip = tp.d < Real(0) ? 1 : 0;
     W = 0.0;
-    double num[3] = {0, 0, 0};
+    Real num[3] = {0, 0, 0};
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       W += w[i];
-      double rs[3];
+      Real rs[3];
       mat3_vec(R, S1[i], rs);
       for (int j = 0; j < 3; ++j) num[j] += w[i] * (S2[i][j] - rs[j]);
     }
@@ -364,22 +383,22 @@ struct ForceEq {
     reward = 0.0;
 #pragma unroll
     for (int f = 0; f < T; ++f) {
-      double diff[3], dir[3], ne[3], force[3];
+      Real diff[3], dir[3], ne[3], force[3];
       residual(f, diff);
       dn[f] = sqrt(dot3(diff, diff));
       for (int i = 0; i < 3; ++i) { dir[i] = diff[i] / dn[f]; force[i] = comp[f] * (-diff[i]); }
       mat3_vec(R, n[f], ne);
       ang[f] = dot3(dir, ne);
-      mpre[f] = ang[f] - fp.cos_mu;
-      margin[f] = mpre[f] < -0.9999 ? -0.9999 : mpre[f];
+      mpre[f] = ang[f] - (Real)fp.cos_mu;
+      margin[f] = mpre[f] < Real(-0.9999) ? Real(-0.9999) : mpre[f];
       fn[f] = sqrt(dot3(force, force));
-      reward += 0.2 * log(ang[f] + 1) + 0.8 * log(margin[f] + 1);
+      reward += Real(0.2) * log(ang[f] + Real(1)) + Real(0.8) * log(margin[f] + Real(1));
     }
   }
 
   // rot: a record save_rotation wrote for the same inputs, or null (the SVD runs here).
-  CDX_HDM void forward(const ForceEqParams& fp, int T_, const double (*tip)[3], const double* target,
-                      const double* comp, const double (*nrm)[3], const double* noise, const double* rot = nullptr) {
+  CDX_HDM void forward(const ForceEqParams& fp, int T_, const Real (*tip)[3], const Real* target,
+                      const Real* comp, const Real (*nrm)[3], const double* noise, const double* rot = nullptr) {
     setup(fp, T_, tip, target, comp, nrm);
     if (rot)
       load_rotation(rot);
@@ -389,79 +408,79 @@ struct ForceEq {
   }
 
   // diff_f = R·S1_f + t − target_f (S2_f holds target_f)
-  CDX_HDM void residual(int f, double* diff) const {
-    double rs[3];
+  CDX_HDM void residual(int f, Real* diff) const {
+    Real rs[3];
     mat3_vec(R, S1[f], rs);
     for (int i = 0; i < 3; ++i) diff[i] = rs[i] + t[i] - S2[f][i];
   }
 
-  CDX_HDM void backward(double g_rw, const double* g_fn, const double* comp, double (*g_tip)[3], double (*g_target)[3],
-                       double* g_comp) const {
+  CDX_HDM void backward(Real g_rw, const Real* g_fn, const Real* comp, Real (*g_tip)[3], Real (*g_target)[3],
+                       Real* g_comp) const {
     const int T = NT > 0 ? NT : T_rt;
     const int NP = (NT > 0 && G >= 0) ? (G ? NT + 1 : NT) : NP_rt;
-    double gR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g_t[3] = {0, 0, 0};
-    double g_S1[NTA + 1][3], g_S2[NTA + 1][3], g_w[NTA + 1];
+    Real gR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g_t[3] = {0, 0, 0};
+    Real g_S1[NTA + 1][3], g_S2[NTA + 1][3], g_w[NTA + 1];
 #pragma unroll
     for (int i = 0; i < NP; ++i) { g_S1[i][0] = g_S1[i][1] = g_S1[i][2] = 0; g_S2[i][0] = g_S2[i][1] = g_S2[i][2] = 0; g_w[i] = 0; }
 #pragma unroll
     for (int f = 0; f < T; ++f) {
-      double diff[3], dir[3], ne[3];
+      Real diff[3], dir[3], ne[3];
       residual(f, diff);
       for (int i = 0; i < 3; ++i) dir[i] = diff[i] / dn[f];
       mat3_vec(R, n[f], ne);
-      double gang = g_rw * 0.2 / (ang[f] + 1);
-      if (mpre[f] >= -0.9999) gang += g_rw * 0.8 / (margin[f] + 1);
-      double gdiff[3] = {0, 0, 0};
+      Real gang = g_rw * Real(0.2) / (ang[f] + Real(1));
+      if (mpre[f] >= Real(-0.9999)) gang += g_rw * Real(0.8) / (margin[f] + Real(1));
+      Real gdiff[3] = {0, 0, 0};
       // force norm → force = −comp·diff
       if (fn[f] > 0) {
-        double gforce[3];
+        Real gforce[3];
         for (int i = 0; i < 3; ++i) gforce[i] = g_fn[f] * (comp[f] * (-diff[i])) / fn[f];
         g_w[f] += -dot3(gforce, diff);
         for (int i = 0; i < 3; ++i) gdiff[i] += -comp[f] * gforce[i];
       }
       // ang = dir·ne ; ne = R·n (n detached)
-      double gdir[3], gne[3];
+      Real gdir[3], gne[3];
       for (int i = 0; i < 3; ++i) { gdir[i] = gang * ne[i]; gne[i] = gang * dir[i]; }
       for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) gR[3 * r + c] += gne[r] * n[f][c];
-      const double pd = dot3(dir, gdir);
+      const Real pd = dot3(dir, gdir);
       for (int i = 0; i < 3; ++i) gdiff[i] += (gdir[i] - dir[i] * pd) / dn[f];
       // diff = R·S1_f + t − target_f
       for (int i = 0; i < 3; ++i) { g_t[i] += gdiff[i]; g_target[f][i] -= gdiff[i]; }
       for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) gR[3 * r + c] += gdiff[r] * S1[f][c];
-      double rt[3];
+      Real rt[3];
       mat3t_vec(R, gdiff, rt);
       for (int i = 0; i < 3; ++i) g_S1[f][i] += rt[i];
     }
     // t = Σ w_i (S2_i − R·S1_i) / W
     {
-      double gnum[3] = {g_t[0] / W, g_t[1] / W, g_t[2] / W};
-      const double gW = -dot3(g_t, t) / W;
+      Real gnum[3] = {g_t[0] / W, g_t[1] / W, g_t[2] / W};
+      const Real gW = -dot3(g_t, t) / W;
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
-        double rs[3];
+        Real rs[3];
         mat3_vec(R, S1[i], rs);
-        double r_i[3] = {S2[i][0] - rs[0], S2[i][1] - rs[1], S2[i][2] - rs[2]};
+        Real r_i[3] = {S2[i][0] - rs[0], S2[i][1] - rs[1], S2[i][2] - rs[2]};
         g_w[i] += gW + dot3(gnum, r_i);
         for (int j = 0; j < 3; ++j) g_S2[i][j] += w[i] * gnum[j];
         for (int r = 0; r < 3; ++r)
           for (int c = 0; c < 3; ++c) gR[3 * r + c] -= w[i] * gnum[r] * S1[i][c];
-        double rt[3], wg[3] = {w[i] * gnum[0], w[i] * gnum[1], w[i] * gnum[2]};
+        Real rt[3], wg[3] = {w[i] * gnum[0], w[i] * gnum[1], w[i] * gnum[2]};
         mat3t_vec(R, wg, rt);
         for (int j = 0; j < 3; ++j) g_S1[i][j] -= rt[j];
       }
     }
     // R ← SVD(H') ← H = Σ P_i Q_iᵀ
-    double gH[9];
+    Real gH[9];
     kabsch_rotation_bwd(tp, gR, gH);
-    double g_c1[3] = {0, 0, 0}, g_c2[3] = {0, 0, 0};
+    Real g_c1[3] = {0, 0, 0}, g_c2[3] = {0, 0, 0};
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      double gP[3], gQ[3];
-      double d1[3] = {S1[i][0] - c1[0], S1[i][1] - c1[1], S1[i][2] - c1[2]};
-      double d2[3] = {S2[i][0] - c2[0], S2[i][1] - c2[1], S2[i][2] - c2[2]};
-      const double Pm[3] = {w[i] * d1[0], w[i] * d1[1], w[i] * d1[2]}, Qm[3] = {w[i] * d2[0], w[i] * d2[1], w[i] * d2[2]};
+      Real gP[3], gQ[3];
+      Real d1[3] = {S1[i][0] - c1[0], S1[i][1] - c1[1], S1[i][2] - c1[2]};
+      Real d2[3] = {S2[i][0] - c2[0], S2[i][1] - c2[1], S2[i][2] - c2[2]};
+      const Real Pm[3] = {w[i] * d1[0], w[i] * d1[1], w[i] * d1[2]}, Qm[3] = {w[i] * d2[0], w[i] * d2[1], w[i] * d2[2]};
       mat3_vec(gH, Qm, gP);
       mat3t_vec(gH, Pm, gQ);
       g_w[i] += dot3(gP, d1) + dot3(gQ, d2);

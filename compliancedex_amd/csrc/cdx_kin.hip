@@ -20,6 +20,12 @@
 
 namespace {
 
+#if defined(CDX_KIN_FE_F32)  // (A/B: the reward in the reference's float32 — 0.338 → 0.330 ms per Kin iteration, but its
+using FeReal = float;        // SVD backward then divides by S_k² − S_j² = 0 on near-repeated singular values, a NaN the
+#else                        // f64 path does not produce there: profiles/r06g_kin_fe_f32_ab.jsonl)
+using FeReal = double;
+#endif
+
 __device__ __forceinline__ uint64_t kin_mix(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -278,8 +284,19 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
   for (int i = 0; i < 3; ++i) fp.com[i] = (double)p.fe.com[i];
   fp.dummy_target_z = (double)p.fe.dummy_target_z;
   fp.dummy_comp = (double)p.fe.dummy_comp;
-  cdx::ForceEq<NT> fe;
-#if !defined(CDX_KIN_DIAG_NOFE)
+  cdx::ForceEq<NT, -1, FeReal> fe;
+#if defined(CDX_KIN_FE_F32)
+  FeReal cpf[NT];
+#pragma unroll
+  for (int k = 0; k < NT; ++k) cpf[k] = (FeReal)cp[k];
+  {
+    FeReal tpf[NT][3], tgf[NT * 3], nrf[NT][3];  // (the reference's float32 values: exact)
+#pragma unroll
+    for (int k = 0; k < NT; ++k)
+      for (int i = 0; i < 3; ++i) { tpf[k][i] = (FeReal)tp[k][i]; tgf[3 * k + i] = (FeReal)tg[3 * k + i]; nrf[k][i] = (FeReal)nr[k][i]; }
+    fe.forward(fp, NT, tpf, tgf, cpf, nrf, nz);
+  }
+#elif !defined(CDX_KIN_DIAG_NOFE)
   fe.forward(fp, NT, tp, tg, cp, nr, nz);
 #endif
 
@@ -301,7 +318,13 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
     dcost += sd[k];
     tcost += ts[k] * std_[k];
   }
+#if defined(CDX_KIN_FE_F32)
+  double fn[NT];
+#pragma unroll
+  for (int k = 0; k < NT; ++k) fn[k] = (double)fe.fn[k];
+#else
   const double* fn = fe.fn;
+#endif
   double zmax = -fn[0];
   for (int k = 1; k < NT; ++k) zmax = -fn[k] > zmax ? -fn[k] : zmax;
   double ez[NT], esum = 0.0;
@@ -312,11 +335,12 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
     v[k] = fn[k] * sm[k];
     fcost += v[k] > 1.0 ? 1.0 : v[k];
   }
-  const double lval = FK ? -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost + qn * 10.0
-                         : -fe.reward * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost;
+  const double rw = (double)fe.reward;
+  const double lval = FK ? -rw * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost + qn * 10.0
+                         : -rw * 5.0 + 1000.0 * dcost + 10.0 * tcost + cn * 10.0 - fcost;
   if (on && f == 0) loss[e] = lval;
   double mo = 0.0;
-  for (int k = 0; k < NT; ++k) mo = k == f ? fe.margin[k] : mo;
+  for (int k = 0; k < NT; ++k) mo = k == f ? (double)fe.margin[k] : mo;
   if (on) margin[r] = mo;
 
   // ---- backward (dl = 1)
@@ -339,7 +363,23 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
     gsm_dot += g_sm[k] * sm[k];
   }
   for (int k = 0; k < NT; ++k) g_fn[k] += -(sm[k] * (g_sm[k] - gsm_dot));
-#if !defined(CDX_KIN_DIAG_NOFE)
+#if defined(CDX_KIN_FE_F32)
+  {
+    FeReal g_fnf[NT], gtf[NT][3], ggf[NT][3], gcf[NT];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      g_fnf[k] = (FeReal)g_fn[k];
+      gcf[k] = FeReal(0);
+      for (int i = 0; i < 3; ++i) gtf[k][i] = ggf[k][i] = FeReal(0);
+    }
+    fe.backward(FeReal(-5.0), g_fnf, cpf, gtf, ggf, gcf);
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      for (int i = 0; i < 3; ++i) { gt[k][i] += (double)gtf[k][i]; gg[k][i] += (double)ggf[k][i]; }
+      gc[k] += (double)gcf[k];
+    }
+  }
+#elif !defined(CDX_KIN_DIAG_NOFE)
   fe.backward(-5.0, g_fn, cp, gt, gg, gc);
 #endif
   // this lane's fingertip (selects: no dynamic register indexing)
