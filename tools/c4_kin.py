@@ -2,7 +2,7 @@
 iiwa7_allegro candidates, 16 384-face banana) — ms per iteration (HIP events), the TorchSDF work counters, and
 the same for round 4's timed workload ('far': arm base at the origin, q = 0.3·N(0, 1)).
 
-  python tools/c4_kin.py [ITERS] [REPS]
+  python tools/c4_kin.py [ITERS] [REPS] [around,far]
 """
 import json
 import os
@@ -61,5 +61,6 @@ def run(kind, iters, reps):
 if __name__ == "__main__":
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    for kind in ("around", "far"):
+    kinds = sys.argv[3].split(",") if len(sys.argv) > 3 else ["around", "far"]
+    for kind in kinds:
         run(kind, iters, reps)
