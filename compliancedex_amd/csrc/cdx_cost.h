@@ -51,6 +51,20 @@ template <>
 struct Svd3Tol<float> {
   static constexpr float skip = 1e-8f, stop = 6e-8f;
 };
+CDX_HD double svd3_rsqrt(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return rsqrt(x);
+#else
+  return 1.0 / sqrt(x);
+#endif
+}
+CDX_HD float svd3_rsqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return rsqrtf(x);
+#else
+  return 1.0f / sqrtf(x);
+#endif
+}
 template <class Real = double>
 CDX_HD void svd3(const Real* H, Real* U, Real* S, Real* V) {
 #if defined(CDX_DIAG_NOSVD)  // timing-only diagnostic build (outputs wrong): the level kernel without its SVD
@@ -61,7 +75,11 @@ CDX_HD void svd3(const Real* H, Real* U, Real* S, Real* V) {
   Real A[9];
   for (int i = 0; i < 9; ++i) { A[i] = H[i]; V[i] = (i % 4 == 0) ? Real(1) : Real(0); }
   for (int sweep = 0; sweep < 12; ++sweep) {
+#if defined(CDX_SVD_JACOBI_R5)  // (A/B: the round-5 rotation — 3 roots and 4 divisions per pair)
     Real off = Real(0);
+#else
+    bool more = false;
+#endif
     for (int pr = 0; pr < 3; ++pr) {
       const int p = pr == 2 ? 1 : 0, qq = pr == 0 ? 1 : 2;
       Real a = 0, b = 0, g = 0;
@@ -71,12 +89,25 @@ CDX_HD void svd3(const Real* H, Real* U, Real* S, Real* V) {
         g += A[3 * i + p] * A[3 * i + qq];
       }
       if (g == Real(0)) continue;
+#if defined(CDX_SVD_JACOBI_R5)
       const Real rel = fabs(g) / sqrt(a * b);
       off = rel > off ? rel : off;
       if (rel < Svd3Tol<Real>::skip) continue;
       const Real zeta = (b - a) / (Real(2) * g);
       const Real t = (zeta >= 0 ? Real(1) : Real(-1)) / (fabs(zeta) + sqrt(Real(1) + zeta * zeta));
       const Real c = Real(1) / sqrt(Real(1) + t * t), s = c * t;
+#else
+      // the same rotation with one root, one division and one reciprocal root: |g|/sqrt(ab) compared squared,
+      // t = sgn(ζ)/(|ζ| + sqrt(1 + ζ²)) with ζ = (b − a)/2g written as sgn(ζ)·2|g| / (|b − a| + sqrt((b − a)² + 4g²)),
+      // c = rsqrt(1 + t²) — the Jacobi SVD's divisions and roots were ≈ 17 µs of the Kin cost kernel (r05bd)
+      const Real g2 = g * g, ab = a * b;
+      if (!(g2 < Svd3Tol<Real>::stop * Svd3Tol<Real>::stop * ab)) more = true;
+      if (g2 < Svd3Tol<Real>::skip * Svd3Tol<Real>::skip * ab) continue;
+      const Real d = b - a, ag = fabs(g);
+      const Real zs = (d >= 0) == (g >= 0) || d == Real(0) ? Real(2) * ag : Real(-2) * ag;  // sgn(ζ)·2|g|
+      const Real t = zs / (fabs(d) + sqrt(d * d + Real(4) * g2));
+      const Real c = svd3_rsqrt(Real(1) + t * t), s = c * t;
+#endif
       for (int i = 0; i < 3; ++i) {
         const Real ap = A[3 * i + p], aq = A[3 * i + qq];
         A[3 * i + p] = c * ap - s * aq;
@@ -86,7 +117,11 @@ CDX_HD void svd3(const Real* H, Real* U, Real* S, Real* V) {
         V[3 * i + qq] = s * vp + c * vq;
       }
     }
+#if defined(CDX_SVD_JACOBI_R5)
     if (off < Svd3Tol<Real>::stop) break;
+#else
+    if (!more) break;
+#endif
   }
   Real s[3];
   for (int j = 0; j < 3; ++j) s[j] = sqrt(A[j] * A[j] + A[3 + j] * A[3 + j] + A[6 + j] * A[6 + j]);
