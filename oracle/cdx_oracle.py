@@ -439,7 +439,7 @@ def closure_with_grads(problem, q, comp, target, palm, noise):
 
 # ----------------------------------------------------------------------------- Kin mode (config 4)
 def kin_sdf_loop(chain, ee_links, ee_offsets, palm_offset, ref_q, q0, target0, comp0, mu, faces, faces_deflate, sdf,
-                 noise_tape, iters, mass=0.1, com=(0.0, 0.0, 0.0), gravity=True, adam_state=None):
+                 noise_tape, iters, mass=0.1, com=(0.0, 0.0, 0.0), gravity=True, adam_state=None, state_out=None):
     """KinGraspOptimizer.optimize with optimize_target=True (optimize_pregrasp.py:152-227), in the
     reference's float32: FK (:143-150, fresh-state — the loop only calls it recursively), the three
     TorchSDF calls per iteration (:186-188) through ``sdf(points, faces) -> (sqdist, sign, normals,
@@ -450,7 +450,9 @@ def kin_sdf_loop(chain, ee_links, ee_offsets, palm_offset, ref_q, q0, target0, c
     the two agree).  ``adam_state`` (optional): (step, m_q, v_q, m_target, v_target, m_comp, v_comp) — resume from
     another implementation's loop state after ``step`` iterations (Adam's moments and step count, as torch.optim.Adam
     keeps them), so the loop continues from exactly that state (``noise_tape`` then holds the draws from that
-    iteration on).  Returns (loss [iters, E], opt_q, opt_comp, opt_target, success flag)."""
+    iteration on).  ``state_out`` (optional dict): receives the loop state after the last step in the same form
+    (``adam_state`` plus the parameters q, target, comp).  Returns (loss [iters, E], opt_q, opt_comp, opt_target,
+    success flag)."""
     q = torch.as_tensor(q0, dtype=F32).clone().requires_grad_(True)
     comp = torch.as_tensor(comp0, dtype=F32).clone().requires_grad_(True)
     target = torch.as_tensor(target0, dtype=F32).clone().requires_grad_(True)
@@ -497,6 +499,10 @@ def kin_sdf_loop(chain, ee_links, ee_offsets, palm_offset, ref_q, q0, target0, c
                 opt_target[flag] = target[flag]
                 opt_comp[flag] = comp[flag]
         optim.step()
+    if state_out is not None:
+        st = [optim.state[prm] for prm in (q, target, comp)]
+        state_out["adam_state"] = (int(st[0]["step"]), *[t.clone() for x in st for t in (x["exp_avg"], x["exp_avg_sq"])])
+        state_out.update(q=q.detach().clone(), target=target.detach().clone(), comp=comp.detach().clone())
     return torch.stack(trace), opt_q, opt_comp, opt_target, bool((opt_margin > 0.0).all())
 
 

@@ -144,6 +144,48 @@ def test_kin_sdf_loop_oracle_vs_reference_run():
     assert flag == bool(d["flag"])
 
 
+def test_kin_sdf_loop_resumes_from_adam_state():
+    """oracle.kin_sdf_loop resumed from a loop state (parameters, Adam's moments and step count — the form
+    test_config4_kin_divergence_vs_oracle injects from the GPU's loop) continues the uninterrupted run bit for bit:
+    12 iterations of the reference's mode_kin case straight, against 5 + 7 with the state handed over."""
+    import os
+    from compliancedex_amd.optimizers import TriangleMesh, _face_vertices
+    from oracle.cdx_oracle import kin_sdf_loop
+    from tests._sdf_oracle import oracle_sdf
+    from tests.conftest import REPO
+    d = golden("mode_kin.npz")
+    chain, robot = oracle_chain("allegro")
+    cfg = robot["config"]
+    mesh = TriangleMesh.from_npz(os.path.join(REPO, "compliancedex_amd", "data", "meshes", "banana_mesh.npz"))
+    faces = _face_vertices(mesh, "cpu")
+    faces_def = _face_vertices(mesh.scale(0.9, center=[0, 0, 0]), "cpu")
+    args = (chain, cfg["ee_link_name"], cfg["ee_link_offset"], d["palm3"], cfg["ref_q"])
+    iters, k = int(d["iters"]), 5
+    full, *_ = kin_sdf_loop(*args, d["q"], d["target"], d["comp"], 1, faces, faces_def, oracle_sdf, d["noise"], iters)
+    st = {}
+    head, *_ = kin_sdf_loop(*args, d["q"], d["target"], d["comp"], 1, faces, faces_def, oracle_sdf, d["noise"][:k], k,
+                            state_out=st)
+    tail, *_ = kin_sdf_loop(*args, st["q"], st["target"], st["comp"], 1, faces, faces_def, oracle_sdf, d["noise"][k:],
+                            iters - k, adam_state=st["adam_state"])
+    assert torch.equal(torch.cat([head, tail]), full)
+
+
+def test_oracle_kabsch_nonfinite_rows():
+    """The oracle's Kabsch factors only the finite rows (the reference's CUDA SVD returns NaN for a diverged row, where
+    torch's CPU LAPACK raises): the finite rows equal the all-finite call's, a NaN row's rotation is NaN."""
+    from oracle.cdx_oracle import kabsch
+    rng = np.random.default_rng(3)
+    S1, S2 = torch.from_numpy(rng.standard_normal((6, 5, 3))), torch.from_numpy(rng.standard_normal((6, 5, 3)))
+    w, noise = torch.from_numpy(rng.random((6, 5))), torch.from_numpy(rng.random((6, 3, 3)))
+    R, t, flip = kabsch(S1, S2, w, noise)
+    S1b = S1.clone()
+    S1b[2, 1, 0] = float("nan")
+    Rb, tb, _ = kabsch(S1b, S2, w, noise)
+    keep = torch.tensor([0, 1, 3, 4, 5])
+    assert torch.equal(Rb[keep], R[keep]) and torch.equal(tb[keep], t[keep])
+    assert torch.isnan(Rb[2]).all()
+
+
 def test_sdf_mode_loop_oracle_vs_reference_run():
     """The oracle's SDF-mode loop (oracle.sdf_mode_loop: 3 TorchSDF calls through the C oracle → force_eq_reward
     → costs → RMSprop → box clamps, float32) against the reference's own SDFGraspOptimizer run (golden mode_sdf:
