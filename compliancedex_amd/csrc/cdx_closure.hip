@@ -638,6 +638,7 @@ struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;  // main → side before mean A, side → main after it
   hipEvent_t gate = nullptr, joinB = nullptr; // main → side after the ∇std pass, side → main after mean B
+  hipEvent_t late = nullptr;                   // main → side after the refine kernel (mean_sched() 4)
   // the split mean schedule (mean_sched() 2): a second side stream for the mean chunks
   hipStream_t s2 = nullptr;
   hipEvent_t g1 = nullptr, g2 = nullptr, e2a = nullptr, jb = nullptr;
@@ -647,7 +648,10 @@ struct SideStream {
 // after the Kabsch records; 2 the mean in two chunks on a second side stream, each in a window where the
 // main stream runs latency- or bandwidth-bound kernels: rows [0, M1) (CDX_MEAN_CHUNK1 of them, default 0.3)
 // beside the selection / compaction — the refine pass waits for them —, the rest beside the merge and the
-// exact selection after the refine pass; the level kernel follows the all-tip and target rows.
+// exact selection after the refine pass; the level kernel follows the all-tip and target rows; 4 the
+// whole mean after the refine kernel (the side stream waits an event recorded between it and the merge),
+// beside the bandwidth-bound merge and the latency-bound exact selection, instead of whichever of the
+// refine pass and the mean the command processor happens to dispatch first after the records.
 int mean_sched() {
   static const int m = [] {
     const char* e = cdx::ab_env("CDX_MEAN_SCHED");
@@ -758,8 +762,8 @@ bool side_stream(SideStream& out) {
       (void)hipGetLastError();
       return false;
     }
-    hipEvent_t ev[4];
-    for (int i = 0; i < 4; ++i) {
+    hipEvent_t ev[5];
+    for (int i = 0; i < 5; ++i) {
       if (hipEventCreateWithFlags(&ev[i], side_event_flags()) != hipSuccess) {
         for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
         (void)hipStreamDestroy(st);
@@ -772,8 +776,9 @@ bool side_stream(SideStream& out) {
     ss.join = ev[1];
     ss.gate = ev[2];
     ss.joinB = ev[3];
+    ss.late = ev[4];
   }
-  if (mean_sched() >= 2 && !ss.s2) {
+  if ((mean_sched() == 2 || mean_sched() == 3) && !ss.s2) {
     // CDX_SIDEB_PRIO: the mean chunks' stream priority (0 normal, default: the merge's workgroups are
     // dispatched first and the mean fills the CUs around them; > 0 highest, < 0 lowest)
     const char* pe = cdx::ab_env("CDX_SIDEB_PRIO");
@@ -1054,6 +1059,9 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
                            kabsch_noise, seed, w.krot);
       return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
     };
+    // mean_sched 4: the fork runs the records only; launch_late queues the mean and the level kernel behind
+    // the refine kernel's event
+    const bool late = kmode == 1 && vlate && !mean_split() && !mean_first() && mean_sched() == 4;
     auto launch_fork = [&]() -> int {
       forked = true;
       if (hipEventRecord(ss.fork, s) != hipSuccess || hipStreamWaitEvent(ss.s, ss.fork, 0) != hipSuccess) return CDX_ELAUNCH;
@@ -1061,6 +1069,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
         const int r = launch_records(ss.s);
         if (r) return r;
       }
+      if (late) return hipEventRecord(ss.join, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
       int r = cdx_gpis_mean(&p->gpis, w.X, MqA, w.mean, w.gmean, w.normal, side);
       if (r) return r;
       if (kmode == 1 && mean_first() && (r = launch_records(ss.s))) return r;
@@ -1073,6 +1082,18 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
         if (r) return r;
         level_early = true;
       }
+      return hipEventRecord(ss.join, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
+    };
+    auto launch_late = [&]() -> int {  // after the main stream recorded ss.late
+      if (hipStreamWaitEvent(ss.s, ss.late, 0) != hipSuccess) return CDX_ELAUNCH;
+      int r = cdx_gpis_mean(&p->gpis, w.X, Mq, w.mean, w.gmean, w.normal, side);
+      if (r) return r;
+      GpisView gv0;
+      gv0.mean = w.mean; gv0.gmean = w.gmean; gv0.normal = w.normal; gv0.std_ = w.std_; gv0.gstd = w.gstd;
+      gv0.E = E; gv0.T = T; gv0.Lq = p->n_query_levels; gv0.e = 0;
+      r = launch_level<true>(p, E, q, comp, target, kabsch_noise, seed, w, gv0, flip, w.krot, ss.s);
+      if (r) return r;
+      level_early = true;
       return hipEventRecord(ss.join, ss.s) != hipSuccess ? CDX_ELAUNCH : CDX_OK;
     };
     auto launch_b = [&]() -> int {  // mean B, gated behind the work already on `s`
@@ -1090,7 +1111,7 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     // for it).  Phase 2 right after the refine kernel (g2 recorded between it and the merge): B the
     // remaining all-tip / target rows, e2a, the pregrasp / palm rows; A waits e2a, runs the level kernel and
     // records join; B waits join and records jb, which the main stream waits for before the combine.
-    const bool sched2 = fork && kabsch_mode() == 1 && vlate && !mean_split() && mean_sched() >= 2 && ss.s2;
+    const bool sched2 = fork && kabsch_mode() == 1 && vlate && !mean_split() && (mean_sched() == 2 || mean_sched() == 3) && ss.s2;
     // 3: the ∇std pass waits for both side streams (mean chunks, level kernel) instead of the combine, so
     // that no mean / level workgroup holds a CU the pass needs
     const bool wait_before_grad = sched2 && mean_sched() == 3;
@@ -1158,8 +1179,9 @@ int cdx_closure(const cdx_problem* p, int64_t E, const double* q, const double* 
     double* rpart = nullptr;
     int64_t rpad = 0;
     rc = cdx::gpis_refine_launch(p->gpis, w.X, w.rows, w.stats + cdx::SS_EXTRA, (int)Mg, Ms, w.refine_ws, w.V, s, &rpart,
-                                 &rpad, nullptr, true, sched2 ? ss.g2 : nullptr);
+                                 &rpad, nullptr, true, sched2 ? ss.g2 : (late && forked ? ss.late : nullptr));
     if (!rc && sched2) rc = launch_phase2();
+    if (!rc && late && forked) rc = launch_late();
     if (!rc && inject_fail(2)) rc = CDX_ELAUNCH;
     if (rc) return joined(rc);
     if (!sched2 && fp == 3 && (rc = launch_fork())) return joined(rc);
