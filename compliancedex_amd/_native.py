@@ -80,7 +80,7 @@ KIN_OPT_FIELDS = ["pose", "target", "comp", "g_pose", "g_target", "g_comp", "m_p
 class CdxKinOptBuffers(C.Structure):
     _fields_ = ([(n, C.c_void_p) for n in KIN_OPT_FIELDS] + [("margin", C.c_void_p * 2), ("normal", C.c_void_p * 2)] +
                 [(n, C.c_void_p) for n in ("opt_value", "opt_margin", "opt_normal", "opt_pose", "opt_target",
-                                            "opt_comp", "any", "tips")])
+                                            "opt_comp", "any", "tips", "fk_state")])
 
 
 class CdxSdfBatchQuery(C.Structure):
@@ -178,6 +178,7 @@ _SIGS = {
     "cdx_profile_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "cdx_kin_step": (C.c_int, [C.POINTER(CdxChain), C.POINTER(CdxKinOpt), C.POINTER(CdxKinOptBuffers), _I64, C.c_int32,
                                C.c_int32, C.c_int32, _P]),
+    "cdx_kin_fk_state_bytes": (_I64, [_I64, C.c_int32]),
     "cdx_kin_iteration": (C.c_int, [C.POINTER(CdxChain), C.POINTER(CdxKinParams), C.POINTER(CdxKinOpt),
                                     C.POINTER(CdxKinOptBuffers), _I64, C.c_int32] + [_P] * 10 +
                           [C.c_uint64, C.c_int32, _P]),

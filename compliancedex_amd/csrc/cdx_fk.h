@@ -386,38 +386,41 @@ CDX_HD void fk_tip_bwd3(const cdx_chain& c, int k, const Q& q, const float* gpos
   }
 }
 
-// fk_tip_bwd3 with the joints' axes and origins in caller-provided LDS instead of registers (deep chains, where the
-// registers are spent): slot (l, i) of this lane at st[(6·l + i)·64 + lane] (64-lane interleave, conflict-free).
-template <int MAXD, class Q, class GQ>
-CDX_HD void fk_tip_bwd3s(const cdx_chain& c, int k, const Q& q, const float* gpos, GQ&& g_q, float* st, int lane) {
-  const uint32_t mask = chain_path_mask(c, c.tip_body[k]);
-  const int n = path_depth(mask);
-  float R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f}, t[3] = {0.f, 0.f, 0.f};
-  uint32_t dofs = 0u;  // levels with a moving joint
-  uint32_t m = mask;
-#pragma unroll
-  for (int l = 0; l < MAXD; ++l) {
-    if (l < n) {
-      const cdx_body& b = c.bodies[low_bit(m)];
-      m &= m - 1;
-      float Rn[9], tn[3];
-      chain_step(b, q, R, t, Rn, tn);
-      if (b.dof >= 0) {
-        const int ax = b.axis;
-        const float fa[3] = {ax == 0 ? b.F[0] : (ax == 1 ? b.F[1] : b.F[2]), ax == 0 ? b.F[3] : (ax == 1 ? b.F[4] : b.F[5]),
-                             ax == 0 ? b.F[6] : (ax == 1 ? b.F[7] : b.F[8])};
-        float om[3];
-        mat3_vec(R, fa, om);
-        for (int i = 0; i < 3; ++i) {
-          st[(6 * l + i) * 64 + lane] = om[i];
-          st[(6 * l + 3 + i) * 64 + lane] = tn[i];
-        }
-        dofs |= 1u << l;
+// fk_tip_bwd3 with the joints' axes and origins in caller-provided memory instead of registers (deep chains, where the
+// registers are spent), in its two halves, so that a walk done earlier (the fused Kin iteration's next-fingertip FK,
+// which walks the same joint row) can stand in for the first: fk_tip_walk3s leaves the final pose and, through
+// put(l, i, v), each moving joint's slots at path level l (i < 3: ω, 3 ≤ i < 6: o); fk_tip_bwd3_grad takes the
+// per-joint products from get(l, i).  Rolled loops over the path: the unrolled form (MAXD copies of the joint's
+// sin / cos and products) measured ≈ 1.7× the cycles of a walk at one wave per SIMD, kin_cost4_kernel's occupancy
+// (tools/kin_phases.py).
+template <class Q, class PUT>
+CDX_HD void fk_tip_walk3s(const cdx_chain& c, int k, const Q& q, float* R, float* t, PUT&& put) {
+  for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.f : 0.f;
+  t[0] = t[1] = t[2] = 0.f;
+  int l = 0;
+  for (uint32_t m = chain_path_mask(c, c.tip_body[k]); m; m &= m - 1, ++l) {
+    const cdx_body& b = c.bodies[low_bit(m)];
+    float Rn[9], tn[3];
+    chain_step(b, q, R, t, Rn, tn);
+    if (b.dof >= 0) {
+      const int ax = b.axis;
+      const float fa[3] = {ax == 0 ? b.F[0] : (ax == 1 ? b.F[1] : b.F[2]), ax == 0 ? b.F[3] : (ax == 1 ? b.F[4] : b.F[5]),
+                           ax == 0 ? b.F[6] : (ax == 1 ? b.F[7] : b.F[8])};
+      float om[3];
+      mat3_vec(R, fa, om);
+      for (int i = 0; i < 3; ++i) {
+        put(l, i, om[i]);
+        put(l, 3 + i, tn[i]);
       }
-      for (int i = 0; i < 9; ++i) R[i] = Rn[i];
-      for (int i = 0; i < 3; ++i) t[i] = tn[i];
     }
+    for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+    for (int i = 0; i < 3; ++i) t[i] = tn[i];
   }
+}
+
+template <class GQ, class GET>
+CDX_HD void fk_tip_bwd3_grad(const cdx_chain& c, int k, const float* R, const float* t, const float* gpos, GQ&& g_q,
+                             GET&& get) {
   float GR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const float Gt[3] = {gpos[0], gpos[1], gpos[2]};
   if (c.has_offsets) {
@@ -437,22 +440,18 @@ CDX_HD void fk_tip_bwd3s(const cdx_chain& c, int k, const Q& q, const float* gpo
     w[1] += r2 * g0 - r0 * g2;
     w[2] += r0 * g1 - r1 * g0;
   }
-  m = mask;
-#pragma unroll
-  for (int l = 0; l < MAXD; ++l) {
-    if (l < n) {
-      const cdx_body& b = c.bodies[low_bit(m)];
-      m &= m - 1;
-      if ((dofs >> l) & 1u) {
-        float om[3], o[3];
-        for (int i = 0; i < 3; ++i) {
-          om[i] = st[(6 * l + i) * 64 + lane];
-          o[i] = st[(6 * l + 3 + i) * 64 + lane];
-        }
-        const float ox[3] = {o[1] * Gt[2] - o[2] * Gt[1], o[2] * Gt[0] - o[0] * Gt[2], o[0] * Gt[1] - o[1] * Gt[0]};
-        const float dth = om[0] * (w[0] - ox[0]) + om[1] * (w[1] - ox[1]) + om[2] * (w[2] - ox[2]);
-        g_q(b.dof, b.sign * dth);
+  int l = 0;
+  for (uint32_t m = chain_path_mask(c, c.tip_body[k]); m; m &= m - 1, ++l) {
+    const cdx_body& b = c.bodies[low_bit(m)];
+    if (b.dof >= 0) {
+      float om[3], o[3];
+      for (int i = 0; i < 3; ++i) {
+        om[i] = get(l, i);
+        o[i] = get(l, 3 + i);
       }
+      const float ox[3] = {o[1] * Gt[2] - o[2] * Gt[1], o[2] * Gt[0] - o[0] * Gt[2], o[0] * Gt[1] - o[1] * Gt[0]};
+      const float dth = om[0] * (w[0] - ox[0]) + om[1] * (w[1] - ox[1]) + om[2] * (w[2] - ox[2]);
+      g_q(b.dof, b.sign * dth);
     }
   }
 }

@@ -39,6 +39,32 @@ struct QRowLds {
   __device__ __forceinline__ float operator[](int i) const { return p[i]; }
 };
 
+// The fused Kin iteration's FK-walk cache (cdx_kin_opt_buffers::fk_state): per 64-lane workgroup a block of FKS_BLOCK
+// floats holding, per lane, the final pose R (slots 0–8) and t (9–11) of the lane's fingertip chain, each moving joint's
+// world axis and origin at path level l (slots 12 + 6·l … 12 + 6·l + 5) and the joint angles the walk read (the lane's
+// DOFs f + 4u at slot 12 + 6·MAXD + u) — written by the step's next-fingertip walk, read by the next iteration's FK
+// backward when the candidate's joint row still has exactly those bits.  Slot s of lane l at float
+// (s / 4)·256 + 4·l + s % 4: 16-byte units in lane order, so that the writer stores one dwordx4 per four slots
+// (a dword store per slot cost ≈ 30 k cycles a wave) and the reader's LDS-DMA copies the block as it lies.
+constexpr int FKS_PF = CDX_MAX_DOFS / 4;
+constexpr int fks_slots(int maxd) { return 12 + 6 * maxd + FKS_PF; }
+constexpr int FKS_BLOCK = fks_slots(CDX_MAX_DEPTH) * 64;
+__device__ __forceinline__ int fks_at(int slot, int lane) { return (slot >> 2) * 256 + 4 * lane + (slot & 3); }
+static_assert(fks_slots(8) % 4 == 0 && fks_slots(CDX_MAX_DEPTH) % 4 == 0, "whole 1-KB DMA units per block");
+
+#if defined(CDX_KIN_DIAG_PHASES)  // (timing-only diagnostic build: per-wave shader-clock stamps at the kernel's phases)
+__device__ unsigned long long g_kin_phase[4096][16];
+#define KIN_PHASE(i)                                                                                      \
+  do {                                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                                    \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                           \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_kin_phase[blockIdx.x][i] = t_;                          \
+    __builtin_amdgcn_sched_barrier(0);                                                                    \
+  } while (0)
+#else
+#define KIN_PHASE(i) do {} while (0)
+#endif
+
 __device__ __forceinline__ float adam_f32(float p, float g, float& m, float& v, float w1, float b2, float w2, float bc2s,
                                           float eps, float step) {
   // torch.optim.Adam's single-tensor / foreach update in float32 opmath: m.lerp_(g, 1 − β1);
@@ -225,9 +251,15 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
     float* __restrict__ g_target, float* __restrict__ g_comp, float* __restrict__ g_tip, cdx_kin_opt cfg,
     cdx_kin_opt_buffers sb, int it) {
   constexpr int NT = 4;
+  if constexpr (STEP && FK) KIN_PHASE(0);
 #if !defined(CDX_KIN_FK_BWD1)
   __shared__ float s_fk[CDX_MAX_DOFS][64];  // per-DOF FK gradient contributions (then, with STEP, the summed ones)
 #endif
+#if !defined(CDX_KIN_FK_BWD1) && !defined(CDX_KIN_FK_BWD2)
+  // the FK walk's slots (fk_tip_walk3s) behind the final pose; with STEP, the whole FK-walk cache image (FKS_BLOCK)
+  __shared__ float s_jst[fks_slots(MAXD) * 64];
+#endif
+  __shared__ float s_qn[64 / NT][CDX_MAX_DOFS];  // STEP: the candidates' joint rows (cache check), then the updated rows
   // STEP: the step's operands, prefetched (DOFs f + 4u of the candidate's row, this lane's target / compliance)
   constexpr int PF_DOFS = CDX_MAX_DOFS / NT;
   float pf_p[PF_DOFS], pf_m[PF_DOFS], pf_v[PF_DOFS], pf_t[3], pf_tm[3], pf_tv[3], pf_c = 0.f, pf_cm = 0.f, pf_cv = 0.f;
@@ -278,6 +310,29 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
   } else {
     for (int i = 0; i < 9; ++i) nz[i] = (double)(kin_mix(seed ^ kin_mix((uint64_t)(e * 9 + i))) >> 11) * 0x1.0p-53;
   }
+#if !defined(CDX_KIN_FK_BWD1) && !defined(CDX_KIN_FK_BWD2)
+  // STEP (Kin): the previous iteration's FK-walk cache of this workgroup and the candidates' current joint rows, into
+  // LDS by DMA now — they land while the reward runs; the FK backward checks them and skips the chain walk
+  const bool fks = STEP && FK && it > 0 && sb.fk_state != nullptr;
+  if (fks) {
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    const float* gb = sb.fk_state + (int64_t)blockIdx.x * FKS_BLOCK;
+#pragma unroll
+    for (int c = 0; c < fks_slots(MAXD) / 4; ++c)
+      __builtin_amdgcn_global_load_lds(gb + 256 * c + 4 * threadIdx.x, (lds_ptr)(s_jst + 256 * c), 16, 0, 0);
+    // rows e0 … e0 + 15 (16·D floats, contiguous from pose + e0·D; 16-byte units past the block or past E·D re-read
+    // the first unit: those LDS words belong to no live candidate)
+    const int64_t e0 = (int64_t)blockIdx.x * (64 / NT);
+    const float* qb = sb.pose + e0 * D;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int64_t u = 64 * c + threadIdx.x;
+      const bool in = 4 * u + 4 <= (int64_t)(64 / NT) * D && (e0 * D + 4 * u + 4) <= E * D;
+      __builtin_amdgcn_global_load_lds(qb + (in ? 4 * u : 0), (lds_ptr)(&s_qn[0][0] + 256 * c), 16, 0, 0);
+    }
+  }
+#endif
+  if constexpr (STEP && FK) KIN_PHASE(1);
   cdx::ForceEqParams fp;
   fp.cos_mu = (double)p.fe.cos_mu;
   fp.gravity = p.fe.gravity;
@@ -299,6 +354,7 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
 #elif !defined(CDX_KIN_DIAG_NOFE)
   fe.forward(fp, NT, tp, tg, cp, nr, nz);
 #endif
+  if constexpr (STEP && FK) KIN_PHASE(2);
 
   // ---- forward
   double ct[3] = {0, 0, 0}, cg[3] = {0, 0, 0};
@@ -343,6 +399,7 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
   for (int k = 0; k < NT; ++k) mo = k == f ? (double)fe.margin[k] : mo;
   if (on) margin[r] = mo;
 
+  if constexpr (STEP && FK) KIN_PHASE(3);
   // ---- backward (dl = 1)
   double gt[NT][3], gg[NT][3], gc[NT];
   for (int k = 0; k < NT; ++k) {
@@ -382,6 +439,7 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
 #elif !defined(CDX_KIN_DIAG_NOFE)
   fe.backward(-5.0, g_fn, cp, gt, gg, gc);
 #endif
+  if constexpr (STEP && FK) KIN_PHASE(4);
   // this lane's fingertip (selects: no dynamic register indexing)
   double gto[3] = {0, 0, 0}, ggo[3] = {0, 0, 0}, gco = 0.0;
 #pragma unroll
@@ -431,13 +489,67 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
 #if defined(CDX_KIN_FK_BWD2)  // (A/B: two walks, no per-level state)
     cdx::fk_tip_bwd2<MAXD>(kc, f, q + e * D, gpos, [&](int d, float v) { s_fk[d][threadIdx.x] += v; });
 #else  // one walk, each joint's world axis and origin kept in LDS
-    __shared__ float s_jst[6 * MAXD * 64];
-    cdx::fk_tip_bwd3s<MAXD>(kc, f, q + e * D, gpos, [&](int d, float v) { s_fk[d][threadIdx.x] += v; }, s_jst,
-                            (int)threadIdx.x);
+    auto gacc = [&](int d, float v) { s_fk[d][threadIdx.x] += v; };
+    // the joints' slots in s_jst, in the cache's layout (fks_at)
+    auto jput = [&](int l, int i, float v) { s_jst[fks_at(12 + 6 * l + i, threadIdx.x)] = v; };
+    auto jget = [&](int l, int i) { return s_jst[fks_at(12 + 6 * l + i, threadIdx.x)]; };
+    bool cached = false;
+    if constexpr (STEP && FK) KIN_PHASE(12);
+    if (fks) {
+      // the cache holds this candidate's walk if the joint row it was walked on has the current row's bits (every
+      // lane checks its DOFs f + 4u, the candidate's four lanes agree); a row rewritten since (another entry point's
+      // step, a caller) fails the check and walks
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const float* qc = &s_qn[0][0] + (threadIdx.x / NT) * D;
+      int okl = 1;
+#pragma unroll
+      for (int u = 0; u < FKS_PF; ++u) {
+        const int i = f + NT * u;
+        if (i < D && __float_as_uint(s_jst[fks_at(12 + 6 * MAXD + u, threadIdx.x)]) != __float_as_uint(qc[i])) okl = 0;
+      }
+      okl &= __shfl_xor(okl, 1);
+      okl &= __shfl_xor(okl, 2);
+      cached = okl != 0;
+    }
+    if constexpr (STEP && FK) KIN_PHASE(13);
+    if (cached) {
+      float R[9], t[3];
+      for (int i = 0; i < 9; ++i) R[i] = s_jst[fks_at(i, threadIdx.x)];
+      for (int i = 0; i < 3; ++i) t[i] = s_jst[fks_at(9 + i, threadIdx.x)];
+      cdx::fk_tip_bwd3_grad(kc, f, R, t, gpos, gacc, jget);
+    } else {
+      float R[9], t[3];
+      cdx::fk_tip_walk3s(kc, f, q + e * D, R, t, jput);
+      cdx::fk_tip_bwd3_grad(kc, f, R, t, gpos, gacc, jget);
+    }
 #endif
 #endif
+    if constexpr (STEP && FK) KIN_PHASE(14);
     float* fk_g = nullptr;
     (void)fk_g;
+#endif
+#if !defined(CDX_KIN_FK_BWD1)
+    if constexpr (STEP) {
+      // the same sums, DOF by DOF; a lane's own DOFs f + 4u take their joint angle from the step's prefetch (the
+      // loop below re-reads q per DOF behind the previous DOF's g_q store, which q may alias: one load latency each)
+#pragma unroll
+      for (int u = 0; u < PF_DOFS; ++u)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int i = NT * u + j;
+          if (i >= D) break;
+          float s = s_fk[i][threadIdx.x];
+          s += __shfl_xor(s, 1);
+          s += __shfl_xor(s, 2);
+          if (j == f) {
+            const double d = (double)pf_p[u] - (double)p.ref_q[i];
+            const float gq = qn > 0 ? (float)(10.0 * d / qn) : 0.f;
+            if (on) g_q[e * D + i] = gq + s;
+            s_fk[i][threadIdx.x] = gq + s;  // (this lane's own slot: the step below reads it)
+          }
+        }
+    } else
 #endif
     for (int i = 0; i < D; ++i) {
 #if defined(CDX_KIN_FK_BWD1)
@@ -457,6 +569,7 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
       }
     }
   }
+  if constexpr (STEP && FK) KIN_PHASE(5);
   if (on) {
     if (g_tip)
       for (int i = 0; i < 3; ++i) g_tip[3 * r + i] = (float)gto[i];
@@ -486,8 +599,7 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
     }
     if (__any(flag) && threadIdx.x == 0) atomicOr(sb.any + it % 3, 1u);
     const AdamConst ac = adam_const(cfg, it);
-    __shared__ float s_qn[64 / NT][CDX_MAX_DOFS];  // the candidates' updated joint rows, for the FK
-    float* qs = s_qn[threadIdx.x / NT];
+    float* qs = s_qn[threadIdx.x / NT];  // the candidates' updated joint rows, for the FK
 #pragma unroll
     for (int u = 0; u < PF_DOFS; ++u) {
       const int i = f + NT * u;
@@ -519,13 +631,38 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
         sb.v_comp[r] = v;
       }
     }
+    KIN_PHASE(6);
     __syncthreads();
-    if (on && sb.tips) {
+    KIN_PHASE(11);
+    if (sb.tips) {
       const cdx_chain& kc = *(const cdx_chain*)(__builtin_amdgcn_kernarg_segment_ptr());
       float pos[3];
-      cdx::fk_tip(kc, f, QRowLds{qs}, pos, nullptr);
-      for (int i = 0; i < 3; ++i) sb.tips[3 * r + i] = pos[i] + cfg.palm_offset[i];
+      if (sb.fk_state) {  // the walk, kept for the next iteration's FK backward (every lane: its own slots)
+        // the walk's slots into this lane's image in s_jst (the backward is done with it), then the lane's whole image
+        // to memory after the walk — stores inside it would make each level's chain-descriptor load wait for them
+        // (one vmcnt) — one dwordx4 per four slots
+        float R[9], t[3];
+        KIN_PHASE(8);
+        cdx::fk_tip_walk3s(kc, f, QRowLds{qs}, R, t,
+                           [&](int l, int i, float v) { s_jst[fks_at(12 + 6 * l + i, threadIdx.x)] = v; });
+        KIN_PHASE(9);
+        cdx::tip_from_pose(kc, f, R, t, pos, nullptr);
+        for (int i = 0; i < 9; ++i) s_jst[fks_at(i, threadIdx.x)] = R[i];
+        for (int i = 0; i < 3; ++i) s_jst[fks_at(9 + i, threadIdx.x)] = t[i];
+#pragma unroll
+        for (int u = 0; u < FKS_PF; ++u) s_jst[fks_at(12 + 6 * MAXD + u, threadIdx.x)] = f + NT * u < D ? qs[f + NT * u] : 0.f;
+        const float4* l4 = reinterpret_cast<const float4*>(s_jst) + threadIdx.x;
+        float4* gb4 = reinterpret_cast<float4*>(sb.fk_state + (int64_t)blockIdx.x * FKS_BLOCK) + threadIdx.x;
+#pragma unroll
+        for (int c = 0; c < fks_slots(MAXD) / 4; ++c) gb4[64 * c] = l4[64 * c];
+        KIN_PHASE(10);
+      } else {
+        cdx::fk_tip(kc, f, QRowLds{qs}, pos, nullptr);
+      }
+      if (on)
+        for (int i = 0; i < 3; ++i) sb.tips[3 * r + i] = pos[i] + cfg.palm_offset[i];
     }
+    KIN_PHASE(7);
   }
 #endif
   if constexpr (STEP && !FK) {
@@ -824,3 +961,14 @@ extern "C" int cdx_kin_iteration(const cdx_chain* chain, const cdx_kin_params* p
 #undef CDX_KIN4_STEP_LAUNCH
   return hipGetLastError() == hipSuccess ? CDX_OK : CDX_ELAUNCH;
 }
+
+extern "C" int64_t cdx_kin_fk_state_bytes(int64_t E, int32_t n_tips) {
+  if (E <= 0 || n_tips != 4) return 0;  // (only the four-fingertip one-launch iteration keeps the cache)
+  return ((4 * E + 63) / 64) * (int64_t)FKS_BLOCK * (int64_t)sizeof(float);
+}
+
+#if defined(CDX_KIN_DIAG_PHASES)
+extern "C" int cdx_kin_phase_read(unsigned long long* out) {  // [4096][8] stamps of the last fused Kin iteration
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kin_phase), sizeof(g_kin_phase)) == hipSuccess ? 0 : 1;  // [4096][16]
+}
+#endif

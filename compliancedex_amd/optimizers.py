@@ -341,7 +341,15 @@ class KinGraspOptimizer:
             cfg.palm_offset[i] = off[i]
         st = _FusedLoop(E, T, q, tgt, comp, faces, faces_deflate, dev)
         st.buffers.tips = N.ptr(st.tips)
-        one_launch = os.environ.get("CDX_KIN_FUSED_STEP", "1") != "0"  # (A/B: cdx_kin_cost + cdx_kin_step)
+        # (A/B: "0" cdx_kin_cost + cdx_kin_step; "alt" the two forms alternating, even iterations two launches — a
+        # test hook: the one-launch iterations then find the FK-walk cache one step stale and must walk)
+        fused_step = os.environ.get("CDX_KIN_FUSED_STEP", "1")
+        one_launch = fused_step != "0"
+        nb = int(lib.cdx_kin_fk_state_bytes(E, T))
+        if one_launch and nb and os.environ.get("CDX_KIN_FK_CACHE", "1") != "0":  # (A/B: every iteration walks)
+            # the step's FK walk kept for the next iteration's FK backward; 0xFF bytes: no joint row matches it
+            st.fk_state = torch.full((nb // 4,), -1, dtype=torch.int32, device=dev)
+            st.buffers.fk_state = N.ptr(st.fk_state)
         stream = N.stream_ptr(dev)
         N.check(lib.cdx_fk_forward(chain, N.ptr(q), E, N.ptr(st.tips), None, stream), "cdx_fk_forward")
         st.tips.add_(self.palm_offset.float())  # FK + palm offset (:148); later iterations: cdx_kin_step
@@ -353,7 +361,8 @@ class KinGraspOptimizer:
             self._seed += 1
             loss = st.loss_slot(s, self.num_iters)
             qr = [N.ptr(t) for t in st.queries(st.tips, tgt)]
-            if not verbose and one_launch:  # cost, backward and step in one launch (cdx_kin_iteration)
+            if not verbose and one_launch and not (fused_step == "alt" and s % 2 == 0):
+                # cost, backward and step in one launch (cdx_kin_iteration)
                 N.check(lib.cdx_kin_iteration(chain, prm, cfg, st.buffers, E, T, *qr, N.ptr(nz), self._seed, s, stream),
                         "cdx_kin_iteration")
             else:  # two launches (verbose: the compliances printed before the step, as the reference prints them)

@@ -395,7 +395,17 @@ typedef struct {                          /* device pointers, candidate-major */
   float *opt_pose, *opt_target, *opt_comp;
   uint32_t* any;                          /* [3] */
   float* tips;                            /* rule 0: next fingertips [E*n_tips*3] (nullable) */
+  float* fk_state;                        /* rule 0, one-launch iterations with tips: the FK-walk cache, */
+                                          /* cdx_kin_fk_state_bytes(E, n_tips) bytes (nullable; see below) */
 } cdx_kin_opt_buffers;
+
+/* Bytes of the FK-walk cache cdx_kin_iteration's one-launch Kin iteration uses (0: the case does not use one).  The
+ * step's next-fingertip FK walk leaves each fingertip chain's joint axes / origins and final pose there, with the joint
+ * angles it read, and the next iteration's FK backward takes them instead of walking the chain again when the
+ * candidate's joint row still has exactly those bits (else it walks): the same gradient bits either way.  Fill it with
+ * 0xFF bytes before the first iteration (no finite or generated-NaN angle has that pattern); one cache per loop state
+ * and chain. */
+int64_t cdx_kin_fk_state_bytes(int64_t E, int32_t n_tips);
 
 int cdx_kin_step(const cdx_chain* chain, const cdx_kin_opt* cfg, const cdx_kin_opt_buffers* buf, int64_t E,
                  int32_t n_tips, int32_t iteration, int32_t finalize, cdx_stream_t stream);

@@ -575,6 +575,40 @@ def test_kin_one_launch_iteration_equals_two_launches(monkeypatch, robot):
             assert _bitwise_equal_nan_aware(a, b)
 
 
+@pytest.mark.parametrize("mode", ["alt", "nocache"])
+def test_kin_fk_walk_cache_equals_walking(monkeypatch, mode):
+    """The one-launch Kin iteration's FK-walk cache (cdx_kin_opt_buffers::fk_state: the step's next-fingertip walk kept
+    for the next iteration's FK backward, used only when the candidate's joint row still has the bits it was walked on)
+    against walking every iteration: "nocache" runs the one-launch loop without the cache (CDX_KIN_FK_CACHE=0), "alt"
+    alternates two-launch and one-launch iterations, so that every one-launch iteration finds the cache one step stale
+    (written two iterations back) and must detect it and walk.  Both give the bits of the cached loop and of the
+    all-two-launch loop — deep iiwa7_allegro chain, E = 3000 (a partial last workgroup)."""
+    from compliancedex_amd import KinGraspOptimizer
+    from compliancedex_amd.workloads import banana_mesh, config4_kin_inputs
+    E = 3000
+    links, offs, palm, q, target, comp = config4_kin_inputs(E, device=DEV, q_scale=0.3)
+    outs = {}
+    for name, env in (("cached", {"CDX_KIN_FUSED_STEP": "1", "CDX_KIN_FK_CACHE": "1"}),
+                      (mode, {"CDX_KIN_FUSED_STEP": "alt", "CDX_KIN_FK_CACHE": "1"} if mode == "alt" else
+                       {"CDX_KIN_FUSED_STEP": "1", "CDX_KIN_FK_CACHE": "0"}),
+                      ("two", {"CDX_KIN_FUSED_STEP": "0"})):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        kin = KinGraspOptimizer("iiwa7_allegro", links, offs, palm_offset=palm.tolist(), num_iters=8,
+                                optimize_target=True, ref_q=[0.0] * q.shape[1], seed=5)
+        args = [torch.from_numpy(a).to(DEV) for a in (q, target, comp)]
+        res = kin.optimize(*args, 1.0, banana_mesh(), verbose=False, trace_rows=True)
+        torch.cuda.synchronize()
+        outs[name] = ([t.cpu().numpy() for t in res[:3]] + [kin.best_loss.cpu().numpy()] +
+                      [r.cpu().numpy() for r in kin.loss_rows] + [kin.last_tips.cpu().numpy()])
+    for other in (mode, "two"):
+        for a, b in zip(outs["cached"], outs[other]):
+            if a.dtype == np.float64:
+                assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), other
+            else:
+                assert _bitwise_equal_nan_aware(a, b), other
+
+
 def test_sdf_one_launch_iteration_equals_two_launches(monkeypatch):
     """The SDF optimiser's one-launch iteration (kin_cost4_kernel<8, false, STEP>: cost, backward, best iterate, RMSprop
     and the box clamps) against cdx_kin_cost + cdx_kin_step (CDX_KIN_FUSED_STEP=0): the same bits, with fingertips
