@@ -449,13 +449,22 @@ __global__ __launch_bounds__(COMBINE_BLOCK) void closure_combine_kernel(
     const cdx_chain& kc = (*(const cdx_problem*)(__builtin_amdgcn_kernarg_segment_ptr())).chain;
 #if defined(CDX_COMBINE_FK_BWD1)  // (A/B: the stored-rotations backward walk)
     cdx::fk_tip_bwd<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
-#elif !defined(CDX_COMBINE_DIAG_NOFK)  // (timing-only diagnostic build without the FK backward: outputs wrong)
-#if !defined(CDX_COMBINE_FK_BWD2)
-    if constexpr (MAXD <= 8)  // one walk, the joints' axes and origins kept (CDX_COMBINE_FK_BWD2: two walks, A/B)
+#elif defined(CDX_COMBINE_FK_BWD3R)  // (A/B: round 5 — one unrolled walk in registers for the hands, two walks for deep
+                                     // chains)
+    if constexpr (MAXD <= 8)
       cdx::fk_tip_bwd3<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
     else
-#endif
       cdx::fk_tip_bwd2<MAXD>(kc, f, cdx::QRowD{q + ec * D}, gtl, [&](int d, float v) { gcon[d][tid] += v; }, tl);
+#elif !defined(CDX_COMBINE_DIAG_NOFK)  // (timing-only diagnostic build without the FK backward: outputs wrong)
+    // one rolled walk, the joints' axes and origins in LDS, then the per-joint products (fk_tip_bwd3's arithmetic;
+    // deep chains no longer walk twice)
+    __shared__ float s_cst[6 * MAXD * COMBINE_BLOCK];
+    float R[9], t[3];
+    cdx::fk_tip_walk3s(kc, f, cdx::QRowD{q + ec * D}, R, t,
+                       [&](int l, int i, float v) { s_cst[(6 * l + i) * COMBINE_BLOCK + tid] = v; });
+    cdx::tip_from_pose(kc, f, R, t, tl, nullptr);
+    cdx::fk_tip_bwd3_grad(kc, f, R, t, gtl, [&](int d, float v) { gcon[d][tid] += v; },
+                          [&](int l, int i) { return s_cst[(6 * l + i) * COMBINE_BLOCK + tid]; });
 #endif
   }
   double red[12];  // g_palm_pos (3) + g_Rp (9)
