@@ -263,7 +263,8 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
   // STEP: the step's operands, prefetched (DOFs f + 4u of the candidate's row, this lane's target / compliance)
   constexpr int PF_DOFS = CDX_MAX_DOFS / NT;
   float pf_p[PF_DOFS], pf_m[PF_DOFS], pf_v[PF_DOFS], pf_t[3], pf_tm[3], pf_tv[3], pf_c = 0.f, pf_cm = 0.f, pf_cv = 0.f;
-  float pf_ov = 0.f;
+  float pf_ov = 0.f, pf_nm[3] = {0.f, 0.f, 0.f};
+  double pf_mg = 0.0;
   unsigned pf_any = 0u;
   const int64_t tg_ = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t e_raw = tg_ >> 2;
@@ -485,6 +486,13 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
       pf_c = sb.comp[r];
       pf_cm = sb.m_comp[r];
       pf_cv = sb.v_comp[r];
+      if constexpr (FK)
+        if (it > 0) {  // the previous iteration's margin / normal slot, which the step commits when any improved
+          const bool ps = ((it - 1) & 1) != 0;
+          pf_mg = (ps ? sb.margin[1] : sb.margin[0])[r];
+          const float* nm = ps ? sb.normal[1] : sb.normal[0];
+          for (int i = 0; i < 3; ++i) pf_nm[i] = nm[3 * r + i];
+        }
     }
 #if defined(CDX_KIN_FK_BWD2)  // (A/B: two walks, no per-level state)
     cdx::fk_tip_bwd2<MAXD>(kc, f, q + e * D, gpos, [&](int d, float v) { s_fk[d][threadIdx.x] += v; });
@@ -580,12 +588,9 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
   if constexpr (STEP && FK) {
     // ---- cdx_kin_step's iteration `it` (kin_step_kernel, rule 0, T = 4): the previous iteration's margin / normal
     // commit, the best iterate, Adam, the next fingertip
-    if (pf_any && on) {
-      const bool ps = ((it - 1) & 1) != 0;
-      const double* mg = ps ? sb.margin[1] : sb.margin[0];
-      const float* nm = ps ? sb.normal[1] : sb.normal[0];
-      sb.opt_margin[r] = mg[r];
-      for (int i = 0; i < 3; ++i) sb.opt_normal[3 * r + i] = nm[3 * r + i];
+    if (pf_any && on) {  // (prefetched with the step's operands)
+      sb.opt_margin[r] = pf_mg;
+      for (int i = 0; i < 3; ++i) sb.opt_normal[3 * r + i] = pf_nm[i];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) sb.any[(it + 1) % 3] = 0u;
     const bool flag = on && lval < (double)pf_ov;
