@@ -47,8 +47,11 @@ struct QRowLds {
 // (s / 4)·256 + 4·l + s % 4: 16-byte units in lane order, so that the writer stores one dwordx4 per four slots
 // (a dword store per slot cost ≈ 30 k cycles a wave) and the reader's LDS-DMA copies the block as it lies.
 constexpr int FKS_PF = CDX_MAX_DOFS / 4;
-constexpr int fks_slots(int maxd) { return 12 + 6 * maxd + FKS_PF; }
-constexpr int FKS_BLOCK = fks_slots(CDX_MAX_DEPTH) * 64;
+constexpr int fks_slots(int maxd) { return 12 + 6 * maxd + FKS_PF; }  // the LDS image
+// … and behind the image, in memory only, the iteration that wrote the lane's slots + 1 (a tag: the reader at
+// iteration s takes the slots only when it is s — a zero-filled buffer never matches), then 3 free slots
+constexpr int fks_tag(int maxd) { return fks_slots(maxd); }
+constexpr int FKS_BLOCK = (fks_slots(CDX_MAX_DEPTH) + 4) * 64;
 __device__ __forceinline__ int fks_at(int slot, int lane) { return (slot >> 2) * 256 + 4 * lane + (slot & 3); }
 static_assert(fks_slots(8) % 4 == 0 && fks_slots(CDX_MAX_DEPTH) % 4 == 0, "whole 1-KB DMA units per block");
 
@@ -315,9 +318,11 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
   // STEP (Kin): the previous iteration's FK-walk cache of this workgroup and the candidates' current joint rows, into
   // LDS by DMA now — they land while the reward runs; the FK backward checks them and skips the chain walk
   const bool fks = STEP && FK && it > 0 && sb.fk_state != nullptr;
+  unsigned fks_tg = 0u;
   if (fks) {
     typedef __attribute__((address_space(3))) void* lds_ptr;
     const float* gb = sb.fk_state + (int64_t)blockIdx.x * FKS_BLOCK;
+    fks_tg = reinterpret_cast<const unsigned*>(gb)[fks_at(fks_tag(MAXD), threadIdx.x)];
 #pragma unroll
     for (int c = 0; c < fks_slots(MAXD) / 4; ++c)
       __builtin_amdgcn_global_load_lds(gb + 256 * c + 4 * threadIdx.x, (lds_ptr)(s_jst + 256 * c), 16, 0, 0);
@@ -504,13 +509,13 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
     bool cached = false;
     if constexpr (STEP && FK) KIN_PHASE(12);
     if (fks) {
-      // the cache holds this candidate's walk if the joint row it was walked on has the current row's bits (every
-      // lane checks its DOFs f + 4u, the candidate's four lanes agree); a row rewritten since (another entry point's
-      // step, a caller) fails the check and walks
+      // the cache holds this candidate's walk if the previous iteration wrote it (the tag) and the joint row it was
+      // walked on has the current row's bits (every lane checks its DOFs f + 4u, the candidate's four lanes agree); a
+      // row rewritten since (another entry point's step, a caller) fails the check and walks
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
       const float* qc = &s_qn[0][0] + (threadIdx.x / NT) * D;
-      int okl = 1;
+      int okl = fks_tg == (unsigned)it;
 #pragma unroll
       for (int u = 0; u < FKS_PF; ++u) {
         const int i = f + NT * u;
@@ -660,6 +665,8 @@ __global__ __launch_bounds__(64) void kin_cost4_kernel(
         float4* gb4 = reinterpret_cast<float4*>(sb.fk_state + (int64_t)blockIdx.x * FKS_BLOCK) + threadIdx.x;
 #pragma unroll
         for (int c = 0; c < fks_slots(MAXD) / 4; ++c) gb4[64 * c] = l4[64 * c];
+        reinterpret_cast<unsigned*>(sb.fk_state + (int64_t)blockIdx.x * FKS_BLOCK)[fks_at(fks_tag(MAXD), threadIdx.x)] =
+            (unsigned)it + 1u;
         KIN_PHASE(10);
       } else {
         cdx::fk_tip(kc, f, QRowLds{qs}, pos, nullptr);

@@ -402,9 +402,9 @@ typedef struct {                          /* device pointers, candidate-major */
 /* Bytes of the FK-walk cache cdx_kin_iteration's one-launch Kin iteration uses (0: the case does not use one).  The
  * step's next-fingertip FK walk leaves each fingertip chain's joint axes / origins and final pose there, with the joint
  * angles it read, and the next iteration's FK backward takes them instead of walking the chain again when the
- * candidate's joint row still has exactly those bits (else it walks): the same gradient bits either way.  Fill it with
- * 0xFF bytes before the first iteration (no finite or generated-NaN angle has that pattern); one cache per loop state
- * and chain. */
+ * candidate's joint row still has exactly those bits and the previous iteration wrote it (else it walks): the same
+ * gradient bits either way.  Any initial contents work (0xFF bytes in the Python layer); one cache per loop state and
+ * chain. */
 int64_t cdx_kin_fk_state_bytes(int64_t E, int32_t n_tips);
 
 int cdx_kin_step(const cdx_chain* chain, const cdx_kin_opt* cfg, const cdx_kin_opt_buffers* buf, int64_t E,

@@ -27,7 +27,11 @@ def main():
     fs = st.fk_state.view(torch.float32).cpu().numpy()
     pose = st.pose.cpu().numpy().reshape(E, -1)
     D = pose.shape[1]
-    blk = 116 * 64
+    blk = 120 * 64  # FKS_BLOCK: the 116-slot image + the tag chunk
+
+    def at(slot, lane):  # 16-byte units in lane order (cdx_kin.hip fks_at)
+        return (slot >> 2) * 256 + 4 * lane + (slot & 3)
+    tags = [int(fs[b * blk + at(116, l)].view(np.uint32)) for b in range(4 * E // 64) for l in range(64)]
     ok, bad = 0, 0
     for lane_g in range(4 * E):
         b, l = divmod(lane_g, 64)
@@ -36,14 +40,14 @@ def main():
             i = f + 4 * u
             if i >= D:
                 continue
-            v = fs[b * blk + (12 + 6 * 16 + u) * 64 + l]
+            v = fs[b * blk + at(12 + 6 * 16 + u, l)]
             if v.view(np.uint32) == pose[e, i].view(np.uint32):
                 ok += 1
             else:
                 bad += 1
-    R0 = fs[0 * blk + np.arange(9) * 64 + 0]
-    print(json.dumps({"qcheck_ok": ok, "qcheck_bad": bad, "R_lane0": R0.tolist(),
-                      "first_bad_words": fs[:8].view(np.uint32).tolist()}))
+    R0 = np.array([fs[at(i, 0)] for i in range(9)])
+    print(json.dumps({"qcheck_ok": ok, "qcheck_bad": bad, "tags": sorted(set(tags)), "iterations": 3,
+                      "R_lane0": R0.tolist()}))
 
 
 if __name__ == "__main__":
