@@ -347,7 +347,7 @@ class KinGraspOptimizer:
         one_launch = fused_step != "0"
         nb = int(lib.cdx_kin_fk_state_bytes(E, T))
         if one_launch and nb and os.environ.get("CDX_KIN_FK_CACHE", "1") != "0":  # (A/B: every iteration walks)
-            # the step's FK walk kept for the next iteration's FK backward; 0xFF bytes: no joint row matches it
+            # the step's FK walk kept for the next iteration's FK backward (any contents: the kernel tags what it wrote)
             st.fk_state = torch.full((nb // 4,), -1, dtype=torch.int32, device=dev)
             st.buffers.fk_state = N.ptr(st.fk_state)
         stream = N.stream_ptr(dev)
