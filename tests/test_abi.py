@@ -76,6 +76,11 @@ def test_bad_arguments_are_rejected_without_launch():
     cfg.rule = 0
     assert lib.cdx_kin_iteration(None, prm, cfg, buf, 4, 4, *[None] * 10, 0, 0, None) == -1  # Kin without a chain
     assert lib.cdx_kin_iteration(c, prm, cfg, buf, 4, 3, *[None] * 10, 0, 0, None) == -1  # tip count mismatch
+    # the FK-walk cache: one block of (12 + 6·16 + 8 + 4) slots × 64 lanes of floats per 64-lane workgroup (four lanes
+    # a candidate), none for other fingertip counts or no candidates
+    assert lib.cdx_kin_fk_state_bytes(16384, 4) == 1024 * 120 * 64 * 4
+    assert lib.cdx_kin_fk_state_bytes(3000, 4) == 188 * 120 * 64 * 4
+    assert lib.cdx_kin_fk_state_bytes(3000, 3) == 0 and lib.cdx_kin_fk_state_bytes(0, 4) == 0
     p = N.CdxProblem()
     assert lib.cdx_closure_workspace(p, 10) == 0
     assert lib.cdx_closure(p, 10, *([None] * 6), ctypes.c_uint64(0), *([None] * 11)) == -1
